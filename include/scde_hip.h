@@ -1,0 +1,151 @@
+/*
+ * scde_hip.h -- C ABI of the MI355X-native scde differential-expression path.
+ *
+ * Two layers:
+ *
+ *  1. Drop-in replacements for the five native entry points the reference
+ *     resolves by name through `.Call(..., PACKAGE = "scde")`
+ *     (NAMESPACE:29 useDynLib(scde); no R_registerRoutines).  Arguments are
+ *     the R objects the R glue passes, flattened to plain pointers:
+ *     matrices are R column-major, list-of-int-vectors become (values,
+ *     offsets[n+1]).  Host pointers in, host pointers out; the GPU work is
+ *     internal.  The `.Call` shim a maintainer would add is in INTEGRATION.md.
+ *
+ *  2. The device-resident pipeline (what bench.py times): counts stay in HBM,
+ *     one call runs scde.expression.difference for one batch of genes.
+ *
+ * Every function returns 0 on success or a nonzero SCDE_E* code; the message
+ * is available from scde_last_error() (thread-local).  Errors are never
+ * silently replaced by a CPU fallback: there is none.
+ */
+#ifndef SCDE_HIP_H
+#define SCDE_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCDE_OK 0
+#define SCDE_EARG 1   /* invalid argument / shape */
+#define SCDE_EHIP 2   /* HIP runtime error (no device, launch failure, OOM) */
+#define SCDE_EINTERNAL 3
+
+const char* scde_last_error(void);
+int scde_version(void); /* 100 * major + minor */
+
+/* ---------------------------------------------------------------- layer 1 */
+
+/* Replaces logBootPosterior  (src/jpmatLogBoot.cpp:100, decl src/jpmatLogBoot.h:8).
+ *  models     ncells x 12 col-major (R `mm`, NaN where a column is absent)
+ *  ucl_vals   concatenated Ucl list (unique counts per cell), ucl_off[ncells+1]
+ *  counti     ngenes x ncells col-major, 0-based index into the cell's Ucl
+ *  magnitudes ngrid natural-log magnitudes (marginals)
+ *  outputs    jp    ngenes x ngrid col-major                   (always)
+ *             modes ngenes x ncells col-major       (return_post in {1,3})
+ *             post  ncells consecutive ngenes x ngrid col-major blocks (return_post in {2,3})
+ */
+int scde_logBootPosterior(const double* models, int ncells, const int* ucl_vals, const int64_t* ucl_off,
+                          const int* counti, int ngenes, const double* magnitudes, int ngrid, int nboot, int seed,
+                          int return_post, int local_theta, int square_logit_conc, int ensemble, double* jp,
+                          double* modes, double* post);
+
+/* Replaces logBootBatchPosterior  (src/jpmatLogBoot.cpp:343, decl .h:9).
+ *  batch_vals/batch_off: BatchIL (0-based cell indices per batch level), nbatch levels
+ *  composition: nbatch draws-per-boot counts (R `table(batch[ii])`).
+ *  return_post 3 is not handled by the reference (falls through to jp only); same here. */
+int scde_logBootBatchPosterior(const double* models, int ncells, const int* ucl_vals, const int64_t* ucl_off,
+                               const int* counti, int ngenes, const double* magnitudes, int ngrid,
+                               const int* batch_vals, const int64_t* batch_off, const int* composition, int nbatch,
+                               int nboot, int seed, int return_post, int local_theta, int square_logit_conc,
+                               double* jp, double* modes, double* post);
+
+/* Replaces jpmatLogBoot  (src/jpmatLogBoot.cpp:11, decl .h:6).  mats: nmat pointers
+ * to nrows x ncols col-major log-posterior matrices.  out: nrows x ncols col-major. */
+int scde_jpmatLogBoot(const double* const* mats, int nmat, int nrows, int ncols, int nboot, int seed, double* out);
+
+/* Replaces jpmatLogBatchBoot  (src/jpmatLogBoot.cpp:48, decl .h:7).  Matll flattened:
+ * type k owns mats[type_off[k] .. type_off[k+1]); comp[k] draws per boot. */
+int scde_jpmatLogBatchBoot(const double* const* mats, const int* type_off, const int* comp, int ntypes, int nrows,
+                           int ncols, int nboot, int seed, double* out);
+
+/* Replaces matSlideMult  (src/matSlideMult.cpp:5, decl src/matSlideMult.h:6).
+ * m1, m2: nrows x ncols col-major; out: nrows x (2*ncols-1) col-major. */
+int scde_matSlideMult(const double* m1, const double* m2, int nrows, int ncols, double* out);
+
+/* calculate.ratio.posterior + quick.distribution.summary (R/functions.R:3491-3510,
+ * 5039-5050) on host buffers.  prior_y may be NULL (skip.prior.adjustment).
+ * diffv: 2n-1 column values (as.numeric(colnames)), zi: 0-based index of the
+ * expectation column.  ratio (nrows x (2n-1) col-major) and res (nrows x 5
+ * col-major: lb, mle, ub, ce, Z) may each be NULL. */
+int scde_ratio_summary(const double* pmat1, const double* pmat2, int nrows, int n, const double* prior_y,
+                       const double* diffv, int zi, double* ratio, double* res);
+
+/* quick.distribution.summary of an existing ratio posterior (R/functions.R:5039-5050):
+ * rpost nrows x m col-major (m odd, rows already normalised), diffv m values, zi the
+ * expectation column.  res: nrows x 5 col-major (lb, mle, ub, ce, Z). */
+int scde_distribution_summary(const double* rpost, int nrows, int m, const double* diffv, int zi, double* res);
+
+/* BH-adjusted cZ = sign(Z) qnorm(p.adjust(pnorm(|Z|, lower=F), "BH"), lower=F)
+ * (R/functions.R:5051).  Host-only. */
+int scde_bh_cz(const double* z, int64_t n, double* cz);
+
+/* ---------------------------------------------------------------- layer 2 */
+
+typedef struct scde_ctx scde_ctx;
+
+int scde_ctx_create(int device, scde_ctx** out);
+void scde_ctx_destroy(scde_ctx* ctx);
+int scde_ctx_synchronize(scde_ctx* ctx);
+/* Per-kernel HIP-event timing on the context's stream (0 = off). */
+int scde_ctx_set_profiling(scde_ctx* ctx, int on);
+/* slot names: 0 tables, 1 boot, 2 ratio_summary, 3 unique, 4 other; ms totals and launch counts */
+int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslots);
+int scde_ctx_reset_kernel_times(scde_ctx* ctx);
+
+/* device buffers owned by the context's allocator */
+int scde_dev_alloc(scde_ctx* ctx, int64_t bytes, void** dptr);
+int scde_dev_free(scde_ctx* ctx, void* dptr);
+int scde_h2d(scde_ctx* ctx, void* dst, const void* src, int64_t bytes);
+int scde_d2h(scde_ctx* ctx, void* dst, const void* src, int64_t bytes);
+
+typedef struct scde_de_params {
+  int ncells;              /* cells (columns of counts) */
+  const double* models;    /* host, ncells x 12 col-major (NaN where absent; corr.a clamp applied inside) */
+  int local_theta;         /* "corr.ltheta.b" present */
+  int square_logit_conc;   /* "conc.a2" present */
+  const int* groups;       /* host, per cell: 0 / 1 (level order), -1 = NA */
+  const double* prior_x;   /* host, ngrid */
+  const double* prior_y;   /* host, ngrid */
+  int ngrid;
+  int nboot;               /* n.randomizations */
+  int n_cores;             /* reference seeding mode: chunk seeds as R's n.cores */
+  int64_t gene_offset;     /* first global gene index of this shard */
+  int64_t ngenes_total;    /* global number of genes (for chunk seeds) */
+  double expectation;      /* R `expectation` (log2 scale) */
+} scde_de_params;
+
+/* scde.expression.difference (R/functions.R:304-407, no batch) on device-resident
+ * counts (int32, column-major, leading dimension ld, rows gene_offset.. of the shard
+ * start at counts_dev).  results: host ngenes x 5 col-major (lb, mle, ub, ce, Z);
+ * cZ is left to scde_bh_cz (it needs every shard's Z).  jp1/jp2 (ngenes x ngrid) and
+ * ratio (ngenes x (2*ngrid-1)) are optional host outputs, col-major. */
+int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes,
+                                   const scde_de_params* p, double* results, double* jp1, double* jp2,
+                                   double* ratio);
+
+/* scde.posteriors (R/functions.R:566-669) on device-resident counts for the cells
+ * listed in cellidx (host, ncells_sel entries).  Outputs are host, col-major.
+ * batch_* may be NULL (no batch).  return_post: R postflag (0..3). */
+int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const int* cellidx,
+                        int ncells_sel, const double* models_sel, int local_theta, int square_logit_conc,
+                        const double* prior_x, int ngrid, int nboot, int n_cores, int64_t gene_offset,
+                        int64_t ngenes_total, int return_post, int ensemble, const int* batch_vals,
+                        const int64_t* batch_off, const int* composition, int nbatch, double* jp, double* modes,
+                        double* post);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SCDE_HIP_H */

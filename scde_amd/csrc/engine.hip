@@ -1,0 +1,1291 @@
+// engine.hip -- host orchestration and the C ABI (include/scde_hip.h).
+//
+// Restates the R glue of the path on the host side (R/functions.R:566-669
+// scde.posteriors, 3491-3531 ratio posterior / Z, 5039-5051 summary / BH) and
+// drives the gfx950 kernels in kernels.hip on one HIP stream per context.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "kernels.h"
+#include "scde_hip.h"
+
+using namespace scde;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HCHK(expr)                                                                     \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess) return fail(SCDE_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define RCHK(expr)            \
+  do {                        \
+    int r_ = (expr);          \
+    if (r_ != SCDE_OK) return r_; \
+  } while (0)
+
+inline long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
+
+// glibc TYPE_3 rand() (srandom_r / random_r) with private state: the
+// reference seeds the process-global generator with srand(Seed) and draws
+// `rj = rand()/(RAND_MAX/n)` with rejection (src/jpmatLogBoot.cpp:220-221,255-257).
+struct GlibcRand {
+  int32_t t[31];
+  int f = 3, r = 0;
+  explicit GlibcRand(unsigned int seed) {
+    if (seed == 0) seed = 1;
+    t[0] = (int32_t)seed;
+    int32_t word = (int32_t)seed;
+    for (int i = 1; i < 31; ++i) {
+      const long hi = word / 127773, lo = word % 127773;
+      word = (int32_t)(16807 * lo - 2836 * hi);
+      if (word < 0) word += 2147483647;
+      t[i] = word;
+    }
+    for (int i = 0; i < 310; ++i) next();
+  }
+  int next() {
+    const uint32_t v = (uint32_t)t[f] + (uint32_t)t[r];
+    t[f] = (int32_t)v;
+    if (++f >= 31) f = 0;
+    if (++r >= 31) r = 0;
+    return (int)(v >> 1);
+  }
+  int draw(int n) {
+    int rj;
+    while (n <= (rj = next() / (2147483647 / n))) {
+    }
+    return rj;
+  }
+};
+
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) {
+      hipError_t e = hipFree(p);
+      p = nullptr;
+      cap = 0;
+      if (e != hipSuccess) return e;
+    }
+    size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+// R's chunk(seq_len(N), n) = split(x, sort(rank(x) %% n)) (R/functions.R:606):
+// label r in 0..n-1 has #{i in 1..N : i %% n == r} genes, chunks in label order.
+std::vector<long long> r_chunk_starts(long long N, int n) {
+  std::vector<long long> starts;
+  long long pos = 0;
+  for (int r = 0; r < n; ++r) {
+    long long cnt = (r == 0) ? N / n : (N >= r ? (N - r) / n + 1 : 0);
+    if (cnt > 0) starts.push_back(pos);
+    pos += cnt;
+  }
+  starts.push_back(N);
+  return starts;
+}
+
+}  // namespace
+
+enum { SLOT_TABLES = 0, SLOT_BOOT = 1, SLOT_RATIO = 2, SLOT_UNIQUE = 3, SLOT_OTHER = 4, NSLOTS = 5 };
+
+struct scde_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // workspace
+  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, ucl, ucl_off, T, E, maxi, has_clamp, base_col, ent, nnz, Wt,
+      Z, draws, degen, uci, cellidx, cmax, cmin, woff, bits, rank, nuniq, wset, prior_y, diffv, jpA, jpB, res,
+      ratio, in1, in2, outbuf;
+  // profiling
+  bool profile = false;
+  struct Pending {
+    int slot;
+    hipEvent_t a, b;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> evpool;
+  double ms[NSLOTS] = {0};
+  long long launches[NSLOTS] = {0};
+  std::vector<void*> user_allocs;
+
+  hipEvent_t get_event() {
+    if (!evpool.empty()) {
+      hipEvent_t e = evpool.back();
+      evpool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  hipEvent_t mark_begin(int slot) {
+    if (!profile) return nullptr;
+    hipEvent_t a = get_event();
+    (void)hipEventRecord(a, stream);
+    (void)slot;
+    return a;
+  }
+  void mark_end(int slot, hipEvent_t a) {
+    if (!profile || !a) return;
+    hipEvent_t b = get_event();
+    (void)hipEventRecord(b, stream);
+    pending.push_back({slot, a, b});
+  }
+  int sync() {
+    HCHK(hipStreamSynchronize(stream));
+    for (auto& p : pending) {
+      float t = 0.f;
+      if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) {
+        ms[p.slot] += t;
+        launches[p.slot] += 1;
+      }
+      evpool.push_back(p.a);
+      evpool.push_back(p.b);
+    }
+    pending.clear();
+    return SCDE_OK;
+  }
+  ~scde_ctx() {
+    Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,   &cellscal, &ucl,   &ucl_off, &T,   &E,
+                  &maxi,   &has_clamp, &base_col, &ent, &nnz, &Wt, &Z, &draws, &degen, &uci, &cellidx,
+                  &cmax,   &cmin, &woff, &bits, &rank, &nuniq, &wset, &prior_y, &diffv, &jpA, &jpB, &res,
+                  &ratio,  &in1, &in2, &outbuf};
+    for (Buf* b : all) b->release();
+    for (void* p : user_allocs) (void)hipFree(p);
+    for (auto& p : pending) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    for (auto e : evpool) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+// ------------------------------------------------------------------ posterior spec
+struct PostSpec {
+  int ncells = 0;
+  const double* models = nullptr;  // host ncells x 12 col-major
+  int localtheta = 0, squarelogit = 0;
+  const double* mag = nullptr;  // host G
+  int G = 0;
+  int nboot = 0;
+  int postflag = 0;
+  int ensemble = 0;
+  bool batch_call = false;  // logBootBatchPosterior semantics
+  // source A: host ucl/uci
+  const int* ucl_host = nullptr;
+  const int64_t* ucl_off_host = nullptr;
+  const int* uci_host = nullptr;
+  // source B: device counts
+  const int* counts_dev = nullptr;
+  long long ld = 0;
+  const int* cellidx_host = nullptr;
+  int ngenes = 0;
+  // seeding: per set seed, per gene set (empty -> all set 0)
+  std::vector<int> seeds;
+  std::vector<int> wset;
+  // batch
+  const int* batch_vals = nullptr;
+  const int64_t* batch_off = nullptr;
+  const int* comp = nullptr;
+  int nbatch = 0;
+  // outputs (device)
+  double* jp = nullptr;
+  long long jp_g = 0, jp_k = 0;
+  double* modes = nullptr;  // ngenes x ncells col-major
+  double* post = nullptr;   // ncells blocks of ngenes x G col-major
+  bool use_baseline = true;
+};
+
+int upload(scde_ctx* cx, Buf& b, const void* src, size_t bytes) {
+  HCHK(b.ensure(bytes));
+  if (bytes) HCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, cx->stream));
+  return SCDE_OK;
+}
+
+// Build ucl/uci for the selected cells on device (R/functions.R:609-610).  Unique
+// counts come out sorted ascending rather than in first-appearance order; the order
+// only permutes table columns, never values.
+int build_unique_device(scde_ctx* cx, const PostSpec& s, std::vector<long long>& ucl_off_h) {
+  const int C = s.ncells, N = s.ngenes;
+  hipStream_t st = cx->stream;
+  hipEvent_t ev = cx->mark_begin(SLOT_UNIQUE);
+  RCHK(upload(cx, cx->cellidx, s.cellidx_host, sizeof(int) * C));
+  HCHK(cx->cmax.ensure(sizeof(int) * C));
+  HCHK(cx->cmin.ensure(sizeof(int) * C));
+  HCHK(launch_cell_minmax(s.counts_dev, s.ld, 0, N, C, cx->cellidx.as<int>(), cx->cmax.as<int>(),
+                          cx->cmin.as<int>(), st));
+  std::vector<int> cmax(C), cmin(C);
+  HCHK(hipMemcpyAsync(cmax.data(), cx->cmax.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  HCHK(hipMemcpyAsync(cmin.data(), cx->cmin.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  HCHK(hipStreamSynchronize(st));
+  std::vector<long long> woff(C + 1, 0);
+  for (int c = 0; c < C; ++c) {
+    if (N > 0 && cmin[c] < 0) return fail(SCDE_EARG, "negative count in cell %d", c);
+    woff[c + 1] = woff[c] + ((long long)cmax[c] >> 6) + 1;
+  }
+  RCHK(upload(cx, cx->woff, woff.data(), sizeof(long long) * (C + 1)));
+  HCHK(cx->bits.ensure(sizeof(unsigned long long) * woff[C]));
+  HCHK(hipMemsetAsync(cx->bits.p, 0, sizeof(unsigned long long) * woff[C], st));
+  HCHK(launch_mark(s.counts_dev, s.ld, 0, N, C, cx->cellidx.as<int>(), cx->woff.as<long long>(),
+                   cx->bits.as<unsigned long long>(), st));
+  HCHK(cx->rank.ensure(sizeof(int) * woff[C]));
+  HCHK(cx->nuniq.ensure(sizeof(int) * C));
+  HCHK(launch_rank(cx->bits.as<unsigned long long>(), cx->woff.as<long long>(), C, cx->rank.as<int>(),
+                   cx->nuniq.as<int>(), st));
+  std::vector<int> nuniq(C);
+  HCHK(hipMemcpyAsync(nuniq.data(), cx->nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  HCHK(hipStreamSynchronize(st));
+  ucl_off_h.assign(C + 1, 0);
+  for (int c = 0; c < C; ++c) ucl_off_h[c + 1] = ucl_off_h[c] + nuniq[c];
+  RCHK(upload(cx, cx->ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
+  HCHK(cx->ucl.ensure(sizeof(int) * std::max<long long>(1, ucl_off_h[C])));
+  HCHK(launch_fill_ucl(cx->bits.as<unsigned long long>(), cx->woff.as<long long>(), C, cx->rank.as<int>(),
+                       cx->ucl_off.as<long long>(), cx->ucl.as<int>(), st));
+  HCHK(cx->uci.ensure(sizeof(int) * std::max<long long>(1, (long long)N * C)));
+  HCHK(launch_uci(s.counts_dev, s.ld, 0, N, C, cx->cellidx.as<int>(), cx->woff.as<long long>(),
+                  cx->bits.as<unsigned long long>(), cx->rank.as<int>(), cx->uci.as<int>(), st));
+  cx->mark_end(SLOT_UNIQUE, ev);
+  return SCDE_OK;
+}
+
+// Draw lists and per-cell multiplicities for each seed set.
+void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<double>& W, int& ndraw) {
+  const int C = s.ncells, B = s.nboot, nsets = (int)s.seeds.size();
+  if (s.batch_call) {
+    ndraw = 0;
+    for (int k = 0; k < s.nbatch; ++k) ndraw += std::max(0, s.comp[k]);
+  } else {
+    ndraw = C;
+  }
+  draws.assign((size_t)nsets * B * std::max(ndraw, 1), 0);
+  W.assign((size_t)nsets * C * Bp, 0.0);
+  for (int set = 0; set < nsets; ++set) {
+    GlibcRand rng((unsigned int)s.seeds[set]);
+    int* dr = draws.data() + (size_t)set * B * std::max(ndraw, 1);
+    double* w = W.data() + (size_t)set * C * Bp;
+    for (int b = 0; b < B; ++b) {
+      int d = 0;
+      if (!s.batch_call) {
+        for (int j = 0; j < C; ++j) {
+          const int rj = rng.draw(C);
+          dr[(size_t)b * ndraw + d++] = rj;
+          w[(size_t)rj * Bp + b] += 1.0;
+        }
+      } else {
+        for (int k = 0; k < s.nbatch; ++k) {
+          const int nsamp = s.comp[k];
+          if (nsamp > 0) {
+            const int* bi = s.batch_vals + s.batch_off[k];
+            const int nb = (int)(s.batch_off[k + 1] - s.batch_off[k]);
+            for (int j = 0; j < nsamp; ++j) {
+              const int cell = bi[rng.draw(nb)];
+              dr[(size_t)b * ndraw + d++] = cell;
+              w[(size_t)cell * Bp + b] += 1.0;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+int run_posterior(scde_ctx* cx, const PostSpec& s) {
+  const int C = s.ncells, G = s.G, N = s.ngenes;
+  const int GS = (int)round_up(G, 16);
+  hipStream_t st = cx->stream;
+  if (C <= 0 || G <= 0) return fail(SCDE_EARG, "ncells and ngrid must be positive");
+  if (s.nboot < 0) return fail(SCDE_EARG, "nboot must be >= 0");
+  if (G > 4096) return fail(SCDE_EARG, "ngrid > 4096 unsupported");
+  if (s.seeds.empty()) return fail(SCDE_EINTERNAL, "no seed sets");
+  // ---- per-cell grid vectors
+  RCHK(upload(cx, cx->models, s.models, sizeof(double) * C * 12));
+  RCHK(upload(cx, cx->mag, s.mag, sizeof(double) * G));
+  const size_t cg = sizeof(double) * (size_t)C * GS;
+  HCHK(cx->mu.ensure(cg));
+  HCHK(cx->lcfp.ensure(cg));
+  HCHK(cx->lcfpr.ensure(cg));
+  HCHK(cx->theta.ensure(cg));
+  HCHK(cx->cellscal.ensure(sizeof(double) * 2 * C));
+  hipEvent_t ev = cx->mark_begin(SLOT_OTHER);
+  HCHK(launch_cell_prep(cx->models.as<double>(), C, G, GS, cx->mag.as<double>(), s.localtheta, s.squarelogit,
+                        cx->mu.as<double>(), cx->lcfp.as<double>(), cx->lcfpr.as<double>(), cx->theta.as<double>(),
+                        cx->cellscal.as<double>(), st));
+  cx->mark_end(SLOT_OTHER, ev);
+  // ---- unique counts
+  std::vector<long long> ucl_off_h;
+  if (s.ucl_host) {
+    ucl_off_h.assign(s.ucl_off_host, s.ucl_off_host + C + 1);
+    if (ucl_off_h[0] != 0) return fail(SCDE_EARG, "ucl_off[0] must be 0");
+    for (int c = 0; c < C; ++c)
+      if (ucl_off_h[c + 1] < ucl_off_h[c]) return fail(SCDE_EARG, "ucl_off must be non-decreasing");
+    RCHK(upload(cx, cx->ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
+    RCHK(upload(cx, cx->ucl, s.ucl_host, sizeof(int) * std::max<long long>(1, ucl_off_h[C])));
+    // validate counti against the per-cell list sizes (the reference would read out of bounds)
+    for (int c = 0; c < C; ++c) {
+      const long long nu = ucl_off_h[c + 1] - ucl_off_h[c];
+      const int* col = s.uci_host + (size_t)N * c;
+      for (int g = 0; g < N; ++g)
+        if (col[g] < 0 || col[g] >= nu) return fail(SCDE_EARG, "counti[%d,%d]=%d out of range [0,%lld)", g, c, col[g], nu);
+    }
+    RCHK(upload(cx, cx->uci, s.uci_host, sizeof(int) * std::max<long long>(1, (long long)N * C)));
+  } else {
+    RCHK(build_unique_device(cx, s, ucl_off_h));
+  }
+  const long long ncols = ucl_off_h[C];
+  // ---- K1 tables
+  HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
+  HCHK(cx->maxi.ensure(sizeof(int) * std::max<long long>(1, ncols)));
+  HCHK(cx->has_clamp.ensure(std::max<long long>(1, ncols)));
+  const bool want_maxi = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
+  TablesArgs ta{};
+  ta.ucl = cx->ucl.as<int>();
+  ta.ucl_off = cx->ucl_off.as<long long>();
+  ta.ncols = ncols;
+  ta.ncells = C;
+  ta.G = G;
+  ta.GS = GS;
+  ta.mu = cx->mu.as<double>();
+  ta.lcfp = cx->lcfp.as<double>();
+  ta.lcfpr = cx->lcfpr.as<double>();
+  ta.theta = cx->theta.as<double>();
+  ta.cellscal = cx->cellscal.as<double>();
+  ta.minlogprob = -1 * DBL_MAX / C / 1.1;
+  ta.T = cx->T.as<double>();
+  ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
+  ta.has_clamp = cx->has_clamp.as<unsigned char>();
+  ev = cx->mark_begin(SLOT_TABLES);
+  HCHK(launch_tables(ta, st));
+  cx->mark_end(SLOT_TABLES, ev);
+  // ---- joint posterior
+  if (!s.batch_call && s.ensemble) {
+    HCHK(cx->E.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
+    HCHK(launch_ensemble_cols(cx->T.as<double>(), ncols, G, GS, cx->E.as<double>(), st));
+    NoBootArgs na{cx->E.as<double>(), G, GS, cx->ucl_off.as<long long>(), cx->uci.as<int>(), N, C, N, 1,
+                  s.jp, s.jp_g, s.jp_k};
+    HCHK(launch_noboot(na, st));
+  } else if (s.nboot == 0 && !s.batch_call) {
+    NoBootArgs na{cx->T.as<double>(), G, GS, cx->ucl_off.as<long long>(), cx->uci.as<int>(), N, C, N, 0,
+                  s.jp, s.jp_g, s.jp_k};
+    HCHK(launch_noboot(na, st));
+  } else if (s.nboot == 0) {
+    // logBootBatchPosterior with Nboot = 0 returns zeros (src/jpmatLogBoot.cpp:469-497)
+    HCHK(hipMemsetAsync(s.jp, 0, sizeof(double) * (size_t)N * G, st));
+  } else {
+    const int Bp = (int)round_up(s.nboot, 16);
+    const int nsets = (int)s.seeds.size();
+    std::vector<int> draws;
+    std::vector<double> W;
+    int ndraw = 0;
+    make_draws(s, Bp, draws, W, ndraw);
+    RCHK(upload(cx, cx->Wt, W.data(), sizeof(double) * W.size()));
+    RCHK(upload(cx, cx->draws, draws.data(), sizeof(int) * draws.size()));
+    HCHK(cx->base_col.ensure(sizeof(int) * C));
+    HCHK(launch_base_cols(cx->ucl.as<int>(), cx->ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
+                          s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
+    HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * C)));
+    HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
+    ev = cx->mark_begin(SLOT_OTHER);
+    HCHK(launch_ell(cx->uci.as<int>(), N, N, C, cx->ucl_off.as<long long>(), cx->base_col.as<int>(),
+                    cx->ent.as<int2>(), cx->nnz.as<int>(), st));
+    HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
+    HCHK(launch_baseline_z(cx->T.as<double>(), G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
+                           cx->Z.as<double>(), st));
+    cx->mark_end(SLOT_OTHER, ev);
+    if (nsets > 1) {
+      if ((int)s.wset.size() != N) return fail(SCDE_EINTERNAL, "wset size mismatch");
+      RCHK(upload(cx, cx->wset, s.wset.data(), sizeof(int) * N));
+    }
+    HCHK(cx->degen.ensure(sizeof(int) * std::max(1, N)));
+    HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, N), st));
+    BootArgs ba{};
+    ba.T = cx->T.as<double>();
+    ba.G = G;
+    ba.GS = GS;
+    ba.ent = cx->ent.as<int2>();
+    ba.nnz = cx->nnz.as<int>();
+    ba.ent_stride = C;
+    ba.base_col = cx->base_col.as<int>();
+    ba.Wt = cx->Wt.as<double>();
+    ba.ncells = C;
+    ba.Bp = Bp;
+    ba.nboot = s.nboot;
+    ba.wset = nsets > 1 ? cx->wset.as<int>() : nullptr;
+    ba.Z = cx->Z.as<double>();
+    ba.norm_mult = (double)s.nboot;
+    ba.degen_thresh = 16777216.0;  // 2^24: beyond this the sums' rounding order matters
+    ba.out = s.jp;
+    ba.out_g = s.jp_g;
+    ba.out_k = s.jp_k;
+    ba.degen = cx->degen.as<int>();
+    ba.ngenes = N;
+    ev = cx->mark_begin(SLOT_BOOT);
+    HCHK(launch_boot(ba, st));
+    cx->mark_end(SLOT_BOOT, ev);
+    ExactArgs xa{};
+    xa.T = cx->T.as<double>();
+    xa.G = G;
+    xa.GS = GS;
+    xa.draws = cx->draws.as<int>();
+    xa.ndraw = ndraw;
+    xa.nboot = s.nboot;
+    xa.wset = ba.wset;
+    xa.ucl_off = cx->ucl_off.as<long long>();
+    xa.uci = cx->uci.as<int>();
+    xa.ld_uci = N;
+    xa.norm_mult = (double)s.nboot;
+    xa.degen = cx->degen.as<int>();
+    xa.out = s.jp;
+    xa.out_g = s.jp_g;
+    xa.out_k = s.jp_k;
+    xa.ngenes = N;
+    HCHK(launch_boot_exact(xa, st));
+  }
+  // ---- individual outputs (src/jpmatLogBoot.cpp:277-328)
+  const bool want_modes = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
+  const bool want_post = s.batch_call ? (s.postflag == 2) : (s.postflag == 2 || s.postflag == 3);
+  if (want_modes && s.modes)
+    HCHK(launch_modes(cx->uci.as<int>(), N, N, C, cx->ucl_off.as<long long>(), cx->maxi.as<int>(),
+                      cx->mag.as<double>(), s.modes, 1, N, st));
+  if (want_post && s.post)
+    for (int c = 0; c < C; ++c)
+      HCHK(launch_post(cx->uci.as<int>(), N, N, c, cx->ucl_off.as<long long>(), cx->T.as<double>(), G, GS,
+                       s.post + (size_t)c * N * G, 1, N, st));
+  return SCDE_OK;
+}
+
+std::mutex g_default_mu;
+scde_ctx* g_default = nullptr;
+
+int default_ctx(scde_ctx** out) {
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  if (!g_default) {
+    int dev = 0;
+    if (const char* e = getenv("SCDE_DEVICE")) dev = atoi(e);
+    scde_ctx* c = nullptr;
+    RCHK(scde_ctx_create(dev, &c));
+    g_default = c;
+  }
+  *out = g_default;
+  return SCDE_OK;
+}
+
+std::vector<double> marginals(const double* prior_x, int G) {
+  // R/functions.R:575-577: log(pmax(10^x - 1, 0))
+  std::vector<double> m(G);
+  for (int k = 0; k < G; ++k) {
+    double v = std::pow(10.0, prior_x[k]) - 1;
+    if (v < 0) v = 0;
+    m[k] = std::log(v);
+  }
+  return m;
+}
+
+// colnames of the ratio posterior as numbers: seq(x1-xn, xn-x1, length = 2n-1)
+// formatted with 15 significant digits and parsed back (R/functions.R:3506, 5040)
+std::vector<double> ratio_diffv(const double* x, int n) {
+  const int m = 2 * n - 1;
+  std::vector<double> rv(m);
+  const double from = x[0] - x[n - 1], to = x[n - 1] - x[0];
+  const double by = (to - from) / (m - 1);
+  for (int i = 0; i < m; ++i) rv[i] = from + (double)i * by;
+  rv[0] = from;
+  rv[m - 1] = to;
+  for (int i = 0; i < m; ++i) {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%.15g", rv[i]);
+    rv[i] = strtod(buf, nullptr);
+  }
+  return rv;
+}
+
+int expectation_index(const std::vector<double>& diffv, double expectation) {
+  const double target = expectation / std::log2(10.0);
+  int zi = 0;
+  double best = INFINITY;
+  for (int i = 0; i < (int)diffv.size(); ++i) {
+    const double d = std::fabs(diffv[i] - target);
+    if (d < best) {
+      best = d;
+      zi = i;
+    }
+  }
+  return zi;
+}
+
+// Reference seeding: one draw set per n.cores chunk overlapping this shard.
+void seeding(int n_cores, long long gene_offset, long long N_total, int ngenes, std::vector<int>& seeds,
+             std::vector<int>& wset) {
+  seeds.clear();
+  wset.clear();
+  if (!(n_cores > 1 && N_total > n_cores)) {
+    seeds.push_back(1);
+    return;
+  }
+  const std::vector<long long> st = r_chunk_starts(N_total, n_cores);
+  wset.assign(ngenes, 0);
+  int cur = -1;
+  long long last_chunk = -1;
+  for (int g = 0; g < ngenes; ++g) {
+    const long long gg = gene_offset + g;
+    const long long ch = std::upper_bound(st.begin(), st.end(), gg) - st.begin() - 1;
+    if (ch != last_chunk) {
+      seeds.push_back((int)(st[ch] + 1));
+      last_chunk = ch;
+      cur = (int)seeds.size() - 1;
+    }
+    wset[g] = cur;
+  }
+  if (seeds.size() == 1) wset.clear();
+}
+
+void transpose_rows_to_colmajor(const double* rows, int N, int G, double* out) {
+  for (int g = 0; g < N; ++g)
+    for (int k = 0; k < G; ++k) out[(size_t)k * N + g] = rows[(size_t)g * G + k];
+}
+
+double pnorm_upper(double x);
+double qnorm_host(double p, bool lower_tail);
+
+}  // namespace
+
+// =================================================================== C ABI
+extern "C" {
+
+const char* scde_last_error(void) { return g_err.c_str(); }
+int scde_version(void) { return 100; }
+
+int scde_ctx_create(int device, scde_ctx** out) {
+  if (!out) return fail(SCDE_EARG, "null out");
+  int n = 0;
+  HCHK(hipGetDeviceCount(&n));
+  if (n <= 0) return fail(SCDE_EHIP, "no HIP device");
+  if (device < 0 || device >= n) return fail(SCDE_EARG, "device %d out of range (%d devices)", device, n);
+  HCHK(hipSetDevice(device));
+  auto* c = new scde_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(SCDE_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
+  }
+  *out = c;
+  return SCDE_OK;
+}
+
+void scde_ctx_destroy(scde_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  {
+    std::lock_guard<std::mutex> lk(g_default_mu);
+    if (ctx == g_default) g_default = nullptr;
+  }
+  delete ctx;
+}
+
+int scde_ctx_synchronize(scde_ctx* ctx) {
+  if (!ctx) return fail(SCDE_EARG, "null ctx");
+  HCHK(hipSetDevice(ctx->device));
+  return ctx->sync();
+}
+
+int scde_ctx_set_profiling(scde_ctx* ctx, int on) {
+  if (!ctx) return fail(SCDE_EARG, "null ctx");
+  ctx->profile = on != 0;
+  return SCDE_OK;
+}
+
+int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslots) {
+  if (!ctx) return fail(SCDE_EARG, "null ctx");
+  RCHK(ctx->sync());
+  for (int i = 0; i < nslots && i < NSLOTS; ++i) {
+    if (ms) ms[i] = ctx->ms[i];
+    if (launches) launches[i] = ctx->launches[i];
+  }
+  return SCDE_OK;
+}
+
+int scde_ctx_reset_kernel_times(scde_ctx* ctx) {
+  if (!ctx) return fail(SCDE_EARG, "null ctx");
+  RCHK(ctx->sync());
+  for (int i = 0; i < NSLOTS; ++i) {
+    ctx->ms[i] = 0;
+    ctx->launches[i] = 0;
+  }
+  return SCDE_OK;
+}
+
+int scde_dev_alloc(scde_ctx* ctx, int64_t bytes, void** dptr) {
+  if (!ctx || !dptr || bytes < 0) return fail(SCDE_EARG, "bad args");
+  HCHK(hipSetDevice(ctx->device));
+  HCHK(hipMalloc(dptr, std::max<int64_t>(bytes, 1)));
+  ctx->user_allocs.push_back(*dptr);
+  return SCDE_OK;
+}
+
+int scde_dev_free(scde_ctx* ctx, void* dptr) {
+  if (!ctx) return fail(SCDE_EARG, "null ctx");
+  auto it = std::find(ctx->user_allocs.begin(), ctx->user_allocs.end(), dptr);
+  if (it == ctx->user_allocs.end()) return fail(SCDE_EARG, "pointer not owned by this context");
+  ctx->user_allocs.erase(it);
+  HCHK(hipFree(dptr));
+  return SCDE_OK;
+}
+
+int scde_h2d(scde_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+  if (!ctx) return fail(SCDE_EARG, "null ctx");
+  HCHK(hipSetDevice(ctx->device));
+  HCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  return ctx->sync();
+}
+
+int scde_d2h(scde_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+  if (!ctx) return fail(SCDE_EARG, "null ctx");
+  HCHK(hipSetDevice(ctx->device));
+  HCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  return ctx->sync();
+}
+
+// ------------------------------------------------------------------ layer 1
+static int logboot_common(bool batch, const double* models, int ncells, const int* ucl_vals, const int64_t* ucl_off,
+                          const int* counti, int ngenes, const double* magnitudes, int ngrid, const int* batch_vals,
+                          const int64_t* batch_off, const int* composition, int nbatch, int nboot, int seed,
+                          int return_post, int local_theta, int square_logit_conc, int ensemble, double* jp,
+                          double* modes, double* post) {
+  if (!models || !ucl_vals || !ucl_off || !counti || !magnitudes || !jp)
+    return fail(SCDE_EARG, "null input pointer");
+  if (ncells <= 0 || ngenes < 0 || ngrid <= 0) return fail(SCDE_EARG, "bad dimensions");
+  if (batch) {
+    for (int k = 0; k < nbatch; ++k) {
+      if (composition[k] > 0 && batch_off[k + 1] - batch_off[k] <= 0)
+        return fail(SCDE_EARG, "batch %d has draws but no cells", k);
+      for (int64_t i = batch_off[k]; i < batch_off[k + 1]; ++i)
+        if (batch_vals[i] < 0 || batch_vals[i] >= ncells) return fail(SCDE_EARG, "BatchIL index out of range");
+    }
+  }
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  const size_t NG = (size_t)ngenes * ngrid;
+  PostSpec s;
+  s.ncells = ncells;
+  s.models = models;
+  s.localtheta = local_theta;
+  s.squarelogit = square_logit_conc;
+  s.mag = magnitudes;
+  s.G = ngrid;
+  s.nboot = nboot;
+  s.postflag = return_post;
+  s.ensemble = batch ? 0 : ensemble;
+  s.batch_call = batch;
+  s.ucl_host = ucl_vals;
+  s.ucl_off_host = ucl_off;
+  s.uci_host = counti;
+  s.ngenes = ngenes;
+  s.seeds = {seed};
+  s.batch_vals = batch_vals;
+  s.batch_off = batch_off;
+  s.comp = composition;
+  s.nbatch = nbatch;
+  const bool want_modes = (batch ? return_post == 1 : (return_post == 1 || return_post == 3)) && modes;
+  const bool want_post = (batch ? return_post == 2 : (return_post == 2 || return_post == 3)) && post;
+  HCHK(cx->jpA.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  s.jp = cx->jpA.as<double>();
+  s.jp_g = 1;  // R layout: ngenes x ngrid column-major
+  s.jp_k = ngenes;
+  if (want_modes) {
+    HCHK(cx->jpB.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * ncells)));
+    s.modes = cx->jpB.as<double>();
+  }
+  if (want_post) {
+    HCHK(cx->outbuf.ensure(sizeof(double) * std::max<size_t>(1, NG * ncells)));
+    s.post = cx->outbuf.as<double>();
+  }
+  RCHK(run_posterior(cx, s));
+  if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, cx->stream));
+  if (want_modes && ngenes)
+    HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * ngenes * ncells, hipMemcpyDeviceToHost, cx->stream));
+  if (want_post && NG)
+    HCHK(hipMemcpyAsync(post, s.post, sizeof(double) * NG * ncells, hipMemcpyDeviceToHost, cx->stream));
+  return cx->sync();
+}
+
+int scde_logBootPosterior(const double* models, int ncells, const int* ucl_vals, const int64_t* ucl_off,
+                          const int* counti, int ngenes, const double* magnitudes, int ngrid, int nboot, int seed,
+                          int return_post, int local_theta, int square_logit_conc, int ensemble, double* jp,
+                          double* modes, double* post) {
+  return logboot_common(false, models, ncells, ucl_vals, ucl_off, counti, ngenes, magnitudes, ngrid, nullptr,
+                        nullptr, nullptr, 0, nboot, seed, return_post, local_theta, square_logit_conc, ensemble, jp,
+                        modes, post);
+}
+
+int scde_logBootBatchPosterior(const double* models, int ncells, const int* ucl_vals, const int64_t* ucl_off,
+                               const int* counti, int ngenes, const double* magnitudes, int ngrid,
+                               const int* batch_vals, const int64_t* batch_off, const int* composition, int nbatch,
+                               int nboot, int seed, int return_post, int local_theta, int square_logit_conc,
+                               double* jp, double* modes, double* post) {
+  if (!batch_vals || !batch_off || !composition) return fail(SCDE_EARG, "null batch input");
+  return logboot_common(true, models, ncells, ucl_vals, ucl_off, counti, ngenes, magnitudes, ngrid, batch_vals,
+                        batch_off, composition, nbatch, nboot, seed, return_post, local_theta, square_logit_conc, 0,
+                        jp, modes, post);
+}
+
+// jpmat*: the matrices are the "cells", their rows the "genes", their columns the grid.
+static int jpmat_common(const double* const* mats, int nmat, const int* type_off, const int* comp, int ntypes,
+                        int nrows, int ncols, int nboot, int seed, double* out) {
+  if (!mats || !out || nmat <= 0 || nrows < 0 || ncols <= 0) return fail(SCDE_EARG, "bad jpmat arguments");
+  if (ncols > 4096) return fail(SCDE_EARG, "ncols > 4096 unsupported");
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  hipStream_t st = cx->stream;
+  const int GS = (int)round_up(ncols, 16);
+  const size_t per = (size_t)nrows * ncols;
+  // stage matrices as row-major tables: column (m, r) = m * nrows + r
+  HCHK(cx->T.ensure(sizeof(double) * std::max<size_t>(1, (size_t)nmat * nrows * GS)));
+  HCHK(cx->in1.ensure(sizeof(double) * std::max<size_t>(1, per)));
+  for (int m = 0; m < nmat; ++m) {
+    HCHK(hipMemcpyAsync(cx->in1.p, mats[m], sizeof(double) * per, hipMemcpyHostToDevice, st));
+    HCHK(launch_colmajor_to_rows(cx->in1.as<double>(), nrows, ncols, GS, cx->T.as<double>() + (size_t)m * nrows * GS,
+                                 st));
+  }
+  // draws
+  const int Bp = (int)round_up(std::max(nboot, 1), 16);
+  int ndraw = 0;
+  std::vector<int> draws;
+  std::vector<double> W((size_t)nmat * Bp, 0.0);
+  GlibcRand rng((unsigned int)seed);
+  if (!type_off) {
+    ndraw = nmat;
+    draws.resize((size_t)std::max(nboot, 1) * ndraw);
+    for (int b = 0; b < nboot; ++b)
+      for (int j = 0; j < nmat; ++j) {
+        const int rj = rng.draw(nmat);
+        draws[(size_t)b * ndraw + j] = rj;
+        W[(size_t)rj * Bp + b] += 1.0;
+      }
+  } else {
+    for (int k = 0; k < ntypes; ++k) {
+      ndraw += std::max(0, comp[k]);
+      if (comp[k] > 0 && type_off[k + 1] - type_off[k] <= 0) return fail(SCDE_EARG, "type %d has no matrices", k);
+    }
+    draws.resize((size_t)std::max(nboot, 1) * std::max(ndraw, 1));
+    for (int b = 0; b < nboot; ++b) {
+      int d = 0;
+      for (int k = 0; k < ntypes; ++k)
+        for (int j = 0; j < comp[k]; ++j) {
+          const int m = type_off[k] + rng.draw(type_off[k + 1] - type_off[k]);
+          draws[(size_t)b * ndraw + d++] = m;
+          W[(size_t)m * Bp + b] += 1.0;
+        }
+    }
+  }
+  // every row takes every matrix (no baseline)
+  std::vector<int2> ent((size_t)std::max(1, nrows) * nmat);
+  for (int r = 0; r < nrows; ++r)
+    for (int m = 0; m < nmat; ++m) ent[(size_t)r * nmat + m] = make_int2(m, m * nrows + r);
+  std::vector<int> nnz(std::max(1, nrows), nmat);
+  RCHK(upload(cx, cx->ent, ent.data(), sizeof(int2) * ent.size()));
+  RCHK(upload(cx, cx->nnz, nnz.data(), sizeof(int) * nnz.size()));
+  RCHK(upload(cx, cx->Wt, W.data(), sizeof(double) * W.size()));
+  RCHK(upload(cx, cx->draws, draws.data(), sizeof(int) * draws.size()));
+  HCHK(cx->degen.ensure(sizeof(int) * std::max(1, nrows)));
+  HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, nrows), st));
+  HCHK(cx->jpA.ensure(sizeof(double) * std::max<size_t>(1, per)));
+  if (nboot == 0) {
+    HCHK(hipMemsetAsync(cx->jpA.p, 0, sizeof(double) * std::max<size_t>(1, per), st));
+  } else {
+    BootArgs ba{};
+    ba.T = cx->T.as<double>();
+    ba.G = ncols;
+    ba.GS = GS;
+    ba.ent = cx->ent.as<int2>();
+    ba.nnz = cx->nnz.as<int>();
+    ba.ent_stride = nmat;
+    ba.base_col = nullptr;
+    ba.Wt = cx->Wt.as<double>();
+    ba.ncells = nmat;
+    ba.Bp = Bp;
+    ba.nboot = nboot;
+    ba.wset = nullptr;
+    ba.Z = nullptr;
+    ba.norm_mult = 1.0;  // jpmat* do not divide by nboot (src/jpmatLogBoot.cpp:36-38)
+    ba.degen_thresh = 16777216.0;
+    ba.out = cx->jpA.as<double>();
+    ba.out_g = 1;
+    ba.out_k = nrows;
+    ba.degen = cx->degen.as<int>();
+    ba.ngenes = nrows;
+    hipEvent_t ev = cx->mark_begin(SLOT_BOOT);
+    HCHK(launch_boot(ba, st));
+    cx->mark_end(SLOT_BOOT, ev);
+    ExactArgs xa{};
+    xa.T = ba.T;
+    xa.G = ncols;
+    xa.GS = GS;
+    xa.draws = cx->draws.as<int>();
+    xa.ndraw = ndraw;
+    xa.nboot = nboot;
+    xa.wset = nullptr;
+    xa.ucl_off = nullptr;
+    xa.uci = nullptr;
+    xa.ld_uci = 0;
+    xa.norm_mult = 1.0;
+    xa.degen = ba.degen;
+    xa.out = ba.out;
+    xa.out_g = 1;
+    xa.out_k = nrows;
+    xa.ngenes = nrows;
+    HCHK(launch_boot_exact(xa, st));
+  }
+  if (per) HCHK(hipMemcpyAsync(out, cx->jpA.p, sizeof(double) * per, hipMemcpyDeviceToHost, st));
+  return cx->sync();
+}
+
+int scde_jpmatLogBoot(const double* const* mats, int nmat, int nrows, int ncols, int nboot, int seed, double* out) {
+  return jpmat_common(mats, nmat, nullptr, nullptr, 0, nrows, ncols, nboot, seed, out);
+}
+
+int scde_jpmatLogBatchBoot(const double* const* mats, const int* type_off, const int* comp, int ntypes, int nrows,
+                           int ncols, int nboot, int seed, double* out) {
+  if (!type_off || !comp || ntypes <= 0) return fail(SCDE_EARG, "bad jpmatLogBatchBoot arguments");
+  return jpmat_common(mats, type_off[ntypes], type_off, comp, ntypes, nrows, ncols, nboot, seed, out);
+}
+
+static int ratio_common(const double* pmat1, const double* pmat2, int nrows, int n, const double* prior_y,
+                        const double* diffv, int zi, int normalize, double* ratio, double* res) {
+  if (!pmat1 || !pmat2 || nrows < 0 || n <= 0) return fail(SCDE_EARG, "bad ratio arguments");
+  if (res && (!diffv || zi < 0 || zi >= 2 * n - 1)) return fail(SCDE_EARG, "bad diffv/zi");
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  hipStream_t st = cx->stream;
+  const size_t per = (size_t)nrows * n, m = 2 * (size_t)n - 1;
+  RCHK(upload(cx, cx->in1, pmat1, sizeof(double) * std::max<size_t>(1, per)));
+  RCHK(upload(cx, cx->in2, pmat2, sizeof(double) * std::max<size_t>(1, per)));
+  if (prior_y) RCHK(upload(cx, cx->prior_y, prior_y, sizeof(double) * n));
+  if (res) RCHK(upload(cx, cx->diffv, diffv, sizeof(double) * m));
+  HCHK(cx->ratio.ensure(sizeof(double) * std::max<size_t>(1, nrows * m)));
+  HCHK(cx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)nrows * 5)));
+  RatioArgs ra{};
+  ra.jp1 = cx->in1.as<double>();
+  ra.j1g = 1;
+  ra.j1k = nrows;
+  ra.jp2 = cx->in2.as<double>();
+  ra.j2g = 1;
+  ra.j2k = nrows;
+  ra.prior_y = prior_y ? cx->prior_y.as<double>() : nullptr;
+  ra.n = n;
+  ra.ngenes = nrows;
+  ra.normalize = normalize;
+  ra.ratio = cx->ratio.as<double>();
+  ra.rg = 1;
+  ra.ro = nrows;
+  ra.diffv = res ? cx->diffv.as<double>() : nullptr;
+  ra.zi = zi;
+  ra.res = res ? cx->res.as<double>() : nullptr;
+  ra.res_ld = nrows;
+  hipEvent_t ev = cx->mark_begin(SLOT_RATIO);
+  HCHK(launch_ratio_summary(ra, st));
+  cx->mark_end(SLOT_RATIO, ev);
+  if (ratio && nrows) HCHK(hipMemcpyAsync(ratio, ra.ratio, sizeof(double) * nrows * m, hipMemcpyDeviceToHost, st));
+  if (res && nrows) HCHK(hipMemcpyAsync(res, ra.res, sizeof(double) * nrows * 5, hipMemcpyDeviceToHost, st));
+  return cx->sync();
+}
+
+int scde_distribution_summary(const double* rpost, int nrows, int m, const double* diffv, int zi, double* res) {
+  if (!rpost || !diffv || !res || nrows < 0 || m < 1 || (m % 2) == 0) return fail(SCDE_EARG, "bad summary arguments");
+  if (zi < 0 || zi >= m) return fail(SCDE_EARG, "zi out of range");
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  hipStream_t st = cx->stream;
+  const int n = (m + 1) / 2;
+  RCHK(upload(cx, cx->in1, rpost, sizeof(double) * std::max<size_t>(1, (size_t)nrows * m)));
+  RCHK(upload(cx, cx->diffv, diffv, sizeof(double) * m));
+  HCHK(cx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)nrows * 5)));
+  RatioArgs ra{};
+  ra.n = n;
+  ra.ngenes = nrows;
+  ra.xin = cx->in1.as<double>();
+  ra.xg = 1;
+  ra.xo = nrows;
+  ra.diffv = cx->diffv.as<double>();
+  ra.zi = zi;
+  ra.res = cx->res.as<double>();
+  ra.res_ld = nrows;
+  HCHK(launch_ratio_summary(ra, st));
+  if (nrows) HCHK(hipMemcpyAsync(res, ra.res, sizeof(double) * nrows * 5, hipMemcpyDeviceToHost, st));
+  return cx->sync();
+}
+
+int scde_matSlideMult(const double* m1, const double* m2, int nrows, int ncols, double* out) {
+  if (!out) return fail(SCDE_EARG, "null out");
+  return ratio_common(m1, m2, nrows, ncols, nullptr, nullptr, 0, 0, out, nullptr);
+}
+
+int scde_ratio_summary(const double* pmat1, const double* pmat2, int nrows, int n, const double* prior_y,
+                       const double* diffv, int zi, double* ratio, double* res) {
+  return ratio_common(pmat1, pmat2, nrows, n, prior_y, diffv, zi, 1, ratio, res);
+}
+
+// ------------------------------------------------------------------ layer 2
+int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const int* cellidx,
+                        int ncells_sel, const double* models_sel, int local_theta, int square_logit_conc,
+                        const double* prior_x, int ngrid, int nboot, int n_cores, int64_t gene_offset,
+                        int64_t ngenes_total, int return_post, int ensemble, const int* batch_vals,
+                        const int64_t* batch_off, const int* composition, int nbatch, double* jp, double* modes,
+                        double* post) {
+  if (!ctx || !counts_dev || !cellidx || !models_sel || !prior_x || !jp) return fail(SCDE_EARG, "null argument");
+  if (ngenes < 0 || ncells_sel <= 0 || ngrid <= 0) return fail(SCDE_EARG, "bad dimensions");
+  HCHK(hipSetDevice(ctx->device));
+  const bool batch = batch_vals != nullptr;
+  std::vector<double> mm(models_sel, models_sel + (size_t)ncells_sel * 12);
+  for (int c = 0; c < ncells_sel; ++c) {
+    double& ca = mm[(size_t)c + (size_t)ncells_sel * 4];
+    if (ca < 1e-10) ca = 1e-10;  // R/functions.R:579-583
+  }
+  const std::vector<double> mag = marginals(prior_x, ngrid);
+  PostSpec s;
+  s.ncells = ncells_sel;
+  s.models = mm.data();
+  s.localtheta = local_theta;
+  s.squarelogit = square_logit_conc;
+  s.mag = mag.data();
+  s.G = ngrid;
+  s.nboot = nboot;
+  s.postflag = return_post;
+  s.ensemble = batch ? 0 : ensemble;
+  s.batch_call = batch;
+  s.counts_dev = counts_dev;
+  s.ld = ld;
+  s.cellidx_host = cellidx;
+  s.ngenes = ngenes;
+  seeding(n_cores, gene_offset, ngenes_total, ngenes, s.seeds, s.wset);
+  s.batch_vals = batch_vals;
+  s.batch_off = batch_off;
+  s.comp = composition;
+  s.nbatch = nbatch;
+  const size_t NG = (size_t)ngenes * ngrid;
+  HCHK(ctx->jpA.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  s.jp = ctx->jpA.as<double>();
+  s.jp_g = 1;
+  s.jp_k = ngenes;
+  const bool want_modes = (batch ? return_post == 1 : (return_post == 1 || return_post == 3)) && modes;
+  const bool want_post = (batch ? return_post == 2 : (return_post == 2 || return_post == 3)) && post;
+  if (want_modes) {
+    HCHK(ctx->jpB.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * ncells_sel)));
+    s.modes = ctx->jpB.as<double>();
+  }
+  if (want_post) {
+    HCHK(ctx->outbuf.ensure(sizeof(double) * std::max<size_t>(1, NG * ncells_sel)));
+    s.post = ctx->outbuf.as<double>();
+  }
+  RCHK(run_posterior(ctx, s));
+  if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, ctx->stream));
+  if (want_modes && ngenes)
+    HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * ngenes * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
+  if (want_post && NG)
+    HCHK(hipMemcpyAsync(post, s.post, sizeof(double) * NG * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
+  return ctx->sync();
+}
+
+int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes,
+                                   const scde_de_params* p, double* results, double* jp1, double* jp2,
+                                   double* ratio) {
+  if (!ctx || !counts_dev || !p || !p->models || !p->groups || !p->prior_x || !p->prior_y)
+    return fail(SCDE_EARG, "null argument");
+  if (ngenes < 0 || p->ncells <= 0 || p->ngrid <= 1) return fail(SCDE_EARG, "bad dimensions");
+  HCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const int C = p->ncells, G = p->ngrid;
+  // split cells by group (R/functions.R:372-374, tapply over levels)
+  std::vector<int> idx[2];
+  for (int c = 0; c < C; ++c)
+    if (p->groups[c] == 0 || p->groups[c] == 1) idx[p->groups[c]].push_back(c);
+  if (idx[0].empty() || idx[1].empty()) return fail(SCDE_EARG, "both groups need at least one cell");
+  const std::vector<double> mag = marginals(p->prior_x, G);
+  std::vector<int> seeds, wset;
+  seeding(p->n_cores, p->gene_offset, p->ngenes_total > 0 ? p->ngenes_total : ngenes, ngenes, seeds, wset);
+  const size_t NG = (size_t)ngenes * G;
+  HCHK(ctx->jpA.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  HCHK(ctx->jpB.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  std::vector<double> mm[2];
+  for (int gi = 0; gi < 2; ++gi) {
+    const int Cg = (int)idx[gi].size();
+    mm[gi].assign((size_t)Cg * 12, NAN);
+    for (int j = 0; j < 12; ++j)
+      for (int c = 0; c < Cg; ++c) mm[gi][(size_t)c + (size_t)Cg * j] = p->models[(size_t)idx[gi][c] + (size_t)C * j];
+    for (int c = 0; c < Cg; ++c) {
+      double& ca = mm[gi][(size_t)c + (size_t)Cg * 4];
+      if (ca < 1e-10) ca = 1e-10;
+    }
+    PostSpec s;
+    s.ncells = Cg;
+    s.models = mm[gi].data();
+    s.localtheta = p->local_theta;
+    s.squarelogit = p->square_logit_conc;
+    s.mag = mag.data();
+    s.G = G;
+    s.nboot = p->nboot;
+    s.counts_dev = counts_dev;
+    s.ld = ld;
+    s.cellidx_host = idx[gi].data();
+    s.ngenes = ngenes;
+    s.seeds = seeds;
+    s.wset = wset;
+    s.jp = (gi == 0 ? ctx->jpA : ctx->jpB).as<double>();
+    s.jp_g = G;  // gene-major rows for the ratio kernel
+    s.jp_k = 1;
+    RCHK(run_posterior(ctx, s));
+  }
+  // ratio posterior + summary
+  const std::vector<double> diffv = ratio_diffv(p->prior_x, G);
+  const int zi = expectation_index(diffv, p->expectation);
+  const size_t m = 2 * (size_t)G - 1;
+  RCHK(upload(ctx, ctx->prior_y, p->prior_y, sizeof(double) * G));
+  RCHK(upload(ctx, ctx->diffv, diffv.data(), sizeof(double) * m));
+  HCHK(ctx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * 5)));
+  if (ratio) HCHK(ctx->ratio.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * m)));
+  RatioArgs ra{};
+  ra.jp1 = ctx->jpA.as<double>();
+  ra.j1g = G;
+  ra.j1k = 1;
+  ra.jp2 = ctx->jpB.as<double>();
+  ra.j2g = G;
+  ra.j2k = 1;
+  ra.prior_y = ctx->prior_y.as<double>();
+  ra.n = G;
+  ra.ngenes = ngenes;
+  ra.normalize = 1;
+  ra.ratio = ratio ? ctx->ratio.as<double>() : nullptr;
+  ra.rg = 1;
+  ra.ro = ngenes;
+  ra.diffv = ctx->diffv.as<double>();
+  ra.zi = zi;
+  ra.res = ctx->res.as<double>();
+  ra.res_ld = ngenes;
+  hipEvent_t ev = ctx->mark_begin(SLOT_RATIO);
+  HCHK(launch_ratio_summary(ra, st));
+  ctx->mark_end(SLOT_RATIO, ev);
+  if (results && ngenes)
+    HCHK(hipMemcpyAsync(results, ra.res, sizeof(double) * ngenes * 5, hipMemcpyDeviceToHost, st));
+  if (ratio && ngenes) HCHK(hipMemcpyAsync(ratio, ra.ratio, sizeof(double) * ngenes * m, hipMemcpyDeviceToHost, st));
+  std::vector<double> tmp;
+  if ((jp1 || jp2) && NG) tmp.resize(NG);
+  if (jp1 && NG) {
+    HCHK(hipMemcpyAsync(tmp.data(), ctx->jpA.p, sizeof(double) * NG, hipMemcpyDeviceToHost, st));
+    RCHK(ctx->sync());
+    transpose_rows_to_colmajor(tmp.data(), ngenes, G, jp1);
+  }
+  if (jp2 && NG) {
+    HCHK(hipMemcpyAsync(tmp.data(), ctx->jpB.p, sizeof(double) * NG, hipMemcpyDeviceToHost, st));
+    RCHK(ctx->sync());
+    transpose_rows_to_colmajor(tmp.data(), ngenes, G, jp2);
+  }
+  return ctx->sync();
+}
+
+// ------------------------------------------------------------------ BH (host)
+int scde_bh_cz(const double* z, int64_t n, double* cz) {
+  if (n < 0 || (n > 0 && (!z || !cz))) return fail(SCDE_EARG, "bad arguments");
+  // p.adjust(p, "BH"): i <- n:1; o <- order(p, decreasing = TRUE); pmin(1, cummin(n/i * p[o]))[ro]
+  // NA (NaN) p-values are dropped from the adjustment and stay NA, as in R.
+  std::vector<double> p(n);
+  std::vector<int64_t> o;
+  o.reserve(n);
+  for (int64_t i = 0; i < n; ++i) {
+    p[i] = pnorm_upper(std::fabs(z[i]));
+    if (!std::isnan(p[i])) o.push_back(i);
+  }
+  const int64_t lp = (int64_t)o.size();
+  if (lp <= 1) {  // `if (n <= 1) return(p0)`: nothing to adjust
+    for (int64_t i = 0; i < n; ++i) {
+      const double s = (z[i] > 0) ? 1.0 : (z[i] < 0 ? -1.0 : (std::isnan(z[i]) ? NAN : 0.0));
+      cz[i] = s * qnorm_host(p[i], false);
+    }
+    return SCDE_OK;
+  }
+  std::stable_sort(o.begin(), o.end(), [&](int64_t a, int64_t b) { return p[a] > p[b]; });
+  std::vector<double> adj(n, NAN);
+  double cm = INFINITY;
+  for (int64_t r = 0; r < lp; ++r) {
+    const double i = (double)(lp - r);
+    const double v = ((double)lp / i) * p[o[r]];
+    if (v < cm) cm = v;
+    adj[o[r]] = cm < 1 ? cm : 1;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const double s = (z[i] > 0) ? 1.0 : (z[i] < 0 ? -1.0 : (std::isnan(z[i]) ? NAN : 0.0));
+    cz[i] = s * qnorm_host(adj[i], false);
+  }
+  return SCDE_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// R pnorm upper tail (Cody, R nmath pnorm.c pnorm_both), x >= 0 path used by BH
+double pnorm_upper(double x) {
+  static const double a[5] = {2.2352520354606839287, 161.02823106855587881, 1067.6894854603709582,
+                              18154.981253343561249, 0.065682337918207449113};
+  static const double b[4] = {47.20258190468824187, 976.09855173777669322, 10260.932208618978205,
+                              45507.789335026729956};
+  static const double c[9] = {0.39894151208813466764, 8.8831497943883759412, 93.506656132177855979,
+                              597.27027639480026226,  2494.5375852903726711, 6848.1904505362823326,
+                              11602.651437647350124,  9842.7148383839780218, 1.0765576773720192317e-8};
+  static const double d[8] = {22.266688044328115691, 235.38790178262499861, 1519.377599407554805,
+                              6485.558298266760755,  18615.571640885098091, 34900.952721145977266,
+                              38912.003286093271411, 19685.429676859990727};
+  static const double pp[6] = {0.21589853405795699,     0.1274011611602473639, 0.022235277870649807,
+                               0.001421619193227893466, 2.9112874951168792e-5, 0.02307344176494017303};
+  static const double q[5] = {1.28426009614491121, 0.468238212480865118, 0.0659881378689285515,
+                              0.00378239633202758244, 7.29751555083966205e-5};
+  const double M_1_SQRT_2PI = 0.398942280401432677939946059934, M_SQRT_32 = 5.656854249492380195206754896838;
+  if (std::isnan(x)) return x;
+  const double y = std::fabs(x);
+  double xnum, xden, temp, xsq, del, cum, ccum;
+  if (y <= 0.67448975) {
+    if (y > DBL_EPSILON * 0.5) {
+      xsq = x * x;
+      xnum = a[4] * xsq;
+      xden = xsq;
+      for (int i = 0; i < 3; ++i) {
+        xnum = (xnum + a[i]) * xsq;
+        xden = (xden + b[i]) * xsq;
+      }
+    } else {
+      xnum = xden = 0.0;
+    }
+    temp = x * (xnum + a[3]) / (xden + b[3]);
+    cum = 0.5 + temp;
+    ccum = 0.5 - temp;
+  } else if (y <= M_SQRT_32) {
+    xnum = c[8] * y;
+    xden = y;
+    for (int i = 0; i < 7; ++i) {
+      xnum = (xnum + c[i]) * y;
+      xden = (xden + d[i]) * y;
+    }
+    temp = (xnum + c[7]) / (xden + d[7]);
+    xsq = std::trunc(y * 16) / 16;
+    del = (y - xsq) * (y + xsq);
+    cum = std::exp(-xsq * xsq * 0.5) * std::exp(-del * 0.5) * temp;
+    ccum = 1.0 - cum;
+    if (x > 0.) std::swap(cum, ccum);
+  } else if ((-37.5193 < x && x < 8.2924) || (-8.2924 < x && x < 37.5193)) {
+    xsq = 1.0 / (x * x);
+    xnum = pp[5] * xsq;
+    xden = xsq;
+    for (int i = 0; i < 4; ++i) {
+      xnum = (xnum + pp[i]) * xsq;
+      xden = (xden + q[i]) * xsq;
+    }
+    temp = xsq * (xnum + pp[4]) / (xden + q[4]);
+    temp = (M_1_SQRT_2PI - temp) / y;
+    xsq = std::trunc(x * 16) / 16;
+    del = (x - xsq) * (x + xsq);
+    cum = std::exp(-xsq * xsq * 0.5) * std::exp(-del * 0.5) * temp;
+    ccum = 1.0 - cum;
+    if (x > 0.) std::swap(cum, ccum);
+  } else {
+    if (x > 0) {
+      cum = 1.;
+      ccum = 0.;
+    } else {
+      cum = 0.;
+      ccum = 1.;
+    }
+  }
+  return ccum;
+}
+
+double qnorm_host(double p, bool lower_tail) {
+  if (std::isnan(p)) return p;
+  if (p < 0 || p > 1) return NAN;
+  if (p == 0) return lower_tail ? -INFINITY : INFINITY;
+  if (p == 1) return lower_tail ? INFINITY : -INFINITY;
+  const double p_ = lower_tail ? p : (0.5 - p + 0.5);
+  const double q = p_ - 0.5;
+  double r, val;
+  if (std::fabs(q) <= .425) {
+    r = .180625 - q * q;
+    return q *
+           (((((((r * 2509.0809287301226727 + 33430.575583588128105) * r + 67265.770927008700853) * r +
+                45921.953931549871457) * r + 13731.693765509461125) * r + 1971.5909503065514427) * r +
+             133.14166789178437745) * r + 3.387132872796366608) /
+           (((((((r * 5226.495278852545925 + 28729.085735721942674) * r + 39307.89580009271061) * r +
+                21213.794301586595867) * r + 5394.1960214247511077) * r + 687.1870074920579083) * r +
+             42.313330701600911252) * r + 1.);
+  }
+  if (q < 0)
+    r = lower_tail ? p : (0.5 - p + 0.5);
+  else
+    r = lower_tail ? (0.5 - p + 0.5) : p;
+  r = std::sqrt(-std::log(r));
+  if (r <= 5.) {
+    r += -1.6;
+    val = (((((((r * 7.7454501427834140764e-4 + .0227238449892691845833) * r + .24178072517745061177) * r +
+                1.27045825245236838258) * r + 3.64784832476320460504) * r + 5.7694972214606914055) * r +
+             4.6303378461565452959) * r + 1.42343711074968357734) /
+          (((((((r * 1.05075007164441684324e-9 + 5.475938084995344946e-4) * r + .0151986665636164571966) * r +
+                .14810397642748007459) * r + .68976733498510000455) * r + 1.6763848301838038494) * r +
+             2.05319162663775882187) * r + 1.);
+  } else {
+    r += -5.;
+    val = (((((((r * 2.01033439929228813265e-7 + 2.71155556874348757815e-5) * r + .0012426609473880784386) * r +
+                .026532189526576123093) * r + .29656057182850489123) * r + 1.7848265399172913358) * r +
+             5.4637849111641143699) * r + 6.6579046435011037772) /
+          (((((((r * 2.04426310338993978564e-15 + 1.4215117583164458887e-7) * r + 1.8463183175100546818e-5) * r +
+                7.868691311456132591e-4) * r + .0148753612908506148525) * r + .13692988092273580531) * r +
+             .59983220655588793769) * r + 1.);
+  }
+  if (q < 0.0) val = -val;
+  return val;
+}
+
+}  // namespace

@@ -1,0 +1,122 @@
+// kernels.h -- argument blocks and launchers for kernels.hip (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace scde {
+
+struct TablesArgs {
+  const int* ucl;            // flat unique counts, [ncols]
+  const long long* ucl_off;  // [ncells + 1]
+  long long ncols;
+  int ncells;
+  int G, GS;
+  const double* mu;          // [ncells][GS]
+  const double* lcfp;        // [ncells][GS]
+  const double* lcfpr;       // [ncells][GS]
+  const double* theta;       // [ncells][GS]
+  const double* cellscal;    // [ncells][2] = {max log cfp, exp(fail.r)}
+  double minlogprob;         // -DBL_MAX / ncells / 1.1
+  double* T;                 // [ncols][GS] log-posterior columns
+  int* maxi;                 // [ncols] argmax (nullable)
+  unsigned char* has_clamp;  // [ncols]
+};
+
+struct BootArgs {
+  const double* T;  // [ncols][GS]
+  int G, GS;
+  const int2* ent;  // [ngenes][ent_stride] (cell, flat column)
+  const int* nnz;   // [ngenes]
+  int ent_stride;
+  const int* base_col;  // [ncells] baseline column (count 0) or -1; nullable
+  const double* Wt;     // [nsets][ncells][Bp] draw multiplicities
+  int ncells, Bp, nboot;
+  const int* wset;   // [ngenes] draw-set id per gene (nullable -> 0)
+  const double* Z;   // [nsets][Bp][GS] baseline sums (nullable)
+  double norm_mult;  // nboot for logBoot*Posterior, 1 for jpmat*
+  double degen_thresh;
+  double* out;
+  long long out_g, out_k;
+  int* degen;  // [ngenes]
+  int ngenes;
+};
+
+struct ExactArgs {
+  const double* T;
+  int G, GS;
+  const int* draws;  // [nsets][nboot][ndraw] cell index per draw, reference order
+  int ndraw, nboot;
+  const int* wset;
+  const long long* ucl_off;
+  const int* uci;  // [ld_uci x ncells] or null for jpmat (column = cell*ngenes + g)
+  long long ld_uci;
+  double norm_mult;
+  const int* degen;
+  double* out;
+  long long out_g, out_k;
+  int ngenes;
+};
+
+struct NoBootArgs {
+  const double* T;  // log tables, or normalised exp tables for ensemble
+  int G, GS;
+  const long long* ucl_off;
+  const int* uci;
+  long long ld_uci;
+  int ncells, ngenes;
+  int ensemble;
+  double* out;
+  long long out_g, out_k;
+};
+
+struct RatioArgs {
+  const double* jp1;
+  long long j1g, j1k;
+  const double* jp2;
+  long long j2g, j2k;
+  const double* prior_y;  // nullable: skip.prior.adjustment
+  int n, ngenes;
+  int normalize;  // 1: divide by the (long double) row sum (calculate.ratio.posterior); 0: raw matSlideMult
+  const double* xin;  // nullable: summarise this ratio matrix [g*xg + o*xo] (m = 2n-1 columns) instead
+  long long xg, xo;
+  double* ratio;  // nullable; [g*rg + o*ro]
+  long long rg, ro;
+  const double* diffv;  // [2n-1]
+  int zi;
+  double* res;  // nullable; column-major res_ld x 5 (lb, mle, ub, ce, Z)
+  long long res_ld;
+};
+
+hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,
+                            double* mu, double* lcfp, double* lcfpr, double* theta, double* cellscal,
+                            hipStream_t s);
+hipError_t launch_tables(const TablesArgs& a, hipStream_t s);
+hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells, const unsigned char* has_clamp,
+                            int use_baseline, int* base_col, hipStream_t s);
+hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
+                      const int* base_col, int2* ent, int* nnz, hipStream_t s);
+hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
+                             int Bp, int nsets, double* Z, hipStream_t s);
+hipError_t launch_boot(const BootArgs& a, hipStream_t s);
+hipError_t launch_boot_exact(const ExactArgs& a, hipStream_t s);
+hipError_t launch_noboot(const NoBootArgs& a, hipStream_t s);
+hipError_t launch_ensemble_cols(const double* T, long long ncols, int G, int GS, double* E, hipStream_t s);
+hipError_t launch_modes(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
+                        const int* maxi, const double* mag, double* modes, long long mg, long long mc,
+                        hipStream_t s);
+hipError_t launch_post(const int* uci, long long ld_uci, int ngenes, int c, const long long* ucl_off,
+                       const double* T, int G, int GS, double* post, long long pg, long long pk, hipStream_t s);
+hipError_t launch_cell_minmax(const int* counts, long long ld, long long g0, int ngenes, int ncells,
+                              const int* cellidx, int* cmax, int* cmin, hipStream_t s);
+hipError_t launch_mark(const int* counts, long long ld, long long g0, int ngenes, int ncells, const int* cellidx,
+                       const long long* woff, unsigned long long* bits, hipStream_t s);
+hipError_t launch_rank(const unsigned long long* bits, const long long* woff, int ncells, int* rank, int* nuniq,
+                       hipStream_t s);
+hipError_t launch_fill_ucl(const unsigned long long* bits, const long long* woff, int ncells, const int* rank,
+                           const long long* ucl_off, int* ucl, hipStream_t s);
+hipError_t launch_uci(const int* counts, long long ld, long long g0, int ngenes, int ncells, const int* cellidx,
+                      const long long* woff, const unsigned long long* bits, const int* rank, int* uci,
+                      hipStream_t s);
+hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int GS, double* dst, hipStream_t s);
+hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s);
+
+}  // namespace scde

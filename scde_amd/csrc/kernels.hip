@@ -1,0 +1,1010 @@
+// kernels.hip -- gfx950 (CDNA4) FP64 kernels for the scde differential-
+// expression hot path.  See DESIGN.md for the data layout and rooflines.
+//
+//   k_cell_prep      per-cell grid vectors mu, log cfp, log(1-cfp), theta
+//                    (src/jpmatLogBoot.cpp:131-162)
+//   k_tables         per-(cell, unique count) NB/Poisson mixture log-posterior
+//                    column + argmax + clamp (src/jpmatLogBoot.cpp:164-210);
+//                    one wavefront per column, lanes over grid points
+//   k_boot           bootstrap joint posterior (src/jpmatLogBoot.cpp:251-271):
+//                    one workgroup per gene, lanes over grid points, 16
+//                    bootstrap accumulators per lane, draws folded into
+//                    per-cell multiplicities, zero-count baseline
+//   k_boot_exact     reference-order fallback for rows whose sums are
+//                    dominated by clamp values
+//   k_ratio_summary  prior-weighted matSlideMult (src/matSlideMult.cpp:5-23)
+//                    + row normalisation + lb/mle/ub/ce/Z epilogue
+//                    (R/functions.R:3491-3531, 5039-5050)
+//   unique-count builder (R/functions.R:609-610 done on device), ELL entry
+//   builder, modes/post gathers, ensemble and nboot==0 variants.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "device_math.h"
+#include "kernels.h"
+
+namespace scde {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = fmax(v, __shfl_xor(v, m, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+// arma-style max: NaN never wins (first-max semantics live in the argmax path)
+__device__ __forceinline__ double gt_max(double a, double b) { return (b > a) ? b : a; }
+
+// ------------------------------------------------------------------ K0: cell prep
+// models: ncells x 12 column-major (R `mm`), columns per src/jpmatLogBoot.cpp:88-99
+__global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ models, int ncells, int G, int GS,
+                                                   const double* __restrict__ mag, int localtheta,
+                                                   int squarelogit, double* __restrict__ mu,
+                                                   double* __restrict__ lcfp, double* __restrict__ lcfpr,
+                                                   double* __restrict__ theta, double* __restrict__ cellscal) {
+  const int c = blockIdx.x;
+  auto M = [&](int col) { return models[(long long)c + (long long)ncells * col]; };
+  const double concb = M(0), conca = M(1), failr = M(2), corrb = M(3), corra = M(4), corrt = M(5);
+  const double ltb = M(6), ltt = M(7), ltm = M(8), lts = M(9), ltr = M(10), conca2 = M(11);
+  double lmax = -INFINITY;
+  for (int k = threadIdx.x; k < G; k += blockDim.x) {
+    const double m = mag[k];
+    mu[(long long)c * GS + k] = exp(m * corra + corrb);
+    double cf = squarelogit ? (conca + m * conca2) * m : m * conca;
+    cf += concb;
+    cf = 1.0 / (exp(cf) + 1.0);
+    const double lc = log(cf);
+    lcfpr[(long long)c * GS + k] = log(1.0 - cf);
+    lcfp[(long long)c * GS + k] = lc;
+    lmax = gt_max(lmax, lc);
+    double th = corrt;
+    if (localtheta) {
+      double t = -1.0 * m + ltm;
+      t *= lts;
+      t = pow(10.0, t) + 1.0;
+      t = pow(t, ltr);
+      t = (ltt - ltb) / t;
+      t += ltb;
+      t = exp(-1.0 * t);
+      if ((!isfinite(t)) || (t < 1.0e-2)) t = 1.0e-2;
+      if (t > 1.0e+3) t = 1.0e+3;
+      th = t;
+    }
+    theta[(long long)c * GS + k] = th;
+  }
+  __shared__ double red[16];
+  lmax = wave_max(lmax);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = lmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double m = red[0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) m = gt_max(m, red[w]);
+    cellscal[2 * c] = m;
+    cellscal[2 * c + 1] = exp(failr);
+  }
+}
+
+// ------------------------------------------------------------------ K1: tables
+template <int NJ>
+__global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
+  const int lane = threadIdx.x & 63;
+  const long long col = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (col >= a.ncols) return;
+  int lo = 0, hi = a.ncells;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (a.ucl_off[mid] <= col) lo = mid; else hi = mid;
+  }
+  const int c = lo;
+  const int G = a.G;
+  const double x = (double)a.ucl[col];
+  const double* mu = a.mu + (long long)c * a.GS;
+  const double* lcfp = a.lcfp + (long long)c * a.GS;
+  const double* lcfpr = a.lcfpr + (long long)c * a.GS;
+  const double* th = a.theta + (long long)c * a.GS;
+  const double maxcfp = a.cellscal[2 * c];
+  const double fp = dpois_log(x, a.cellscal[2 * c + 1]);
+  double v[NJ];
+  double lmax = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k = lane + 64 * j;
+    v[j] = -INFINITY;
+    if (k < G) {
+      double muv = mu[k];
+      const bool last = (k == G - 1);
+      const double mnext = last ? 0.0 : mu[k + 1];
+      if ((!last && x > muv && x < mnext) || (last && x > muv)) muv = x;
+      const double t = th[k];
+      double nb = dnbinom_log(x, t, t / (t + muv));
+      nb += lcfpr[k];
+      v[j] = nb;
+      lmax = gt_max(lmax, nb);
+    }
+  }
+  double maxp = lmax;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) maxp = gt_max(maxp, __shfl_xor(maxp, m, 64));
+  if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
+  double ls = 0.0;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k = lane + 64 * j;
+    if (k < G) {
+      v[j] = exp(v[j] - maxp) + exp(lcfp[k] + fp - maxp);
+      ls += v[j];
+    }
+  }
+  const double s = wave_sum(ls);
+  double bv = -INFINITY;
+  int bi = 0x7fffffff;
+  bool clamp = false;
+  double* out = a.T + col * a.GS;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int k = lane + 64 * j;
+    if (k < G) {
+      double r = log(v[j] / s);
+      if (r > bv) {
+        bv = r;
+        bi = k;
+      }
+      if (r < a.minlogprob) {
+        r = a.minlogprob;
+        clamp = true;
+      }
+      out[k] = r;
+    }
+  }
+  if (a.maxi) {
+    // first maximum over the grid (Armadillo max(index), strict '>')
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const double ov = __shfl_xor(bv, m, 64);
+      const int oi = __shfl_xor(bi, m, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) a.maxi[col] = (bi == 0x7fffffff) ? 0 : bi;
+  }
+  const unsigned long long anyc = __ballot(clamp);
+  if (lane == 0) a.has_clamp[col] = anyc ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ baseline / ELL
+// base_col[c] = flat column of count 0 in cell c when that column has no
+// clamped value, else -1 (cells without a usable baseline are always explicit).
+__global__ void k_base_cols(const int* __restrict__ ucl, const long long* __restrict__ ucl_off, int ncells,
+                            const unsigned char* __restrict__ has_clamp, int use_baseline,
+                            int* __restrict__ base_col) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncells) return;
+  int bc = -1;
+  if (use_baseline) {
+    for (long long i = ucl_off[c]; i < ucl_off[c + 1]; ++i) {
+      if (ucl[i] == 0) {
+        if (!has_clamp[i]) bc = (int)i;
+        break;
+      }
+    }
+  }
+  base_col[c] = bc;
+}
+
+// Per-gene ELL list of explicit (cell, column) entries, cell order ascending.
+__global__ void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes, int ncells,
+                      const long long* __restrict__ ucl_off, const int* __restrict__ base_col,
+                      int2* __restrict__ ent, int* __restrict__ nnz) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngenes) return;
+  int n = 0;
+  int2* E = ent + (long long)g * ncells;
+  for (int c = 0; c < ncells; ++c) {
+    const int col = (int)(ucl_off[c] + uci[(long long)g + ld_uci * c]);
+    if (col == base_col[c]) continue;
+    E[n++] = make_int2(c, col);
+  }
+  nnz[g] = n;
+}
+
+// Z[set][b][k] = sum over baseline cells of W[set][c][b] * T[base_col[c]][k]
+__global__ __launch_bounds__(512) void k_baseline_z(const double* __restrict__ T, int G, int GS,
+                                                    const int* __restrict__ base_col, int ncells,
+                                                    const double* __restrict__ Wt, int Bp,
+                                                    double* __restrict__ Z) {
+  const int b = blockIdx.x, set = blockIdx.y;
+  const double* W = Wt + (long long)set * ncells * Bp;
+  for (int k = threadIdx.x; k < GS; k += blockDim.x) {
+    double z = 0.0;
+    if (k < G) {
+      for (int c = 0; c < ncells; ++c) {
+        const int bc = base_col[c];
+        if (bc < 0) continue;
+        const double w = W[(long long)c * Bp + b];
+        if (w != 0.0) z = fma(w, T[(long long)bc * GS + k], z);
+      }
+    }
+    Z[((long long)set * Bp + b) * GS + k] = z;
+  }
+}
+
+// ------------------------------------------------------------------ K2: bootstrap
+// Wave-level reduce-scatter of BC values: after it, lane l holds the value for
+// boot index (l >> (6 - log2 BC)) & (BC - 1) reduced over all 64 lanes.
+template <int BC, bool MAX>
+__device__ __forceinline__ double wave_reduce_scatter(double (&v)[BC], int lane) {
+  constexpr int L2 = (BC == 16) ? 4 : (BC == 8) ? 3 : (BC == 4) ? 2 : (BC == 2) ? 1 : 0;
+#pragma unroll
+  for (int s = 0; s < L2; ++s) {
+    const int half = BC >> (s + 1);
+    const int mask = 32 >> s;
+    const bool up = (lane & mask) != 0;
+#pragma unroll
+    for (int j = 0; j < half; ++j) {
+      const double send = up ? v[j] : v[j + half];
+      const double keep = up ? v[j + half] : v[j];
+      const double r = __shfl_xor(send, mask, 64);
+      v[j] = MAX ? gt_max(keep, r) : keep + r;
+    }
+  }
+  double x = v[0];
+#pragma unroll
+  for (int mask = 32 >> L2; mask >= 1; mask >>= 1) {
+    const double r = __shfl_xor(x, mask, 64);
+    x = MAX ? gt_max(x, r) : x + r;
+  }
+  return x;
+}
+
+template <int BC, bool MAX>
+__device__ __forceinline__ void block_reduce_bc(double (&v)[BC], double* red, double* fin, int lane, int wid,
+                                                int nw) {
+  constexpr int L2 = (BC == 16) ? 4 : (BC == 8) ? 3 : (BC == 4) ? 2 : (BC == 2) ? 1 : 0;
+  const double x = wave_reduce_scatter<BC, MAX>(v, lane);
+  const int idx = (lane >> (6 - L2)) & (BC - 1);
+  if ((lane & ((64 >> L2) - 1)) == 0) red[wid * 16 + idx] = x;
+  __syncthreads();
+  if (threadIdx.x < BC) {
+    double r = red[threadIdx.x];
+    for (int w = 1; w < nw; ++w) r = MAX ? gt_max(r, red[w * 16 + threadIdx.x]) : r + red[w * 16 + threadIdx.x];
+    fin[threadIdx.x] = r;
+  }
+  __syncthreads();
+}
+
+template <int BC, int KPT>
+__device__ __forceinline__ void boot_pass(const BootArgs& a, int g, int b0, int n, const int2* __restrict__ E,
+                                          const double* __restrict__ W, const double* __restrict__ Zs,
+                                          double (&jpv)[KPT], double* red, double* fin, double* fin2) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  const int G = a.G, GS = a.GS;
+  double acc[KPT][BC];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int k = tid + j * blockDim.x;
+#pragma unroll
+    for (int i = 0; i < BC; ++i) acc[j][i] = (Zs && k < G) ? Zs[(long long)(b0 + i) * GS + k] : 0.0;
+  }
+  const double* __restrict__ T = a.T;
+  for (int e = 0; e < n; ++e) {
+    const int2 en = E[e];
+    const int cell = __builtin_amdgcn_readfirstlane(en.x);
+    const int col = __builtin_amdgcn_readfirstlane(en.y);
+    const int bc = __builtin_amdgcn_readfirstlane(a.base_col ? a.base_col[cell] : -1);
+    const double* __restrict__ w = W + (long long)cell * a.Bp + b0;
+    double wv[BC];
+#pragma unroll
+    for (int i = 0; i < BC; ++i) wv[i] = w[i];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int k = tid + j * blockDim.x;
+      if (k < G) {
+        double v = T[(long long)col * GS + k];
+        if (bc >= 0) v -= T[(long long)bc * GS + k];
+#pragma unroll
+        for (int i = 0; i < BC; ++i) acc[j][i] = fma(wv[i], v, acc[j][i]);
+      }
+    }
+  }
+  // ---- per-boot softmax over the grid (max, exp, sum) ----
+  double t[BC];
+#pragma unroll
+  for (int i = 0; i < BC; ++i) {
+    double m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j)
+      if (tid + j * (int)blockDim.x < G) m = gt_max(m, acc[j][i]);
+    t[i] = m;
+  }
+  block_reduce_bc<BC, true>(t, red, fin, lane, wid, nw);
+  double mx[BC];
+#pragma unroll
+  for (int i = 0; i < BC; ++i) mx[i] = fin[i];
+#pragma unroll
+  for (int i = 0; i < BC; ++i) {
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int k = tid + j * blockDim.x;
+      const double d = acc[j][i] - mx[i];
+      // exp(d) underflows to exactly 0 for d < -745.14; skip the call there
+      const double ev = (k < G && d >= -746.0) ? exp(d) : 0.0;
+      acc[j][i] = ev;
+      s += ev;
+    }
+    t[i] = s;
+  }
+  block_reduce_bc<BC, false>(t, red, fin2, lane, wid, nw);
+  if (tid < BC) {
+    const int b = b0 + tid;
+    const double m = mx[tid];
+    if (b < a.nboot && !(fabs(m) <= a.degen_thresh)) a.degen[g] = 1;
+    fin2[tid] = (b < a.nboot) ? 1.0 / (fin2[tid] * a.norm_mult) : 0.0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < BC; ++i) {
+    const double r = fin2[i];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) jpv[j] = fma(acc[j][i], r, jpv[j]);
+  }
+  __syncthreads();
+}
+
+template <int KPT>
+__global__ __launch_bounds__(1024) void k_boot(BootArgs a) {
+  __shared__ double red[16 * 16];
+  __shared__ double fin[16];
+  __shared__ double fin2[16];
+  const int tid = threadIdx.x;
+  for (int g = blockIdx.x; g < a.ngenes; g += gridDim.x) {
+    const int n = a.nnz[g];
+    const int2* E = a.ent + (long long)g * a.ent_stride;
+    const int set = a.wset ? a.wset[g] : 0;
+    const double* W = a.Wt + (long long)set * a.ncells * a.Bp;
+    const double* Zs = a.Z ? a.Z + (long long)set * a.Bp * a.GS : nullptr;
+    double jpv[KPT];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) jpv[j] = 0.0;
+    int b0 = 0;
+    for (; b0 + 16 <= a.nboot; b0 += 16) boot_pass<16, KPT>(a, g, b0, n, E, W, Zs, jpv, red, fin, fin2);
+    if (a.nboot - b0 >= 8) {
+      boot_pass<8, KPT>(a, g, b0, n, E, W, Zs, jpv, red, fin, fin2);
+      b0 += 8;
+    }
+    if (a.nboot - b0 >= 4) {
+      boot_pass<4, KPT>(a, g, b0, n, E, W, Zs, jpv, red, fin, fin2);
+      b0 += 4;
+    }
+    if (a.nboot - b0 > 0) boot_pass<4, KPT>(a, g, b0, n, E, W, Zs, jpv, red, fin, fin2);
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int k = tid + j * blockDim.x;
+      if (k < a.G) a.out[(long long)g * a.out_g + (long long)k * a.out_k] = jpv[j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ block reductions (simple)
+__device__ inline double block_max(double v, double* sh) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  double r = sh[0];
+  for (int w = 1; w < nw; ++w) r = gt_max(r, sh[w]);
+  return r;
+}
+__device__ inline double block_sum(double v, double* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wid] = v;
+  __syncthreads();
+  double r = sh[0];
+  for (int w = 1; w < nw; ++w) r += sh[w];
+  return r;
+}
+
+// Reference-order fallback: tjp accumulated draw by draw exactly as
+// src/jpmatLogBoot.cpp:251-270 does, for genes flagged degenerate by k_boot.
+template <int KPT>
+__global__ __launch_bounds__(1024) void k_boot_exact(ExactArgs a) {
+  __shared__ double sh[16];
+  const int g = blockIdx.x;
+  if (!a.degen[g]) return;
+  const int tid = threadIdx.x;
+  const int set = a.wset ? a.wset[g] : 0;
+  const int* dr = a.draws + (long long)set * a.nboot * a.ndraw;
+  double jpv[KPT];
+  for (int j = 0; j < KPT; ++j) jpv[j] = 0.0;
+  for (int b = 0; b < a.nboot; ++b) {
+    double t[KPT];
+    for (int j = 0; j < KPT; ++j) t[j] = 0.0;
+    for (int d = 0; d < a.ndraw; ++d) {
+      const int cell = dr[(long long)b * a.ndraw + d];
+      long long col;
+      if (a.uci)
+        col = a.ucl_off[cell] + a.uci[(long long)g + a.ld_uci * cell];
+      else
+        col = (long long)cell * a.ngenes + g;  // jpmat layout: matrix-major rows
+      for (int j = 0; j < KPT; ++j) {
+        const int k = tid + j * blockDim.x;
+        if (k < a.G) t[j] = __dadd_rn(t[j], a.T[col * a.GS + k]);
+      }
+    }
+    double m = -INFINITY;
+    for (int j = 0; j < KPT; ++j)
+      if (tid + j * (int)blockDim.x < a.G) m = gt_max(m, t[j]);
+    m = block_max(m, sh);
+    double s = 0.0;
+    for (int j = 0; j < KPT; ++j) {
+      const int k = tid + j * blockDim.x;
+      t[j] = (k < a.G) ? exp(t[j] - m) : 0.0;
+      s += t[j];
+    }
+    s = block_sum(s, sh);
+    const double den = s * a.norm_mult;
+    for (int j = 0; j < KPT; ++j) jpv[j] += t[j] / den;
+  }
+  for (int j = 0; j < KPT; ++j) {
+    const int k = tid + j * blockDim.x;
+    if (k < a.G) a.out[(long long)g * a.out_g + (long long)k * a.out_k] = jpv[j];
+  }
+}
+
+// nboot == 0 (src/jpmatLogBoot.cpp:237-248): sum over cells in order, softmax.
+template <int KPT>
+__global__ __launch_bounds__(1024) void k_noboot(NoBootArgs a) {
+  __shared__ double sh[16];
+  const int g = blockIdx.x, tid = threadIdx.x;
+  double t[KPT];
+  for (int j = 0; j < KPT; ++j) t[j] = 0.0;
+  for (int c = 0; c < a.ncells; ++c) {
+    const long long col = a.ucl_off[c] + a.uci[(long long)g + a.ld_uci * c];
+    const double* src = a.T + col * a.GS;
+    for (int j = 0; j < KPT; ++j) {
+      const int k = tid + j * blockDim.x;
+      if (k < a.G) t[j] = __dadd_rn(t[j], src[k]);
+    }
+  }
+  if (a.ensemble) {
+    double s = 0.0;
+    for (int j = 0; j < KPT; ++j) s += (tid + j * (int)blockDim.x < a.G) ? t[j] : 0.0;
+    s = block_sum(s, sh);
+    for (int j = 0; j < KPT; ++j) t[j] = t[j] / s;
+  } else {
+    double m = -INFINITY;
+    for (int j = 0; j < KPT; ++j)
+      if (tid + j * (int)blockDim.x < a.G) m = gt_max(m, t[j]);
+    m = block_max(m, sh);
+    double s = 0.0;
+    for (int j = 0; j < KPT; ++j) {
+      const int k = tid + j * blockDim.x;
+      t[j] = (k < a.G) ? exp(t[j] - m) : 0.0;
+      s += t[j];
+    }
+    s = block_sum(s, sh);
+    for (int j = 0; j < KPT; ++j) t[j] = t[j] / s;
+  }
+  for (int j = 0; j < KPT; ++j) {
+    const int k = tid + j * blockDim.x;
+    if (k < a.G) a.out[(long long)g * a.out_g + (long long)k * a.out_k] = t[j];
+  }
+}
+
+// ensemble: E = exp(T) / colsum(exp(T)) per column (src/jpmatLogBoot.cpp:226-229)
+__global__ __launch_bounds__(256) void k_ensemble_cols(const double* __restrict__ T, long long ncols, int G, int GS,
+                                                       double* __restrict__ Eo) {
+  const int lane = threadIdx.x & 63;
+  const long long col = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (col >= ncols) return;
+  double ls = 0.0;
+  for (int k = lane; k < G; k += 64) ls += exp(T[col * GS + k]);
+  const double s = wave_sum(ls);
+  for (int k = lane; k < G; k += 64) Eo[col * GS + k] = exp(T[col * GS + k]) / s;
+}
+
+// ------------------------------------------------------------------ modes / post gathers
+__global__ void k_modes(const int* __restrict__ uci, long long ld_uci, int ngenes, int ncells,
+                        const long long* __restrict__ ucl_off, const int* __restrict__ maxi,
+                        const double* __restrict__ mag, double* __restrict__ modes, long long mg, long long mc) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)ngenes * ncells) return;
+  const int g = (int)(i % ngenes), c = (int)(i / ngenes);
+  const long long col = ucl_off[c] + uci[(long long)g + ld_uci * c];
+  modes[g * mg + c * mc] = mag[maxi[col]];
+}
+
+__global__ void k_post(const int* __restrict__ uci, long long ld_uci, int ngenes, int c,
+                       const long long* __restrict__ ucl_off, const double* __restrict__ T, int G, int GS,
+                       double* __restrict__ post, long long pg, long long pk) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)ngenes * G) return;
+  const int g = (int)(i % ngenes), k = (int)(i / ngenes);
+  const long long col = ucl_off[c] + uci[(long long)g + ld_uci * c];
+  post[g * pg + k * pk] = T[col * GS + k];
+}
+
+// ------------------------------------------------------------------ device unique-count builder
+// counts: column-major, column = cellidx[c], rows g0 .. g0+ngenes
+__global__ void k_cell_minmax(const int* __restrict__ counts, long long ld, long long g0, int ngenes,
+                              const int* __restrict__ cellidx, int* __restrict__ cmax, int* __restrict__ cmin) {
+  __shared__ int smax[16], smin[16];
+  const int c = blockIdx.x;
+  const int* col = counts + (long long)cellidx[c] * ld + g0;
+  int mx = 0, mn = 0x7fffffff;
+  for (int g = threadIdx.x; g < ngenes; g += blockDim.x) {
+    const int x = col[g];
+    mx = max(mx, x);
+    mn = min(mn, x);
+  }
+  for (int m = 32; m >= 1; m >>= 1) {
+    mx = max(mx, __shfl_xor(mx, m, 64));
+    mn = min(mn, __shfl_xor(mn, m, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    smax[threadIdx.x >> 6] = mx;
+    smin[threadIdx.x >> 6] = mn;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+      mx = max(mx, smax[w]);
+      mn = min(mn, smin[w]);
+    }
+    mx = max(mx, smax[0]);
+    mn = min(mn, smin[0]);
+    cmax[c] = mx;
+    cmin[c] = mn;
+  }
+}
+
+__global__ void k_mark(const int* __restrict__ counts, long long ld, long long g0, int ngenes, int ncells,
+                       const int* __restrict__ cellidx, const long long* __restrict__ woff,
+                       unsigned long long* __restrict__ bits) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)ngenes * ncells) return;
+  const int g = (int)(i % ngenes), c = (int)(i / ngenes);
+  const int x = counts[(long long)cellidx[c] * ld + g0 + g];
+  atomicOr(&bits[woff[c] + (x >> 6)], 1ull << (x & 63));
+}
+
+// per cell: exclusive popcount prefix of its bitmap words -> rank, and #unique
+__global__ __launch_bounds__(256) void k_rank(const unsigned long long* __restrict__ bits,
+                                              const long long* __restrict__ woff, int* __restrict__ rank,
+                                              int* __restrict__ nuniq) {
+  __shared__ int wsum[4];
+  __shared__ int carry;
+  const int c = blockIdx.x;
+  const long long w0 = woff[c], w1 = woff[c + 1];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (long long base = w0; base < w1; base += blockDim.x) {
+    const long long w = base + threadIdx.x;
+    const int pc = (w < w1) ? __popcll(bits[w]) : 0;
+    int incl = pc;
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += o;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    int pre = carry;
+    for (int v = 0; v < wid; ++v) pre += wsum[v];
+    if (w < w1) rank[w] = pre + incl - pc;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) nuniq[c] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_fill_ucl(const unsigned long long* __restrict__ bits,
+                                                  const long long* __restrict__ woff,
+                                                  const int* __restrict__ rank,
+                                                  const long long* __restrict__ ucl_off, int* __restrict__ ucl) {
+  const int c = blockIdx.x;
+  const long long w0 = woff[c], w1 = woff[c + 1];
+  for (long long w = w0 + threadIdx.x; w < w1; w += blockDim.x) {
+    unsigned long long b = bits[w];
+    long long pos = ucl_off[c] + rank[w];
+    while (b) {
+      const int t = __ffsll((long long)b) - 1;
+      ucl[pos++] = (int)((w - w0) * 64 + t);
+      b &= b - 1;
+    }
+  }
+}
+
+__global__ void k_uci(const int* __restrict__ counts, long long ld, long long g0, int ngenes, int ncells,
+                      const int* __restrict__ cellidx, const long long* __restrict__ woff,
+                      const unsigned long long* __restrict__ bits, const int* __restrict__ rank,
+                      int* __restrict__ uci) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)ngenes * ncells) return;
+  const int g = (int)(i % ngenes), c = (int)(i / ngenes);
+  const int x = counts[(long long)cellidx[c] * ld + g0 + g];
+  const long long w = woff[c] + (x >> 6);
+  const unsigned long long below = bits[w] & ((1ull << (x & 63)) - 1ull);
+  uci[(long long)g + (long long)ngenes * c] = rank[w] + __popcll(below);
+}
+
+// ------------------------------------------------------------------ jpmat: transpose column-major -> row-major
+__global__ void k_colmajor_to_rows(const double* __restrict__ src, int nrows, int ncols, int GS,
+                                   double* __restrict__ dst) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)nrows * ncols) return;
+  const int r = (int)(i % nrows), k = (int)(i / nrows);
+  dst[(long long)r * GS + k] = src[i];
+}
+
+// ------------------------------------------------------------------ K3: ratio posterior + summary
+__global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
+  extern __shared__ double sh[];
+  const int n = a.n, m = 2 * a.n - 1;
+  double* A = sh;
+  double* B = sh + n;
+  double* X = sh + 2 * n;
+  __shared__ double red[8];
+  __shared__ double red2[8];
+  __shared__ int ired[8];
+  __shared__ int ired2[8];
+  __shared__ int ired3[8];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  for (int g = blockIdx.x; g < a.ngenes; g += gridDim.x) {
+    for (int k = tid; k < n && !a.xin; k += blockDim.x) {
+      const double y = a.prior_y ? a.prior_y[k] : 1.0;
+      const double p1 = a.jp1[(long long)g * a.j1g + (long long)k * a.j1k];
+      const double p2 = a.jp2[(long long)g * a.j2g + (long long)k * a.j2k];
+      A[k] = a.prior_y ? __dmul_rn(p1, y) : p1;
+      B[k] = a.prior_y ? __dmul_rn(p2, y) : p2;
+    }
+    __syncthreads();
+    // matSlideMult: X[o] = sum_t A[t + max(s,0)] * B[t + max(-s,0)], s = o - (n-1), t ascending
+    dd ls = {0.0, 0.0};
+    for (int o = tid; o < m && a.xin; o += blockDim.x) X[o] = a.xin[(long long)g * a.xg + (long long)o * a.xo];
+    for (int o = tid; o < m && !a.xin; o += blockDim.x) {
+      const int s = o - (n - 1);
+      const int o1 = s > 0 ? s : 0, o2 = s < 0 ? -s : 0;
+      const int len = n - (s < 0 ? -s : s);
+      double acc = 0.0;
+      for (int t = 0; t < len; ++t) acc = __dadd_rn(acc, __dmul_rn(A[t + o1], B[t + o2]));
+      X[o] = acc;
+      ls = dd_add_d(ls, acc);
+    }
+    // row sum (R rowSums accumulates in long double): double-double block reduce
+    for (int d = 32; d >= 1; d >>= 1) {
+      dd o2;
+      o2.hi = __shfl_xor(ls.hi, d, 64);
+      o2.lo = __shfl_xor(ls.lo, d, 64);
+      ls = dd_add(ls, o2);
+    }
+    if (lane == 0) {
+      red[wid] = ls.hi;
+      red2[wid] = ls.lo;
+    }
+    __syncthreads();
+    dd tot = {red[0], red2[0]};
+    for (int w = 1; w < nw; ++w) tot = dd_add(tot, dd{red[w], red2[w]});
+    const bool norm = a.normalize && !a.xin;
+    const double rs = norm ? dd_to_d(tot) : 1.0;
+    __syncthreads();
+    for (int o = tid; o < m; o += blockDim.x) {
+      const double p = norm ? X[o] / rs : X[o];
+      X[o] = p;
+      if (a.ratio) a.ratio[(long long)g * a.rg + (long long)o * a.ro] = p;
+    }
+    __syncthreads();
+    if (!a.res) continue;
+    // ---- quick.distribution.summary: contiguous chunk per thread ----
+    const int per = (m + blockDim.x - 1) / blockDim.x;
+    const int c0 = tid * per, c1 = min(m, c0 + per);
+    dd csum = {0.0, 0.0}, zsum = {0.0, 0.0};
+    double bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int o = c0; o < c1; ++o) {
+      const double p = X[o];
+      csum = dd_add_d(csum, p);
+      zsum = dd_add_d(zsum, p + 1e-15);
+      if (p > bv) {
+        bv = p;
+        bi = o;
+      }
+    }
+    // block scan of chunk sums (dd): inclusive within the wave, then exclusive
+    dd incl = csum;
+    for (int d = 1; d < 64; d <<= 1) {
+      dd o2;
+      o2.hi = __shfl_up(incl.hi, d, 64);
+      o2.lo = __shfl_up(incl.lo, d, 64);
+      if (lane >= d) incl = dd_add(o2, incl);
+    }
+    dd excl;
+    excl.hi = __shfl_up(incl.hi, 1, 64);
+    excl.lo = __shfl_up(incl.lo, 1, 64);
+    if (lane == 0) excl = dd{0.0, 0.0};
+    // argmax (first max)
+    for (int d = 32; d >= 1; d >>= 1) {
+      const double ov = __shfl_xor(bv, d, 64);
+      const int oi = __shfl_xor(bi, d, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    // z-sum total
+    dd zt = zsum;
+    for (int d = 32; d >= 1; d >>= 1) {
+      dd o2;
+      o2.hi = __shfl_xor(zt.hi, d, 64);
+      o2.lo = __shfl_xor(zt.lo, d, 64);
+      zt = dd_add(zt, o2);
+    }
+    __syncthreads();
+    if (lane == 63) {
+      red[wid] = incl.hi;
+      red2[wid] = incl.lo;
+    }
+    if (lane == 0) {
+      ired[wid] = bi;
+      X[m + wid] = bv;  // scratch after the row (allocated)
+      X[m + 8 + wid] = zt.hi;
+      X[m + 16 + wid] = zt.lo;
+    }
+    __syncthreads();
+    dd pre = {0.0, 0.0};
+    for (int w = 0; w < wid; ++w) pre = dd_add(pre, dd{red[w], red2[w]});
+    dd run = dd_add(pre, excl);
+    // walk chunk: lb = last o with cs < 0.025, ub = first o with cs > 0.975
+    int lbi = -1, ubi = 0x7fffffff;
+    for (int o = c0; o < c1; ++o) {
+      run = dd_add_d(run, X[o]);
+      const double cs = dd_to_d(run);
+      if (cs < 0.025) lbi = o;
+      if (cs > (1 - 0.025) && ubi == 0x7fffffff) ubi = o;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+      lbi = max(lbi, __shfl_xor(lbi, d, 64));
+      ubi = min(ubi, __shfl_xor(ubi, d, 64));
+    }
+    __syncthreads();
+    if (lane == 0) {
+      ired2[wid] = lbi;
+      ired3[wid] = ubi;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int lb = ired2[0], ub = ired3[0];
+      double mb = X[m];
+      int mi = ired[0];
+      dd zt2 = {X[m + 8], X[m + 16]};
+      for (int w = 1; w < nw; ++w) {
+        lb = max(lb, ired2[w]);
+        ub = min(ub, ired3[w]);
+        const double v = X[m + w];
+        if (v > mb || (v == mb && ired[w] < mi)) {
+          mb = v;
+          mi = ired[w];
+        }
+        zt2 = dd_add(zt2, dd{X[m + 8 + w], X[m + 16 + w]});
+      }
+      if (lb < 0) lb = 0;
+      if (ub == 0x7fffffff) ub = m - 1;
+      if (mi == 0x7fffffff) mi = 0;
+      const double l10_2 = 0.30102999566398119521;
+      const double lbv = a.diffv[lb] / l10_2, mlev = a.diffv[mi] / l10_2, ubv = a.diffv[ub] / l10_2;
+      double ce = 0.0;
+      if (lbv > 0) ce = lbv;
+      if (ubv < 0) ce = ubv;
+      // Z: rpost = (p + 1e-15) / rowSums, gs = sum(rpost[1:(zi-1)]), zv = rpost[zi]
+      const double rs2 = dd_to_d(zt2);
+      dd gs = {0.0, 0.0};
+      if (a.zi == 0) gs = dd_add_d(gs, (X[0] + 1e-15) / rs2);
+      for (int o = 0; o < a.zi; ++o) gs = dd_add_d(gs, (X[o] + 1e-15) / rs2);
+      const double gsd = dd_to_d(gs);
+      const double zv = (X[a.zi] + 1e-15) / rs2;
+      double zl = qnorm(gsd, false);
+      if (zl > 0) zl = 0;
+      double zg = qnorm(gsd + zv, false);
+      if (zg < 0) zg = 0;
+      const double z = (fabs(zl) > fabs(zg)) ? zl : zg;
+      const long long N = a.res_ld;
+      a.res[g] = lbv;
+      a.res[g + N] = mlev;
+      a.res[g + 2 * N] = ubv;
+      a.res[g + 3 * N] = ce;
+      a.res[g + 4 * N] = z;
+    }
+    __syncthreads();
+  }
+}
+
+// ================================================================== launchers
+static inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,
+                            double* mu, double* lcfp, double* lcfpr, double* theta, double* cellscal,
+                            hipStream_t s) {
+  if (ncells <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cell_prep, dim3(ncells), dim3(256), 0, s, models, ncells, G, GS, mag, lt, sq, mu, lcfp,
+                     lcfpr, theta, cellscal);
+  return hipGetLastError();
+}
+
+hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
+  if (a.ncols <= 0) return hipSuccess;
+  const dim3 grid(div_up(a.ncols, 4)), block(256);
+  const int nj = (a.G + 63) / 64;
+  if (nj <= 8)
+    hipLaunchKernelGGL(k_tables<8>, grid, block, 0, s, a);
+  else if (nj <= 16)
+    hipLaunchKernelGGL(k_tables<16>, grid, block, 0, s, a);
+  else if (nj <= 32)
+    hipLaunchKernelGGL(k_tables<32>, grid, block, 0, s, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells, const unsigned char* has_clamp,
+                            int use_baseline, int* base_col, hipStream_t s) {
+  if (ncells <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_base_cols, dim3(div_up(ncells, 128)), dim3(128), 0, s, ucl, ucl_off, ncells, has_clamp,
+                     use_baseline, base_col);
+  return hipGetLastError();
+}
+
+hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
+                      const int* base_col, int2* ent, int* nnz, hipStream_t s) {
+  if (ngenes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 128)), dim3(128), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
+                     base_col, ent, nnz);
+  return hipGetLastError();
+}
+
+hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
+                             int Bp, int nsets, double* Z, hipStream_t s) {
+  hipLaunchKernelGGL(k_baseline_z, dim3(Bp, nsets), dim3(512), 0, s, T, G, GS, base_col, ncells, Wt, Bp, Z);
+  return hipGetLastError();
+}
+
+static inline int block_for_grid(int G, int* kpt) {
+  int b = ((G + 63) / 64) * 64;
+  *kpt = 1;
+  while (b > 1024) {
+    *kpt *= 2;
+    b = ((G + *kpt * 64 - 1) / (*kpt * 64)) * 64;
+  }
+  return b;
+}
+
+hipError_t launch_boot(const BootArgs& a, hipStream_t s) {
+  if (a.ngenes <= 0) return hipSuccess;
+  int kpt;
+  const int block = block_for_grid(a.G, &kpt);
+  const int grid = a.ngenes;
+  switch (kpt) {
+    case 1: hipLaunchKernelGGL(k_boot<1>, dim3(grid), dim3(block), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_boot<2>, dim3(grid), dim3(block), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(k_boot<4>, dim3(grid), dim3(block), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_boot_exact(const ExactArgs& a, hipStream_t s) {
+  if (a.ngenes <= 0) return hipSuccess;
+  int kpt;
+  const int block = block_for_grid(a.G, &kpt);
+  switch (kpt) {
+    case 1: hipLaunchKernelGGL(k_boot_exact<1>, dim3(a.ngenes), dim3(block), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_boot_exact<2>, dim3(a.ngenes), dim3(block), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(k_boot_exact<4>, dim3(a.ngenes), dim3(block), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_noboot(const NoBootArgs& a, hipStream_t s) {
+  if (a.ngenes <= 0) return hipSuccess;
+  int kpt;
+  const int block = block_for_grid(a.G, &kpt);
+  switch (kpt) {
+    case 1: hipLaunchKernelGGL(k_noboot<1>, dim3(a.ngenes), dim3(block), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_noboot<2>, dim3(a.ngenes), dim3(block), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(k_noboot<4>, dim3(a.ngenes), dim3(block), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ensemble_cols(const double* T, long long ncols, int G, int GS, double* E, hipStream_t s) {
+  if (ncols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_ensemble_cols, dim3(div_up(ncols, 4)), dim3(256), 0, s, T, ncols, G, GS, E);
+  return hipGetLastError();
+}
+
+hipError_t launch_modes(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
+                        const int* maxi, const double* mag, double* modes, long long mg, long long mc,
+                        hipStream_t s) {
+  const long long n = (long long)ngenes * ncells;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_modes, dim3(div_up(n, 256)), dim3(256), 0, s, uci, ld_uci, ngenes, ncells, ucl_off, maxi,
+                     mag, modes, mg, mc);
+  return hipGetLastError();
+}
+
+hipError_t launch_post(const int* uci, long long ld_uci, int ngenes, int c, const long long* ucl_off,
+                       const double* T, int G, int GS, double* post, long long pg, long long pk, hipStream_t s) {
+  const long long n = (long long)ngenes * G;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_post, dim3(div_up(n, 256)), dim3(256), 0, s, uci, ld_uci, ngenes, c, ucl_off, T, G, GS,
+                     post, pg, pk);
+  return hipGetLastError();
+}
+
+hipError_t launch_cell_minmax(const int* counts, long long ld, long long g0, int ngenes, int ncells,
+                              const int* cellidx, int* cmax, int* cmin, hipStream_t s) {
+  if (ncells <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cell_minmax, dim3(ncells), dim3(256), 0, s, counts, ld, g0, ngenes, cellidx, cmax, cmin);
+  return hipGetLastError();
+}
+
+hipError_t launch_mark(const int* counts, long long ld, long long g0, int ngenes, int ncells, const int* cellidx,
+                       const long long* woff, unsigned long long* bits, hipStream_t s) {
+  const long long n = (long long)ngenes * ncells;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mark, dim3(div_up(n, 256)), dim3(256), 0, s, counts, ld, g0, ngenes, ncells, cellidx, woff,
+                     bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_rank(const unsigned long long* bits, const long long* woff, int ncells, int* rank, int* nuniq,
+                       hipStream_t s) {
+  if (ncells <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rank, dim3(ncells), dim3(256), 0, s, bits, woff, rank, nuniq);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_ucl(const unsigned long long* bits, const long long* woff, int ncells, const int* rank,
+                           const long long* ucl_off, int* ucl, hipStream_t s) {
+  if (ncells <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_ucl, dim3(ncells), dim3(256), 0, s, bits, woff, rank, ucl_off, ucl);
+  return hipGetLastError();
+}
+
+hipError_t launch_uci(const int* counts, long long ld, long long g0, int ngenes, int ncells, const int* cellidx,
+                      const long long* woff, const unsigned long long* bits, const int* rank, int* uci,
+                      hipStream_t s) {
+  const long long n = (long long)ngenes * ncells;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_uci, dim3(div_up(n, 256)), dim3(256), 0, s, counts, ld, g0, ngenes, ncells, cellidx, woff,
+                     bits, rank, uci);
+  return hipGetLastError();
+}
+
+hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int GS, double* dst, hipStream_t s) {
+  const long long n = (long long)nrows * ncols;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_colmajor_to_rows, dim3(div_up(n, 256)), dim3(256), 0, s, src, nrows, ncols, GS, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s) {
+  if (a.ngenes <= 0) return hipSuccess;
+  const size_t shm = sizeof(double) * (size_t)(4 * a.n + 32);
+  const int grid = a.ngenes < 65536 ? a.ngenes : 65536;
+  hipLaunchKernelGGL(k_ratio_summary, dim3(grid), dim3(256), shm, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace scde
