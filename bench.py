@@ -1,0 +1,196 @@
+"""bench.py -- genes/sec for scde.expression.difference (401-pt grid, 100 randomizations).
+
+Workload (BASELINE.json configs[1]): synthetic 20,000 genes x 200 cells (100/100 groups),
+400-point prior (G = 401 grid points), n.randomizations = 100, reference seeding n.cores = 1.
+One step = one scde.expression.difference pass over the batch on counts resident in HBM:
+unique-count tables, per-cell NB/Poisson log-posterior tables, bootstrap joint posteriors
+for both groups, ratio posterior + lb/mle/ub/ce/Z summary, results to host, BH cZ.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): genes shard across
+ranks with a fixed 20,000 genes per rank (weak scaling); the one exchange is a gather
+of per-gene Z to rank 0 (RCCL) for the global BH adjustment.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+N_GENES = 20000
+N_CELLS = 200
+NBOOT = 100
+LENGTH_OUT = 400
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def synthetic(seed: int, ngenes=N_GENES, ncells=N_CELLS):
+    """SURVEY.md §8(d) generator: o.ifm-resampled models, log-FPM ~ N(2.5, 2), 10% DE genes,
+    NB/Poisson-mixture counts with the models' own dropout curve."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "esmef500.npz"), allow_pickle=False)
+    from scde_amd.models import MODEL_COLUMNS
+    base = g["models"]
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rows = rng.integers(0, base.shape[0], ncells)
+    mm = base[rows]
+    models = {c: mm[:, j] for j, c in enumerate(MODEL_COLUMNS) if not np.all(np.isnan(mm[:, j]))}
+    groups = np.repeat([0, 1], ncells // 2).astype(np.int32)
+    m = rng.normal(2.5, 2.0, ngenes)
+    shift = np.where(rng.random(ngenes) < 0.1, rng.normal(0, 1.5, ngenes), 0.0)
+    M = m[:, None] + shift[:, None] * groups[None, :]
+    pfail = 1.0 / (1.0 + np.exp(models["conc.b"][None, :] + models["conc.a"][None, :] * M))
+    mu = np.exp(models["corr.b"][None, :] + models["corr.a"][None, :] * M)
+    theta = models["corr.theta"][None, :]
+    nb = rng.negative_binomial(theta, theta / (theta + mu))
+    pois = rng.poisson(np.exp(models["fail.r"])[None, :], size=M.shape)
+    counts = np.where(rng.random(M.shape) < pfail, pois, nb).astype(np.int32)
+    return models, np.asfortranarray(counts), groups
+
+
+def dominant_kernel_bytes(ngenes, cells_per_group):
+    """SURVEY.md §8(d) algorithmic bytes for one bootstrap launch (one group): each gene reads
+    each cell's posterior column once (8G B) + its count index (4 B) and writes one jp row."""
+    G = LENGTH_OUT + 1
+    return ngenes * (cells_per_group * (4 + 8 * G) + 8 * G)
+
+
+def cpu_baseline(models, counts, groups, prior, sample_genes):
+    """The oracle (C restatement of the reference loops, 1 core) on a bounded gene sample."""
+    from oracle import oracle as O
+    sub = np.ascontiguousarray(counts[:sample_genes])
+    t0 = time.perf_counter()
+    O.scde_expression_difference(models, sub, prior["x"], prior["y"], groups, n_randomizations=NBOOT, n_cores=1)
+    dt = time.perf_counter() - t0
+    return sample_genes / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=2000, help="genes timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist  # noqa: F811
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from scde_amd import api
+    from scde_amd.prior import expression_prior
+
+    models, counts, groups = synthetic(2002 + rank)
+    zero_frac = float(np.mean(counts == 0))
+    prior = expression_prior(models, counts, length_out=LENGTH_OUT)
+    ctx = api.Context(local_rank)
+    dc = api.DeviceCounts(ctx, counts)
+    from scde_amd.models import model_matrix
+    mm, lt, sq = model_matrix(models)
+    px = np.ascontiguousarray(prior["x"], np.float64)
+    py = np.ascontiguousarray(prior["y"], np.float64)
+    codes = np.ascontiguousarray(groups, np.int32)
+    G = len(px)
+    params = api.DEParams(N_CELLS, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
+                          NBOOT, 1, rank * N_GENES, world * N_GENES, 0.0, api.get_rand_kind())
+    res = np.zeros((N_GENES, 5), order="F")
+    L = api.lib()
+    import ctypes
+
+    def step():
+        api.check(L.scde_expression_difference_dev(ctx.handle, dc.ptr, N_GENES, N_GENES, ctypes.byref(params),
+                                                   res.ctypes.data_as(ctypes.c_void_p), None, None, None))
+        z = np.ascontiguousarray(res[:, 4])
+        if dist is not None:
+            import torch
+            zt = torch.from_numpy(z).cuda()
+            gathered = [torch.empty_like(zt) for _ in range(world)] if rank == 0 else None
+            dist.gather(zt, gathered, dst=0)
+            if rank == 0:
+                api.bh_cz(torch.cat(gathered).cpu().numpy())
+        else:
+            api.bh_cz(z)
+
+    def barrier():
+        ctx.synchronize()
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    if not args.no_profile:
+        ctx.set_profiling(True)
+    ctx.reset_kernel_times()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    dt = time.perf_counter() - t0
+    kt = ctx.kernel_times()
+    if dist is not None:
+        import torch
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+
+    total_genes = N_GENES * world * args.steps
+    value = total_genes / dt
+    boot_ms, boot_n = kt["boot"]
+    boot_avg_s = (boot_ms / max(boot_n, 1)) / 1e3
+    per_launch_bytes = dominant_kernel_bytes(N_GENES, N_CELLS // 2)
+    achieved = per_launch_bytes / boot_avg_s / 1e9 if boot_n else None
+    out = {
+        "metric": "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)",
+        "value": value,
+        "unit": "genes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic (PCG64 seed 2002+rank; o.ifm-resampled models; zero fraction {zero_frac:.3f})",
+        "config": {"workload": "config2: synthetic 20000 genes x 200 cells (100/100), 401-pt grid, "
+                               "100 bootstraps, n.cores=1 seeding", "genes_per_gpu": N_GENES, "cells": N_CELLS,
+                   "grid": G, "n_randomizations": NBOOT, "parallelism": f"gene-shard x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_boot (bootstrap joint posterior)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
+                     "algorithmic_bytes_per_launch": per_launch_bytes},
+        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
+    }
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        gps, secs = cpu_baseline(models, counts, groups, prior, args.cpu_sample)
+        out["cpu_baseline"] = {"value": gps, "unit": "genes/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle C restatement, first {args.cpu_sample} genes of the same batch, "
+                                         f"both groups + ratio + summary + BH, {secs:.1f}s"}
+    if rank == 0:
+        print(json.dumps(out))
+    dc.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -35,6 +35,17 @@ extern "C" {
 const char* scde_last_error(void);
 int scde_version(void); /* 100 * major + minor */
 
+/* Which C-library rand() the bootstrap draws reproduce (the reference calls the
+ * platform's srand()/rand(), src/jpmatLogBoot.cpp:221,256):
+ *   SCDE_RAND_GLIBC  glibc TYPE_3 (Linux; the default)
+ *   SCDE_RAND_DARWIN Darwin/BSD libc Park-Miller (macOS; reproduces the vignette)
+ * Process-wide default for layer 1 and scde_posteriors_dev; also read once from
+ * the environment variable SCDE_RAND=glibc|darwin. */
+#define SCDE_RAND_GLIBC 0
+#define SCDE_RAND_DARWIN 2
+int scde_set_rand_kind(int kind);
+int scde_get_rand_kind(void);
+
 /* ---------------------------------------------------------------- layer 1 */
 
 /* Replaces logBootPosterior  (src/jpmatLogBoot.cpp:100, decl src/jpmatLogBoot.h:8).
@@ -124,6 +135,7 @@ typedef struct scde_de_params {
   int64_t gene_offset;     /* first global gene index of this shard */
   int64_t ngenes_total;    /* global number of genes (for chunk seeds) */
   double expectation;      /* R `expectation` (log2 scale) */
+  int rand_kind;           /* SCDE_RAND_GLIBC / SCDE_RAND_DARWIN */
 } scde_de_params;
 
 /* scde.expression.difference (R/functions.R:304-407, no batch) on device-resident

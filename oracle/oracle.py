@@ -20,6 +20,7 @@ R glue restated here (file:line into the reference):
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import subprocess
 
@@ -69,6 +70,7 @@ def lib():
         L.o_ratio_posterior.argtypes = [P, P, P, i, i, P]
         L.o_summary.argtypes = [P, i, i, P, d, P]
         L.o_bh_cz.argtypes = [P, i, P]
+        L.o_set_rng_kind.argtypes = [i]
         _lib = L
     return _lib
 
@@ -86,6 +88,11 @@ def _i32(a):
 
 
 # ---------------------------------------------------------------- scalars
+def set_rng(kind):
+    """0 = glibc TYPE_3 (Linux), 2 = Darwin/BSD Park-Miller (macOS; the vignette's platform)."""
+    lib().o_set_rng_kind(int(kind))
+
+
 def rand_stream(seed, n):
     out = np.zeros(n, np.int32)
     lib().o_rand_stream(seed, n, _p(out))
@@ -207,8 +214,8 @@ def matSlideMult(m1, m2):
 
 # ---------------------------------------------------------------- R glue
 def marginals_from_prior_x(x):
-    """R/functions.R:575-577."""
-    m = 10.0 ** np.asarray(x, np.float64) - 1
+    """R/functions.R:575-577.  R's `^` is libm pow() (R_pow), so use math.pow, not numpy."""
+    m = np.array([math.pow(10.0, v) for v in np.asarray(x, np.float64)]) - 1
     m[m < 0] = 0
     with np.errstate(divide="ignore"):
         return np.log(m)

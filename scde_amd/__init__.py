@@ -8,7 +8,7 @@ The numeric work runs in ``libscde_hip.so`` (hand-written HIP kernels, C ABI in
 from .api import (Context, DeviceCounts, RatioPosterior, ScdeError, bh_cz, calculate_ratio_posterior,  # noqa: F401
                   expectation_column, jpmatLogBatchBoot, jpmatLogBoot, logBootBatchPosterior, logBootPosterior,
                   marginals, matSlideMult, quick_distribution_summary, ratio_columns, scde_expression_difference,
-                  scde_posteriors)
+                  scde_posteriors, set_rand)
 from .prior import expression_prior  # noqa: F401
 
 __version__ = "0.1.0"

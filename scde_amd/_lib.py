@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libscde_hip.so")
 
 # Symbols declared in include/scde_hip.h (checked by tests/test_abi.py).
 EXPORTS = [
-    "scde_last_error", "scde_version",
+    "scde_last_error", "scde_version", "scde_set_rand_kind", "scde_get_rand_kind",
     "scde_logBootPosterior", "scde_logBootBatchPosterior", "scde_jpmatLogBoot", "scde_jpmatLogBatchBoot",
     "scde_matSlideMult", "scde_ratio_summary", "scde_distribution_summary", "scde_bh_cz",
     "scde_ctx_create", "scde_ctx_destroy", "scde_ctx_synchronize", "scde_ctx_set_profiling",
@@ -42,6 +42,7 @@ class DEParams(ctypes.Structure):
         ("gene_offset", ctypes.c_int64),
         ("ngenes_total", ctypes.c_int64),
         ("expectation", ctypes.c_double),
+        ("rand_kind", ctypes.c_int),
     ]
 
 
@@ -64,6 +65,8 @@ def lib():
     P, i, i64, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
     L.scde_last_error.restype = ctypes.c_char_p
     L.scde_version.restype = i
+    L.scde_set_rand_kind.argtypes = [i]
+    L.scde_get_rand_kind.restype = i
     L.scde_logBootPosterior.argtypes = [P, i, P, P, P, i, P, i, i, i, i, i, i, i, P, P, P]
     L.scde_logBootBatchPosterior.argtypes = [P, i, P, P, P, i, P, i, P, P, P, i, i, i, i, i, i, P, P, P]
     L.scde_jpmatLogBoot.argtypes = [P, i, i, i, i, i, P]

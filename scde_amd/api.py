@@ -18,6 +18,7 @@ genes x cells integer matrix whose columns are named by cell, ``prior`` has
 from __future__ import annotations
 
 import ctypes
+import math
 
 import numpy as np
 
@@ -138,10 +139,24 @@ def matSlideMult(Mat1, Mat2):
     return out
 
 
+# ================================================================== platform rand()
+RAND_KINDS = {"glibc": 0, "darwin": 2}
+
+
+def set_rand(kind: str):
+    """Select which C-library rand() the bootstrap reproduces: "glibc" (Linux, default) or
+    "darwin" (macOS/BSD Park-Miller; the generator behind the vignette's printed numbers)."""
+    check(lib().scde_set_rand_kind(RAND_KINDS[kind]))
+
+
+def get_rand_kind() -> int:
+    return int(lib().scde_get_rand_kind())
+
+
 # ================================================================== R glue helpers (host)
 def marginals(prior_x):
-    """R/functions.R:575-577: log(pmax(10^x - 1, 0))."""
-    m = 10.0 ** np.asarray(prior_x, np.float64) - 1
+    """R/functions.R:575-577: log(pmax(10^x - 1, 0)); R's `^` is libm pow()."""
+    m = np.array([math.pow(10.0, v) for v in np.asarray(prior_x, np.float64)]) - 1
     m[m < 0] = 0
     with np.errstate(divide="ignore"):
         return np.log(m)
@@ -411,7 +426,7 @@ def scde_expression_difference(models, counts, prior, groups=None, batch=None, n
     dc = DeviceCounts(ctx, mat)
     try:
         params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
-                          int(n_randomizations), int(n_cores), 0, N, float(expectation))
+                          int(n_randomizations), int(n_cores), 0, N, float(expectation), get_rand_kind())
         res = np.zeros((N, 5), order="F")
         jp1 = np.zeros((N, G), order="F") if return_posteriors else None
         jp2 = np.zeros((N, G), order="F") if return_posteriors else None
@@ -467,4 +482,4 @@ def bh_cz(z):
 __all__ = ["scde_posteriors", "scde_expression_difference", "calculate_ratio_posterior", "quick_distribution_summary",
            "logBootPosterior", "logBootBatchPosterior", "jpmatLogBoot", "jpmatLogBatchBoot", "matSlideMult",
            "marginals", "ratio_columns", "expectation_column", "Context", "DeviceCounts", "RatioPosterior",
-           "ScdeError", "bh_cz"]
+           "ScdeError", "bh_cz", "set_rand"]

@@ -51,13 +51,25 @@ int fail(int code, const char* fmt, ...) {
 
 inline long long round_up(long long a, long long b) { return (a + b - 1) / b * b; }
 
-// glibc TYPE_3 rand() (srandom_r / random_r) with private state: the
-// reference seeds the process-global generator with srand(Seed) and draws
-// `rj = rand()/(RAND_MAX/n)` with rejection (src/jpmatLogBoot.cpp:220-221,255-257).
-struct GlibcRand {
+// The C library rand() the reference calls (srand(Seed), then
+// `rj = rand()/(RAND_MAX/n)` with rejection; src/jpmatLogBoot.cpp:220-221,255-257),
+// with private state.  Its output depends on the platform libc:
+//   SCDE_RAND_GLIBC  (0) glibc TYPE_3 additive feedback generator (Linux);
+//   SCDE_RAND_DARWIN (2) Darwin/BSD libc: Park-Miller "minimal standard"
+//                        x = 16807 x mod (2^31-1), srand(s) keeps s, returns x --
+//                        the generator behind the package vignette's printed
+//                        results (vignettes/diffexp.md:113-139).
+int g_rand_kind = 0;
+
+struct PlatformRand {
+  int kind;
   int32_t t[31];
   int f = 3, r = 0;
-  explicit GlibcRand(unsigned int seed) {
+  PlatformRand(unsigned int seed, int k) : kind(k) {
+    if (kind == 2) {
+      t[0] = (int32_t)seed;
+      return;
+    }
     if (seed == 0) seed = 1;
     t[0] = (int32_t)seed;
     int32_t word = (int32_t)seed;
@@ -70,6 +82,13 @@ struct GlibcRand {
     for (int i = 0; i < 310; ++i) next();
   }
   int next() {
+    if (kind == 2) {
+      const long hi = t[0] / 127773, lo = t[0] % 127773;
+      long x = 16807 * lo - 2836 * hi;
+      if (x < 0) x += 0x7fffffff;
+      t[0] = (int32_t)x;
+      return (int)x;
+    }
     const uint32_t v = (uint32_t)t[f] + (uint32_t)t[r];
     t[f] = (int32_t)v;
     if (++f >= 31) f = 0;
@@ -237,6 +256,7 @@ struct PostSpec {
   double* modes = nullptr;  // ngenes x ncells col-major
   double* post = nullptr;   // ncells blocks of ngenes x G col-major
   bool use_baseline = true;
+  int rand_kind = 0;
 };
 
 int upload(scde_ctx* cx, Buf& b, const void* src, size_t bytes) {
@@ -303,7 +323,7 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
   draws.assign((size_t)nsets * B * std::max(ndraw, 1), 0);
   W.assign((size_t)nsets * C * Bp, 0.0);
   for (int set = 0; set < nsets; ++set) {
-    GlibcRand rng((unsigned int)s.seeds[set]);
+    PlatformRand rng((unsigned int)s.seeds[set], s.rand_kind);
     int* dr = draws.data() + (size_t)set * B * std::max(ndraw, 1);
     double* w = W.data() + (size_t)set * C * Bp;
     for (int b = 0; b < B; ++b) {
@@ -340,6 +360,15 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
   if (s.nboot < 0) return fail(SCDE_EARG, "nboot must be >= 0");
   if (G > 4096) return fail(SCDE_EARG, "ngrid > 4096 unsupported");
   if (s.seeds.empty()) return fail(SCDE_EINTERNAL, "no seed sets");
+  if (s.batch_call) {
+    for (int k = 0; k < s.nbatch; ++k) {
+      if (s.comp[k] < 0) return fail(SCDE_EARG, "negative composition");
+      if (s.comp[k] > 0 && s.batch_off[k + 1] - s.batch_off[k] <= 0)
+        return fail(SCDE_EARG, "batch %d has draws but no cells", k);
+      for (int64_t i = s.batch_off[k]; i < s.batch_off[k + 1]; ++i)
+        if (s.batch_vals[i] < 0 || s.batch_vals[i] >= C) return fail(SCDE_EARG, "BatchIL index out of range");
+    }
+  }
   // ---- per-cell grid vectors
   RCHK(upload(cx, cx->models, s.models, sizeof(double) * C * 12));
   RCHK(upload(cx, cx->mag, s.mag, sizeof(double) * G));
@@ -504,6 +533,10 @@ int default_ctx(scde_ctx** out) {
   if (!g_default) {
     int dev = 0;
     if (const char* e = getenv("SCDE_DEVICE")) dev = atoi(e);
+    if (const char* r = getenv("SCDE_RAND")) {
+      if (!strcmp(r, "darwin")) g_rand_kind = SCDE_RAND_DARWIN;
+      if (!strcmp(r, "glibc")) g_rand_kind = SCDE_RAND_GLIBC;
+    }
     scde_ctx* c = nullptr;
     RCHK(scde_ctx_create(dev, &c));
     g_default = c;
@@ -595,6 +628,13 @@ double qnorm_host(double p, bool lower_tail);
 extern "C" {
 
 const char* scde_last_error(void) { return g_err.c_str(); }
+
+int scde_set_rand_kind(int kind) {
+  if (kind != SCDE_RAND_GLIBC && kind != SCDE_RAND_DARWIN) return fail(SCDE_EARG, "unknown rand kind %d", kind);
+  g_rand_kind = kind;
+  return SCDE_OK;
+}
+int scde_get_rand_kind(void) { return g_rand_kind; }
 int scde_version(void) { return 100; }
 
 int scde_ctx_create(int device, scde_ctx** out) {
@@ -726,6 +766,7 @@ static int logboot_common(bool batch, const double* models, int ncells, const in
   s.uci_host = counti;
   s.ngenes = ngenes;
   s.seeds = {seed};
+  s.rand_kind = g_rand_kind;
   s.batch_vals = batch_vals;
   s.batch_off = batch_off;
   s.comp = composition;
@@ -797,7 +838,7 @@ static int jpmat_common(const double* const* mats, int nmat, const int* type_off
   int ndraw = 0;
   std::vector<int> draws;
   std::vector<double> W((size_t)nmat * Bp, 0.0);
-  GlibcRand rng((unsigned int)seed);
+  PlatformRand rng((unsigned int)seed, g_rand_kind);
   if (!type_off) {
     ndraw = nmat;
     draws.resize((size_t)std::max(nboot, 1) * ndraw);
@@ -1005,6 +1046,7 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
   s.cellidx_host = cellidx;
   s.ngenes = ngenes;
   seeding(n_cores, gene_offset, ngenes_total, ngenes, s.seeds, s.wset);
+  s.rand_kind = g_rand_kind;
   s.batch_vals = batch_vals;
   s.batch_off = batch_off;
   s.comp = composition;
@@ -1077,6 +1119,7 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
     s.ngenes = ngenes;
     s.seeds = seeds;
     s.wset = wset;
+    s.rand_kind = p->rand_kind;
     s.jp = (gi == 0 ? ctx->jpA : ctx->jpB).as<double>();
     s.jp_g = G;  // gene-major rows for the ratio kernel
     s.jp_k = 1;

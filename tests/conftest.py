@@ -1,0 +1,61 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels through the C ABI)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+def golden(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def assert_posterior_close(a, b, rel=1e-6, floor=1e-12, abs_small=1e-18, what=""):
+    """SURVEY.md §8(d) tolerance: |a-b| <= rel*max(|a|,|b|) for entries >= floor*rowmax,
+    absolute abs_small below that (underflow tails).  Rows are the first axis."""
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape, (what, a.shape, b.shape)
+    if a.size == 0:
+        return
+    a2 = a.reshape(a.shape[0], -1)
+    b2 = b.reshape(b.shape[0], -1)
+    rowmax = np.maximum(np.abs(a2).max(1), np.abs(b2).max(1))[:, None]
+    big = np.maximum(np.abs(a2), np.abs(b2)) >= floor * rowmax
+    err = np.abs(a2 - b2)
+    tol = np.where(big, rel * np.maximum(np.abs(a2), np.abs(b2)), abs_small)
+    bad = ~(err <= tol) & ~(np.isnan(a2) & np.isnan(b2)) & ~(a2 == b2)
+    if bad.any():
+        i, j = np.argwhere(bad)[0]
+        raise AssertionError(f"{what}: {bad.sum()} entries out of tolerance; first at {i},{j}: "
+                             f"{a2[i, j]!r} vs {b2[i, j]!r}")
+
+
+def gpu_available():
+    try:
+        import ctypes
+        from scde_amd import _lib
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        rc = L.scde_ctx_create(0, ctypes.byref(h))
+        if rc == 0:
+            L.scde_ctx_destroy(h)
+            return True
+    except Exception:
+        return False
+    return False
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as O
+    O.lib()
+    return O

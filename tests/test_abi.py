@@ -1,0 +1,71 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/scde_hip.h
+declares, fails loudly without a GPU, and its host-only code (BH / cZ) matches the oracle."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, gpu_available
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "scde_hip.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(scde_[a-zA-Z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    from scde_amd import _lib
+    L = _lib.lib()
+    names = header_functions()
+    assert len(names) >= 20
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(_lib.EXPORTS)
+    assert L.scde_version() >= 100
+
+
+@pytest.mark.skipif(gpu_available(), reason="checks the no-GPU error path")
+def test_no_gpu_fails_loudly():
+    from scde_amd import _lib, api
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    assert L.scde_ctx_create(0, ctypes.byref(h)) == 2
+    assert b"device" in L.scde_last_error().lower()
+    with pytest.raises(_lib.ScdeError):
+        api.matSlideMult(np.ones((2, 3)), np.ones((2, 3)))
+
+
+def test_bh_cz_matches_oracle(oracle):
+    from scde_amd import api
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 7, 1000):
+        z = rng.normal(0, 3, n)
+        z[: n // 10] = 7.16  # ties at the cap, as in real runs
+        if n > 3:
+            z[3] = 0.0
+        cz_o = np.zeros(n)
+        zz = np.ascontiguousarray(z)
+        oracle.lib().o_bh_cz(zz.ctypes.data_as(ctypes.c_void_p), n, cz_o.ctypes.data_as(ctypes.c_void_p))
+        np.testing.assert_array_equal(api.bh_cz(z), cz_o)
+
+
+def test_rand_kind_switch():
+    from scde_amd import api
+    assert api.get_rand_kind() == 0
+    api.set_rand("darwin")
+    assert api.get_rand_kind() == 2
+    api.set_rand("glibc")
+    assert api.get_rand_kind() == 0
+
+
+def test_host_glue_matches_oracle(oracle):
+    from scde_amd import api
+    from conftest import golden
+    g = golden("esmef500.npz")
+    np.testing.assert_array_equal(api.ratio_columns(g["prior_x"]), oracle.ratio_grid(g["prior_x"]))
+    np.testing.assert_array_equal(api.marginals(g["prior_x"]), oracle.marginals_from_prior_x(g["prior_x"]))
+    dv = api.ratio_columns(g["prior_x"])
+    assert api.expectation_column(dv, 0) == 400

@@ -1,0 +1,305 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference's published known answers.  Tolerance: posteriors
+|a-b| <= 1e-6 max(|a|,|b|) above 1e-12 of the row max, 1e-18 absolute below;
+grid-valued outputs (lb/mle/ub/ce, modes) exact; matSlideMult bit-exact."""
+import numpy as np
+import pytest
+
+from conftest import assert_posterior_close, golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def api():
+    from scde_amd import api as A
+    A.set_rand("glibc")
+    return A
+
+
+def _models(g, key="models"):
+    from oracle.oracle import MODEL_COLUMNS
+    m = g[key]
+    return {c: m[:, j] for j, c in enumerate(MODEL_COLUMNS) if not np.all(np.isnan(m[:, j]))}
+
+
+def _group_inputs(oracle, g, genes, cells):
+    models = _models(g)
+    sub = {k: v[cells] for k, v in models.items()}
+    mm, lt, sq = oracle.model_matrix(sub)
+    ucl, uci = oracle.ucl_uci(g["counts"][genes][:, cells])
+    mag = oracle.marginals_from_prior_x(g["prior_x"])
+    return mm, lt, sq, ucl, uci, mag
+
+
+# ------------------------------------------------------------------ .Call layer
+@pytest.mark.parametrize("nboot,seed,postflag,ensemble", [
+    (50, 1, 0, 0), (17, 1379, 1, 0), (0, 1, 2, 0), (20, 5, 3, 0), (10, 1, 0, 1), (1, 7, 0, 0), (100, 2, 0, 0)])
+def test_logBootPosterior_esmef(api, oracle, nboot, seed, postflag, ensemble):
+    g = golden("esmef500.npz")
+    genes = np.arange(0, 500, 3)
+    cells = np.nonzero(g["groups"] == 0)[0]
+    mm, lt, sq, ucl, uci, mag = _group_inputs(oracle, g, genes, cells)
+    ref = oracle.logBootPosterior(mm, ucl, uci, mag, nboot, seed, postflag, lt, sq, ensemble)
+    got = api.logBootPosterior(mm, ucl, uci, mag, nboot, seed, postflag, lt, sq, ensemble)
+    if postflag == 0:
+        assert_posterior_close(got, ref, what="jp")
+        return
+    assert_posterior_close(got["jp"], ref["jp"], what="jp")
+    if "modes" in ref:
+        np.testing.assert_array_equal(got["modes"], ref["modes"])
+    if "post" in ref:
+        for i, (a, b) in enumerate(zip(got["post"], ref["post"])):
+            np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-13, err_msg=f"post cell {i}")
+
+
+def test_logBootPosterior_knn_localtheta(api, oracle):
+    """12-column models: local theta fit + squared-logit concomitant."""
+    g = golden("knn300.npz")
+    models = _models(g)
+    mm, lt, sq = oracle.model_matrix(models)
+    assert lt == 1 and sq == 1
+    ucl, uci = oracle.ucl_uci(g["counts"])
+    mag = oracle.marginals_from_prior_x(g["prior_x"])
+    got = api.logBootPosterior(mm, ucl, uci, mag, int(g["nboot"]), 1, 1, lt, sq, 0)
+    assert_posterior_close(got["jp"], g["jp"], what="knn jp vs golden")
+    np.testing.assert_array_equal(got["modes"], g["modes"])
+    ref = oracle.logBootPosterior(mm, ucl, uci, mag, 7, 11, 3, lt, sq, 0)
+    got = api.logBootPosterior(mm, ucl, uci, mag, 7, 11, 3, lt, sq, 0)
+    assert_posterior_close(got["jp"], ref["jp"], what="knn jp")
+    for a, b in zip(got["post"][:8], ref["post"][:8]):
+        np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("postflag", [0, 1, 2, 3])
+def test_logBootBatchPosterior(api, oracle, postflag):
+    g = golden("esmef500.npz")
+    genes = np.arange(0, 500, 4)
+    cells = np.arange(40)
+    mm, lt, sq, ucl, uci, mag = _group_inputs(oracle, g, genes, cells)
+    batch = (np.arange(40) * 7) % 3
+    batchil = [np.nonzero(batch == b)[0].astype(np.int32) for b in range(3)]
+    comp = [5, 0, 9]
+    ref = oracle.logBootBatchPosterior(mm, ucl, uci, mag, batchil, comp, 12, 3, postflag, lt, sq)
+    got = api.logBootBatchPosterior(mm, ucl, uci, mag, batchil, comp, 12, 3, postflag, lt, sq)
+    if isinstance(ref, dict):
+        assert_posterior_close(got["jp"], ref["jp"], what="batch jp")
+        if "modes" in ref:
+            np.testing.assert_array_equal(got["modes"], ref["modes"])
+        if "post" in ref:
+            for a, b in zip(got["post"], ref["post"]):
+                np.testing.assert_allclose(a, b, rtol=1e-11, atol=1e-13)
+    else:
+        assert_posterior_close(got, ref, what="batch jp")
+
+
+def test_jpmat(api, oracle):
+    rng = np.random.default_rng(5)
+    mats = [np.asfortranarray(-rng.gamma(2.0, 30.0, (37, 53))) for _ in range(9)]
+    ref = oracle.jpmatLogBoot(mats, 13, 4)
+    got = api.jpmatLogBoot(mats, 13, 4)
+    assert_posterior_close(got, ref, what="jpmatLogBoot")
+    matll = [mats[:4], mats[4:]]
+    ref = oracle.jpmatLogBatchBoot(matll, [3, 2], 6, 9)
+    got = api.jpmatLogBatchBoot(matll, [3, 2], 6, 9)
+    assert_posterior_close(got, ref, what="jpmatLogBatchBoot")
+
+
+def test_jpmat_degenerate_rows_exact(api, oracle):
+    """Rows whose sums are dominated by huge magnitudes go through the reference-order
+    fallback and must match the oracle bit for bit."""
+    n, G = 6, 40
+    mats = []
+    for m in range(5):
+        a = np.full((n, G), -3.0)
+        a[:, m % 2::2] = -1e300 * (1 + 0.01 * m)
+        a[:, 7] = -1.5
+        mats.append(np.asfortranarray(a + np.arange(G)[None, :] * 1e-3))
+    ref = oracle.jpmatLogBoot(mats, 8, 2)
+    got = api.jpmatLogBoot(mats, 8, 2)
+    np.testing.assert_array_equal(got, ref)
+
+
+def test_logboot_degenerate_exact(api, oracle):
+    """Every grid point clamped in some drawn cell: the fallback reproduces the reference's
+    rounding-determined result exactly."""
+    g = golden("esmef500.npz")
+    mag = oracle.marginals_from_prior_x(g["prior_x"])
+    mm = np.full((2, 12), np.nan, order="F")
+    mm[0, :6] = [-10.0, 500.0, np.log(0.1), 0.7, 2.0, 1000.0]
+    mm[1, :6] = [-1.4, 0.56, np.log(0.1), 0.7, 0.65, 0.77]
+    counts = np.array([[0, 100000], [0, 0], [3, 5]], np.int32)
+    ucl, uci = oracle.ucl_uci(counts)
+    for nboot, seed in ((10, 1), (33, 2)):
+        ref = oracle.logBootPosterior(mm, ucl, uci, mag, nboot, seed, 0)
+        got = api.logBootPosterior(mm, ucl, uci, mag, nboot, seed, 0)
+        np.testing.assert_allclose(got[0], ref[0], rtol=1e-13, atol=0)
+        assert_posterior_close(got, ref, what="degenerate jp")
+
+
+def test_matSlideMult_bit_exact(api, oracle):
+    rng = np.random.default_rng(11)
+    for nr, n in ((17, 401), (5, 801), (3, 1), (1, 2), (64, 33)):
+        a = np.asfortranarray(rng.random((nr, n)))
+        b = np.asfortranarray(rng.random((nr, n)) ** 3)
+        np.testing.assert_array_equal(api.matSlideMult(a, b), oracle.matSlideMult(a, b))
+
+
+def test_ratio_and_summary(api, oracle):
+    g = golden("esmef500.npz")
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    rp = api.calculate_ratio_posterior(g["jp1"], g["jp2"], prior)
+    ref = oracle.calculate_ratio_posterior(g["jp1"], g["jp2"], g["prior_y"])
+    assert_posterior_close(rp.values, ref, rel=1e-12, what="ratio")
+    np.testing.assert_allclose(rp.values, g["ratio"], rtol=1e-12, atol=1e-300)
+    s = api.quick_distribution_summary(rp)
+    for k in ("lb", "mle", "ub", "ce"):
+        np.testing.assert_array_equal(s[k].to_numpy(), g[k], err_msg=k)
+    np.testing.assert_allclose(s["Z"].to_numpy(), g["Z"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(s["cZ"].to_numpy(), g["cZ"], rtol=1e-9, atol=1e-9)
+
+
+# ------------------------------------------------------------------ R-level API
+def _frame_inputs(g):
+    import pandas as pd
+    models = pd.DataFrame(_models(g), index=list(g["cells"]))
+    counts = pd.DataFrame(g["counts"], index=list(g["genes"]), columns=list(g["cells"]))
+    groups = pd.Series(pd.Categorical(np.where(g["groups"] == 0, "ESC", "MEF"), categories=["ESC", "MEF"]),
+                       index=list(g["cells"]))
+    return models, counts, groups
+
+
+def test_expression_difference_golden(api):
+    g = golden("esmef500.npz")
+    models, counts, groups = _frame_inputs(g)
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    out = api.scde_expression_difference(models, counts, prior, groups=groups, n_randomizations=int(g["nboot"]),
+                                         n_cores=1, return_posteriors=True)
+    assert_posterior_close(out["joint.posteriors"][0], g["jp1"], what="jp1")
+    assert_posterior_close(out["joint.posteriors"][1], g["jp2"], what="jp2")
+    assert_posterior_close(out["difference.posterior"].values, g["ratio"], what="ratio")
+    res = out["results"]
+    for k in ("lb", "mle", "ub", "ce"):
+        np.testing.assert_array_equal(res[k].to_numpy(), g[k], err_msg=k)
+    np.testing.assert_allclose(res["Z"].to_numpy(), g["Z"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(res["cZ"].to_numpy(), g["cZ"], rtol=1e-6, atol=1e-6)
+
+
+def test_vignette_table_on_gpu(api):
+    """The published table (vignettes/diffexp.md:113-119) reproduced on the GPU, all 12,142 genes."""
+    from test_oracle import VIGNETTE_TOP6
+    v = golden("esmef_vignette_inputs.npz")
+    models, counts, groups = _frame_inputs(v)
+    prior = {"x": v["prior_x"], "y": v["prior_y"]}
+    api.set_rand("darwin")
+    try:
+        res = api.scde_expression_difference(models, counts, prior, groups=groups, n_randomizations=100, n_cores=1)
+    finally:
+        api.set_rand("glibc")
+    top = res.sort_values("Z", ascending=False, kind="stable").head(6)
+    assert list(top.index) == list(VIGNETTE_TOP6)
+    for name, ref in VIGNETTE_TOP6.items():
+        got = res.loc[name, ["lb", "mle", "ub", "ce", "Z", "cZ"]].to_numpy(dtype=float)
+        np.testing.assert_allclose(got, ref, atol=5e-7, rtol=0, err_msg=name)
+    gd = golden("esmef_vignette_darwin.npz")
+    for k in ("lb", "mle", "ub", "ce"):
+        assert np.mean(res[k].to_numpy() == gd[k]) > 0.999, k
+    np.testing.assert_allclose(res["Z"].to_numpy(), gd["Z"], rtol=1e-5, atol=1e-5)
+
+
+def test_vignette_glibc_all_genes(api):
+    v = golden("esmef_vignette_inputs.npz")
+    gd = golden("esmef_vignette_glibc.npz")
+    models, counts, groups = _frame_inputs(v)
+    res = api.scde_expression_difference(models, counts, {"x": v["prior_x"], "y": v["prior_y"]}, groups=groups,
+                                         n_randomizations=100, n_cores=1)
+    for k in ("lb", "mle", "ub", "ce"):
+        assert np.mean(res[k].to_numpy() == gd[k]) > 0.999, k
+    np.testing.assert_allclose(res["Z"].to_numpy(), gd["Z"], rtol=1e-5, atol=1e-5)
+
+
+def test_n_cores_chunk_seeds(api, oracle):
+    """n.cores > 1 changes the per-chunk seeds (R/functions.R:606-617) exactly as in R."""
+    g = golden("esmef500.npz")
+    models = _models(g)
+    cells = np.nonzero(g["groups"] == 1)[0]
+    sub = {k: v[cells] for k, v in models.items()}
+    counts = g["counts"][:300][:, cells]
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    for nc in (1, 10, 7):
+        ref = oracle.scde_posteriors(sub, counts, g["prior_x"], n_randomizations=15, n_cores=nc)
+        got = api.scde_posteriors(sub, counts, prior, n_randomizations=15, n_cores=nc)
+        assert_posterior_close(got, ref, what=f"n_cores={nc}")
+
+
+def test_posteriors_modes_and_post(api, oracle):
+    g = golden("knn300.npz")
+    models = _models(g)
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    counts = g["counts"][:80]
+    ref = oracle.scde_posteriors(models, counts, g["prior_x"], n_randomizations=9, return_individual_posteriors=True,
+                                 return_individual_posterior_modes=True, n_cores=1)
+    got = api.scde_posteriors(models, counts, prior, n_randomizations=9, return_individual_posteriors=True,
+                              return_individual_posterior_modes=True, n_cores=1)
+    assert_posterior_close(got["jp"], ref["jp"], what="jp")
+    np.testing.assert_array_equal(got["modes"], ref["modes"])
+    for a, b in zip(got["post"], ref["post"]):
+        np.testing.assert_allclose(a, b, rtol=1e-10, atol=1e-12)
+
+
+def test_edge_cases(api, oracle):
+    g = golden("esmef500.npz")
+    models = _models(g)
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    cells = np.arange(6)
+    sub = {k: v[cells] for k, v in models.items()}
+    cases = {
+        "single gene": g["counts"][[17]][:, cells],
+        "all zero": np.zeros((3, 6), np.int32),
+        "no zeros anywhere": g["counts"][:20][:, cells] + 1,
+        "huge counts": np.array([[0, 1, 2, 100000, 2000000, 7]] * 2, np.int32),
+    }
+    for name, c in cases.items():
+        c = np.ascontiguousarray(c, np.int32)
+        ref = oracle.scde_posteriors(sub, c, g["prior_x"], n_randomizations=11, n_cores=1)
+        got = api.scde_posteriors(sub, c, prior, n_randomizations=11, n_cores=1)
+        assert_posterior_close(got, ref, what=name)
+    one = {k: v[[3]] for k, v in models.items()}
+    ref = oracle.scde_posteriors(one, g["counts"][:30][:, [3]], g["prior_x"], n_randomizations=5, n_cores=1)
+    got = api.scde_posteriors(one, g["counts"][:30][:, [3]], prior, n_randomizations=5, n_cores=1)
+    assert_posterior_close(got, ref, what="single cell")
+
+
+def test_negative_counts_rejected(api):
+    g = golden("esmef500.npz")
+    models = {k: v[:4] for k, v in _models(g).items()}
+    with pytest.raises(Exception):
+        api.scde_posteriors(models, -np.ones((3, 4), np.int32), {"x": g["prior_x"], "y": g["prior_y"]}, n_cores=1)
+
+
+def test_batch_corrected_difference(api, oracle):
+    """Batch branch (R/functions.R:321-399) against the oracle's .Call restatements."""
+    g = golden("esmef500.npz")
+    models, counts, groups = _frame_inputs(g)
+    counts = counts.iloc[:120]
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    batch = np.array(["b1" if (i * 5) % 3 else "b2" for i in range(40)])
+    out = api.scde_expression_difference(models, counts, prior, groups=groups, batch=batch, n_randomizations=10,
+                                         n_cores=1, return_posteriors=True)
+    # recompute the batch posteriors with the oracle
+    md = _models(g)
+    cnt = g["counts"][:120]
+    codes = g["groups"]
+    bjp = []
+    for lv in (0, 1):
+        ii = np.nonzero(codes == lv)[0]
+        comp = [int(np.sum(batch[ii] == b)) for b in ("b1", "b2")]
+        bjp.append(oracle.scde_posteriors(md, cnt, g["prior_x"], n_randomizations=10, batch=list(batch),
+                                          composition=comp, n_cores=1))
+    bratio = oracle.calculate_ratio_posterior(bjp[0], bjp[1], g["prior_y"])
+    ratio = out["difference.posterior"].values
+    a_ref = oracle.calculate_ratio_posterior(ratio, bratio, None)
+    assert_posterior_close(out["batch.adjusted.difference.posterior"].values, a_ref, rel=1e-5, what="batch-adjusted")
+    s_ref = oracle.quick_distribution_summary(a_ref, oracle.ratio_grid(oracle.ratio_grid(g["prior_x"])))
+    for k in ("lb", "mle", "ub"):
+        assert np.mean(out["batch.adjusted"][k].to_numpy() == s_ref[k]) > 0.98, k
