@@ -354,7 +354,7 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
 
 int run_posterior(scde_ctx* cx, const PostSpec& s) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
-  const int GS = (int)round_up(G, 16);
+  const int GS = (int)round_up(G, 64);  // >= the k_boot2 block, so its lanes never read past a column
   hipStream_t st = cx->stream;
   if (C <= 0 || G <= 0) return fail(SCDE_EARG, "ncells and ngrid must be positive");
   if (s.nboot < 0) return fail(SCDE_EARG, "nboot must be >= 0");
@@ -443,7 +443,9 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     // logBootBatchPosterior with Nboot = 0 returns zeros (src/jpmatLogBoot.cpp:469-497)
     HCHK(hipMemsetAsync(s.jp, 0, sizeof(double) * (size_t)N * G, st));
   } else {
-    const int Bp = (int)round_up(s.nboot, 16);
+    const bool fast = ((G + 63) / 64) * 64 <= 1024;
+    const int nb = fast ? boot2_nb(s.nboot) : 16;
+    const int Bp = (int)round_up(s.nboot, nb);
     const int nsets = (int)s.seeds.size();
     std::vector<int> draws;
     std::vector<double> W;
@@ -454,11 +456,15 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     HCHK(cx->base_col.ensure(sizeof(int) * C));
     HCHK(launch_base_cols(cx->ucl.as<int>(), cx->ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
                           s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
-    HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * C)));
+    const int stride = (int)round_up(C, 8);
+    HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * stride)));
     HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
     ev = cx->mark_begin(SLOT_OTHER);
-    HCHK(launch_ell(cx->uci.as<int>(), N, N, C, cx->ucl_off.as<long long>(), cx->base_col.as<int>(),
-                    cx->ent.as<int2>(), cx->nnz.as<int>(), st));
+    HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
+    HCHK(launch_delta(cx->T.as<double>(), cx->ucl_off.as<long long>(), C, ncols, cx->base_col.as<int>(), G, GS,
+                      cx->E.as<double>(), st));
+    HCHK(launch_ell(cx->uci.as<int>(), N, N, C, cx->ucl_off.as<long long>(), cx->base_col.as<int>(), stride,
+                    (int)ncols, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
     HCHK(launch_baseline_z(cx->T.as<double>(), G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
                            cx->Z.as<double>(), st));
@@ -469,29 +475,57 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     }
     HCHK(cx->degen.ensure(sizeof(int) * std::max(1, N)));
     HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, N), st));
-    BootArgs ba{};
-    ba.T = cx->T.as<double>();
-    ba.G = G;
-    ba.GS = GS;
-    ba.ent = cx->ent.as<int2>();
-    ba.nnz = cx->nnz.as<int>();
-    ba.ent_stride = C;
-    ba.base_col = cx->base_col.as<int>();
-    ba.Wt = cx->Wt.as<double>();
-    ba.ncells = C;
-    ba.Bp = Bp;
-    ba.nboot = s.nboot;
-    ba.wset = nsets > 1 ? cx->wset.as<int>() : nullptr;
-    ba.Z = cx->Z.as<double>();
-    ba.norm_mult = (double)s.nboot;
-    ba.degen_thresh = 16777216.0;  // 2^24: beyond this the sums' rounding order matters
-    ba.out = s.jp;
-    ba.out_g = s.jp_g;
-    ba.out_k = s.jp_k;
-    ba.degen = cx->degen.as<int>();
-    ba.ngenes = N;
+    const int* wset_d = nsets > 1 ? cx->wset.as<int>() : nullptr;
+    const double thresh = 16777216.0;  // 2^24: beyond this the sums' rounding order matters
     ev = cx->mark_begin(SLOT_BOOT);
-    HCHK(launch_boot(ba, st));
+    if (fast) {
+      Boot2Args b2{};
+      b2.D = cx->E.as<double>();
+      b2.ent = cx->ent.as<int2>();
+      b2.nnz = cx->nnz.as<int>();
+      b2.ent_stride = stride;
+      b2.Wt = cx->Wt.as<double>();
+      b2.Bp = Bp;
+      b2.ncells = C;
+      b2.wset = wset_d;
+      b2.Z = cx->Z.as<double>();
+      b2.G = G;
+      b2.GS = GS;
+      b2.nboot = s.nboot;
+      b2.nb = nb;
+      b2.zero_col = (int)ncols;
+      b2.norm_mult = (double)s.nboot;
+      b2.degen_thresh = thresh;
+      b2.out = s.jp;
+      b2.out_g = s.jp_g;
+      b2.out_k = s.jp_k;
+      b2.degen = cx->degen.as<int>();
+      b2.ngenes = N;
+      HCHK(launch_boot2(b2, st));
+    } else {
+      BootArgs ba{};
+      ba.T = cx->T.as<double>();
+      ba.G = G;
+      ba.GS = GS;
+      ba.ent = cx->ent.as<int2>();
+      ba.nnz = cx->nnz.as<int>();
+      ba.ent_stride = stride;
+      ba.base_col = cx->base_col.as<int>();
+      ba.Wt = cx->Wt.as<double>();
+      ba.ncells = C;
+      ba.Bp = Bp;
+      ba.nboot = s.nboot;
+      ba.wset = wset_d;
+      ba.Z = cx->Z.as<double>();
+      ba.norm_mult = (double)s.nboot;
+      ba.degen_thresh = thresh;
+      ba.out = s.jp;
+      ba.out_g = s.jp_g;
+      ba.out_k = s.jp_k;
+      ba.degen = cx->degen.as<int>();
+      ba.ngenes = N;
+      HCHK(launch_boot(ba, st));
+    }
     cx->mark_end(SLOT_BOOT, ev);
     ExactArgs xa{};
     xa.T = cx->T.as<double>();
@@ -500,7 +534,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     xa.draws = cx->draws.as<int>();
     xa.ndraw = ndraw;
     xa.nboot = s.nboot;
-    xa.wset = ba.wset;
+    xa.wset = wset_d;
     xa.ucl_off = cx->ucl_off.as<long long>();
     xa.uci = cx->uci.as<int>();
     xa.ld_uci = N;

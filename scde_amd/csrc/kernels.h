@@ -40,6 +40,24 @@ struct BootArgs {
   int ngenes;
 };
 
+struct Boot2Args {
+  const double* D;  // [ncols + 1][GS] baseline-delta columns (k_delta)
+  const int2* ent;  // [ngenes][ent_stride] (cell, column) -- the k_ell list
+  const int* nnz;
+  int ent_stride;
+  const double* Wt;  // [nsets][ncells][Bp], Bp a multiple of nb
+  int Bp, ncells;
+  const int* wset;
+  const double* Z;  // [nsets][Bp][GS]
+  int G, GS, nboot, nb;
+  int zero_col;  // index of an all-zero column of T (pipeline padding / no-baseline entries)
+  double norm_mult, degen_thresh;
+  double* out;
+  long long out_g, out_k;
+  int* degen;
+  int ngenes;
+};
+
 struct ExactArgs {
   const double* T;
   int G, GS;
@@ -93,11 +111,15 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s);
 hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells, const unsigned char* has_clamp,
                             int use_baseline, int* base_col, hipStream_t s);
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
-                      const int* base_col, int2* ent, int* nnz, hipStream_t s);
+                      const int* base_col, int stride, int pad_col, int2* ent, int* nnz, hipStream_t s);
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
                              int Bp, int nsets, double* Z, hipStream_t s);
 hipError_t launch_boot(const BootArgs& a, hipStream_t s);
 hipError_t launch_boot_exact(const ExactArgs& a, hipStream_t s);
+int boot2_nb(int nboot);
+hipError_t launch_boot2(const Boot2Args& a, hipStream_t s);
+hipError_t launch_delta(const double* T, const long long* ucl_off, int ncells, long long ncols, const int* base_col,
+                        int G, int GS, double* D, hipStream_t s);
 hipError_t launch_noboot(const NoBootArgs& a, hipStream_t s);
 hipError_t launch_ensemble_cols(const double* T, long long ncols, int G, int GS, double* E, hipStream_t s);
 hipError_t launch_modes(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,

@@ -197,20 +197,46 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
   base_col[c] = bc;
 }
 
-// Per-gene ELL list of explicit (cell, column) entries, cell order ascending.
+// Per-gene ELL list of explicit (cell, column) entries, cell order ascending; rows
+// have `stride` slots and are padded up to a multiple of 8 with (0, pad_col).
 __global__ void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes, int ncells,
-                      const long long* __restrict__ ucl_off, const int* __restrict__ base_col,
-                      int2* __restrict__ ent, int* __restrict__ nnz) {
+                      const long long* __restrict__ ucl_off, const int* __restrict__ base_col, int stride,
+                      int pad_col, int2* __restrict__ ent, int* __restrict__ nnz) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= ngenes) return;
   int n = 0;
-  int2* E = ent + (long long)g * ncells;
+  int2* E = ent + (long long)g * stride;
   for (int c = 0; c < ncells; ++c) {
     const int col = (int)(ucl_off[c] + uci[(long long)g + ld_uci * c]);
     if (col == base_col[c]) continue;
     E[n++] = make_int2(c, col);
   }
   nnz[g] = n;
+  for (int p = n; p < ((n + 7) & ~7) && p < stride; ++p) E[p] = make_int2(0, pad_col);
+}
+
+// D[col] = T[col] - T[baseline column of its cell] (or T[col] when the cell has no
+// baseline); column ncols is all zeros.  One wavefront per column.
+__global__ __launch_bounds__(256) void k_delta(const double* __restrict__ T, const long long* __restrict__ ucl_off,
+                                              int ncells, long long ncols, const int* __restrict__ base_col, int G,
+                                              int GS, double* __restrict__ D) {
+  const int lane = threadIdx.x & 63;
+  const long long col = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (col > ncols) return;
+  if (col == ncols) {
+    for (int k = lane; k < GS; k += 64) D[col * GS + k] = 0.0;
+    return;
+  }
+  int lo = 0, hi = ncells;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (ucl_off[mid] <= col) lo = mid; else hi = mid;
+  }
+  const int bc = base_col[lo];
+  for (int k = lane; k < GS; k += 64) {
+    const double t = (k < G) ? T[col * GS + k] : 0.0;
+    D[col * GS + k] = (bc >= 0 && k < G) ? t - T[(long long)bc * GS + k] : t;
+  }
 }
 
 // Z[set][b][k] = sum over baseline cells of W[set][c][b] * T[base_col[c]][k]
@@ -266,6 +292,7 @@ template <int BC, bool MAX>
 __device__ __forceinline__ void block_reduce_bc(double (&v)[BC], double* red, double* fin, int lane, int wid,
                                                 int nw) {
   constexpr int L2 = (BC == 16) ? 4 : (BC == 8) ? 3 : (BC == 4) ? 2 : (BC == 2) ? 1 : 0;
+  static_assert(BC == 16 || BC == 8 || BC == 4 || BC == 2 || BC == 1, "BC must be a power of two <= 16");
   const double x = wave_reduce_scatter<BC, MAX>(v, lane);
   const int idx = (lane >> (6 - L2)) & (BC - 1);
   if ((lane & ((64 >> L2) - 1)) == 0) red[wid * 16 + idx] = x;
@@ -388,6 +415,98 @@ __global__ __launch_bounds__(1024) void k_boot(BootArgs a) {
       const int k = tid + j * blockDim.x;
       if (k < a.G) a.out[(long long)g * a.out_g + (long long)k * a.out_k] = jpv[j];
     }
+  }
+}
+
+// ------------------------------------------------------------------ K2 (fast path)
+// Lanes over grid points (k = threadIdx.x, G <= blockDim <= GS), NB bootstrap
+// accumulators per lane held in VGPRs for one pass; per ELL entry the NB draw
+// multiplicities are wave-uniform and come in through scalar loads as the FMA's
+// SGPR operand, the T column is one coalesced 8-byte load per lane, prefetched
+// one entry ahead.  Softmax per boot by butterfly reduce-scatter + LDS.
+template <int BC, int NB>
+__device__ __forceinline__ void softmax_chunk(double (&acc)[NB], int i0, int b0, int nboot, int G,
+                                              double degen_thresh, double norm_mult, int* degen_g, double* red,
+                                              double* fin, double& jpv) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  const bool live = tid < G;
+  double t[BC];
+#pragma unroll
+  for (int i = 0; i < BC; ++i) t[i] = live ? acc[i0 + i] : -INFINITY;
+  block_reduce_bc<BC, true>(t, red, fin, lane, wid, nw);
+#pragma unroll
+  for (int i = 0; i < BC; ++i) {
+    const double d = acc[i0 + i] - fin[i];
+    acc[i0 + i] = (live && d >= -746.0) ? exp(d) : 0.0;
+    t[i] = acc[i0 + i];
+  }
+  if (tid < BC) {
+    const int b = b0 + i0 + tid;
+    if (b < nboot && !(fabs(fin[tid]) <= degen_thresh)) *degen_g = 1;
+  }
+  block_reduce_bc<BC, false>(t, red, fin, lane, wid, nw);
+  if (tid < BC) {
+    const int b = b0 + i0 + tid;
+    fin[16 + tid] = (b < nboot) ? 1.0 / (fin[tid] * norm_mult) : 0.0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < BC; ++i) jpv = fma(acc[i0 + i], fin[16 + i], jpv);
+  __syncthreads();
+}
+
+template <int NB>
+__global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, const int2* __restrict__ ent,
+                                                const int* __restrict__ nnz, int ent_stride,
+                                                const double* __restrict__ Wt, int Bp, int ncells,
+                                                const int* __restrict__ wset, const double* __restrict__ Z, int G,
+                                                int GS, int zc, int nboot, double norm_mult, double degen_thresh,
+                                                double* __restrict__ out, long long out_g, long long out_k,
+                                                int* __restrict__ degen, int ngenes) {
+  __shared__ double red[16 * 16];
+  __shared__ double fin[32];
+  const int tid = threadIdx.x;
+  for (int g = blockIdx.x; g < ngenes; g += gridDim.x) {
+    const int n = nnz[g];
+    const int2* __restrict__ E = ent + (long long)g * ent_stride;
+    const int set = wset ? wset[g] : 0;
+    const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
+    const double* __restrict__ Zs = Z ? Z + (long long)set * Bp * GS : nullptr;
+    double jpv = 0.0;
+    for (int b0 = 0; b0 < nboot; b0 += NB) {
+      double acc[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) acc[i] = Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0;
+      // entries in batches of EB: all EB column loads are issued before the first FMA
+      // that consumes them; the tail of a batch points at the all-zero column zc.
+      constexpr int EB = 8;
+      for (int e0 = 0; e0 < n; e0 += EB) {
+        int cell[EB];
+        double v[EB];
+        // the ELL rows are padded to a multiple of EB with (cell 0, zero column) entries
+        const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
+#pragma unroll
+        for (int j = 0; j < EB / 2; ++j) {
+          const int4 t = E4[j];
+          cell[2 * j] = t.x;
+          cell[2 * j + 1] = t.z;
+          v[2 * j] = D[(long long)t.y * GS + tid];
+          v[2 * j + 1] = D[(long long)t.w * GS + tid];
+        }
+#pragma unroll
+        for (int j = 0; j < EB; ++j) {
+          const double* __restrict__ w = W + (long long)__builtin_amdgcn_readfirstlane(cell[j]) * Bp + b0;
+#pragma unroll
+          for (int i = 0; i < NB; ++i) acc[i] = fma(w[i], v[j], acc[i]);
+        }
+      }
+      int* dg = degen + g;
+      // softmax four boots at a time: bounds the live temporaries of the exp/reduce code
+#pragma unroll
+      for (int i0 = 0; i0 < NB; i0 += 4)
+        softmax_chunk<4, NB>(acc, i0, b0, nboot, G, degen_thresh, norm_mult, dg, red, fin, jpv);
+    }
+    if (tid < G) out[(long long)g * out_g + (long long)tid * out_k] = jpv;
   }
 }
 
@@ -864,10 +983,17 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 }
 
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
-                      const int* base_col, int2* ent, int* nnz, hipStream_t s) {
+                      const int* base_col, int stride, int pad_col, int2* ent, int* nnz, hipStream_t s) {
   if (ngenes <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 128)), dim3(128), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
-                     base_col, ent, nnz);
+                     base_col, stride, pad_col, ent, nnz);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta(const double* T, const long long* ucl_off, int ncells, long long ncols, const int* base_col,
+                        int G, int GS, double* D, hipStream_t s) {
+  hipLaunchKernelGGL(k_delta, dim3(div_up(ncols + 1, 4)), dim3(256), 0, s, T, ucl_off, ncells, ncols, base_col, G,
+                     GS, D);
   return hipGetLastError();
 }
 
@@ -898,6 +1024,41 @@ hipError_t launch_boot(const BootArgs& a, hipStream_t s) {
     case 4: hipLaunchKernelGGL(k_boot<4>, dim3(grid), dim3(block), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+int boot2_nb(int nboot) {
+  // boots per register pass: fewest passes, then least padding
+  static const int cand[] = {20, 32, 16, 24, 28, 12, 8, 4};
+  int best = 0, best_cost = 1 << 30;
+  for (int nb : cand) {
+    const int passes = (nboot + nb - 1) / nb;
+    const int cost = passes * 64 + passes * nb;  // per-pass T re-read + padded FMAs
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = nb;
+    }
+  }
+  return best;
+}
+
+hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
+  if (a.ngenes <= 0) return hipSuccess;
+  const int block = ((a.G + 63) / 64) * 64;
+  if (block > 1024 || block > a.GS) return hipErrorInvalidValue;
+  const int grid = a.ngenes;
+#define SCDE_B2(NBV)                                                                                              \
+  case NBV:                                                                                                        \
+    hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid), dim3(block), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, a.zero_col, a.nboot, a.norm_mult, a.degen_thresh,     \
+                       a.out, a.out_g,                                                                             \
+                       a.out_k, a.degen, a.ngenes);                                                                \
+    break;
+  switch (a.nb) {
+    SCDE_B2(4) SCDE_B2(8) SCDE_B2(12) SCDE_B2(16) SCDE_B2(20) SCDE_B2(24) SCDE_B2(28) SCDE_B2(32)
+    default: return hipErrorInvalidValue;
+  }
+#undef SCDE_B2
   return hipGetLastError();
 }
 
