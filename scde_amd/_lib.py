@@ -9,7 +9,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libscde_hip.so")
+# SCDE_LIB overrides the library path (tuning builds); the default is the in-tree build.
+LIB_PATH = os.environ.get("SCDE_LIB") or os.path.join(_HERE, "libscde_hip.so")
 
 # Symbols declared in include/scde_hip.h (checked by tests/test_abi.py).
 EXPORTS = [

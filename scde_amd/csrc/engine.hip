@@ -154,7 +154,7 @@ struct scde_ctx {
   // workspace
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, ucl, ucl_off, T, E, maxi, has_clamp, base_col, ent, nnz, Wt,
       Z, draws, degen, uci, cellidx, cmax, cmin, woff, bits, rank, nuniq, wset, prior_y, diffv, jpA, jpB, res,
-      ratio, in1, in2, outbuf;
+      ratio, in1, in2, outbuf, part;
   // profiling
   bool profile = false;
   struct Pending {
@@ -208,7 +208,7 @@ struct scde_ctx {
     Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,   &cellscal, &ucl,   &ucl_off, &T,   &E,
                   &maxi,   &has_clamp, &base_col, &ent, &nnz, &Wt, &Z, &draws, &degen, &uci, &cellidx,
                   &cmax,   &cmin, &woff, &bits, &rank, &nuniq, &wset, &prior_y, &diffv, &jpA, &jpB, &res,
-                  &ratio,  &in1, &in2, &outbuf};
+                  &ratio,  &in1, &in2, &outbuf, &part};
     for (Buf* b : all) b->release();
     for (void* p : user_allocs) (void)hipFree(p);
     for (auto& p : pending) {
@@ -354,7 +354,9 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
 
 int run_posterior(scde_ctx* cx, const PostSpec& s) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
-  const int GS = (int)round_up(G, 64);  // >= the k_boot2 block, so its lanes never read past a column
+  // column stride: >= the k_boot2 block (lanes never read past a column); 512 lets
+  // k_boot3 move a column as four whole 1 KB LDS-DMA pieces
+  const int GS = G <= 448 ? 512 : (int)round_up(G, 64);
   hipStream_t st = cx->stream;
   if (C <= 0 || G <= 0) return fail(SCDE_EARG, "ncells and ngrid must be positive");
   if (s.nboot < 0) return fail(SCDE_EARG, "nboot must be >= 0");
@@ -444,7 +446,13 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     HCHK(hipMemsetAsync(s.jp, 0, sizeof(double) * (size_t)N * G, st));
   } else {
     const bool fast = ((G + 63) / 64) * 64 <= 1024;
-    const int nb = fast ? boot2_nb(s.nboot) : 16;
+    int nb = fast ? boot2_nb(s.nboot) : 16;
+    if (fast) {
+      if (const char* ev_nb = getenv("SCDE_BOOT_NB")) {  // tuning override: a multiple of 4 in [4, 32]
+        const int v = atoi(ev_nb);
+        if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
+      }
+    }
     const int Bp = (int)round_up(s.nboot, nb);
     const int nsets = (int)s.seeds.size();
     std::vector<int> draws;
@@ -456,7 +464,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     HCHK(cx->base_col.ensure(sizeof(int) * C));
     HCHK(launch_base_cols(cx->ucl.as<int>(), cx->ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
                           s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
-    const int stride = (int)round_up(C, 8);
+    const int stride = (int)round_up(C, 8) + 8;  // + one look-ahead batch (k_boot2)
     HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * stride)));
     HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
     ev = cx->mark_begin(SLOT_OTHER);
@@ -493,7 +501,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
       b2.GS = GS;
       b2.nboot = s.nboot;
       b2.nb = nb;
-      b2.zero_col = (int)ncols;
+      b2.lds_stage = 0;  // LDS-DMA staging measured slower than k_boot2 at config 2
+      if (const char* ls = getenv("SCDE_LDS_STAGE")) b2.lds_stage = atoi(ls) != 0;
+      const int P = (s.nboot + nb - 1) / nb;
+      b2.part_stride = (long long)N * GS;
+      HCHK(cx->part.ensure(sizeof(double) * std::max<size_t>(1, (size_t)P * N * GS)));
+      b2.part = cx->part.as<double>();
       b2.norm_mult = (double)s.nboot;
       b2.degen_thresh = thresh;
       b2.out = s.jp;

@@ -1,5 +1,9 @@
 // kernels.h -- argument blocks and launchers for kernels.hip (internal).
 #pragma once
+
+#ifndef SCDE_BOOT_DIAG
+#define SCDE_BOOT_DIAG 0  // bit switches that remove parts of k_boot2 for timing studies
+#endif
 #include <hip/hip_runtime.h>
 
 namespace scde {
@@ -50,8 +54,10 @@ struct Boot2Args {
   const int* wset;
   const double* Z;  // [nsets][Bp][GS]
   int G, GS, nboot, nb;
-  int zero_col;  // index of an all-zero column of T (pipeline padding / no-baseline entries)
+  int lds_stage;  // use the LDS-DMA staged kernel (needs GS == 512, G <= 448)
   double norm_mult, degen_thresh;
+  double* part;  // [ceil(nboot/nb)][ngenes][GS] per-slab partial jp rows
+  long long part_stride;
   double* out;
   long long out_g, out_k;
   int* degen;

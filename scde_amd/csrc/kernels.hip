@@ -212,7 +212,8 @@ __global__ void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
     E[n++] = make_int2(c, col);
   }
   nnz[g] = n;
-  for (int p = n; p < ((n + 7) & ~7) && p < stride; ++p) E[p] = make_int2(0, pad_col);
+  // pad to a multiple of 8 plus one more batch of 8 (the k_boot2 look-ahead)
+  for (int p = n; p < ((n + 7) & ~7) + 8 && p < stride; ++p) E[p] = make_int2(0, pad_col);
 }
 
 // D[col] = T[col] - T[baseline column of its cell] (or T[col] when the cell has no
@@ -273,8 +274,12 @@ __device__ __forceinline__ double wave_reduce_scatter(double (&v)[BC], int lane)
     const bool up = (lane & mask) != 0;
 #pragma unroll
     for (int j = 0; j < half; ++j) {
-      const double send = up ? v[j] : v[j + half];
-      const double keep = up ? v[j + half] : v[j];
+      // Both halves are read unconditionally first: a ternary over the array elements
+      // lets the optimizer merge the two reads into one lane-dependent index, which
+      // lowers to a compare/select chain over the whole register array.
+      const double lo = v[j], hi = v[j + half];
+      const double send = up ? lo : hi;
+      const double keep = up ? hi : lo;
       const double r = __shfl_xor(send, mask, 64);
       v[j] = MAX ? gt_max(keep, r) : keep + r;
     }
@@ -419,95 +424,273 @@ __global__ __launch_bounds__(1024) void k_boot(BootArgs a) {
 }
 
 // ------------------------------------------------------------------ K2 (fast path)
-// Lanes over grid points (k = threadIdx.x, G <= blockDim <= GS), NB bootstrap
-// accumulators per lane held in VGPRs for one pass; per ELL entry the NB draw
-// multiplicities are wave-uniform and come in through scalar loads as the FMA's
-// SGPR operand, the T column is one coalesced 8-byte load per lane, prefetched
-// one entry ahead.  Softmax per boot by butterfly reduce-scatter + LDS.
-template <int BC, int NB>
-__device__ __forceinline__ void softmax_chunk(double (&acc)[NB], int i0, int b0, int nboot, int G,
-                                              double degen_thresh, double norm_mult, int* degen_g, double* red,
-                                              double* fin, double& jpv) {
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
-  const bool live = tid < G;
+// Reduce-scatter the per-lane values of segment [I0, I0+BC) across the wave and park
+// the wave's partials in red[wid][I0 + idx] (no barrier here).
+template <int BC, bool MAX, int NB>
+__device__ __forceinline__ void wave_partials(const double (&x)[NB], int I0, bool live, double* red, int lane,
+                                              int wid) {
+  constexpr int L2 = (BC == 16) ? 4 : (BC == 8) ? 3 : (BC == 4) ? 2 : (BC == 2) ? 1 : 0;
   double t[BC];
 #pragma unroll
-  for (int i = 0; i < BC; ++i) t[i] = live ? acc[i0 + i] : -INFINITY;
-  block_reduce_bc<BC, true>(t, red, fin, lane, wid, nw);
+  for (int i = 0; i < BC; ++i) t[i] = live ? x[I0 + i] : (MAX ? -INFINITY : 0.0);
+  const double r = wave_reduce_scatter<BC, MAX>(t, lane);
+  const int idx = (lane >> (6 - L2)) & (BC - 1);
+  if ((lane & ((64 >> L2) - 1)) == 0) red[wid * 32 + I0 + idx] = r;
+}
+
+// All NB boots of a slab at once: one LDS round per reduction.  NB = 16a + 8b + 4c.
+template <bool MAX, int NB>
+__device__ __forceinline__ void block_reduce_all(const double (&x)[NB], bool live, double* red, double* fin,
+                                                 int lane, int wid, int nw) {
 #pragma unroll
-  for (int i = 0; i < BC; ++i) {
-    const double d = acc[i0 + i] - fin[i];
-    acc[i0 + i] = (live && d >= -746.0) ? exp(d) : 0.0;
-    t[i] = acc[i0 + i];
-  }
-  if (tid < BC) {
-    const int b = b0 + i0 + tid;
-    if (b < nboot && !(fabs(fin[tid]) <= degen_thresh)) *degen_g = 1;
-  }
-  block_reduce_bc<BC, false>(t, red, fin, lane, wid, nw);
-  if (tid < BC) {
-    const int b = b0 + i0 + tid;
-    fin[16 + tid] = (b < nboot) ? 1.0 / (fin[tid] * norm_mult) : 0.0;
-  }
+  for (int i0 = 0; i0 + 16 <= NB; i0 += 16) wave_partials<16, MAX, NB>(x, i0, live, red, lane, wid);
+  if constexpr ((NB % 16) >= 8) wave_partials<8, MAX, NB>(x, NB - (NB % 16), live, red, lane, wid);
+  if constexpr ((NB % 8) >= 4) wave_partials<4, MAX, NB>(x, NB - (NB % 8), live, red, lane, wid);
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < BC; ++i) jpv = fma(acc[i0 + i], fin[16 + i], jpv);
+  if ((int)threadIdx.x < NB) {
+    double r = red[threadIdx.x];
+    for (int w = 1; w < nw; ++w) r = MAX ? gt_max(r, red[w * 32 + threadIdx.x]) : r + red[w * 32 + threadIdx.x];
+    fin[threadIdx.x] = r;
+  }
   __syncthreads();
 }
 
+// One block per (gene, boot slab of NB).  Lanes over grid points (k = threadIdx.x,
+// G <= blockDim <= GS); NB bootstrap accumulators per lane in VGPRs.  Per ELL entry
+// the NB draw multiplicities are wave-uniform (scalar loads, the FMA's SGPR operand)
+// and the baseline-delta column is one coalesced 8-byte load per lane.  The P slabs
+// of a gene are placed 8 blocks apart (same XCD under round-robin dispatch) so they
+// share the gene's columns in L2; each writes a partial jp row, summed in slab order
+// by k_sum_partials.
 template <int NB>
 __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, const int2* __restrict__ ent,
                                                 const int* __restrict__ nnz, int ent_stride,
                                                 const double* __restrict__ Wt, int Bp, int ncells,
                                                 const int* __restrict__ wset, const double* __restrict__ Z, int G,
-                                                int GS, int zc, int nboot, double norm_mult, double degen_thresh,
-                                                double* __restrict__ out, long long out_g, long long out_k,
+                                                int GS, int P, int nboot, double norm_mult, double degen_thresh,
+                                                double* __restrict__ part, long long part_stride,
                                                 int* __restrict__ degen, int ngenes) {
-  __shared__ double red[16 * 16];
+  static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
+  constexpr int diag = SCDE_BOOT_DIAG;  // timing-only builds (tools/); 0 in production
+  __shared__ double red[16 * 32];
   __shared__ double fin[32];
-  const int tid = threadIdx.x;
-  for (int g = blockIdx.x; g < ngenes; g += gridDim.x) {
-    const int n = nnz[g];
-    const int2* __restrict__ E = ent + (long long)g * ent_stride;
-    const int set = wset ? wset[g] : 0;
-    const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
-    const double* __restrict__ Zs = Z ? Z + (long long)set * Bp * GS : nullptr;
-    double jpv = 0.0;
-    for (int b0 = 0; b0 < nboot; b0 += NB) {
-      double acc[NB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  const bool live = tid < G;
+  const int within = blockIdx.x % (8 * P);
+  const int p = within >> 3;
+  const int g = (blockIdx.x / (8 * P)) * 8 + (within & 7);
+  if (g >= ngenes) return;
+  const int b0 = p * NB;
+  const int n = nnz[g];
+  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  const int set = wset ? wset[g] : 0;
+  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
+  const double* __restrict__ Zs = Z ? Z + (long long)set * Bp * GS : nullptr;
+  double acc[NB];
 #pragma unroll
-      for (int i = 0; i < NB; ++i) acc[i] = Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0;
-      // entries in batches of EB: all EB column loads are issued before the first FMA
-      // that consumes them; the tail of a batch points at the all-zero column zc.
-      constexpr int EB = 8;
-      for (int e0 = 0; e0 < n; e0 += EB) {
-        int cell[EB];
-        double v[EB];
-        // the ELL rows are padded to a multiple of EB with (cell 0, zero column) entries
-        const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
+  for (int i = 0; i < NB; ++i) acc[i] = Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0;
+  // Entries in batches of EB, double-buffered in registers: batch e+1's column loads are
+  // in flight while batch e accumulates.  ELL rows are padded to a multiple of EB plus
+  // one extra batch of zero-column entries, so the look-ahead load is unconditional.
+  // The multiplicities come in two boots x EB entries per scalar-load round.
+  constexpr int EB = 8;
+  int cell[EB];
+  double v[EB];
+  auto load_batch = [&](int e0, int (&c)[EB], double (&x)[EB]) {
+    const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
 #pragma unroll
-        for (int j = 0; j < EB / 2; ++j) {
-          const int4 t = E4[j];
-          cell[2 * j] = t.x;
-          cell[2 * j + 1] = t.z;
-          v[2 * j] = D[(long long)t.y * GS + tid];
-          v[2 * j + 1] = D[(long long)t.w * GS + tid];
-        }
+    for (int j = 0; j < EB / 2; ++j) {
+      const int4 t = E4[j];
+      c[2 * j] = t.x;
+      c[2 * j + 1] = t.z;
+      if (diag & 2) {  // timing diagnostic: no column loads
+        x[2 * j] = 1e-3 * t.y;
+        x[2 * j + 1] = 1e-3 * t.w;
+      } else {
+        x[2 * j] = D[(long long)t.y * GS + tid];
+        x[2 * j + 1] = D[(long long)t.w * GS + tid];
+      }
+    }
+  };
+  load_batch(0, cell, v);
+  for (int e0 = 0; e0 < n; e0 += EB) {
+    int celln[EB];
+    double vn[EB];
+    load_batch(e0 + EB, celln, vn);
 #pragma unroll
-        for (int j = 0; j < EB; ++j) {
-          const double* __restrict__ w = W + (long long)__builtin_amdgcn_readfirstlane(cell[j]) * Bp + b0;
+    for (int i0 = 0; i0 < NB; i0 += 2) {
+      double2 w[EB];
 #pragma unroll
-          for (int i = 0; i < NB; ++i) acc[i] = fma(w[i], v[j], acc[i]);
+      for (int j = 0; j < EB; ++j) {
+        if (diag & 1) {  // timing diagnostic: no multiplicity loads
+          w[j].x = 1.0 + __builtin_amdgcn_readfirstlane(cell[j]);
+          w[j].y = 2.0 + __builtin_amdgcn_readfirstlane(cell[j]);
+        } else {
+          w[j] = *reinterpret_cast<const double2*>(W + (long long)__builtin_amdgcn_readfirstlane(cell[j]) * Bp +
+                                                   b0 + i0);
         }
       }
-      int* dg = degen + g;
-      // softmax four boots at a time: bounds the live temporaries of the exp/reduce code
 #pragma unroll
-      for (int i0 = 0; i0 < NB; i0 += 4)
-        softmax_chunk<4, NB>(acc, i0, b0, nboot, G, degen_thresh, norm_mult, dg, red, fin, jpv);
+      for (int j = 0; j < EB; ++j) {
+        acc[i0] = fma(w[j].x, v[j], acc[i0]);
+        acc[i0 + 1] = fma(w[j].y, v[j], acc[i0 + 1]);
+      }
     }
-    if (tid < G) out[(long long)g * out_g + (long long)tid * out_k] = jpv;
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      cell[j] = celln[j];
+      v[j] = vn[j];
+    }
   }
+  // ---- per-boot softmax over the grid: max, exp, sum (one LDS round each) ----
+  if (diag & 8) {  // timing diagnostic: no reductions
+    if (tid < NB) fin[tid] = acc[0];
+    __syncthreads();
+  } else {
+    block_reduce_all<true, NB>(acc, live, red, fin, lane, wid, nw);
+  }
+  if (tid < NB && b0 + tid < nboot && !(fabs(fin[tid]) <= degen_thresh)) degen[g] = 1;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const double d = acc[i] - fin[i];
+    // exp(d) underflows to exactly 0 for d < -745.14; skip the call there
+    if (diag & 4)  // timing diagnostic: no exp
+      acc[i] = live ? d : 0.0;
+    else
+      acc[i] = (live && d >= -746.0) ? exp(d) : 0.0;
+    if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+  if (diag & 8) {
+    if (tid < NB) fin[tid] = acc[1];
+    __syncthreads();
+  } else {
+    block_reduce_all<false, NB>(acc, live, red, fin, lane, wid, nw);
+  }
+  if (tid < NB) fin[tid] = (b0 + tid < nboot) ? 1.0 / (fin[tid] * norm_mult) : 0.0;
+  __syncthreads();
+  double jpv = 0.0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) jpv = fma(acc[i], fin[i], jpv);
+  if (live) part[(long long)p * part_stride + (long long)g * GS + tid] = jpv;
+}
+
+// ---- K2 with LDS-DMA staging (k_boot3) ----
+// Same slab decomposition as k_boot2, for G <= 448 with GS == 512: the block is 8
+// waves (512 lanes; lanes >= G only stage).  An 8-entry batch of baseline-delta
+// columns (8 x 4 KB) is moved HBM/L2 -> LDS by global_load_lds_dwordx4: each wave
+// issues exactly 4 lane-linear 1 KB pieces per batch, so a counted vmcnt(4) retires
+// the previous batch while the next one stays in flight across the raw s_barrier.
+template <int NB>
+__global__ __launch_bounds__(512, 2) void k_boot3(const double* __restrict__ D, const int2* __restrict__ ent,
+                                                  const int* __restrict__ nnz, int ent_stride,
+                                                  const double* __restrict__ Wt, int Bp, int ncells,
+                                                  const int* __restrict__ wset, const double* __restrict__ Z, int G,
+                                                  int P, int nboot, double norm_mult, double degen_thresh,
+                                                  double* __restrict__ part, long long part_stride,
+                                                  int* __restrict__ degen, int ngenes) {
+  static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
+  constexpr int GS = 512, EB = 8;
+  __shared__ __attribute__((aligned(16))) double stage[2][EB][GS];
+  __shared__ double red[16 * 32];
+  __shared__ double fin[32];
+  const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar entry loads)
+  const bool live = tid < G;
+  const int within = blockIdx.x % (8 * P);
+  const int p = within >> 3;
+  const int g = (blockIdx.x / (8 * P)) * 8 + (within & 7);
+  if (g >= ngenes) return;  // uniform over the block
+  const int b0 = p * NB;
+  const int n = nnz[g];
+  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  const int set = wset ? wset[g] : 0;
+  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
+  const double* __restrict__ Zs = Z ? Z + (long long)set * Bp * GS : nullptr;
+  // wave w stages column (w >> 2) * 2 + {0,1}... simpler: piece q = w*4 + i covers
+  // column q >> 2, quarter q & 3 (EB * 4 = 32 pieces, 8 waves x 4)
+  // The DMA is issued from inline asm so the compiler's waitcnt pass does not see it
+  // (it would drain it with vmcnt(0) before every LDS read); this kernel counts it:
+  // every wave has exactly 4 pieces in flight per batch.
+  auto issue = [&](int e0, int buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = wid * 4 + i;
+      const int j = q >> 2, quarter = q & 3;
+      const int col = __builtin_amdgcn_readfirstlane(E[e0 + j].y);
+      const double* src = D + (long long)col * GS + quarter * 128 + lane * 2;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(
+          (unsigned)(unsigned long long)(const void*)&stage[buf][j][quarter * 128]);
+      unsigned keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(src), "s"(dst)
+          : "memory");
+    }
+  };
+  double acc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) acc[i] = Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));  // materialise now: no compiler vmcnt in the loop
+  issue(0, 0);
+  int buf = 0;
+  for (int e0 = 0; e0 < n; e0 += EB) {
+    issue(e0 + EB, buf ^ 1);  // ELL rows carry one extra zero-column batch
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    int cell[EB];
+    double v[EB];
+#pragma unroll
+    for (int j = 0; j < EB; ++j) {
+      cell[j] = E[e0 + j].x;
+      v[j] = stage[buf][j][tid];
+    }
+#pragma unroll
+    for (int i0 = 0; i0 < NB; i0 += 2) {
+      double2 w[EB];
+#pragma unroll
+      for (int j = 0; j < EB; ++j)
+        w[j] = *reinterpret_cast<const double2*>(W + (long long)__builtin_amdgcn_readfirstlane(cell[j]) * Bp + b0 +
+                                                 i0);
+#pragma unroll
+      for (int j = 0; j < EB; ++j) {
+        acc[i0] = fma(w[j].x, v[j], acc[i0]);
+        acc[i0 + 1] = fma(w[j].y, v[j], acc[i0 + 1]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone has read `buf` before it is refilled
+    buf ^= 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // ---- per-boot softmax over the grid: max, exp, sum (one LDS round each) ----
+  block_reduce_all<true, NB>(acc, live, red, fin, lane, wid, nw);
+  if (tid < NB && b0 + tid < nboot && !(fabs(fin[tid]) <= degen_thresh)) degen[g] = 1;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const double d = acc[i] - fin[i];
+    acc[i] = (live && d >= -746.0) ? exp(d) : 0.0;
+    if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+  }
+  block_reduce_all<false, NB>(acc, live, red, fin, lane, wid, nw);
+  if (tid < NB) fin[tid] = (b0 + tid < nboot) ? 1.0 / (fin[tid] * norm_mult) : 0.0;
+  __syncthreads();
+  double jpv = 0.0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) jpv = fma(acc[i], fin[i], jpv);
+  if (live) part[(long long)p * part_stride + (long long)g * GS + tid] = jpv;
+}
+
+// jp[g, k] = sum over slabs p (in order) of part[p][g][k]
+__global__ void k_sum_partials(const double* __restrict__ part, long long part_stride, int P, int ngenes, int G,
+                               int GS, double* __restrict__ out, long long out_g, long long out_k) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)ngenes * G) return;
+  const int g = (int)(i / G), k = (int)(i % G);
+  double s = part[(long long)g * GS + k];
+  for (int p = 1; p < P; ++p) s += part[(long long)p * part_stride + (long long)g * GS + k];
+  out[(long long)g * out_g + (long long)k * out_k] = s;
 }
 
 // ------------------------------------------------------------------ block reductions (simple)
@@ -1028,14 +1211,14 @@ hipError_t launch_boot(const BootArgs& a, hipStream_t s) {
 }
 
 int boot2_nb(int nboot) {
-  // boots per register pass: fewest passes, then least padding
-  static const int cand[] = {20, 32, 16, 24, 28, 12, 8, 4};
-  int best = 0, best_cost = 1 << 30;
+  // boots per block slab (a multiple of 4 that fits 4 waves/SIMD without spills):
+  // fewest padded boots, then the larger slab
+  static const int cand[] = {20, 16, 12, 8, 4};
+  int best = 4, best_pad = 1 << 30;
   for (int nb : cand) {
-    const int passes = (nboot + nb - 1) / nb;
-    const int cost = passes * 64 + passes * nb;  // per-pass T re-read + padded FMAs
-    if (cost < best_cost) {
-      best_cost = cost;
+    const int pad = (nboot + nb - 1) / nb * nb - nboot;
+    if (pad < best_pad) {
+      best_pad = pad;
       best = nb;
     }
   }
@@ -1046,19 +1229,38 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const int block = ((a.G + 63) / 64) * 64;
   if (block > 1024 || block > a.GS) return hipErrorInvalidValue;
-  const int grid = a.ngenes;
+  const int P = (a.nboot + a.nb - 1) / a.nb;
+  const int grid = (a.ngenes + 7) / 8 * 8 * P;
 #define SCDE_B2(NBV)                                                                                              \
   case NBV:                                                                                                        \
     hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid), dim3(block), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
-                       a.ncells, a.wset, a.Z, a.G, a.GS, a.zero_col, a.nboot, a.norm_mult, a.degen_thresh,     \
-                       a.out, a.out_g,                                                                             \
-                       a.out_k, a.degen, a.ngenes);                                                                \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
+                       a.part_stride, a.degen, a.ngenes);                                                         \
     break;
-  switch (a.nb) {
-    SCDE_B2(4) SCDE_B2(8) SCDE_B2(12) SCDE_B2(16) SCDE_B2(20) SCDE_B2(24) SCDE_B2(28) SCDE_B2(32)
-    default: return hipErrorInvalidValue;
+#define SCDE_B3(NBV)                                                                                              \
+  case NBV:                                                                                                        \
+    hipLaunchKernelGGL(k_boot3<NBV>, dim3(grid), dim3(512), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,   \
+                       a.ncells, a.wset, a.Z, a.G, P, a.nboot, a.norm_mult, a.degen_thresh, a.part, a.part_stride, \
+                       a.degen, a.ngenes);                                                                         \
+    break;
+  if (a.GS == 512 && a.G <= 448 && a.lds_stage) {
+    switch (a.nb) {
+      SCDE_B3(4) SCDE_B3(8) SCDE_B3(12) SCDE_B3(16) SCDE_B3(20) SCDE_B3(24) SCDE_B3(28) SCDE_B3(32)
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (a.nb) {
+      SCDE_B2(4) SCDE_B2(8) SCDE_B2(12) SCDE_B2(16) SCDE_B2(20) SCDE_B2(24) SCDE_B2(28) SCDE_B2(32)
+      default: return hipErrorInvalidValue;
+    }
   }
 #undef SCDE_B2
+#undef SCDE_B3
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const long long n = (long long)a.ngenes * a.G;
+  hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
+                     a.G, a.GS, a.out, a.out_g, a.out_k);
   return hipGetLastError();
 }
 
