@@ -62,6 +62,26 @@ def dominant_kernel_bytes(ngenes, cells_per_group):
     return ngenes * (cells_per_group * (4 + 8 * G) + 8 * G)
 
 
+def profiled_traffic():
+    """HBM-side bytes per launch of the bootstrap kernel from the newest committed rocprofv3
+    summary (profiles/rNN_summary.json, written by tools/profile.sh + tools/pmc_summary.py from
+    separate --pmc passes of this same command; FETCH_SIZE x2 per MI355X_MICROARCH.md)."""
+    d = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(d):
+        return None
+    cands = sorted(f for f in os.listdir(d) if f.endswith("_summary.json"))
+    if not cands:
+        return None
+    with open(os.path.join(d, cands[-1])) as f:
+        ks = json.load(f)["kernels"]
+    boots = {k: v for k, v in ks.items() if k.startswith("k_boot") and "exact" not in k}
+    if not boots:
+        return None
+    name, e = max(boots.items(), key=lambda kv: kv[1]["pct"])
+    return {"file": "profiles/" + cands[-1], "kernel": name, "avg_ms": e["avg_ms"],
+            "traffic_bytes": e.get("traffic_bytes")}
+
+
 def cpu_baseline(models, counts, groups, prior, sample_genes):
     """The oracle (C restatement of the reference loops, 1 core) on a bounded gene sample."""
     from oracle import oracle as O
@@ -77,7 +97,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cpu-sample", type=int, default=2000, help="genes timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=5000, help="genes timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
 
@@ -156,6 +176,9 @@ def main():
     boot_avg_s = (boot_ms / max(boot_n, 1)) / 1e3
     per_launch_bytes = dominant_kernel_bytes(N_GENES, N_CELLS // 2)
     achieved = per_launch_bytes / boot_avg_s / 1e9 if boot_n else None
+    prof = profiled_traffic()
+    # reference-formulation FP64 adds per launch: B x C x G x N
+    ref_adds = NBOOT * (N_CELLS // 2) * G * N_GENES
     out = {
         "metric": "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)",
         "value": value,
@@ -174,9 +197,13 @@ def main():
                    "grid": G, "n_randomizations": NBOOT, "parallelism": f"gene-shard x{world}"},
         "roofline": {"bound": "hbm", "kernel": "k_boot (bootstrap joint posterior)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+                     "traffic": prof["traffic_bytes"] if prof else None,
+                     "traffic_source": (f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms)"
+                                        if prof else None),
                      "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
-                     "algorithmic_bytes_per_launch": per_launch_bytes},
+                     "algorithmic_bytes_per_launch": per_launch_bytes,
+                     "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
     }
     if rank == 0 and world == 1 and args.cpu_sample > 0:

@@ -257,10 +257,15 @@ def ucl_uci(counts_sub):
 
 def scde_posteriors(models, counts, prior_x, n_randomizations=100, batch=None, composition=None,
                     return_individual_posteriors=False, return_individual_posterior_modes=False,
-                    ensemble_posterior=False, n_cores=20):
-    """Restates scde.posteriors (R/functions.R:566-669).  counts: N x C int, columns = model rows."""
+                    ensemble_posterior=False, n_cores=20, gene_offset=0, ngenes_total=None):
+    """Restates scde.posteriors (R/functions.R:566-669).  counts: N x C int, columns = model rows.
+
+    gene_offset / ngenes_total (test harness for sharding): ``counts`` holds rows
+    [gene_offset, gene_offset + N) of an ngenes_total-gene call; chunks and seeds are those of
+    the whole call (R/functions.R:606-617), restricted to this row range."""
     counts = np.asarray(counts)
     N, C = counts.shape
+    NT = N if ngenes_total is None else int(ngenes_total)
     marg = marginals_from_prior_x(prior_x)
     mm, lt, sq = model_matrix(models)
     postflag = 0
@@ -280,8 +285,12 @@ def scde_posteriors(models, counts, prior_x, n_randomizations=100, batch=None, c
                                          postflag, lt, sq)
         return logBootPosterior(mm, ucl, uci, marg, n_randomizations, seed, postflag, lt, sq, ens)
 
-    if n_cores > 1 and N > n_cores:
-        parts = [call(ii, int(ii[0]) + 1) for ii in r_chunks(N, n_cores)]
+    if n_cores > 1 and NT > n_cores:
+        parts = []
+        for ii in r_chunks(NT, n_cores):
+            loc = ii[(ii >= gene_offset) & (ii < gene_offset + N)] - gene_offset
+            if len(loc):
+                parts.append(call(loc, int(ii[0]) + 1))
         if postflag == 0:
             return np.vstack(parts)
         out = {"jp": np.vstack([p["jp"] for p in parts])}
@@ -337,7 +346,7 @@ def quick_distribution_summary(rpost, diffv, expectation=0.0):
 
 
 def scde_expression_difference(models, counts, prior_x, prior_y, groups, n_randomizations=150, n_cores=10,
-                               return_posteriors=False, expectation=0.0):
+                               return_posteriors=False, expectation=0.0, gene_offset=0, ngenes_total=None):
     """Restates scde.expression.difference (R/functions.R:304-407), no batch.
 
     groups: per-cell labels in {0, 1} (level order) or -1 for NA."""
@@ -347,7 +356,7 @@ def scde_expression_difference(models, counts, prior_x, prior_y, groups, n_rando
         ii = np.nonzero(groups == lv)[0]
         sub = {k: np.asarray(v)[ii] for k, v in models.items()}
         jpl.append(scde_posteriors(sub, np.asarray(counts)[:, ii], prior_x, n_randomizations=n_randomizations,
-                                   n_cores=n_cores))
+                                   n_cores=n_cores, gene_offset=gene_offset, ngenes_total=ngenes_total))
     bdiffp = calculate_ratio_posterior(jpl[0], jpl[1], prior_y)
     res = quick_distribution_summary(bdiffp, ratio_grid(prior_x), expectation)
     if return_posteriors:

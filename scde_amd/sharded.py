@@ -1,0 +1,94 @@
+"""Gene-sharded scde.expression.difference: one process per GPU.
+
+Genes are independent once the draw lists are fixed, so each rank takes a contiguous,
+balanced gene range and runs the whole per-gene pipeline (unique tables, both groups'
+bootstrap posteriors, ratio posterior, lb/mle/ub/ce/Z) on its own GPU with the seeding
+of the *whole* call: with n.cores > 1 the reference splits the N genes into chunks whose
+seeds are the chunk starts (R/functions.R:606-617); a shard carries its global offset so
+every gene keeps its chunk's draw list (engine.hip ``seeding``).
+
+The single exchange is a gather of the per-gene rows (lb, mle, ub, ce, Z) to rank 0,
+where cZ = BH over all genes is computed (R/functions.R:5051).  Over RCCL this is one
+``gather`` of a padded (ceil(N/world) x 5) fp64 tensor per rank -- 800 KB at 20k genes.
+
+``compute`` is the per-shard function; the default is the HIP path.  Tests substitute a
+CPU checker to run the distributed logic under ``gloo`` without a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import api
+from ._lib import DEParams, check, lib
+from .models import model_matrix
+
+
+def shard_range(ngenes: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous balanced range [lo, hi) of rank ``rank`` among ``world``."""
+    base, extra = divmod(ngenes, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def device_shard(models, counts_shard, prior, codes, n_randomizations, n_cores, expectation, gene_offset,
+                 ngenes_total, ctx=None):
+    """Rows (lb, mle, ub, ce, Z) for one shard, computed on this rank's GPU."""
+    ctx = ctx or api.default_context()
+    mat = np.asfortranarray(counts_shard, dtype=np.int32)
+    n, C = mat.shape
+    mm, lt, sq = model_matrix(models)
+    px = np.ascontiguousarray(prior["x"], np.float64)
+    py = np.ascontiguousarray(prior["y"], np.float64)
+    codes = np.ascontiguousarray(codes, np.int32)
+    res = np.zeros((n, 5), order="F")
+    if n == 0:
+        return res
+    dc = api.DeviceCounts(ctx, mat)
+    try:
+        params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, len(px),
+                          int(n_randomizations), int(n_cores), int(gene_offset), int(ngenes_total),
+                          float(expectation), api.get_rand_kind())
+        check(lib().scde_expression_difference_dev(ctx.handle, dc.ptr, n, n, ctypes.byref(params),
+                                                   res.ctypes.data_as(ctypes.c_void_p), None, None, None))
+    finally:
+        dc.free()
+    return res
+
+
+def expression_difference(models, counts, prior, groups, n_randomizations=150, n_cores=10, expectation=0.0,
+                          compute=None, process_group=None, device=None):
+    """Sharded scde.expression.difference over the ranks of ``torch.distributed``.
+
+    Every rank passes the full inputs (or at least the same N and its own rows -- only
+    rows [lo, hi) of ``counts`` are read).  Returns the N x 6 result table (lb, mle, ub,
+    ce, Z, cZ as a pandas DataFrame) on rank 0 and None on the other ranks.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(process_group)
+    rank = dist.get_rank(process_group)
+    mat, genes = api._align_counts(models, counts)
+    N = mat.shape[0]
+    codes = api._groups_vector(models, groups)
+    lo, hi = shard_range(N, world, rank)
+    fn = compute or device_shard
+    rows = fn(models, mat[lo:hi], prior, codes, n_randomizations, n_cores, expectation, lo, N)
+    rows = np.asarray(rows, np.float64).reshape(hi - lo, 5)
+    per = -(-N // world)
+    buf = torch.zeros((per, 5), dtype=torch.float64)
+    buf[: hi - lo] = torch.from_numpy(np.ascontiguousarray(rows))
+    if device is not None:
+        buf = buf.to(device)
+    parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+    dist.gather(buf, parts, dst=0, group=process_group)
+    if rank != 0:
+        return None
+    res = np.vstack([parts[r][: (lambda b: b[1] - b[0])(shard_range(N, world, r))].cpu().numpy()
+                     for r in range(world)])
+    return api._result_frame(np.asfortranarray(res), api._bh(res[:, 4]), genes)
+
+
+__all__ = ["shard_range", "device_shard", "expression_difference"]

@@ -1,0 +1,110 @@
+"""Gene sharding across ranks: CPU tests under gloo with the oracle as
+the per-shard checker, and a GPU test of the device path's global-offset seeding.
+
+The property: sharding is invisible -- for any world size, the gathered table (including
+cZ, a global BH over all genes) equals the single-process result, with n.cores chunks
+(and so bootstrap seeds) that straddle shard boundaries."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from conftest import golden
+
+NRAND = 12
+NCORES = 7
+NGENES = 90
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs():
+    g = golden("esmef500.npz")
+    from oracle import oracle as O
+    models = {c: g["models"][:, j] for j, c in enumerate(O.MODEL_COLUMNS) if not np.all(np.isnan(g["models"][:, j]))}
+    counts = np.asfortranarray(g["counts"][:NGENES])
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    return models, counts, prior, g["groups"]
+
+
+def oracle_shard(models, counts_shard, prior, codes, nrand, n_cores, expectation, lo, N):
+    """Per-shard compute for the CPU tests: the oracle restatement on rows [lo, lo+n)."""
+    from oracle import oracle as O
+    r = O.scde_expression_difference(models, counts_shard, prior["x"], prior["y"], codes, n_randomizations=nrand,
+                                     n_cores=n_cores, expectation=expectation, gene_offset=lo, ngenes_total=N)
+    return np.column_stack([r[k] for k in ("lb", "mle", "ub", "ce", "Z")])
+
+
+def _worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from scde_amd import sharded
+        models, counts, prior, groups = _inputs()
+        tab = sharded.expression_difference(models, counts, prior, list(groups), n_randomizations=NRAND,
+                                            n_cores=NCORES, compute=oracle_shard)
+        if rank == 0:
+            np.save(out_path, tab[["lb", "mle", "ub", "ce", "Z", "cZ"]].to_numpy())
+        else:
+            assert tab is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_range_partition():
+    from scde_amd.sharded import shard_range
+    for N in (0, 1, 7, 90, 20000, 20001):
+        for world in (1, 2, 3, 8):
+            rs = [shard_range(N, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == N
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            sizes = [hi - lo for lo, hi in rs]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_oracle_shards_compose(oracle):
+    """Row ranges computed with global offsets concatenate to the unsharded oracle."""
+    models, counts, prior, groups = _inputs()
+    full = oracle_shard(models, counts, prior, groups, NRAND, NCORES, 0.0, 0, NGENES)
+    parts = [oracle_shard(models, counts[lo:hi], prior, groups, NRAND, NCORES, 0.0, lo, NGENES)
+             for lo, hi in ((0, 31), (31, 32), (32, NGENES))]
+    np.testing.assert_array_equal(np.vstack(parts), full)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_sharded_matches_single_process(world, tmp_path, oracle):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "tab.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    from oracle import oracle as O
+    models, counts, prior, groups = _inputs()
+    ref = O.scde_expression_difference(models, counts, prior["x"], prior["y"], groups, n_randomizations=NRAND,
+                                       n_cores=NCORES)
+    want = np.column_stack([ref[k] for k in ("lb", "mle", "ub", "ce", "Z", "cZ")])
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.gpu
+def test_device_shards_match_unsharded():
+    """The HIP path with gene_offset/ngenes_total: shards of one call reproduce it exactly."""
+    from scde_amd import api, sharded
+    models, counts, prior, groups = _inputs()
+    api.set_rand("glibc")
+    codes = np.asarray(groups, np.int32)
+    full = sharded.device_shard(models, counts, prior, codes, NRAND, NCORES, 0.0, 0, NGENES)
+    parts = [sharded.device_shard(models, counts[lo:hi], prior, codes, NRAND, NCORES, 0.0, lo, NGENES)
+             for lo, hi in ((0, 31), (31, 32), (32, NGENES))]
+    np.testing.assert_array_equal(np.vstack(parts), full)
+    want = oracle_shard(models, counts, prior, codes, NRAND, NCORES, 0.0, 0, NGENES)
+    for j in range(4):
+        np.testing.assert_array_equal(full[:, j], want[:, j])
+    np.testing.assert_allclose(full[:, 4], want[:, 4], rtol=1e-6, atol=1e-9)

@@ -12,4 +12,6 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc2 -o run -- python3 bench.py $ARGS > $OUT/pmc2.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD TCC_HIT_sum --output-format csv -d $OUT/pmc3 -o run -- python3 bench.py $ARGS > $OUT/pmc3.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum WRITE_SIZE --output-format csv -d $OUT/pmc4 -o run -- python3 bench.py $ARGS > $OUT/pmc4.log 2>&1
+# summary -> profiles/ (PROFILE_PREFIX, e.g. profiles/r01)
+[ -n "$PROFILE_PREFIX" ] && python3 tools/pmc_summary.py $OUT $PROFILE_PREFIX
 echo profile done
