@@ -206,6 +206,17 @@ def main():
                      "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
     }
+    if rank == 0 and world == 1 and not args.no_profile:
+        # PCIe-inclusive rate through the host-buffer API (counts uploaded, table incl. cZ
+        # returned per call) -- reported beside `value`, never as it.
+        ctx.set_profiling(False)
+        api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
+                                       n_cores=1, ctx=ctx)
+        t1 = time.perf_counter()
+        for _ in range(3):
+            api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
+                                           n_cores=1, ctx=ctx)
+        out["host_buffers_genes_per_s"] = 3 * N_GENES / (time.perf_counter() - t1)
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         gps, secs = cpu_baseline(models, counts, groups, prior, args.cpu_sample)
         out["cpu_baseline"] = {"value": gps, "unit": "genes/s", "cores": 1, "kind": "port",

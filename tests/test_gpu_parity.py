@@ -264,6 +264,11 @@ def test_edge_cases(api, oracle):
         ref = oracle.scde_posteriors(sub, c, g["prior_x"], n_randomizations=11, n_cores=1)
         got = api.scde_posteriors(sub, c, prior, n_randomizations=11, n_cores=1)
         assert_posterior_close(got, ref, what=name)
+    empty = api.scde_posteriors(sub, np.zeros((0, 6), np.int32), prior, n_randomizations=11, n_cores=1)
+    assert np.asarray(empty).shape == (0, len(g["prior_x"]))
+    tab = api.scde_expression_difference(models, np.zeros((0, len(g["groups"])), np.int32), prior,
+                                         groups=list(g["groups"]), n_randomizations=5, n_cores=1)
+    assert len(tab) == 0
     one = {k: v[[3]] for k, v in models.items()}
     ref = oracle.scde_posteriors(one, g["counts"][:30][:, [3]], g["prior_x"], n_randomizations=5, n_cores=1)
     got = api.scde_posteriors(one, g["counts"][:30][:, [3]], prior, n_randomizations=5, n_cores=1)
