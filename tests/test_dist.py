@@ -95,7 +95,10 @@ def test_gloo_sharded_matches_single_process(world, tmp_path, oracle):
 
 @pytest.mark.gpu
 def test_device_shards_match_unsharded():
-    """The HIP path with gene_offset/ngenes_total: shards of one call reproduce it exactly."""
+    """The HIP path with gene_offset/ngenes_total: shards of one call reproduce it (lb/mle/ub/ce
+    exactly, Z to the parity tolerance: a shard's unique-count set can differ from the whole
+    call's, e.g. no zero count for a cell, which changes the bootstrap's summation order by
+    ulps -- the reference's own chunking does the same)."""
     from scde_amd import api, sharded
     models, counts, prior, groups = _inputs()
     api.set_rand("glibc")
@@ -103,7 +106,9 @@ def test_device_shards_match_unsharded():
     full = sharded.device_shard(models, counts, prior, codes, NRAND, NCORES, 0.0, 0, NGENES)
     parts = [sharded.device_shard(models, counts[lo:hi], prior, codes, NRAND, NCORES, 0.0, lo, NGENES)
              for lo, hi in ((0, 31), (31, 32), (32, NGENES))]
-    np.testing.assert_array_equal(np.vstack(parts), full)
+    sh = np.vstack(parts)
+    np.testing.assert_array_equal(sh[:, :4], full[:, :4])
+    np.testing.assert_allclose(sh[:, 4], full[:, 4], rtol=1e-6, atol=1e-9)
     want = oracle_shard(models, counts, prior, codes, NRAND, NCORES, 0.0, 0, NGENES)
     for j in range(4):
         np.testing.assert_array_equal(full[:, j], want[:, j])
