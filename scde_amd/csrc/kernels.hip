@@ -869,14 +869,43 @@ __global__ void k_cell_minmax(const int* __restrict__ counts, long long ld, long
   }
 }
 
-__global__ void k_mark(const int* __restrict__ counts, long long ld, long long g0, int ngenes, int ncells,
-                       const int* __restrict__ cellidx, const long long* __restrict__ woff,
-                       unsigned long long* __restrict__ bits) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)ngenes * ncells) return;
-  const int g = (int)(i % ngenes), c = (int)(i / ngenes);
-  const int x = counts[(long long)cellidx[c] * ld + g0 + g];
-  atomicOr(&bits[woff[c] + (x >> 6)], 1ull << (x & 63));
+// One cell per blockIdx.y, KM genes per thread.  Counts below 64*MW set bits in an LDS
+// copy of the cell's first MW bitmap words (most counts are small, and 0 alone is ~2/3 of
+// them: global atomics on that one word serialised at L2); the block then flushes at most
+// MW global atomicOr.  Larger counts go straight to global memory (sparse words).
+template <int KM, int MW>
+__global__ __launch_bounds__(256) void k_mark(const int* __restrict__ counts, long long ld, long long g0,
+                                              int ngenes, const int* __restrict__ cellidx,
+                                              const long long* __restrict__ woff,
+                                              unsigned long long* __restrict__ bits) {
+  __shared__ unsigned long long lw[MW];
+  const int c = blockIdx.y;
+  if (threadIdx.x < MW) lw[threadIdx.x] = 0ull;
+  __syncthreads();
+  const int* __restrict__ col = counts + (long long)cellidx[c] * ld + g0;
+  unsigned long long* __restrict__ cb = bits + woff[c];
+  const int base = blockIdx.x * (256 * KM) + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < KM; ++j) {
+    const int g = base + j * 256;
+    const bool valid = g < ngenes;
+    const int x = valid ? col[g] : 0;
+    // count 0 (the common case) by ballot: one LDS atomic per wave instead of up to 64
+    if (__ballot(valid && x == 0) && (threadIdx.x & 63) == 0) atomicOr(&lw[0], 1ull);
+    if (valid && x != 0) {
+      const unsigned long long bit = 1ull << (x & 63);
+      if ((x >> 6) < MW)
+        atomicOr(&lw[x >> 6], bit);
+      else
+        atomicOr(&cb[x >> 6], bit);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < MW) {
+    const unsigned long long v = lw[threadIdx.x];
+    // words beyond the cell's own bitmap are never set (x <= cmax)
+    if (v) atomicOr(&cb[threadIdx.x], v);
+  }
 }
 
 // per cell: exclusive popcount prefix of its bitmap words -> rank, and #unique
@@ -953,9 +982,12 @@ __global__ void k_colmajor_to_rows(const double* __restrict__ src, int nrows, in
 __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
   extern __shared__ double sh[];
   const int n = a.n, m = 2 * a.n - 1;
+  // A, B: prior-weighted rows, zero-padded by 4 so the sliding windows below may read past
+  // the end (a padded term adds +0 to a non-negative sum: bit-identical).  X: the row of
+  // 2n-1 outputs, then 48 doubles of per-wave scratch.
   double* A = sh;
-  double* B = sh + n;
-  double* X = sh + 2 * n;
+  double* B = sh + (n + 4);
+  double* X = sh + 2 * (n + 4);
   __shared__ double red[8];
   __shared__ double red2[8];
   __shared__ int ired[8];
@@ -963,7 +995,12 @@ __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
   __shared__ int ired3[8];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
   for (int g = blockIdx.x; g < a.ngenes; g += gridDim.x) {
-    for (int k = tid; k < n && !a.xin; k += blockDim.x) {
+    for (int k = tid; k < n + 4 && !a.xin; k += blockDim.x) {
+      if (k >= n) {
+        A[k] = 0.0;
+        B[k] = 0.0;
+        continue;
+      }
       const double y = a.prior_y ? a.prior_y[k] : 1.0;
       const double p1 = a.jp1[(long long)g * a.j1g + (long long)k * a.j1k];
       const double p2 = a.jp2[(long long)g * a.j2g + (long long)k * a.j2k];
@@ -971,17 +1008,75 @@ __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
       B[k] = a.prior_y ? __dmul_rn(p2, y) : p2;
     }
     __syncthreads();
-    // matSlideMult: X[o] = sum_t A[t + max(s,0)] * B[t + max(-s,0)], s = o - (n-1), t ascending
+    // matSlideMult (src/matSlideMult.cpp:12-20): X[o] = sum_t A[t + max(s,0)] * B[t + max(-s,0)],
+    // s = o - (n-1), t ascending, each product and sum rounded separately.  Four adjacent
+    // outputs per thread share one sliding register window: per t one new A (s >= 0) or
+    // B (s < 0) value and one shared operand feed four independent sums.
     dd ls = {0.0, 0.0};
     for (int o = tid; o < m && a.xin; o += blockDim.x) X[o] = a.xin[(long long)g * a.xg + (long long)o * a.xo];
-    for (int o = tid; o < m && !a.xin; o += blockDim.x) {
-      const int s = o - (n - 1);
-      const int o1 = s > 0 ? s : 0, o2 = s < 0 ? -s : 0;
-      const int len = n - (s < 0 ? -s : s);
-      double acc = 0.0;
-      for (int t = 0; t < len; ++t) acc = __dadd_rn(acc, __dmul_rn(A[t + o1], B[t + o2]));
-      X[o] = acc;
-      ls = dd_add_d(ls, acc);
+    for (int o0 = tid * 4; o0 < m && !a.xin; o0 += blockDim.x * 4) {
+      const int s0 = o0 - (n - 1);
+      double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+      if (s0 >= 0) {
+        // output r: sum_{t < n-s0-r} A[t+s0+r] B[t]; run all four to the longest (r = 0)
+        double w0 = A[s0], w1 = A[s0 + 1], w2 = A[s0 + 2], w3 = A[s0 + 3];
+        const int len = n - s0;
+        for (int t = 0; t < len; ++t) {
+          const double b = B[t];
+          c0 = __dadd_rn(c0, __dmul_rn(w0, b));
+          c1 = __dadd_rn(c1, __dmul_rn(w1, b));
+          c2 = __dadd_rn(c2, __dmul_rn(w2, b));
+          c3 = __dadd_rn(c3, __dmul_rn(w3, b));
+          w0 = w1;
+          w1 = w2;
+          w2 = w3;
+          w3 = A[t + s0 + 4];
+        }
+      } else if (s0 + 3 < 0) {
+        // output r: sum_{t < n+s0+r} A[t] B[t-s0-r]; run all four to the longest (r = 3)
+        double w0 = B[-s0], w1 = B[-s0 - 1], w2 = B[-s0 - 2], w3 = B[-s0 - 3];
+        const int len = n + s0 + 3;
+        for (int t = 0; t < len; ++t) {
+          const double av = A[t];
+          c0 = __dadd_rn(c0, __dmul_rn(av, w0));
+          c1 = __dadd_rn(c1, __dmul_rn(av, w1));
+          c2 = __dadd_rn(c2, __dmul_rn(av, w2));
+          c3 = __dadd_rn(c3, __dmul_rn(av, w3));
+          w3 = w2;
+          w2 = w1;
+          w1 = w0;
+          w0 = B[t + 1 - s0];
+        }
+      } else {
+        // the group that straddles s = 0: one output at a time
+        double cc[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int r = 0; r < 4; ++r) {
+          const int s = s0 + r;
+          const int o1 = s > 0 ? s : 0, o2 = s < 0 ? -s : 0;
+          const int len = n - (s < 0 ? -s : s);
+          double acc = 0.0;
+          for (int t = 0; t < len; ++t) acc = __dadd_rn(acc, __dmul_rn(A[t + o1], B[t + o2]));
+          cc[r] = acc;
+        }
+        c0 = cc[0];
+        c1 = cc[1];
+        c2 = cc[2];
+        c3 = cc[3];
+      }
+      X[o0] = c0;
+      ls = dd_add_d(ls, c0);
+      if (o0 + 1 < m) {
+        X[o0 + 1] = c1;
+        ls = dd_add_d(ls, c1);
+      }
+      if (o0 + 2 < m) {
+        X[o0 + 2] = c2;
+        ls = dd_add_d(ls, c2);
+      }
+      if (o0 + 3 < m) {
+        X[o0 + 3] = c3;
+        ls = dd_add_d(ls, c3);
+      }
     }
     // row sum (R rowSums accumulates in long double): double-double block reduce
     for (int d = 32; d >= 1; d >>= 1) {
@@ -1084,11 +1179,31 @@ __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
       ired3[wid] = ubi;
     }
     __syncthreads();
+    // Z (R/functions.R:3514-3531): rpost = (p + 1e-15) / rowSums(p + 1e-15);
+    // gs = sum(rpost[1:(zi-1)]) (R's 1:0 selects column 1 when zi is the first column),
+    // as a block-parallel double-double sum over each thread's chunk.
+    dd zt2 = {X[m + 8], X[m + 16]};
+    for (int w = 1; w < nw; ++w) zt2 = dd_add(zt2, dd{X[m + 8 + w], X[m + 16 + w]});
+    const double rs2 = dd_to_d(zt2);
+    const int zend = a.zi == 0 ? 1 : a.zi;
+    dd gp = {0.0, 0.0};
+    for (int o = c0; o < min(c1, zend); ++o) gp = dd_add_d(gp, (X[o] + 1e-15) / rs2);
+    for (int d = 32; d >= 1; d >>= 1) {
+      dd o2;
+      o2.hi = __shfl_xor(gp.hi, d, 64);
+      o2.lo = __shfl_xor(gp.lo, d, 64);
+      gp = dd_add(gp, o2);
+    }
+    if (lane == 0) {
+      X[m + 24 + wid] = gp.hi;
+      X[m + 32 + wid] = gp.lo;
+    }
+    __syncthreads();
     if (tid == 0) {
       int lb = ired2[0], ub = ired3[0];
       double mb = X[m];
       int mi = ired[0];
-      dd zt2 = {X[m + 8], X[m + 16]};
+      dd gs = {X[m + 24], X[m + 32]};
       for (int w = 1; w < nw; ++w) {
         lb = max(lb, ired2[w]);
         ub = min(ub, ired3[w]);
@@ -1097,7 +1212,7 @@ __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
           mb = v;
           mi = ired[w];
         }
-        zt2 = dd_add(zt2, dd{X[m + 8 + w], X[m + 16 + w]});
+        gs = dd_add(gs, dd{X[m + 24 + w], X[m + 32 + w]});
       }
       if (lb < 0) lb = 0;
       if (ub == 0x7fffffff) ub = m - 1;
@@ -1107,11 +1222,6 @@ __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
       double ce = 0.0;
       if (lbv > 0) ce = lbv;
       if (ubv < 0) ce = ubv;
-      // Z: rpost = (p + 1e-15) / rowSums, gs = sum(rpost[1:(zi-1)]), zv = rpost[zi]
-      const double rs2 = dd_to_d(zt2);
-      dd gs = {0.0, 0.0};
-      if (a.zi == 0) gs = dd_add_d(gs, (X[0] + 1e-15) / rs2);
-      for (int o = 0; o < a.zi; ++o) gs = dd_add_d(gs, (X[o] + 1e-15) / rs2);
       const double gsd = dd_to_d(gs);
       const double zv = (X[a.zi] + 1e-15) / rs2;
       double zl = qnorm(gsd, false);
@@ -1326,8 +1436,8 @@ hipError_t launch_mark(const int* counts, long long ld, long long g0, int ngenes
                        const long long* woff, unsigned long long* bits, hipStream_t s) {
   const long long n = (long long)ngenes * ncells;
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_mark, dim3(div_up(n, 256)), dim3(256), 0, s, counts, ld, g0, ngenes, ncells, cellidx, woff,
-                     bits);
+  hipLaunchKernelGGL((k_mark<8, 16>), dim3(div_up(ngenes, 256 * 8), ncells), dim3(256), 0, s, counts, ld, g0,
+                     ngenes, cellidx, woff, bits);
   return hipGetLastError();
 }
 
@@ -1364,7 +1474,7 @@ hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int 
 
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
-  const size_t shm = sizeof(double) * (size_t)(4 * a.n + 32);
+  const size_t shm = sizeof(double) * (size_t)(2 * (a.n + 4) + (2 * a.n - 1) + 48);
   const int grid = a.ngenes < 65536 ? a.ngenes : 65536;
   hipLaunchKernelGGL(k_ratio_summary, dim3(grid), dim3(256), shm, s, a);
   return hipGetLastError();
