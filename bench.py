@@ -125,25 +125,27 @@ def main():
     py = np.ascontiguousarray(prior["y"], np.float64)
     codes = np.ascontiguousarray(groups, np.int32)
     G = len(px)
+    # one rank: cZ (BH) in the same call on device; several: Z gathered to rank 0, BH there
     params = api.DEParams(N_CELLS, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
-                          NBOOT, 1, rank * N_GENES, world * N_GENES, 0.0, api.get_rand_kind())
-    res = np.zeros((N_GENES, 5), order="F")
+                          NBOOT, 1, rank * N_GENES, world * N_GENES, 0.0, api.get_rand_kind(), int(world == 1))
+    res = np.zeros((N_GENES, 6 if world == 1 else 5), order="F")
     L = api.lib()
     import ctypes
 
     def step():
         api.check(L.scde_expression_difference_dev(ctx.handle, dc.ptr, N_GENES, N_GENES, ctypes.byref(params),
                                                    res.ctypes.data_as(ctypes.c_void_p), None, None, None))
-        z = np.ascontiguousarray(res[:, 4])
         if dist is not None:
             import torch
-            zt = torch.from_numpy(z).cuda()
+            zt = torch.from_numpy(np.ascontiguousarray(res[:, 4])).cuda()
             gathered = [torch.empty_like(zt) for _ in range(world)] if rank == 0 else None
             dist.gather(zt, gathered, dst=0)
             if rank == 0:
-                api.bh_cz(torch.cat(gathered).cpu().numpy())
-        else:
-            api.bh_cz(z)
+                zall = torch.cat(gathered)
+                cz = torch.empty_like(zall)
+                torch.cuda.current_stream().synchronize()
+                api.bh_cz_device(ctx, zall.data_ptr(), zall.numel(), cz.data_ptr())
+                cz_host = cz.cpu()  # noqa: F841  (the table's last column, on the host)
 
     def barrier():
         ctx.synchronize()

@@ -121,6 +121,11 @@ int scde_dev_free(scde_ctx* ctx, void* dptr);
 int scde_h2d(scde_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int scde_d2h(scde_ctx* ctx, void* dst, const void* src, int64_t bytes);
 
+/* The same BH cZ on device buffers (z_dev, cz_dev: n doubles in HBM), on the context's
+ * stream: pnorm, stable descending radix sort, cummin scan, qnorm.  For the gathered Z
+ * of a sharded call (R/functions.R:5051). */
+int scde_bh_cz_dev(scde_ctx* ctx, const double* z_dev, int64_t n, double* cz_dev);
+
 typedef struct scde_de_params {
   int ncells;              /* cells (columns of counts) */
   const double* models;    /* host, ncells x 12 col-major (NaN where absent; corr.a clamp applied inside) */
@@ -136,12 +141,14 @@ typedef struct scde_de_params {
   int64_t ngenes_total;    /* global number of genes (for chunk seeds) */
   double expectation;      /* R `expectation` (log2 scale) */
   int rand_kind;           /* SCDE_RAND_GLIBC / SCDE_RAND_DARWIN */
+  int compute_cz;          /* 1: this call covers every gene; results gain a 6th column cZ (device BH) */
 } scde_de_params;
 
 /* scde.expression.difference (R/functions.R:304-407, no batch) on device-resident
  * counts (int32, column-major, leading dimension ld, rows gene_offset.. of the shard
- * start at counts_dev).  results: host ngenes x 5 col-major (lb, mle, ub, ce, Z);
- * cZ is left to scde_bh_cz (it needs every shard's Z).  jp1/jp2 (ngenes x ngrid) and
+ * start at counts_dev).  results: host ngenes x 5 col-major (lb, mle, ub, ce, Z), or
+ * x 6 with cZ when p->compute_cz (whole call = all genes); for shards cZ is left to
+ * scde_bh_cz / scde_bh_cz_dev over the gathered Z.  jp1/jp2 (ngenes x ngrid) and
  * ratio (ngenes x (2*ngrid-1)) are optional host outputs, col-major. */
 int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes,
                                    const scde_de_params* p, double* results, double* jp1, double* jp2,

@@ -842,30 +842,32 @@ static int cmp_desc(const void* a, const void* b) {
     return (i < j) ? -1 : (i > j);
 }
 int o_bh_cz(const double* z, int n, double* cz) {
-    double* p = (double*)malloc(sizeof(double) * n);
-    int* o = (int*)malloc(sizeof(int) * n);
-    double* adj = (double*)malloc(sizeof(double) * n);
+    /* p.adjust (R stats): NA p-values are dropped (p <- p[nna]) and stay NA; the default
+     * n = length(p) is a promise forced after that subsetting, so n = lp = #non-NA;
+     * `if (n <= 1) return(p0)` returns the unadjusted p (NAs included). */
+    double* p = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
+    int* o = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+    double* adj = (double*)malloc(sizeof(double) * (n > 0 ? n : 1));
     double cm = INFINITY;
-    int i;
+    int i, lp = 0;
     for (i = 0; i < n; i++) {
         p[i] = o_pnorm(fabs(z[i]), 0);
-        o[i] = i;
+        adj[i] = p[i];
+        if (!isnan(p[i])) o[lp++] = i;
     }
     cmp_p = p;
-    qsort(o, n, sizeof(int), cmp_desc);
-    if (n <= 1) { /* p.adjust: `if (n <= 1) return(p0)` */
-        for (i = 0; i < n; i++) adj[i] = p[i];
-    } else {
+    qsort(o, lp, sizeof(int), cmp_desc); /* ties by index: R's order(decreasing=TRUE) is stable */
+    if (lp > 1) {
         /* i <- lp:1L ; o <- order(p, decreasing = TRUE); pmin(1, cummin(n/i * p[o]))[ro] */
-        for (i = 0; i < n; i++) {
-            double rank = (double)(n - i);
-            double v = ((double)n / rank) * p[o[i]];
+        for (i = 0; i < lp; i++) {
+            double rank = (double)(lp - i);
+            double v = ((double)lp / rank) * p[o[i]];
             if (v < cm) cm = v;
             adj[o[i]] = cm < 1 ? cm : 1;
         }
     }
     for (i = 0; i < n; i++) {
-        double s = (z[i] > 0) ? 1.0 : (z[i] < 0 ? -1.0 : 0.0);
+        double s = (z[i] > 0) ? 1.0 : (z[i] < 0 ? -1.0 : (isnan(z[i]) ? NAN : 0.0));
         cz[i] = s * o_qnorm(adj[i], 0);
     }
     free(p);

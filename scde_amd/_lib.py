@@ -20,7 +20,7 @@ EXPORTS = [
     "scde_ctx_create", "scde_ctx_destroy", "scde_ctx_synchronize", "scde_ctx_set_profiling",
     "scde_ctx_kernel_times", "scde_ctx_reset_kernel_times",
     "scde_dev_alloc", "scde_dev_free", "scde_h2d", "scde_d2h",
-    "scde_expression_difference_dev", "scde_posteriors_dev",
+    "scde_expression_difference_dev", "scde_posteriors_dev", "scde_bh_cz_dev",
 ]
 
 
@@ -44,6 +44,7 @@ class DEParams(ctypes.Structure):
         ("ngenes_total", ctypes.c_int64),
         ("expectation", ctypes.c_double),
         ("rand_kind", ctypes.c_int),
+        ("compute_cz", ctypes.c_int),
     ]
 
 
@@ -87,6 +88,7 @@ def lib():
     L.scde_dev_free.argtypes = [P, P]
     L.scde_h2d.argtypes = [P, P, P, i64]
     L.scde_d2h.argtypes = [P, P, P, i64]
+    L.scde_bh_cz_dev.argtypes = [P, P, i64, P]
     L.scde_expression_difference_dev.argtypes = [P, P, i64, i, ctypes.POINTER(DEParams), P, P, P, P]
     L.scde_posteriors_dev.argtypes = [P, P, i64, i, P, i, P, i, i, P, i, i, i, i64, i64, i, i, P, P, P, i, P, P, P]
     _lib = L

@@ -426,8 +426,8 @@ def scde_expression_difference(models, counts, prior, groups=None, batch=None, n
     dc = DeviceCounts(ctx, mat)
     try:
         params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
-                          int(n_randomizations), int(n_cores), 0, N, float(expectation), get_rand_kind())
-        res = np.zeros((N, 5), order="F")
+                          int(n_randomizations), int(n_cores), 0, N, float(expectation), get_rand_kind(), 1)
+        res = np.zeros((N, 6), order="F")  # lb, mle, ub, ce, Z, cZ (BH on device)
         jp1 = np.zeros((N, G), order="F") if return_posteriors else None
         jp2 = np.zeros((N, G), order="F") if return_posteriors else None
         ratio = np.zeros((N, 2 * G - 1), order="F") if return_posteriors else None
@@ -435,7 +435,7 @@ def scde_expression_difference(models, counts, prior, groups=None, batch=None, n
                                                    _p(jp1), _p(jp2), _p(ratio)))
     finally:
         dc.free()
-    table = _result_frame(res, _bh(res[:, 4]), genes)
+    table = _result_frame(res[:, :5], res[:, 5].copy(), genes)
     if return_posteriors:
         return {"results": table, "difference.posterior": RatioPosterior(ratio, ratio_columns(px), genes),
                 "joint.posteriors": [jp1, jp2]}
@@ -479,7 +479,12 @@ def bh_cz(z):
     return _bh(z)
 
 
+def bh_cz_device(ctx: Context, z_ptr: int, n: int, cz_ptr: int):
+    """cZ from Z for device buffers (HBM pointers, n doubles each), on the context's stream."""
+    check(lib().scde_bh_cz_dev(ctx.handle, ctypes.c_void_p(z_ptr), int(n), ctypes.c_void_p(cz_ptr)))
+
+
 __all__ = ["scde_posteriors", "scde_expression_difference", "calculate_ratio_posterior", "quick_distribution_summary",
            "logBootPosterior", "logBootBatchPosterior", "jpmatLogBoot", "jpmatLogBatchBoot", "matSlideMult",
            "marginals", "ratio_columns", "expectation_column", "Context", "DeviceCounts", "RatioPosterior",
-           "ScdeError", "bh_cz", "set_rand"]
+           "ScdeError", "bh_cz", "bh_cz_device", "set_rand"]

@@ -154,7 +154,7 @@ struct scde_ctx {
   // workspace
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, ucl, ucl_off, T, E, maxi, has_clamp, base_col, ent, nnz, Wt,
       Z, draws, degen, uci, cellidx, cmax, cmin, woff, bits, rank, nuniq, wset, prior_y, diffv, jpA, jpB, res,
-      ratio, in1, in2, outbuf, part;
+      ratio, in1, in2, outbuf, part, bhw;
   // profiling
   bool profile = false;
   struct Pending {
@@ -208,7 +208,7 @@ struct scde_ctx {
     Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,   &cellscal, &ucl,   &ucl_off, &T,   &E,
                   &maxi,   &has_clamp, &base_col, &ent, &nnz, &Wt, &Z, &draws, &degen, &uci, &cellidx,
                   &cmax,   &cmin, &woff, &bits, &rank, &nuniq, &wset, &prior_y, &diffv, &jpA, &jpB, &res,
-                  &ratio,  &in1, &in2, &outbuf, &part};
+                  &ratio,  &in1, &in2, &outbuf, &part, &bhw};
     for (Buf* b : all) b->release();
     for (void* p : user_allocs) (void)hipFree(p);
     for (auto& p : pending) {
@@ -1178,7 +1178,8 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
   const size_t m = 2 * (size_t)G - 1;
   RCHK(upload(ctx, ctx->prior_y, p->prior_y, sizeof(double) * G));
   RCHK(upload(ctx, ctx->diffv, diffv.data(), sizeof(double) * m));
-  HCHK(ctx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * 5)));
+  const int ncol = p->compute_cz ? 6 : 5;
+  HCHK(ctx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * ncol)));
   if (ratio) HCHK(ctx->ratio.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * m)));
   RatioArgs ra{};
   ra.jp1 = ctx->jpA.as<double>();
@@ -1201,8 +1202,14 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
   hipEvent_t ev = ctx->mark_begin(SLOT_RATIO);
   HCHK(launch_ratio_summary(ra, st));
   ctx->mark_end(SLOT_RATIO, ev);
+  if (p->compute_cz && ngenes) {
+    size_t wb = 0;
+    HCHK(launch_bh_cz(nullptr, ngenes, nullptr, nullptr, &wb, st));
+    HCHK(ctx->bhw.ensure(wb));
+    HCHK(launch_bh_cz(ra.res + (size_t)4 * ngenes, ngenes, ra.res + (size_t)5 * ngenes, ctx->bhw.p, &wb, st));
+  }
   if (results && ngenes)
-    HCHK(hipMemcpyAsync(results, ra.res, sizeof(double) * ngenes * 5, hipMemcpyDeviceToHost, st));
+    HCHK(hipMemcpyAsync(results, ra.res, sizeof(double) * ngenes * ncol, hipMemcpyDeviceToHost, st));
   if (ratio && ngenes) HCHK(hipMemcpyAsync(ratio, ra.ratio, sizeof(double) * ngenes * m, hipMemcpyDeviceToHost, st));
   std::vector<double> tmp;
   if ((jp1 || jp2) && NG) tmp.resize(NG);
@@ -1220,6 +1227,18 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
 }
 
 // ------------------------------------------------------------------ BH (host)
+int scde_bh_cz_dev(scde_ctx* ctx, const double* z_dev, int64_t n, double* cz_dev) {
+  if (!ctx || n < 0 || (n > 0 && (!z_dev || !cz_dev))) return fail(SCDE_EARG, "bad arguments");
+  if (n > 0x7fffffff) return fail(SCDE_EARG, "n too large");
+  if (n == 0) return SCDE_OK;
+  HCHK(hipSetDevice(ctx->device));
+  size_t wb = 0;
+  HCHK(launch_bh_cz(nullptr, (int)n, nullptr, nullptr, &wb, ctx->stream));
+  HCHK(ctx->bhw.ensure(wb));
+  HCHK(launch_bh_cz(z_dev, (int)n, cz_dev, ctx->bhw.p, &wb, ctx->stream));
+  return ctx->sync();
+}
+
 int scde_bh_cz(const double* z, int64_t n, double* cz) {
   if (n < 0 || (n > 0 && (!z || !cz))) return fail(SCDE_EARG, "bad arguments");
   // p.adjust(p, "BH"): i <- n:1; o <- order(p, decreasing = TRUE); pmin(1, cummin(n/i * p[o]))[ro]

@@ -145,6 +145,8 @@ hipError_t launch_uci(const int* counts, long long ld, long long g0, int ngenes,
                       const long long* woff, const unsigned long long* bits, const int* rank, int* uci,
                       hipStream_t s);
 hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int GS, double* dst, hipStream_t s);
+// device BH cZ (bh.hip); work == nullptr -> *work_bytes = required size
+hipError_t launch_bh_cz(const double* z, int n, double* cz, void* work, size_t* work_bytes, hipStream_t s);
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s);
 
 }  // namespace scde

@@ -86,9 +86,18 @@ def expression_difference(models, counts, prior, groups, n_randomizations=150, n
     dist.gather(buf, parts, dst=0, group=process_group)
     if rank != 0:
         return None
-    res = np.vstack([parts[r][: (lambda b: b[1] - b[0])(shard_range(N, world, r))].cpu().numpy()
-                     for r in range(world)])
-    return api._result_frame(np.asfortranarray(res), api._bh(res[:, 4]), genes)
+    rows_all = torch.cat([parts[r][: (lambda b: b[1] - b[0])(shard_range(N, world, r))] for r in range(world)])
+    res = rows_all.cpu().numpy()
+    if rows_all.is_cuda and N > 0:
+        # BH over all genes on rank 0's GPU (scde_bh_cz_dev)
+        z = rows_all[:, 4].contiguous()
+        cz = torch.empty_like(z)
+        torch.cuda.current_stream().synchronize()
+        api.bh_cz_device(api.default_context(), z.data_ptr(), N, cz.data_ptr())
+        czh = cz.cpu().numpy()
+    else:
+        czh = api._bh(res[:, 4])
+    return api._result_frame(np.asfortranarray(res), czh, genes)
 
 
 __all__ = ["shard_range", "device_shard", "expression_difference"]

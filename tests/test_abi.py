@@ -46,9 +46,16 @@ def test_bh_cz_matches_oracle(oracle):
         z[: n // 10] = 7.16  # ties at the cap, as in real runs
         if n > 3:
             z[3] = 0.0
+        if n >= 7:
+            z[5] = np.nan  # NA p-values: dropped from the adjustment, n = #non-NA
         cz_o = np.zeros(n)
         zz = np.ascontiguousarray(z)
         oracle.lib().o_bh_cz(zz.ctypes.data_as(ctypes.c_void_p), n, cz_o.ctypes.data_as(ctypes.c_void_p))
+        np.testing.assert_array_equal(api.bh_cz(z), cz_o)
+    for z in (np.array([np.nan, 1.5]), np.array([np.nan]), np.array([])):
+        cz_o = np.zeros(z.size)
+        zz = np.ascontiguousarray(z)
+        oracle.lib().o_bh_cz(zz.ctypes.data_as(ctypes.c_void_p), z.size, cz_o.ctypes.data_as(ctypes.c_void_p))
         np.testing.assert_array_equal(api.bh_cz(z), cz_o)
 
 

@@ -308,3 +308,42 @@ def test_batch_corrected_difference(api, oracle):
     s_ref = oracle.quick_distribution_summary(a_ref, oracle.ratio_grid(oracle.ratio_grid(g["prior_x"])))
     for k in ("lb", "mle", "ub"):
         assert np.mean(out["batch.adjusted"][k].to_numpy() == s_ref[k]) > 0.98, k
+
+
+@pytest.mark.parametrize("case", ["random", "ties_nan", "tiny"])
+def test_bh_cz_device(api, oracle, case):
+    """Device BH (scde_bh_cz_dev: pnorm, stable radix sort, cummin scan, qnorm) against the
+    oracle's p.adjust restatement."""
+    import ctypes
+    from scde_amd._lib import lib
+    rng = np.random.default_rng(7)
+    if case == "random":
+        z = rng.normal(0, 2.5, 20011)
+    elif case == "ties_nan":
+        z = np.round(rng.normal(0, 2, 5000), 1)
+        z[::37] = np.nan
+        z[5::101] = 0.0
+        z[7::211] = 40.0
+        z[9::223] = -40.0
+    else:
+        z = np.array([1.3])
+    ctx = api.default_context()
+    for zz in ([z] if case != "tiny" else [z, np.array([np.nan, 2.0]), np.array([-0.5, 2.0])]):
+        zz = np.ascontiguousarray(zz, np.float64)
+        n = zz.size
+        zd, cd = ctypes.c_void_p(), ctypes.c_void_p()
+        api.check(lib().scde_dev_alloc(ctx.handle, 8 * n, ctypes.byref(zd)))
+        api.check(lib().scde_dev_alloc(ctx.handle, 8 * n, ctypes.byref(cd)))
+        try:
+            api.check(lib().scde_h2d(ctx.handle, zd, zz.ctypes.data_as(ctypes.c_void_p), 8 * n))
+            api.bh_cz_device(ctx, zd.value, n, cd.value)
+            got = np.zeros(n)
+            api.check(lib().scde_d2h(ctx.handle, got.ctypes.data_as(ctypes.c_void_p), cd, 8 * n))
+        finally:
+            lib().scde_dev_free(ctx.handle, zd)
+            lib().scde_dev_free(ctx.handle, cd)
+        want = np.zeros(n)
+        oracle.lib().o_bh_cz(oracle._p(zz), n, oracle._p(want))
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(want))
+        ok = ~np.isnan(want)
+        np.testing.assert_allclose(got[ok], want[ok], rtol=1e-12, atol=1e-12)
