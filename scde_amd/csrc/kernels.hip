@@ -424,6 +424,116 @@ __global__ __launch_bounds__(1024) void k_boot(BootArgs a) {
 }
 
 // ------------------------------------------------------------------ K2 (fast path)
+// Softmax exp for d in [-746, 0]: exp(d) = 2^(k/64) * e^r, k = rint(64 d / ln 2),
+// r = d - k ln2/64 (Cody-Waite, |r| <= ln2/128), e^r - 1 by its degree-5 Taylor
+// polynomial (truncation 3.5e-17), 2^(j/64) from a 64-entry LDS table, ldexp for
+// 2^(k >> 6) (denormal results round once there).  exp(0) is exactly 1.  ~12 VALU
+// slots against ~43 for the library exp whose degree-11 polynomial materialises
+// most coefficients with v_mov; <= 2 ulp.
+__device__ __constant__ const double kExp2Frac64[64] = {
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951};
+
+__device__ __forceinline__ double exp_tab(double d, const double* __restrict__ tab) {
+  const double kd = __builtin_rint(d * 92.33248261689366);  // 64 / ln 2
+  const int k = (int)kd;
+  double r = fma(kd, -0.010830424667801708, d);  // ln2/64, high 29 bits: kd * hi is exact
+  r = fma(kd, -2.8447437476627285e-11, r);       // ln2/64 - hi
+  const double r2 = r * r;
+  double q = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  q = fma(q, r, 1.0 / 6.0);
+  q = fma(q, r, 0.5);
+  const double em1 = fma(q, r2, r);
+  const double t = tab[k & 63];
+  return ldexp(fma(t, em1, t), k >> 6);
+}
+
+// Cross-lane moves on VALU (no LDS path): gfx950 v_permlane{32,16}_swap exchange the
+// upper half-wave / odd rows of one register with the lower half / even rows of another;
+// DPP row_mirror (lane ^ 15), row_half_mirror (lane ^ 7), quad_perm (lane ^ 2, ^ 1).
+__device__ __forceinline__ void swap32(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                   false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                   false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                   false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                   false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+constexpr int kDppMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
+
+template <bool MAX>
+__device__ __forceinline__ double red_op(double a, double b) {
+  return MAX ? gt_max(a, b) : a + b;
+}
+
+// Reduce-scatter of BC in {4, 8, 16} values over the wave, all on VALU.  Halving stages
+// pair lanes by bit 5, 4 (swaps: after the swap, a + b is the pair sum on every lane,
+// no selects), then bit 3 (lane ^ 15), bit 2 (lane ^ 7) with a keep/send select; the
+// remaining bits are plain butterflies.  Lane l ends with boot index
+// (l >> (6 - log2 BC)) & (BC - 1), summed over all 64 lanes (the masks 32, 16, 15, 7,
+// 2, 1 span the six lane bits).
+template <int BC, bool MAX>
+__device__ __forceinline__ double wave_reduce_scatter_v(double (&v)[BC], int lane) {
+  static_assert(BC == 4 || BC == 8 || BC == 16, "BC must be 4, 8 or 16");
+#pragma unroll
+  for (int j = 0; j < BC / 2; ++j) {
+    swap32(v[j], v[j + BC / 2]);
+    v[j] = red_op<MAX>(v[j], v[j + BC / 2]);
+  }
+#pragma unroll
+  for (int j = 0; j < BC / 4; ++j) {
+    swap16(v[j], v[j + BC / 4]);
+    v[j] = red_op<MAX>(v[j], v[j + BC / 4]);
+  }
+  if constexpr (BC >= 8) {
+    const bool up = (lane & 8) != 0;
+#pragma unroll
+    for (int j = 0; j < BC / 8; ++j) {
+      const double lo = v[j], hi = v[j + BC / 8];
+      v[j] = red_op<MAX>(up ? hi : lo, dpp_d<kDppMirror>(up ? lo : hi));
+    }
+  }
+  if constexpr (BC >= 16) {
+    const bool up = (lane & 4) != 0;
+    const double lo = v[0], hi = v[1];
+    v[0] = red_op<MAX>(up ? hi : lo, dpp_d<kDppHalfMirror>(up ? lo : hi));
+  }
+  double x = v[0];
+  if constexpr (BC <= 4) x = red_op<MAX>(x, dpp_d<kDppMirror>(x));
+  if constexpr (BC <= 8) x = red_op<MAX>(x, dpp_d<kDppHalfMirror>(x));
+  x = red_op<MAX>(x, dpp_d<kDppXor2>(x));
+  x = red_op<MAX>(x, dpp_d<kDppXor1>(x));
+  return x;
+}
+
 // Reduce-scatter the per-lane values of segment [I0, I0+BC) across the wave and park
 // the wave's partials in red[wid][I0 + idx] (no barrier here).
 template <int BC, bool MAX, int NB>
@@ -432,8 +542,8 @@ __device__ __forceinline__ void wave_partials(const double (&x)[NB], int I0, boo
   constexpr int L2 = (BC == 16) ? 4 : (BC == 8) ? 3 : (BC == 4) ? 2 : (BC == 2) ? 1 : 0;
   double t[BC];
 #pragma unroll
-  for (int i = 0; i < BC; ++i) t[i] = live ? x[I0 + i] : (MAX ? -INFINITY : 0.0);
-  const double r = wave_reduce_scatter<BC, MAX>(t, lane);
+  for (int i = 0; i < BC; ++i) t[i] = x[I0 + i];  // dead lanes hold -inf / 0 already
+  const double r = wave_reduce_scatter_v<BC, MAX>(t, lane);
   const int idx = (lane >> (6 - L2)) & (BC - 1);
   if ((lane & ((64 >> L2) - 1)) == 0) red[wid * 32 + I0 + idx] = r;
 }
@@ -474,7 +584,9 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
   constexpr int diag = SCDE_BOOT_DIAG;  // timing-only builds (tools/); 0 in production
   __shared__ double red[16 * 32];
   __shared__ double fin[32];
+  __shared__ double etab[64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  if (tid < 64) etab[tid] = kExp2Frac64[tid];  // visible after the first reduction's barrier
   const bool live = tid < G;
   const int within = blockIdx.x % (8 * P);
   const int p = within >> 3;
@@ -487,8 +599,10 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
   const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
   const double* __restrict__ Zs = Z ? Z + (long long)set * Bp * GS : nullptr;
   double acc[NB];
+  // lanes past the grid start at -inf: their pad columns are 0, so they stay -inf, never
+  // win a max and exp to 0 -- the reductions need no per-lane select
 #pragma unroll
-  for (int i = 0; i < NB; ++i) acc[i] = Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0;
+  for (int i = 0; i < NB; ++i) acc[i] = !live ? -INFINITY : (Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0);
   // Entries in batches of EB, double-buffered in registers: batch e+1's column loads are
   // in flight while batch e accumulates.  ELL rows are padded to a multiple of EB plus
   // one extra batch of zero-column entries, so the look-ahead load is unconditional.
@@ -557,7 +671,7 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
     if (diag & 4)  // timing diagnostic: no exp
       acc[i] = live ? d : 0.0;
     else
-      acc[i] = (live && d >= -746.0) ? exp(d) : 0.0;
+      acc[i] = (live && d >= -746.0) ? exp_tab(d, etab) : 0.0;
     if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
   }
   if (diag & 8) {
@@ -588,6 +702,8 @@ __global__ __launch_bounds__(512, 2) void k_boot3(const double* __restrict__ D, 
                                                   int P, int nboot, double norm_mult, double degen_thresh,
                                                   double* __restrict__ part, long long part_stride,
                                                   int* __restrict__ degen, int ngenes) {
+  __shared__ double etab[64];
+  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];  // read after the first barrier
   static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
   constexpr int GS = 512, EB = 8;
   __shared__ __attribute__((aligned(16))) double stage[2][EB][GS];
@@ -629,8 +745,10 @@ __global__ __launch_bounds__(512, 2) void k_boot3(const double* __restrict__ D, 
     }
   };
   double acc[NB];
+  // lanes past the grid start at -inf: their pad columns are 0, so they stay -inf, never
+  // win a max and exp to 0 -- the reductions need no per-lane select
 #pragma unroll
-  for (int i = 0; i < NB; ++i) acc[i] = Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0;
+  for (int i = 0; i < NB; ++i) acc[i] = !live ? -INFINITY : (Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0);
 #pragma unroll
   for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));  // materialise now: no compiler vmcnt in the loop
   issue(0, 0);
@@ -670,7 +788,7 @@ __global__ __launch_bounds__(512, 2) void k_boot3(const double* __restrict__ D, 
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const double d = acc[i] - fin[i];
-    acc[i] = (live && d >= -746.0) ? exp(d) : 0.0;
+    acc[i] = (live && d >= -746.0) ? exp_tab(d, etab) : 0.0;
     if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
   }
   block_reduce_all<false, NB>(acc, live, red, fin, lane, wid, nw);
