@@ -565,6 +565,91 @@ __device__ __forceinline__ void block_reduce_all(const double (&x)[NB], bool liv
   __syncthreads();
 }
 
+// ---- per-boot maximum in f32 (the softmax shift) ----
+// softmax(acc) is invariant to the shift; the reference subtracts the exact row max, we
+// subtract m' = (double)(f32 max).  For |m| <= 2^24 (every row that is not flagged
+// degenerate) |m - m'| <= 1, so the largest term is exp(m - m') in [1/e, e]: no overflow,
+// no loss, results equal to rounding.  Rows beyond 2^24 (including maxima below -FLT_MAX,
+// which convert to -inf) are flagged and recomputed in exact order by k_boot_exact.
+__device__ __forceinline__ void swap32f(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+__device__ __forceinline__ void swap16f(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  a = __uint_as_float(r[0]);
+  b = __uint_as_float(r[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float gt_maxf(float a, float b) { return (b > a) ? b : a; }
+
+// f32 twin of wave_reduce_scatter_v (same lane -> index mapping), max only.
+template <int BC>
+__device__ __forceinline__ float wave_max_scatter_f(float (&v)[BC], int lane) {
+  static_assert(BC == 4 || BC == 8 || BC == 16, "BC must be 4, 8 or 16");
+#pragma unroll
+  for (int j = 0; j < BC / 2; ++j) {
+    swap32f(v[j], v[j + BC / 2]);
+    v[j] = gt_maxf(v[j], v[j + BC / 2]);
+  }
+#pragma unroll
+  for (int j = 0; j < BC / 4; ++j) {
+    swap16f(v[j], v[j + BC / 4]);
+    v[j] = gt_maxf(v[j], v[j + BC / 4]);
+  }
+  if constexpr (BC >= 8) {
+    const bool up = (lane & 8) != 0;
+#pragma unroll
+    for (int j = 0; j < BC / 8; ++j) {
+      const float lo = v[j], hi = v[j + BC / 8];
+      v[j] = gt_maxf(up ? hi : lo, dpp_f<kDppMirror>(up ? lo : hi));
+    }
+  }
+  if constexpr (BC >= 16) {
+    const bool up = (lane & 4) != 0;
+    const float lo = v[0], hi = v[1];
+    v[0] = gt_maxf(up ? hi : lo, dpp_f<kDppHalfMirror>(up ? lo : hi));
+  }
+  float x = v[0];
+  if constexpr (BC <= 4) x = gt_maxf(x, dpp_f<kDppMirror>(x));
+  if constexpr (BC <= 8) x = gt_maxf(x, dpp_f<kDppHalfMirror>(x));
+  x = gt_maxf(x, dpp_f<kDppXor2>(x));
+  x = gt_maxf(x, dpp_f<kDppXor1>(x));
+  return x;
+}
+
+template <int BC, int NB>
+__device__ __forceinline__ void wave_max_partials(const double (&x)[NB], int I0, float* redf, int lane, int wid) {
+  constexpr int L2 = (BC == 16) ? 4 : (BC == 8) ? 3 : 2;
+  float t[BC];
+#pragma unroll
+  for (int i = 0; i < BC; ++i) t[i] = (float)x[I0 + i];
+  const float r = wave_max_scatter_f<BC>(t, lane);
+  const int idx = (lane >> (6 - L2)) & (BC - 1);
+  if ((lane & ((64 >> L2) - 1)) == 0) redf[wid * 32 + I0 + idx] = r;
+}
+
+// All NB boots' approximate maxima -> fin (as double).  redf: 16 x 32 floats.
+template <int NB>
+__device__ __forceinline__ void block_max_f32(const double (&x)[NB], float* redf, double* fin, int lane, int wid,
+                                              int nw) {
+#pragma unroll
+  for (int i0 = 0; i0 + 16 <= NB; i0 += 16) wave_max_partials<16, NB>(x, i0, redf, lane, wid);
+  if constexpr ((NB % 16) >= 8) wave_max_partials<8, NB>(x, NB - (NB % 16), redf, lane, wid);
+  if constexpr ((NB % 8) >= 4) wave_max_partials<4, NB>(x, NB - (NB % 8), redf, lane, wid);
+  __syncthreads();
+  if ((int)threadIdx.x < NB) {
+    float r = redf[threadIdx.x];
+    for (int w = 1; w < nw; ++w) r = gt_maxf(r, redf[w * 32 + threadIdx.x]);
+    fin[threadIdx.x] = (double)r;
+  }
+  __syncthreads();
+}
+
 // One block per (gene, boot slab of NB).  Lanes over grid points (k = threadIdx.x,
 // G <= blockDim <= GS); NB bootstrap accumulators per lane in VGPRs.  Per ELL entry
 // the NB draw multiplicities are wave-uniform (scalar loads, the FMA's SGPR operand)
@@ -608,6 +693,9 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
   // one extra batch of zero-column entries, so the look-ahead load is unconditional.
   // The multiplicities come in two boots x EB entries per scalar-load round.
   constexpr int EB = 8;
+  const int cell0 = __builtin_amdgcn_readfirstlane(E[0].x), col0 = __builtin_amdgcn_readfirstlane(E[0].y);
+  (void)cell0;
+  (void)col0;
   int cell[EB];
   double v[EB];
   auto load_batch = [&](int e0, int (&c)[EB], double (&x)[EB]) {
@@ -617,9 +705,9 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
       const int4 t = E4[j];
       c[2 * j] = t.x;
       c[2 * j + 1] = t.z;
-      if (diag & 2) {  // timing diagnostic: no column loads
-        x[2 * j] = 1e-3 * t.y;
-        x[2 * j + 1] = 1e-3 * t.w;
+      if (diag & 2) {  // timing diagnostic: every entry reads the first entry's column (loop-invariant)
+        x[2 * j] = D[(long long)col0 * GS + tid] * (1.0 + j);
+        x[2 * j + 1] = D[(long long)col0 * GS + tid] * (2.0 + j);
       } else {
         x[2 * j] = D[(long long)t.y * GS + tid];
         x[2 * j + 1] = D[(long long)t.w * GS + tid];
@@ -636,9 +724,8 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
       double2 w[EB];
 #pragma unroll
       for (int j = 0; j < EB; ++j) {
-        if (diag & 1) {  // timing diagnostic: no multiplicity loads
-          w[j].x = 1.0 + __builtin_amdgcn_readfirstlane(cell[j]);
-          w[j].y = 2.0 + __builtin_amdgcn_readfirstlane(cell[j]);
+        if (diag & 1) {  // timing diagnostic: every entry reads the first entry's multiplicities
+          w[j] = *reinterpret_cast<const double2*>(W + (long long)cell0 * Bp + b0 + i0);
         } else {
           w[j] = *reinterpret_cast<const double2*>(W + (long long)__builtin_amdgcn_readfirstlane(cell[j]) * Bp +
                                                    b0 + i0);
@@ -661,7 +748,7 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
     if (tid < NB) fin[tid] = acc[0];
     __syncthreads();
   } else {
-    block_reduce_all<true, NB>(acc, live, red, fin, lane, wid, nw);
+    block_max_f32<NB>(acc, reinterpret_cast<float*>(red), fin, lane, wid, nw);
   }
   if (tid < NB && b0 + tid < nboot && !(fabs(fin[tid]) <= degen_thresh)) degen[g] = 1;
 #pragma unroll
