@@ -97,6 +97,55 @@ __device__ inline double dnbinom_log(double x, double size, double prob) {
   return log(p) + ans;
 }
 
+// dnbinom_log for one count x and a size (theta) that is the same at every grid point:
+// the terms that depend only on (size, x) -- three stirlerr (two of them lgamma calls for
+// size < 15), the log factor and log(size/(size+x)) -- are computed once per column.
+// dnbinom_log_c then evaluates exactly dnbinom_log's operations in the same order, so the
+// result is bit-identical.
+struct NbConst {
+  double x, size, n, nx, S, lf, lp;
+  bool trivial;  // x == 0 && size == 0 -> 0; or non-finite inputs handled by dnbinom_log
+};
+
+__device__ inline NbConst nb_const(double x, double size) {
+  NbConst c;
+  c.trivial = isnan(x) || isnan(size) || size < 0 || x < 0 || !isfinite(x) || (x == 0 && size == 0);
+  x = rint(x);
+  if (!isfinite(size)) size = DBL_MAX;
+  c.x = x;
+  c.size = size;
+  c.n = x + size;           // dbinom_raw's n
+  c.nx = c.n - size;        // its n - x
+  c.S = 0.0;
+  c.lf = 0.0;
+  if (!c.trivial && size != c.n && size > 0) {
+    c.S = stirlerr(c.n) - stirlerr(size) - stirlerr(c.nx);
+    c.lf = kLn2Pi + log(size) + log1p(-size / c.n);
+  }
+  c.lp = log(size / (size + x));
+  return c;
+}
+
+__device__ inline double dnbinom_log_c(const NbConst& c, double x_in, double size_in, double prob) {
+  if (c.trivial || isnan(prob)) return dnbinom_log(x_in, size_in, prob);
+  if (prob <= 0 || prob > 1) return NAN;
+  const double X = c.size, n = c.n, p = prob, q = 1 - prob;
+  double ans;
+  if (p == 0)
+    ans = (X == 0) ? 0.0 : -INFINITY;
+  else if (q == 0)
+    ans = (X == n) ? 0.0 : -INFINITY;
+  else if (X == 0)
+    ans = (n == 0) ? 0.0 : ((p < 0.1) ? -bd0(n, n * q) - n * p : n * log(q));
+  else if (X == n)
+    ans = (q < 0.1) ? -bd0(n, n * p) - n * q : n * log(p);
+  else {
+    const double lc = c.S - bd0(X, n * p) - bd0(c.nx, n * q);
+    ans = lc - 0.5 * c.lf;
+  }
+  return c.lp + ans;
+}
+
 // log dpois(x; lambda)
 __device__ inline double dpois_log(double x, double lambda) {
   if (isnan(x) || isnan(lambda)) return x + lambda;

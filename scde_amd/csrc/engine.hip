@@ -427,6 +427,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
   ta.T = cx->T.as<double>();
   ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
   ta.has_clamp = cx->has_clamp.as<unsigned char>();
+  ta.const_theta = s.localtheta ? 0 : 1;
   ev = cx->mark_begin(SLOT_TABLES);
   HCHK(launch_tables(ta, st));
   cx->mark_end(SLOT_TABLES, ev);

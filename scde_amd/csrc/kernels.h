@@ -23,6 +23,7 @@ struct TablesArgs {
   double* T;                 // [ncols][GS] log-posterior columns
   int* maxi;                 // [ncols] argmax (nullable)
   unsigned char* has_clamp;  // [ncols]
+  int const_theta;           // theta is the same at every grid point (no local theta fit)
 };
 
 struct BootArgs {

@@ -108,6 +108,8 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const double* th = a.theta + (long long)c * a.GS;
   const double maxcfp = a.cellscal[2 * c];
   const double fp = dpois_log(x, a.cellscal[2 * c + 1]);
+  // constant theta: the (theta, x)-only terms of dnbinom once per column
+  const NbConst nc = a.const_theta ? nb_const(x, th[0]) : NbConst{};
   double v[NJ];
   double lmax = -INFINITY;
 #pragma unroll
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
       const double mnext = last ? 0.0 : mu[k + 1];
       if ((!last && x > muv && x < mnext) || (last && x > muv)) muv = x;
       const double t = th[k];
-      double nb = dnbinom_log(x, t, t / (t + muv));
+      double nb = a.const_theta ? dnbinom_log_c(nc, x, t, t / (t + muv)) : dnbinom_log(x, t, t / (t + muv));
       nb += lcfpr[k];
       v[j] = nb;
       lmax = gt_max(lmax, nb);
