@@ -1186,7 +1186,7 @@ __global__ void k_colmajor_to_rows(const double* __restrict__ src, int nrows, in
 }
 
 // ------------------------------------------------------------------ K3: ratio posterior + summary
-__global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
+__global__ __launch_bounds__(128) void k_ratio_summary(RatioArgs a) {
   extern __shared__ double sh[];
   const int n = a.n, m = 2 * a.n - 1;
   // A, B: prior-weighted rows, zero-padded by 4 so the sliding windows below may read past
@@ -1221,68 +1221,94 @@ __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
     // B (s < 0) value and one shared operand feed four independent sums.
     dd ls = {0.0, 0.0};
     for (int o = tid; o < m && a.xin; o += blockDim.x) X[o] = a.xin[(long long)g * a.xg + (long long)o * a.xo];
-    for (int o0 = tid * 4; o0 < m && !a.xin; o0 += blockDim.x * 4) {
-      const int s0 = o0 - (n - 1);
-      double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
-      if (s0 >= 0) {
-        // output r: sum_{t < n-s0-r} A[t+s0+r] B[t]; run all four to the longest (r = 0)
-        double w0 = A[s0], w1 = A[s0 + 1], w2 = A[s0 + 2], w3 = A[s0 + 3];
-        const int len = n - s0;
-        for (int t = 0; t < len; ++t) {
-          const double b = B[t];
-          c0 = __dadd_rn(c0, __dmul_rn(w0, b));
-          c1 = __dadd_rn(c1, __dmul_rn(w1, b));
-          c2 = __dadd_rn(c2, __dmul_rn(w2, b));
-          c3 = __dadd_rn(c3, __dmul_rn(w3, b));
-          w0 = w1;
-          w1 = w2;
-          w2 = w3;
-          w3 = A[t + s0 + 4];
+    // Output groups q (4 adjacent outputs each) have tent-shaped lengths; pairing q with
+    // q + ceil(NQ/2) gives every task ~n iterations, so no wave waits on a longer one.
+    const int NQ = (m + 3) / 4, halfq = (NQ + 1) / 2;
+    for (int task = tid; task < halfq && !a.xin; task += blockDim.x) {
+      for (int h = 0; h < 2; ++h) {
+        const int q = task + h * halfq;
+        if (q >= NQ) break;
+        const int o0 = 4 * q;
+        const int s0 = o0 - (n - 1);
+        double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
+        if (s0 >= 0) {
+          // output r: sum_{t < n-s0-r} A[t+s0+r] B[t]; run all four to the longest (r = 0)
+          double w0 = A[s0], w1 = A[s0 + 1], w2 = A[s0 + 2], w3 = A[s0 + 3];
+          const int len = n - s0;
+          auto step = [&](double b, double anew) {
+            c0 = __dadd_rn(c0, __dmul_rn(w0, b));
+            c1 = __dadd_rn(c1, __dmul_rn(w1, b));
+            c2 = __dadd_rn(c2, __dmul_rn(w2, b));
+            c3 = __dadd_rn(c3, __dmul_rn(w3, b));
+            w0 = w1;
+            w1 = w2;
+            w2 = w3;
+            w3 = anew;
+          };
+          int t = 0;
+          for (; t + 4 <= len; t += 4) {  // reads issued together: one LDS wait per 4 steps
+            const double b0 = B[t], b1 = B[t + 1], b2 = B[t + 2], b3 = B[t + 3];
+            const double a4 = A[t + s0 + 4], a5 = A[t + s0 + 5], a6 = A[t + s0 + 6], a7 = A[t + s0 + 7];
+            step(b0, a4);
+            step(b1, a5);
+            step(b2, a6);
+            step(b3, a7);
+          }
+          for (; t < len; ++t) step(B[t], A[t + s0 + 4]);
+        } else if (s0 + 3 < 0) {
+          // output r: sum_{t < n+s0+r} A[t] B[t-s0-r]; run all four to the longest (r = 3)
+          double w0 = B[-s0], w1 = B[-s0 - 1], w2 = B[-s0 - 2], w3 = B[-s0 - 3];
+          const int len = n + s0 + 3;
+          auto step = [&](double av, double bnew) {
+            c0 = __dadd_rn(c0, __dmul_rn(av, w0));
+            c1 = __dadd_rn(c1, __dmul_rn(av, w1));
+            c2 = __dadd_rn(c2, __dmul_rn(av, w2));
+            c3 = __dadd_rn(c3, __dmul_rn(av, w3));
+            w3 = w2;
+            w2 = w1;
+            w1 = w0;
+            w0 = bnew;
+          };
+          int t = 0;
+          for (; t + 4 <= len; t += 4) {
+            const double a0 = A[t], a1 = A[t + 1], a2 = A[t + 2], a3 = A[t + 3];
+            const double b1 = B[t + 1 - s0], b2 = B[t + 2 - s0], b3 = B[t + 3 - s0], b4 = B[t + 4 - s0];
+            step(a0, b1);
+            step(a1, b2);
+            step(a2, b3);
+            step(a3, b4);
+          }
+          for (; t < len; ++t) step(A[t], B[t + 1 - s0]);
+        } else {
+          // the group that straddles s = 0: one output at a time
+          double cc[4] = {0.0, 0.0, 0.0, 0.0};
+          for (int r = 0; r < 4; ++r) {
+            const int s = s0 + r;
+            const int o1 = s > 0 ? s : 0, o2 = s < 0 ? -s : 0;
+            const int len = n - (s < 0 ? -s : s);
+            double acc = 0.0;
+            for (int t = 0; t < len; ++t) acc = __dadd_rn(acc, __dmul_rn(A[t + o1], B[t + o2]));
+            cc[r] = acc;
+          }
+          c0 = cc[0];
+          c1 = cc[1];
+          c2 = cc[2];
+          c3 = cc[3];
         }
-      } else if (s0 + 3 < 0) {
-        // output r: sum_{t < n+s0+r} A[t] B[t-s0-r]; run all four to the longest (r = 3)
-        double w0 = B[-s0], w1 = B[-s0 - 1], w2 = B[-s0 - 2], w3 = B[-s0 - 3];
-        const int len = n + s0 + 3;
-        for (int t = 0; t < len; ++t) {
-          const double av = A[t];
-          c0 = __dadd_rn(c0, __dmul_rn(av, w0));
-          c1 = __dadd_rn(c1, __dmul_rn(av, w1));
-          c2 = __dadd_rn(c2, __dmul_rn(av, w2));
-          c3 = __dadd_rn(c3, __dmul_rn(av, w3));
-          w3 = w2;
-          w2 = w1;
-          w1 = w0;
-          w0 = B[t + 1 - s0];
+        X[o0] = c0;
+        ls = dd_add_d(ls, c0);
+        if (o0 + 1 < m) {
+          X[o0 + 1] = c1;
+          ls = dd_add_d(ls, c1);
         }
-      } else {
-        // the group that straddles s = 0: one output at a time
-        double cc[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int r = 0; r < 4; ++r) {
-          const int s = s0 + r;
-          const int o1 = s > 0 ? s : 0, o2 = s < 0 ? -s : 0;
-          const int len = n - (s < 0 ? -s : s);
-          double acc = 0.0;
-          for (int t = 0; t < len; ++t) acc = __dadd_rn(acc, __dmul_rn(A[t + o1], B[t + o2]));
-          cc[r] = acc;
+        if (o0 + 2 < m) {
+          X[o0 + 2] = c2;
+          ls = dd_add_d(ls, c2);
         }
-        c0 = cc[0];
-        c1 = cc[1];
-        c2 = cc[2];
-        c3 = cc[3];
-      }
-      X[o0] = c0;
-      ls = dd_add_d(ls, c0);
-      if (o0 + 1 < m) {
-        X[o0 + 1] = c1;
-        ls = dd_add_d(ls, c1);
-      }
-      if (o0 + 2 < m) {
-        X[o0 + 2] = c2;
-        ls = dd_add_d(ls, c2);
-      }
-      if (o0 + 3 < m) {
-        X[o0 + 3] = c3;
-        ls = dd_add_d(ls, c3);
+        if (o0 + 3 < m) {
+          X[o0 + 3] = c3;
+          ls = dd_add_d(ls, c3);
+        }
       }
     }
     // row sum (R rowSums accumulates in long double): double-double block reduce
@@ -1683,7 +1709,7 @@ hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const size_t shm = sizeof(double) * (size_t)(2 * (a.n + 4) + (2 * a.n - 1) + 48);
   const int grid = a.ngenes < 65536 ? a.ngenes : 65536;
-  hipLaunchKernelGGL(k_ratio_summary, dim3(grid), dim3(256), shm, s, a);
+  hipLaunchKernelGGL(k_ratio_summary, dim3(grid), dim3(128), shm, s, a);
   return hipGetLastError();
 }
 
