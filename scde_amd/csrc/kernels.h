@@ -1,6 +1,9 @@
 // kernels.h -- argument blocks and launchers for kernels.hip (internal).
 #pragma once
 
+#ifndef SCDE_BOOT_EB
+#define SCDE_BOOT_EB 4  // ELL entries per k_boot2 batch (rows are padded to a multiple of 8, plus 8)
+#endif
 #ifndef SCDE_BOOT_DIAG
 #define SCDE_BOOT_DIAG 0  // bit switches that remove parts of k_boot2 for timing studies
 #endif

@@ -694,7 +694,7 @@ __global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, co
   // in flight while batch e accumulates.  ELL rows are padded to a multiple of EB plus
   // one extra batch of zero-column entries, so the look-ahead load is unconditional.
   // The multiplicities come in two boots x EB entries per scalar-load round.
-  constexpr int EB = 8;
+  constexpr int EB = SCDE_BOOT_EB;
   const int cell0 = __builtin_amdgcn_readfirstlane(E[0].x), col0 = __builtin_amdgcn_readfirstlane(E[0].y);
   (void)cell0;
   (void)col0;
