@@ -1,6 +1,9 @@
 // kernels.h -- argument blocks and launchers for kernels.hip (internal).
 #pragma once
 
+#ifndef SCDE_BOOT_WPE
+#define SCDE_BOOT_WPE 8  // k_boot2 (NB <= 20) occupancy target: 8 waves per SIMD = 64 VGPRs
+#endif
 #ifndef SCDE_BOOT_EB
 #define SCDE_BOOT_EB 4  // ELL entries per k_boot2 batch (rows are padded to a multiple of 8, plus 8)
 #endif

@@ -660,7 +660,7 @@ __device__ __forceinline__ void block_max_f32(const double (&x)[NB], float* redf
 // share the gene's columns in L2; each writes a partial jp row, summed in slab order
 // by k_sum_partials.
 template <int NB>
-__global__ __launch_bounds__(1024) void k_boot2(const double* __restrict__ D, const int2* __restrict__ ent,
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ? SCDE_BOOT_WPE : 1))) void k_boot2(const double* __restrict__ D, const int2* __restrict__ ent,
                                                 const int* __restrict__ nnz, int ent_stride,
                                                 const double* __restrict__ Wt, int Bp, int ncells,
                                                 const int* __restrict__ wset, const double* __restrict__ Z, int G,
