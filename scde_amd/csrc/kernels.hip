@@ -93,6 +93,9 @@ template <int NJ>
 __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const int lane = threadIdx.x & 63;
   const long long col = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ double etab[64];
+  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
+  __syncthreads();
   if (col >= a.ncols) return;
   int lo = 0, hi = a.ncells;
   while (hi - lo > 1) {
@@ -137,7 +140,9 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   for (int j = 0; j < NJ; ++j) {
     const int k = lane + 64 * j;
     if (k < G) {
-      v[j] = exp(v[j] - maxp) + exp(lcfp[k] + fp - maxp);
+      // both arguments are <= 0 (maxp bounds them); exp_tab below -746 would underflow anyway
+      const double d1 = v[j] - maxp, d2 = lcfp[k] + fp - maxp;
+      v[j] = (d1 >= -746.0 ? exp_tab(d1, etab) : 0.0) + (d2 >= -746.0 ? exp_tab(d2, etab) : 0.0);
       ls += v[j];
     }
   }
@@ -426,44 +431,6 @@ __global__ __launch_bounds__(1024) void k_boot(BootArgs a) {
 }
 
 // ------------------------------------------------------------------ K2 (fast path)
-// Softmax exp for d in [-746, 0]: exp(d) = 2^(k/64) * e^r, k = rint(64 d / ln 2),
-// r = d - k ln2/64 (Cody-Waite, |r| <= ln2/128), e^r - 1 by its degree-5 Taylor
-// polynomial (truncation 3.5e-17), 2^(j/64) from a 64-entry LDS table, ldexp for
-// 2^(k >> 6) (denormal results round once there).  exp(0) is exactly 1.  ~12 VALU
-// slots against ~43 for the library exp whose degree-11 polynomial materialises
-// most coefficients with v_mov; <= 2 ulp.
-__device__ __constant__ const double kExp2Frac64[64] = {
-    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
-    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
-    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
-    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
-    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
-    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
-    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
-    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
-    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
-    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
-    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
-    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
-    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
-    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
-    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
-    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951};
-
-__device__ __forceinline__ double exp_tab(double d, const double* __restrict__ tab) {
-  const double kd = __builtin_rint(d * 92.33248261689366);  // 64 / ln 2
-  const int k = (int)kd;
-  double r = fma(kd, -0.010830424667801708, d);  // ln2/64, high 29 bits: kd * hi is exact
-  r = fma(kd, -2.8447437476627285e-11, r);       // ln2/64 - hi
-  const double r2 = r * r;
-  double q = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  q = fma(q, r, 1.0 / 6.0);
-  q = fma(q, r, 0.5);
-  const double em1 = fma(q, r2, r);
-  const double t = tab[k & 63];
-  return ldexp(fma(t, em1, t), k >> 6);
-}
-
 // Cross-lane moves on VALU (no LDS path): gfx950 v_permlane{32,16}_swap exchange the
 // upper half-wave / odd rows of one register with the lower half / even rows of another;
 // DPP row_mirror (lane ^ 15), row_half_mirror (lane ^ 7), quad_perm (lane ^ 2, ^ 1).
