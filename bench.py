@@ -1,20 +1,26 @@
 """bench.py -- genes/sec for scde.expression.difference (401-pt grid, 100 randomizations).
 
-Workload (BASELINE.json configs[1]): synthetic 20,000 genes x 200 cells (100/100 groups),
-400-point prior (G = 401 grid points), n.randomizations = 100, reference seeding n.cores = 1.
-One step = one scde.expression.difference pass over the batch on counts resident in HBM:
-unique-count tables, per-cell NB/Poisson log-posterior tables, bootstrap joint posteriors
-for both groups, ratio posterior + lb/mle/ub/ce/Z summary, results to host, BH cZ.
+Default workload (BASELINE.json configs[1] = SURVEY.md §8(d) config 2): synthetic 20,000 genes
+x 200 cells (100/100 groups), 400-point prior (G = 401 grid points), n.randomizations = 100,
+reference seeding n.cores = 1.  One step = one scde.expression.difference pass over the batch
+on counts resident in HBM: unique-count tables, per-cell NB/Poisson log-posterior tables,
+bootstrap joint posteriors for both groups, ratio posterior + lb/mle/ub/ce/Z summary, BH cZ,
+results to host.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): genes shard across
-ranks with a fixed 20,000 genes per rank (weak scaling); the one exchange is a gather
-of per-gene Z to rank 0 (RCCL) for the global BH adjustment.
+--config 3: 20,000 genes x 1,000 cells (500/500), the north_star's headline shape.
+--config 4: scde.posteriors(return.individual.posterior.modes = TRUE) on 30,000 genes x 2,000
+cells (one group); one step returns jp (N x 401) and modes (N x 2000) to the host.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): genes shard across ranks
+with a fixed gene count per rank (weak scaling); the one exchange is a gather of per-gene Z
+to rank 0 (RCCL) for the global BH adjustment, done there on the device.
 
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -25,14 +31,25 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-N_GENES = 20000
-N_CELLS = 200
 NBOOT = 100
 LENGTH_OUT = 400
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+METRIC = "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)"
+
+CONFIGS = {
+    2: dict(genes=20000, cells=200, seed=2002, kind="de", cpu_sample=5000,
+            workload="config2: synthetic 20000 genes x 200 cells (100/100), 401-pt grid, 100 bootstraps, "
+                     "n.cores=1 seeding"),
+    3: dict(genes=20000, cells=1000, seed=2003, kind="de", cpu_sample=1000,
+            workload="config3: synthetic 20000 genes x 1000 cells (500/500), 401-pt grid, 100 bootstraps, "
+                     "n.cores=1 seeding"),
+    4: dict(genes=30000, cells=2000, seed=2004, kind="posteriors", cpu_sample=100,
+            workload="config4: scde.posteriors, synthetic 30000 genes x 2000 cells (one group), 401-pt grid, "
+                     "100 bootstraps, return.individual.posterior.modes, n.cores=1 seeding"),
+}
 
 
-def synthetic(seed: int, ngenes=N_GENES, ncells=N_CELLS):
+def synthetic(seed: int, ngenes: int, ncells: int, two_groups: bool = True):
     """SURVEY.md §8(d) generator: o.ifm-resampled models, log-FPM ~ N(2.5, 2), 10% DE genes,
     NB/Poisson-mixture counts with the models' own dropout curve."""
     g = np.load(os.path.join(ROOT, "tests", "golden", "esmef500.npz"), allow_pickle=False)
@@ -42,7 +59,7 @@ def synthetic(seed: int, ngenes=N_GENES, ncells=N_CELLS):
     rows = rng.integers(0, base.shape[0], ncells)
     mm = base[rows]
     models = {c: mm[:, j] for j, c in enumerate(MODEL_COLUMNS) if not np.all(np.isnan(mm[:, j]))}
-    groups = np.repeat([0, 1], ncells // 2).astype(np.int32)
+    groups = np.repeat([0, 1], ncells // 2).astype(np.int32) if two_groups else np.zeros(ncells, np.int32)
     m = rng.normal(2.5, 2.0, ngenes)
     shift = np.where(rng.random(ngenes) < 0.1, rng.normal(0, 1.5, ngenes), 0.0)
     M = m[:, None] + shift[:, None] * groups[None, :]
@@ -82,12 +99,16 @@ def profiled_traffic():
             "traffic_bytes": e.get("traffic_bytes")}
 
 
-def cpu_baseline(models, counts, groups, prior, sample_genes):
+def cpu_baseline(cfg, models, counts, groups, prior, sample_genes):
     """The oracle (C restatement of the reference loops, 1 core) on a bounded gene sample."""
     from oracle import oracle as O
     sub = np.ascontiguousarray(counts[:sample_genes])
     t0 = time.perf_counter()
-    O.scde_expression_difference(models, sub, prior["x"], prior["y"], groups, n_randomizations=NBOOT, n_cores=1)
+    if cfg["kind"] == "de":
+        O.scde_expression_difference(models, sub, prior["x"], prior["y"], groups, n_randomizations=NBOOT, n_cores=1)
+    else:
+        O.scde_posteriors(models, sub, prior["x"], n_randomizations=NBOOT, return_individual_posterior_modes=True,
+                          n_cores=1)
     dt = time.perf_counter() - t0
     return sample_genes / dt, dt
 
@@ -97,9 +118,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cpu-sample", type=int, default=5000, help="genes timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-sample", type=int, default=None, help="genes timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true")
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    NG, NC = cfg["genes"], cfg["cells"]
+    cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -112,28 +137,39 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     from scde_amd import api
+    from scde_amd.models import model_matrix
     from scde_amd.prior import expression_prior
 
-    models, counts, groups = synthetic(2002 + rank)
+    de = cfg["kind"] == "de"
+    models, counts, groups = synthetic(cfg["seed"] + rank, NG, NC, two_groups=de)
     zero_frac = float(np.mean(counts == 0))
     prior = expression_prior(models, counts, length_out=LENGTH_OUT)
     ctx = api.Context(local_rank)
     dc = api.DeviceCounts(ctx, counts)
-    from scde_amd.models import model_matrix
     mm, lt, sq = model_matrix(models)
     px = np.ascontiguousarray(prior["x"], np.float64)
     py = np.ascontiguousarray(prior["y"], np.float64)
     codes = np.ascontiguousarray(groups, np.int32)
     G = len(px)
-    # one rank: cZ (BH) in the same call on device; several: Z gathered to rank 0, BH there
-    params = api.DEParams(N_CELLS, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
-                          NBOOT, 1, rank * N_GENES, world * N_GENES, 0.0, api.get_rand_kind(), int(world == 1))
-    res = np.zeros((N_GENES, 6 if world == 1 else 5), order="F")
     L = api.lib()
-    import ctypes
+    P = api._p
+    if de:
+        # one rank: cZ (BH) in the same call on device; several: Z gathered to rank 0, BH there
+        params = api.DEParams(NC, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
+                              NBOOT, 1, rank * NG, world * NG, 0.0, api.get_rand_kind(), int(world == 1))
+        res = np.zeros((NG, 6 if world == 1 else 5), order="F")
+    else:
+        cellidx = np.arange(NC, dtype=np.int32)
+        jp = np.zeros((NG, G), order="F")
+        modes = np.zeros((NG, NC), order="F")
 
     def step():
-        api.check(L.scde_expression_difference_dev(ctx.handle, dc.ptr, N_GENES, N_GENES, ctypes.byref(params),
+        if not de:
+            api.check(L.scde_posteriors_dev(ctx.handle, dc.ptr, NG, NG, P(cellidx), NC, P(mm), lt, sq, P(px), G, NBOOT,
+                                            1, rank * NG, world * NG, 1, 0, None, None, None, 0, P(jp), P(modes),
+                                            None))
+            return
+        api.check(L.scde_expression_difference_dev(ctx.handle, dc.ptr, NG, NG, ctypes.byref(params),
                                                    res.ctypes.data_as(ctypes.c_void_p), None, None, None))
         if dist is not None:
             import torch
@@ -172,17 +208,19 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
-    total_genes = N_GENES * world * args.steps
+    total_genes = NG * world * args.steps
     value = total_genes / dt
     boot_ms, boot_n = kt["boot"]
     boot_avg_s = (boot_ms / max(boot_n, 1)) / 1e3
-    per_launch_bytes = dominant_kernel_bytes(N_GENES, N_CELLS // 2)
+    cpg = NC // 2 if de else NC
+    per_launch_bytes = dominant_kernel_bytes(NG, cpg)
     achieved = per_launch_bytes / boot_avg_s / 1e9 if boot_n else None
-    prof = profiled_traffic()
+    prof = profiled_traffic() if args.config == 2 else None
     # reference-formulation FP64 adds per launch: B x C x G x N
-    ref_adds = NBOOT * (N_CELLS // 2) * G * N_GENES
+    ref_adds = NBOOT * cpg * G * NG
     out = {
-        "metric": "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)",
+        "metric": METRIC if de else "genes/sec for scde.posteriors with posterior modes (400-pt grid, "
+                                    "100 randomizations)",
         "value": value,
         "unit": "genes/s",
         "n_gpus": world,
@@ -193,11 +231,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": f"synthetic (PCG64 seed 2002+rank; o.ifm-resampled models; zero fraction {zero_frac:.3f})",
-        "config": {"workload": "config2: synthetic 20000 genes x 200 cells (100/100), 401-pt grid, "
-                               "100 bootstraps, n.cores=1 seeding", "genes_per_gpu": N_GENES, "cells": N_CELLS,
-                   "grid": G, "n_randomizations": NBOOT, "parallelism": f"gene-shard x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_boot (bootstrap joint posterior)",
+        "data": f"synthetic (PCG64 seed {cfg['seed']}+rank; o.ifm-resampled models; zero fraction {zero_frac:.3f})",
+        "config": {"workload": cfg["workload"], "genes_per_gpu": NG, "cells": NC, "grid": G,
+                   "n_randomizations": NBOOT, "parallelism": f"gene-shard x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_boot2 (bootstrap joint posterior)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
                      "traffic": prof["traffic_bytes"] if prof else None,
@@ -208,9 +245,9 @@ def main():
                      "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None},
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
     }
-    if rank == 0 and world == 1 and not args.no_profile:
+    if rank == 0 and world == 1 and de and not args.no_profile:
         # PCIe-inclusive rate through the host-buffer API (counts uploaded, table incl. cZ
-        # returned per call) -- reported beside `value`, never as it (DESIGN.md §6).
+        # returned per call) -- reported beside `value`, never as it (DESIGN.md §5).
         ctx.set_profiling(False)
         api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
                                        n_cores=1, ctx=ctx)
@@ -218,12 +255,13 @@ def main():
         for _ in range(3):
             api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
                                            n_cores=1, ctx=ctx)
-        out["host_buffers_genes_per_s"] = 3 * N_GENES / (time.perf_counter() - t1)
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        gps, secs = cpu_baseline(models, counts, groups, prior, args.cpu_sample)
+        out["host_buffers_genes_per_s"] = 3 * NG / (time.perf_counter() - t1)
+    if rank == 0 and world == 1 and cpu_sample > 0:
+        gps, secs = cpu_baseline(cfg, models, counts, groups, prior, cpu_sample)
+        what = "both groups + ratio + summary + BH" if de else "posteriors + modes"
         out["cpu_baseline"] = {"value": gps, "unit": "genes/s", "cores": 1, "kind": "port",
-                               "sample": f"oracle C restatement, first {args.cpu_sample} genes of the same batch, "
-                                         f"both groups + ratio + summary + BH, {secs:.1f}s"}
+                               "sample": f"oracle C restatement, first {cpu_sample} genes of the same batch, "
+                                         f"{what}, {secs:.1f}s"}
     if rank == 0:
         print(json.dumps(out))
     dc.free()
