@@ -52,9 +52,12 @@ __device__ inline double stirlerr(double n) {
 }
 
 // deviance term bd0(x, np) = x log(x/np) + np - x, Taylor form near x == np
+#ifndef SCDE_TABLES_DIAG
+#define SCDE_TABLES_DIAG 0  // timing-only builds: 1 = bd0 without its series, 2 = trivial dnbinom
+#endif
 __device__ inline double bd0(double x, double np) {
   if (!isfinite(x) || !isfinite(np) || np == 0.0) return NAN;
-  if (fabs(x - np) < 0.1 * (x + np)) {
+  if (!(SCDE_TABLES_DIAG & 1) && fabs(x - np) < 0.1 * (x + np)) {
     double v = (x - np) / (x + np);
     double s = (x - np) * v;
     if (fabs(s) < DBL_MIN) return s;
@@ -127,6 +130,7 @@ __device__ inline NbConst nb_const(double x, double size) {
 }
 
 __device__ inline double dnbinom_log_c(const NbConst& c, double x_in, double size_in, double prob) {
+  if (SCDE_TABLES_DIAG & 2) return c.lp - prob * c.S;
   if (c.trivial || isnan(prob)) return dnbinom_log(x_in, size_in, prob);
   if (prob <= 0 || prob > 1) return NAN;
   const double X = c.size, n = c.n, p = prob, q = 1 - prob;

@@ -206,21 +206,35 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
 
 // Per-gene ELL list of explicit (cell, column) entries, cell order ascending; rows
 // have `stride` slots and are padded up to a multiple of 8 with (0, pad_col).
-__global__ void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes, int ncells,
-                      const long long* __restrict__ ucl_off, const int* __restrict__ base_col, int stride,
-                      int pad_col, int2* __restrict__ ent, int* __restrict__ nnz) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+// One wavefront per gene, lanes over cells: each 64-cell step ballots the cells whose
+// count is not the baseline and writes their (cell, column) pairs contiguously (mbcnt
+// prefix), keeping the cell order.  The row is padded with zero-column entries to a
+// multiple of 8 plus one more batch of 8 (the k_boot2 look-ahead).
+__global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
+                                             int ncells, const long long* __restrict__ ucl_off,
+                                             const int* __restrict__ base_col, int stride, int pad_col,
+                                             int2* __restrict__ ent, int* __restrict__ nnz) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= ngenes) return;
-  int n = 0;
   int2* E = ent + (long long)g * stride;
-  for (int c = 0; c < ncells; ++c) {
-    const int col = (int)(ucl_off[c] + uci[(long long)g + ld_uci * c]);
-    if (col == base_col[c]) continue;
-    E[n++] = make_int2(c, col);
+  int n = 0;
+  for (int c0 = 0; c0 < ncells; c0 += 64) {
+    const int c = c0 + lane;
+    int col = -1;
+    bool keep = false;
+    if (c < ncells) {
+      col = (int)(ucl_off[c] + uci[(long long)g + ld_uci * c]);
+      keep = col != base_col[c];
+    }
+    const unsigned long long m = __ballot(keep);
+    const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+    if (keep) E[pos] = make_int2(c, col);
+    n += __popcll(m);
   }
-  nnz[g] = n;
-  // pad to a multiple of 8 plus one more batch of 8 (the k_boot2 look-ahead)
-  for (int p = n; p < ((n + 7) & ~7) + 8 && p < stride; ++p) E[p] = make_int2(0, pad_col);
+  if (lane == 0) nnz[g] = n;
+  const int end = ((n + 7) & ~7) + 8;
+  for (int p = n + lane; p < end && p < stride; p += 64) E[p] = make_int2(0, pad_col);
 }
 
 // D[col] = T[col] - T[baseline column of its cell] (or T[col] when the cell has no
@@ -252,19 +266,25 @@ __global__ __launch_bounds__(512) void k_baseline_z(const double* __restrict__ T
                                                     const int* __restrict__ base_col, int ncells,
                                                     const double* __restrict__ Wt, int Bp,
                                                     double* __restrict__ Z) {
+  // four interleaved partial sums (cells c = 4i + r) keep four FMA chains in flight
   const int b = blockIdx.x, set = blockIdx.y;
   const double* W = Wt + (long long)set * ncells * Bp;
   for (int k = threadIdx.x; k < GS; k += blockDim.x) {
-    double z = 0.0;
+    double z[4] = {0.0, 0.0, 0.0, 0.0};
     if (k < G) {
-      for (int c = 0; c < ncells; ++c) {
-        const int bc = base_col[c];
-        if (bc < 0) continue;
-        const double w = W[(long long)c * Bp + b];
-        if (w != 0.0) z = fma(w, T[(long long)bc * GS + k], z);
+      for (int c0 = 0; c0 < ncells; c0 += 4) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = c0 + r;
+          if (c >= ncells) break;
+          const int bc = base_col[c];
+          if (bc < 0) continue;
+          const double w = W[(long long)c * Bp + b];
+          if (w != 0.0) z[r] = fma(w, T[(long long)bc * GS + k], z[r]);
+        }
       }
     }
-    Z[((long long)set * Bp + b) * GS + k] = z;
+    Z[((long long)set * Bp + b) * GS + k] = (z[0] + z[1]) + (z[2] + z[3]);
   }
 }
 
@@ -1478,7 +1498,7 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
                       const int* base_col, int stride, int pad_col, int2* ent, int* nnz, hipStream_t s) {
   if (ngenes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 128)), dim3(128), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
+  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 4)), dim3(256), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
                      base_col, stride, pad_col, ent, nnz);
   return hipGetLastError();
 }
