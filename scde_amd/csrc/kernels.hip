@@ -89,11 +89,17 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
 }
 
 // ------------------------------------------------------------------ K1: tables
-template <int NJ>
+// One wavefront per (cell, unique count) column; lanes over grid points.  The per-point
+// values live in a per-wave LDS row (not a register array), so the grid loops stay rolled:
+// one dnbinom body per kernel instead of one per unrolled point (the unrolled form was
+// ~12k instructions with lgamma inlined 8x).  CT: theta is the same at every grid point,
+// and the (theta, count)-only terms of dnbinom are computed once per column.
+template <bool CT>
 __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
-  const int lane = threadIdx.x & 63;
-  const long long col = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  extern __shared__ double vrow[];  // [4 waves][GS]
   __shared__ double etab[64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const long long col = (long long)blockIdx.x * 4 + wid;
   if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
   __syncthreads();
   if (col >= a.ncols) return;
@@ -111,61 +117,51 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const double* th = a.theta + (long long)c * a.GS;
   const double maxcfp = a.cellscal[2 * c];
   const double fp = dpois_log(x, a.cellscal[2 * c + 1]);
-  // constant theta: the (theta, x)-only terms of dnbinom once per column
-  const NbConst nc = a.const_theta ? nb_const(x, th[0]) : NbConst{};
-  double v[NJ];
+  const NbConst nc = CT ? nb_const(x, th[0]) : NbConst{};
+  double* v = vrow + (long long)wid * a.GS;
   double lmax = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k = lane + 64 * j;
-    v[j] = -INFINITY;
-    if (k < G) {
-      double muv = mu[k];
-      const bool last = (k == G - 1);
-      const double mnext = last ? 0.0 : mu[k + 1];
-      if ((!last && x > muv && x < mnext) || (last && x > muv)) muv = x;
-      const double t = th[k];
-      double nb = a.const_theta ? dnbinom_log_c(nc, x, t, t / (t + muv)) : dnbinom_log(x, t, t / (t + muv));
-      nb += lcfpr[k];
-      v[j] = nb;
-      lmax = gt_max(lmax, nb);
-    }
+#pragma unroll 1
+  for (int k = lane; k < G; k += 64) {
+    double muv = mu[k];
+    const bool last = (k == G - 1);
+    const double mnext = last ? 0.0 : mu[k + 1];
+    if ((!last && x > muv && x < mnext) || (last && x > muv)) muv = x;
+    const double t = th[k];
+    double nb = CT ? dnbinom_log_c(nc, x, t, t / (t + muv)) : dnbinom_log(x, t, t / (t + muv));
+    nb += lcfpr[k];
+    v[k] = nb;
+    lmax = gt_max(lmax, nb);
   }
   double maxp = lmax;
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) maxp = gt_max(maxp, __shfl_xor(maxp, m, 64));
   if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
   double ls = 0.0;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k = lane + 64 * j;
-    if (k < G) {
-      // both arguments are <= 0 (maxp bounds them); exp_tab below -746 would underflow anyway
-      const double d1 = v[j] - maxp, d2 = lcfp[k] + fp - maxp;
-      v[j] = (d1 >= -746.0 ? exp_tab(d1, etab) : 0.0) + (d2 >= -746.0 ? exp_tab(d2, etab) : 0.0);
-      ls += v[j];
-    }
+#pragma unroll 1
+  for (int k = lane; k < G; k += 64) {
+    // both arguments are <= 0 (maxp bounds them); exp_tab below -746 would underflow anyway
+    const double d1 = v[k] - maxp, d2 = lcfp[k] + fp - maxp;
+    const double e = (d1 >= -746.0 ? exp_tab(d1, etab) : 0.0) + (d2 >= -746.0 ? exp_tab(d2, etab) : 0.0);
+    v[k] = e;
+    ls += e;
   }
   const double s = wave_sum(ls);
   double bv = -INFINITY;
   int bi = 0x7fffffff;
   bool clamp = false;
   double* out = a.T + col * a.GS;
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) {
-    const int k = lane + 64 * j;
-    if (k < G) {
-      double r = log(v[j] / s);
-      if (r > bv) {
-        bv = r;
-        bi = k;
-      }
-      if (r < a.minlogprob) {
-        r = a.minlogprob;
-        clamp = true;
-      }
-      out[k] = r;
+#pragma unroll 1
+  for (int k = lane; k < G; k += 64) {
+    double r = log(v[k] / s);
+    if (r > bv) {
+      bv = r;
+      bi = k;
     }
+    if (r < a.minlogprob) {
+      r = a.minlogprob;
+      clamp = true;
+    }
+    out[k] = r;
   }
   if (a.maxi) {
     // first maximum over the grid (Armadillo max(index), strict '>')
@@ -1475,15 +1471,12 @@ hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, con
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   if (a.ncols <= 0) return hipSuccess;
   const dim3 grid(div_up(a.ncols, 4)), block(256);
-  const int nj = (a.G + 63) / 64;
-  if (nj <= 8)
-    hipLaunchKernelGGL(k_tables<8>, grid, block, 0, s, a);
-  else if (nj <= 16)
-    hipLaunchKernelGGL(k_tables<16>, grid, block, 0, s, a);
-  else if (nj <= 32)
-    hipLaunchKernelGGL(k_tables<32>, grid, block, 0, s, a);
+  const size_t shm = sizeof(double) * 4 * (size_t)a.GS;
+  if (shm > 64 * 1024) return hipErrorInvalidValue;
+  if (a.const_theta)
+    hipLaunchKernelGGL(k_tables<true>, grid, block, shm, s, a);
   else
-    return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_tables<false>, grid, block, shm, s, a);
   return hipGetLastError();
 }
 
