@@ -152,9 +152,20 @@ struct scde_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   // workspace
-  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, ucl, ucl_off, T, E, maxi, has_clamp, base_col, ent, nnz, Wt,
-      Z, draws, degen, uci, cellidx, cmax, cmin, woff, bits, rank, nuniq, wset, prior_y, diffv, jpA, jpB, res,
-      ratio, in1, in2, outbuf, part, bhw;
+  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, T, E, maxi, has_clamp, base_col, ent, nnz, Wt, Z, draws,
+      degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
+  // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
+  // unique tables can be built up front, with their host syncs, before the heavy kernels
+  struct UniqueSet {
+    Buf cellidx, cmax, cmin, woff, bits, rank, nuniq, ucl, ucl_off, uci;
+    std::vector<int> cmax_h, cmin_h, nuniq_h;
+    std::vector<long long> woff_h, ucl_off_h;
+    bool ready = false;
+    void release() {
+      Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci};
+      for (Buf* x : b) x->release();
+    }
+  } us[2];
   // profiling
   bool profile = false;
   struct Pending {
@@ -205,11 +216,11 @@ struct scde_ctx {
     return SCDE_OK;
   }
   ~scde_ctx() {
-    Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,   &cellscal, &ucl,   &ucl_off, &T,   &E,
-                  &maxi,   &has_clamp, &base_col, &ent, &nnz, &Wt, &Z, &draws, &degen, &uci, &cellidx,
-                  &cmax,   &cmin, &woff, &bits, &rank, &nuniq, &wset, &prior_y, &diffv, &jpA, &jpB, &res,
-                  &ratio,  &in1, &in2, &outbuf, &part, &bhw};
+    Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &T,      &E,      &maxi,
+                  &has_clamp, &base_col, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
+                  &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw};
     for (Buf* b : all) b->release();
+    for (auto& u : us) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
     for (auto& p : pending) {
       (void)hipEventDestroy(p.a);
@@ -267,46 +278,72 @@ int upload(scde_ctx* cx, Buf& b, const void* src, size_t bytes) {
 
 // Build ucl/uci for the selected cells on device (R/functions.R:609-610).  Unique
 // counts come out sorted ascending rather than in first-appearance order; the order
-// only permutes table columns, never values.
-int build_unique_device(scde_ctx* cx, const PostSpec& s, std::vector<long long>& ucl_off_h) {
+// only permutes table columns, never values.  Three phases separated by host syncs
+// (bitmap sizes need the per-cell maxima; column offsets need the unique counts);
+// build_unique_pair interleaves two groups' phases so a DE call syncs twice, not four
+// times, and before any heavy kernel is queued.
+using UniqueSet = scde_ctx::UniqueSet;
+
+int unique_phase1(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, N = s.ngenes;
   hipStream_t st = cx->stream;
-  hipEvent_t ev = cx->mark_begin(SLOT_UNIQUE);
-  RCHK(upload(cx, cx->cellidx, s.cellidx_host, sizeof(int) * C));
-  HCHK(cx->cmax.ensure(sizeof(int) * C));
-  HCHK(cx->cmin.ensure(sizeof(int) * C));
-  HCHK(launch_cell_minmax(s.counts_dev, s.ld, 0, N, C, cx->cellidx.as<int>(), cx->cmax.as<int>(),
-                          cx->cmin.as<int>(), st));
-  std::vector<int> cmax(C), cmin(C);
-  HCHK(hipMemcpyAsync(cmax.data(), cx->cmax.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
-  HCHK(hipMemcpyAsync(cmin.data(), cx->cmin.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
-  HCHK(hipStreamSynchronize(st));
-  std::vector<long long> woff(C + 1, 0);
+  RCHK(upload(cx, u.cellidx, s.cellidx_host, sizeof(int) * C));
+  HCHK(u.cmax.ensure(sizeof(int) * C));
+  HCHK(u.cmin.ensure(sizeof(int) * C));
+  HCHK(launch_cell_minmax(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.cmax.as<int>(), u.cmin.as<int>(), st));
+  u.cmax_h.assign(C, 0);
+  u.cmin_h.assign(C, 0);
+  HCHK(hipMemcpyAsync(u.cmax_h.data(), u.cmax.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  HCHK(hipMemcpyAsync(u.cmin_h.data(), u.cmin.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  return SCDE_OK;
+}
+
+int unique_phase2(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
+  const int C = s.ncells, N = s.ngenes;
+  hipStream_t st = cx->stream;
+  u.woff_h.assign(C + 1, 0);
   for (int c = 0; c < C; ++c) {
-    if (N > 0 && cmin[c] < 0) return fail(SCDE_EARG, "negative count in cell %d", c);
-    woff[c + 1] = woff[c] + ((long long)cmax[c] >> 6) + 1;
+    if (N > 0 && u.cmin_h[c] < 0) return fail(SCDE_EARG, "negative count in cell %d", c);
+    u.woff_h[c + 1] = u.woff_h[c] + ((long long)u.cmax_h[c] >> 6) + 1;
   }
-  RCHK(upload(cx, cx->woff, woff.data(), sizeof(long long) * (C + 1)));
-  HCHK(cx->bits.ensure(sizeof(unsigned long long) * woff[C]));
-  HCHK(hipMemsetAsync(cx->bits.p, 0, sizeof(unsigned long long) * woff[C], st));
-  HCHK(launch_mark(s.counts_dev, s.ld, 0, N, C, cx->cellidx.as<int>(), cx->woff.as<long long>(),
-                   cx->bits.as<unsigned long long>(), st));
-  HCHK(cx->rank.ensure(sizeof(int) * woff[C]));
-  HCHK(cx->nuniq.ensure(sizeof(int) * C));
-  HCHK(launch_rank(cx->bits.as<unsigned long long>(), cx->woff.as<long long>(), C, cx->rank.as<int>(),
-                   cx->nuniq.as<int>(), st));
-  std::vector<int> nuniq(C);
-  HCHK(hipMemcpyAsync(nuniq.data(), cx->nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
-  HCHK(hipStreamSynchronize(st));
-  ucl_off_h.assign(C + 1, 0);
-  for (int c = 0; c < C; ++c) ucl_off_h[c + 1] = ucl_off_h[c] + nuniq[c];
-  RCHK(upload(cx, cx->ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
-  HCHK(cx->ucl.ensure(sizeof(int) * std::max<long long>(1, ucl_off_h[C])));
-  HCHK(launch_fill_ucl(cx->bits.as<unsigned long long>(), cx->woff.as<long long>(), C, cx->rank.as<int>(),
-                       cx->ucl_off.as<long long>(), cx->ucl.as<int>(), st));
-  HCHK(cx->uci.ensure(sizeof(int) * std::max<long long>(1, (long long)N * C)));
-  HCHK(launch_uci(s.counts_dev, s.ld, 0, N, C, cx->cellidx.as<int>(), cx->woff.as<long long>(),
-                  cx->bits.as<unsigned long long>(), cx->rank.as<int>(), cx->uci.as<int>(), st));
+  RCHK(upload(cx, u.woff, u.woff_h.data(), sizeof(long long) * (C + 1)));
+  HCHK(u.bits.ensure(sizeof(unsigned long long) * u.woff_h[C]));
+  HCHK(hipMemsetAsync(u.bits.p, 0, sizeof(unsigned long long) * u.woff_h[C], st));
+  HCHK(launch_mark(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.woff.as<long long>(),
+                   u.bits.as<unsigned long long>(), st));
+  HCHK(u.rank.ensure(sizeof(int) * u.woff_h[C]));
+  HCHK(u.nuniq.ensure(sizeof(int) * C));
+  HCHK(launch_rank(u.bits.as<unsigned long long>(), u.woff.as<long long>(), C, u.rank.as<int>(),
+                   u.nuniq.as<int>(), st));
+  u.nuniq_h.assign(C, 0);
+  HCHK(hipMemcpyAsync(u.nuniq_h.data(), u.nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  return SCDE_OK;
+}
+
+int unique_phase3(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
+  const int C = s.ncells, N = s.ngenes;
+  hipStream_t st = cx->stream;
+  u.ucl_off_h.assign(C + 1, 0);
+  for (int c = 0; c < C; ++c) u.ucl_off_h[c + 1] = u.ucl_off_h[c] + u.nuniq_h[c];
+  RCHK(upload(cx, u.ucl_off, u.ucl_off_h.data(), sizeof(long long) * (C + 1)));
+  HCHK(u.ucl.ensure(sizeof(int) * std::max<long long>(1, u.ucl_off_h[C])));
+  HCHK(launch_fill_ucl(u.bits.as<unsigned long long>(), u.woff.as<long long>(), C, u.rank.as<int>(),
+                       u.ucl_off.as<long long>(), u.ucl.as<int>(), st));
+  HCHK(u.uci.ensure(sizeof(int) * std::max<long long>(1, (long long)N * C)));
+  HCHK(launch_uci(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.woff.as<long long>(),
+                  u.bits.as<unsigned long long>(), u.rank.as<int>(), u.uci.as<int>(), st));
+  u.ready = true;
+  return SCDE_OK;
+}
+
+// ns (1 or 2) cell subsets of the same device counts
+int build_unique_sets(scde_ctx* cx, const PostSpec* const* s, UniqueSet* const* u, int ns) {
+  hipEvent_t ev = cx->mark_begin(SLOT_UNIQUE);
+  for (int i = 0; i < ns; ++i) RCHK(unique_phase1(cx, *s[i], *u[i]));
+  HCHK(hipStreamSynchronize(cx->stream));
+  for (int i = 0; i < ns; ++i) RCHK(unique_phase2(cx, *s[i], *u[i]));
+  HCHK(hipStreamSynchronize(cx->stream));
+  for (int i = 0; i < ns; ++i) RCHK(unique_phase3(cx, *s[i], *u[i]));
   cx->mark_end(SLOT_UNIQUE, ev);
   return SCDE_OK;
 }
@@ -352,7 +389,7 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
   }
 }
 
-int run_posterior(scde_ctx* cx, const PostSpec& s) {
+int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
   // column stride: >= the k_boot2 block (lanes never read past a column); 512 lets
   // k_boot3 move a column as four whole 1 KB LDS-DMA pieces
@@ -385,15 +422,15 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
                         cx->mu.as<double>(), cx->lcfp.as<double>(), cx->lcfpr.as<double>(), cx->theta.as<double>(),
                         cx->cellscal.as<double>(), st));
   cx->mark_end(SLOT_OTHER, ev);
-  // ---- unique counts
-  std::vector<long long> ucl_off_h;
+  // ---- unique counts (prebuilt by build_unique_sets when u.ready)
+  std::vector<long long>& ucl_off_h = u.ucl_off_h;
   if (s.ucl_host) {
     ucl_off_h.assign(s.ucl_off_host, s.ucl_off_host + C + 1);
     if (ucl_off_h[0] != 0) return fail(SCDE_EARG, "ucl_off[0] must be 0");
     for (int c = 0; c < C; ++c)
       if (ucl_off_h[c + 1] < ucl_off_h[c]) return fail(SCDE_EARG, "ucl_off must be non-decreasing");
-    RCHK(upload(cx, cx->ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
-    RCHK(upload(cx, cx->ucl, s.ucl_host, sizeof(int) * std::max<long long>(1, ucl_off_h[C])));
+    RCHK(upload(cx, u.ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
+    RCHK(upload(cx, u.ucl, s.ucl_host, sizeof(int) * std::max<long long>(1, ucl_off_h[C])));
     // validate counti against the per-cell list sizes (the reference would read out of bounds)
     for (int c = 0; c < C; ++c) {
       const long long nu = ucl_off_h[c + 1] - ucl_off_h[c];
@@ -401,10 +438,13 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
       for (int g = 0; g < N; ++g)
         if (col[g] < 0 || col[g] >= nu) return fail(SCDE_EARG, "counti[%d,%d]=%d out of range [0,%lld)", g, c, col[g], nu);
     }
-    RCHK(upload(cx, cx->uci, s.uci_host, sizeof(int) * std::max<long long>(1, (long long)N * C)));
-  } else {
-    RCHK(build_unique_device(cx, s, ucl_off_h));
+    RCHK(upload(cx, u.uci, s.uci_host, sizeof(int) * std::max<long long>(1, (long long)N * C)));
+  } else if (!u.ready) {
+    const PostSpec* sp[1] = {&s};
+    UniqueSet* up[1] = {&u};
+    RCHK(build_unique_sets(cx, sp, up, 1));
   }
+  u.ready = false;  // consumed by this call
   const long long ncols = ucl_off_h[C];
   // ---- K1 tables
   HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
@@ -412,8 +452,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
   HCHK(cx->has_clamp.ensure(std::max<long long>(1, ncols)));
   const bool want_maxi = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
   TablesArgs ta{};
-  ta.ucl = cx->ucl.as<int>();
-  ta.ucl_off = cx->ucl_off.as<long long>();
+  ta.ucl = u.ucl.as<int>();
+  ta.ucl_off = u.ucl_off.as<long long>();
   ta.ncols = ncols;
   ta.ncells = C;
   ta.G = G;
@@ -435,11 +475,11 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
   if (!s.batch_call && s.ensemble) {
     HCHK(cx->E.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
     HCHK(launch_ensemble_cols(cx->T.as<double>(), ncols, G, GS, cx->E.as<double>(), st));
-    NoBootArgs na{cx->E.as<double>(), G, GS, cx->ucl_off.as<long long>(), cx->uci.as<int>(), N, C, N, 1,
+    NoBootArgs na{cx->E.as<double>(), G, GS, u.ucl_off.as<long long>(), u.uci.as<int>(), N, C, N, 1,
                   s.jp, s.jp_g, s.jp_k};
     HCHK(launch_noboot(na, st));
   } else if (s.nboot == 0 && !s.batch_call) {
-    NoBootArgs na{cx->T.as<double>(), G, GS, cx->ucl_off.as<long long>(), cx->uci.as<int>(), N, C, N, 0,
+    NoBootArgs na{cx->T.as<double>(), G, GS, u.ucl_off.as<long long>(), u.uci.as<int>(), N, C, N, 0,
                   s.jp, s.jp_g, s.jp_k};
     HCHK(launch_noboot(na, st));
   } else if (s.nboot == 0) {
@@ -463,16 +503,16 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     RCHK(upload(cx, cx->Wt, W.data(), sizeof(double) * W.size()));
     RCHK(upload(cx, cx->draws, draws.data(), sizeof(int) * draws.size()));
     HCHK(cx->base_col.ensure(sizeof(int) * C));
-    HCHK(launch_base_cols(cx->ucl.as<int>(), cx->ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
+    HCHK(launch_base_cols(u.ucl.as<int>(), u.ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
                           s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
     const int stride = (int)round_up(C, 8) + 8;  // + one look-ahead batch (k_boot2)
     HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * stride)));
     HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
     ev = cx->mark_begin(SLOT_OTHER);
     HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
-    HCHK(launch_delta(cx->T.as<double>(), cx->ucl_off.as<long long>(), C, ncols, cx->base_col.as<int>(), G, GS,
+    HCHK(launch_delta(cx->T.as<double>(), u.ucl_off.as<long long>(), C, ncols, cx->base_col.as<int>(), G, GS,
                       cx->E.as<double>(), st));
-    HCHK(launch_ell(cx->uci.as<int>(), N, N, C, cx->ucl_off.as<long long>(), cx->base_col.as<int>(), stride,
+    HCHK(launch_ell(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->base_col.as<int>(), stride,
                     (int)ncols, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
     HCHK(launch_baseline_z(cx->T.as<double>(), G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
@@ -549,8 +589,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
     xa.ndraw = ndraw;
     xa.nboot = s.nboot;
     xa.wset = wset_d;
-    xa.ucl_off = cx->ucl_off.as<long long>();
-    xa.uci = cx->uci.as<int>();
+    xa.ucl_off = u.ucl_off.as<long long>();
+    xa.uci = u.uci.as<int>();
     xa.ld_uci = N;
     xa.norm_mult = (double)s.nboot;
     xa.degen = cx->degen.as<int>();
@@ -564,11 +604,11 @@ int run_posterior(scde_ctx* cx, const PostSpec& s) {
   const bool want_modes = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
   const bool want_post = s.batch_call ? (s.postflag == 2) : (s.postflag == 2 || s.postflag == 3);
   if (want_modes && s.modes)
-    HCHK(launch_modes(cx->uci.as<int>(), N, N, C, cx->ucl_off.as<long long>(), cx->maxi.as<int>(),
+    HCHK(launch_modes(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->maxi.as<int>(),
                       cx->mag.as<double>(), s.modes, 1, N, st));
   if (want_post && s.post)
     for (int c = 0; c < C; ++c)
-      HCHK(launch_post(cx->uci.as<int>(), N, N, c, cx->ucl_off.as<long long>(), cx->T.as<double>(), G, GS,
+      HCHK(launch_post(u.uci.as<int>(), N, N, c, u.ucl_off.as<long long>(), cx->T.as<double>(), G, GS,
                        s.post + (size_t)c * N * G, 1, N, st));
   return SCDE_OK;
 }
@@ -833,7 +873,8 @@ static int logboot_common(bool batch, const double* models, int ncells, const in
     HCHK(cx->outbuf.ensure(sizeof(double) * std::max<size_t>(1, NG * ncells)));
     s.post = cx->outbuf.as<double>();
   }
-  RCHK(run_posterior(cx, s));
+  cx->us[0].ready = false;
+  RCHK(run_posterior(cx, s, cx->us[0]));
   if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, cx->stream));
   if (want_modes && ngenes)
     HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * ngenes * ncells, hipMemcpyDeviceToHost, cx->stream));
@@ -1114,7 +1155,8 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
     HCHK(ctx->outbuf.ensure(sizeof(double) * std::max<size_t>(1, NG * ncells_sel)));
     s.post = ctx->outbuf.as<double>();
   }
-  RCHK(run_posterior(ctx, s));
+  ctx->us[0].ready = false;
+  RCHK(run_posterior(ctx, s, ctx->us[0]));
   if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, ctx->stream));
   if (want_modes && ngenes)
     HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * ngenes * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
@@ -1144,6 +1186,7 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
   HCHK(ctx->jpA.ensure(sizeof(double) * std::max<size_t>(1, NG)));
   HCHK(ctx->jpB.ensure(sizeof(double) * std::max<size_t>(1, NG)));
   std::vector<double> mm[2];
+  PostSpec specs[2];
   for (int gi = 0; gi < 2; ++gi) {
     const int Cg = (int)idx[gi].size();
     mm[gi].assign((size_t)Cg * 12, NAN);
@@ -1153,7 +1196,7 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
       double& ca = mm[gi][(size_t)c + (size_t)Cg * 4];
       if (ca < 1e-10) ca = 1e-10;
     }
-    PostSpec s;
+    PostSpec& s = specs[gi];
     s.ncells = Cg;
     s.models = mm[gi].data();
     s.localtheta = p->local_theta;
@@ -1171,8 +1214,16 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
     s.jp = (gi == 0 ? ctx->jpA : ctx->jpB).as<double>();
     s.jp_g = G;  // gene-major rows for the ratio kernel
     s.jp_k = 1;
-    RCHK(run_posterior(ctx, s));
   }
+  // both groups' unique tables first (two host syncs, GPU otherwise idle), then the
+  // heavy per-group kernels back to back on the stream
+  {
+    ctx->us[0].ready = ctx->us[1].ready = false;
+    const PostSpec* sp[2] = {&specs[0], &specs[1]};
+    UniqueSet* up[2] = {&ctx->us[0], &ctx->us[1]};
+    RCHK(build_unique_sets(ctx, sp, up, 2));
+  }
+  for (int gi = 0; gi < 2; ++gi) RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
   // ratio posterior + summary
   const std::vector<double> diffv = ratio_diffv(p->prior_x, G);
   const int zi = expectation_index(diffv, p->expectation);
