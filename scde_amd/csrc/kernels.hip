@@ -1168,16 +1168,88 @@ __global__ void k_colmajor_to_rows(const double* __restrict__ src, int nrows, in
   dst[(long long)r * GS + k] = src[i];
 }
 
+// ------------------------------------------------------------------ K3 helpers
+// matSlideMult (src/matSlideMult.cpp:12-20) for R adjacent outputs starting at shift s0:
+// X[s] = sum_t A[t + max(s,0)] * B[t + max(-s,0)], t ascending, each product and sum
+// rounded separately.  A and B are zero-padded by >= R entries past n, so the R sums can
+// all run to the longest one (a padded term adds +0 to a non-negative sum: bit-identical).
+// One sliding register window and one shared operand feed R independent sums per step;
+// LDS reads are issued 4 steps at a time.
+template <int R>
+__device__ __forceinline__ void slide_group(const double* __restrict__ A, const double* __restrict__ B, int n,
+                                            int s0, double (&c)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) c[r] = 0.0;
+  double w[R];
+  if (s0 >= 0) {
+    // output r: sum_{t < n-s0-r} A[t+s0+r] B[t]; longest is r = 0
+#pragma unroll
+    for (int r = 0; r < R; ++r) w[r] = A[s0 + r];
+    const int len = n - s0;
+    auto step = [&](double b, double anew) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) c[r] = __dadd_rn(c[r], __dmul_rn(w[r], b));
+#pragma unroll
+      for (int r = 0; r + 1 < R; ++r) w[r] = w[r + 1];
+      w[R - 1] = anew;
+    };
+    int t = 0;
+    for (; t + 4 <= len; t += 4) {
+      const double b0 = B[t], b1 = B[t + 1], b2 = B[t + 2], b3 = B[t + 3];
+      const double a0 = A[t + s0 + R], a1 = A[t + s0 + R + 1], a2 = A[t + s0 + R + 2], a3 = A[t + s0 + R + 3];
+      step(b0, a0);
+      step(b1, a1);
+      step(b2, a2);
+      step(b3, a3);
+    }
+    for (; t < len; ++t) step(B[t], A[t + s0 + R]);
+  } else if (s0 + R - 1 < 0) {
+    // output r: sum_{t < n+s0+r} A[t] B[t-s0-r]; longest is r = R-1
+#pragma unroll
+    for (int r = 0; r < R; ++r) w[r] = B[-s0 - r];
+    const int len = n + s0 + R - 1;
+    auto step = [&](double av, double bnew) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) c[r] = __dadd_rn(c[r], __dmul_rn(av, w[r]));
+#pragma unroll
+      for (int r = R - 1; r > 0; --r) w[r] = w[r - 1];
+      w[0] = bnew;
+    };
+    int t = 0;
+    for (; t + 4 <= len; t += 4) {
+      const double a0 = A[t], a1 = A[t + 1], a2 = A[t + 2], a3 = A[t + 3];
+      const double b1 = B[t + 1 - s0], b2 = B[t + 2 - s0], b3 = B[t + 3 - s0], b4 = B[t + 4 - s0];
+      step(a0, b1);
+      step(a1, b2);
+      step(a2, b3);
+      step(a3, b4);
+    }
+    for (; t < len; ++t) step(A[t], B[t + 1 - s0]);
+  } else {
+    // the group that straddles s = 0: one output at a time
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int s = s0 + r;
+      const int o1 = s > 0 ? s : 0, o2 = s < 0 ? -s : 0;
+      const int len = n - (s < 0 ? -s : s);
+      double acc = 0.0;
+      for (int t = 0; t < len; ++t) acc = __dadd_rn(acc, __dmul_rn(A[t + o1], B[t + o2]));
+      c[r] = acc;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ K3: ratio posterior + summary
-__global__ __launch_bounds__(128) void k_ratio_summary(RatioArgs a) {
+template <int R>
+__global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
   extern __shared__ double sh[];
   const int n = a.n, m = 2 * a.n - 1;
-  // A, B: prior-weighted rows, zero-padded by 4 so the sliding windows below may read past
+  // A, B: prior-weighted rows, zero-padded by 8 so the sliding windows below may read past
   // the end (a padded term adds +0 to a non-negative sum: bit-identical).  X: the row of
   // 2n-1 outputs, then 48 doubles of per-wave scratch.
   double* A = sh;
-  double* B = sh + (n + 4);
-  double* X = sh + 2 * (n + 4);
+  double* B = sh + (n + 8);
+  double* X = sh + 2 * (n + 8);
   __shared__ double red[8];
   __shared__ double red2[8];
   __shared__ int ired[8];
@@ -1185,7 +1257,7 @@ __global__ __launch_bounds__(128) void k_ratio_summary(RatioArgs a) {
   __shared__ int ired3[8];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
   for (int g = blockIdx.x; g < a.ngenes; g += gridDim.x) {
-    for (int k = tid; k < n + 4 && !a.xin; k += blockDim.x) {
+    for (int k = tid; k < n + 8 && !a.xin; k += blockDim.x) {
       if (k >= n) {
         A[k] = 0.0;
         B[k] = 0.0;
@@ -1204,93 +1276,22 @@ __global__ __launch_bounds__(128) void k_ratio_summary(RatioArgs a) {
     // B (s < 0) value and one shared operand feed four independent sums.
     dd ls = {0.0, 0.0};
     for (int o = tid; o < m && a.xin; o += blockDim.x) X[o] = a.xin[(long long)g * a.xg + (long long)o * a.xo];
-    // Output groups q (4 adjacent outputs each) have tent-shaped lengths; pairing q with
-    // q + ceil(NQ/2) gives every task ~n iterations, so no wave waits on a longer one.
-    const int NQ = (m + 3) / 4, halfq = (NQ + 1) / 2;
+    // Output groups q (R adjacent outputs each) have tent-shaped lengths; pairing q with
+    // q + ceil(NQ/2) gives every task ~n iterations, so no lane waits on a longer one.
+    const int NQ = (m + R - 1) / R, halfq = (NQ + 1) / 2;
     for (int task = tid; task < halfq && !a.xin; task += blockDim.x) {
       for (int h = 0; h < 2; ++h) {
         const int q = task + h * halfq;
         if (q >= NQ) break;
-        const int o0 = 4 * q;
-        const int s0 = o0 - (n - 1);
-        double c0 = 0.0, c1 = 0.0, c2 = 0.0, c3 = 0.0;
-        if (s0 >= 0) {
-          // output r: sum_{t < n-s0-r} A[t+s0+r] B[t]; run all four to the longest (r = 0)
-          double w0 = A[s0], w1 = A[s0 + 1], w2 = A[s0 + 2], w3 = A[s0 + 3];
-          const int len = n - s0;
-          auto step = [&](double b, double anew) {
-            c0 = __dadd_rn(c0, __dmul_rn(w0, b));
-            c1 = __dadd_rn(c1, __dmul_rn(w1, b));
-            c2 = __dadd_rn(c2, __dmul_rn(w2, b));
-            c3 = __dadd_rn(c3, __dmul_rn(w3, b));
-            w0 = w1;
-            w1 = w2;
-            w2 = w3;
-            w3 = anew;
-          };
-          int t = 0;
-          for (; t + 4 <= len; t += 4) {  // reads issued together: one LDS wait per 4 steps
-            const double b0 = B[t], b1 = B[t + 1], b2 = B[t + 2], b3 = B[t + 3];
-            const double a4 = A[t + s0 + 4], a5 = A[t + s0 + 5], a6 = A[t + s0 + 6], a7 = A[t + s0 + 7];
-            step(b0, a4);
-            step(b1, a5);
-            step(b2, a6);
-            step(b3, a7);
+        const int o0 = R * q;
+        double c[R];
+        slide_group<R>(A, B, n, o0 - (n - 1), c);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (o0 + r < m) {
+            X[o0 + r] = c[r];
+            ls = dd_add_d(ls, c[r]);
           }
-          for (; t < len; ++t) step(B[t], A[t + s0 + 4]);
-        } else if (s0 + 3 < 0) {
-          // output r: sum_{t < n+s0+r} A[t] B[t-s0-r]; run all four to the longest (r = 3)
-          double w0 = B[-s0], w1 = B[-s0 - 1], w2 = B[-s0 - 2], w3 = B[-s0 - 3];
-          const int len = n + s0 + 3;
-          auto step = [&](double av, double bnew) {
-            c0 = __dadd_rn(c0, __dmul_rn(av, w0));
-            c1 = __dadd_rn(c1, __dmul_rn(av, w1));
-            c2 = __dadd_rn(c2, __dmul_rn(av, w2));
-            c3 = __dadd_rn(c3, __dmul_rn(av, w3));
-            w3 = w2;
-            w2 = w1;
-            w1 = w0;
-            w0 = bnew;
-          };
-          int t = 0;
-          for (; t + 4 <= len; t += 4) {
-            const double a0 = A[t], a1 = A[t + 1], a2 = A[t + 2], a3 = A[t + 3];
-            const double b1 = B[t + 1 - s0], b2 = B[t + 2 - s0], b3 = B[t + 3 - s0], b4 = B[t + 4 - s0];
-            step(a0, b1);
-            step(a1, b2);
-            step(a2, b3);
-            step(a3, b4);
-          }
-          for (; t < len; ++t) step(A[t], B[t + 1 - s0]);
-        } else {
-          // the group that straddles s = 0: one output at a time
-          double cc[4] = {0.0, 0.0, 0.0, 0.0};
-          for (int r = 0; r < 4; ++r) {
-            const int s = s0 + r;
-            const int o1 = s > 0 ? s : 0, o2 = s < 0 ? -s : 0;
-            const int len = n - (s < 0 ? -s : s);
-            double acc = 0.0;
-            for (int t = 0; t < len; ++t) acc = __dadd_rn(acc, __dmul_rn(A[t + o1], B[t + o2]));
-            cc[r] = acc;
-          }
-          c0 = cc[0];
-          c1 = cc[1];
-          c2 = cc[2];
-          c3 = cc[3];
-        }
-        X[o0] = c0;
-        ls = dd_add_d(ls, c0);
-        if (o0 + 1 < m) {
-          X[o0 + 1] = c1;
-          ls = dd_add_d(ls, c1);
-        }
-        if (o0 + 2 < m) {
-          X[o0 + 2] = c2;
-          ls = dd_add_d(ls, c2);
-        }
-        if (o0 + 3 < m) {
-          X[o0 + 3] = c3;
-          ls = dd_add_d(ls, c3);
         }
       }
     }
@@ -1687,9 +1688,20 @@ hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int 
 
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
-  const size_t shm = sizeof(double) * (size_t)(2 * (a.n + 4) + (2 * a.n - 1) + 48);
+  const size_t shm = sizeof(double) * (size_t)(2 * (a.n + 8) + (2 * a.n - 1) + 48);
   const int grid = a.ngenes < 65536 ? a.ngenes : 65536;
-  hipLaunchKernelGGL(k_ratio_summary, dim3(grid), dim3(128), shm, s, a);
+  static int rsel = -1, bsel = -1;
+  if (rsel < 0) {  // tuning overrides
+    const char* r = getenv("SCDE_RATIO_R");
+    const char* b = getenv("SCDE_RATIO_BLOCK");
+    rsel = (r && atoi(r) == 8) ? 8 : 4;
+    bsel = b ? atoi(b) : 128;
+    if (bsel != 64 && bsel != 128 && bsel != 256) bsel = 128;
+  }
+  if (rsel == 8)
+    hipLaunchKernelGGL(k_ratio_summary<8>, dim3(grid), dim3(bsel), shm, s, a);
+  else
+    hipLaunchKernelGGL(k_ratio_summary<4>, dim3(grid), dim3(bsel), shm, s, a);
   return hipGetLastError();
 }
 
