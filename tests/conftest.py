@@ -39,6 +39,27 @@ def assert_posterior_close(a, b, rel=1e-6, floor=1e-12, abs_small=1e-18, what=""
                              f"{a2[i, j]!r} vs {b2[i, j]!r}")
 
 
+def assert_z_close(a, b, rel=1e-6, what="Z"):
+    """Z / cZ parity: 1e-6 relative, except where Z is ill-conditioned.
+    Z = qnorm(gs, lower=F) is computed from gs, a double near 1 at the -7.16 cap (and
+    near 0 at the other end).  Near 1, gs has an absolute resolution of 2^-53, so
+    one-ulp differences in gs -- the floor of reproducibility; R itself rounds its long
+    double sum to double -- move Z by far more than 1e-6.  Accept pairs whose upper-tail
+    masses pnorm(-|Z|) agree to 4 ulps of 1 (8.9e-16 absolute)."""
+    from scipy.stats import norm
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape
+    same_nan = np.isnan(a) & np.isnan(b)
+    ok_rel = np.abs(a - b) <= rel * np.maximum(np.abs(a), np.abs(b)) + 1e-12
+    ta, tb = norm.sf(np.abs(a)), norm.sf(np.abs(b))
+    ok_tail = (np.sign(a) == np.sign(b)) & (np.abs(ta - tb) <= 4 * 2.0 ** -53)
+    bad = ~(same_nan | ok_rel | ok_tail)
+    if bad.any():
+        i = np.nonzero(bad)[0][0]
+        raise AssertionError(f"{what}: {bad.sum()} values out of tolerance; first at {i}: {a[i]!r} vs {b[i]!r}")
+
+
 def gpu_available():
     try:
         import ctypes
