@@ -386,3 +386,27 @@ def test_posteriors_modes_config4_shape(api, oracle):
                                  return_individual_posterior_modes=True, n_cores=1)
     assert_posterior_close(got["jp"], ref["jp"], what="jp")
     np.testing.assert_array_equal(got["modes"], ref["modes"])
+
+
+@pytest.mark.parametrize("length_out", [60, 700, 1200])
+def test_expression_difference_grid_sizes(api, oracle, length_out):
+    """Grids other than 401 points: G = 61 (one wave), 701 (11-wave blocks, column stride
+    768), 1201 (> 1024 lanes: the k_boot fallback), with wider tables and ratio rows."""
+    from scde_amd.prior import expression_prior
+    g = golden("esmef500.npz")
+    models = _models(g)
+    counts = np.ascontiguousarray(g["counts"][:70])
+    prior = expression_prior(models, counts, length_out=length_out)
+    api.set_rand("glibc")
+    got = api.scde_expression_difference(models, counts, prior, groups=list(g["groups"]), n_randomizations=10,
+                                         n_cores=2, return_posteriors=True)
+    ref = oracle.scde_expression_difference(models, counts, prior["x"], prior["y"], g["groups"], n_randomizations=10,
+                                            n_cores=2, return_posteriors=True)
+    for i in range(2):
+        assert_posterior_close(got["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"jp{i}")
+    assert_posterior_close(got["difference.posterior"].values, ref["difference.posterior"], what="ratio")
+    res = got["results"]
+    for k in ("lb", "mle", "ub", "ce"):
+        np.testing.assert_array_equal(res[k].to_numpy(), ref["results"][k], err_msg=k)
+    assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"])
+    assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what="cZ")
