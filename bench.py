@@ -155,6 +155,8 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--cpu-sample", type=int, default=None, help="genes timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL, the real path) or gloo (CPU gather; rehearsal with ranks sharing one GPU)")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="forked oracle workers for the parallel CPU baseline (0 = skip; the GPU box's share is 16)")
     args = ap.parse_args()
@@ -165,12 +167,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # SCDE_SAME_DEVICE=1 puts every rank on GPU 0 (rehearsing the multi-rank path on a one-GPU box)
+    device = 0 if os.environ.get("SCDE_SAME_DEVICE") == "1" else local_rank
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist  # noqa: F811
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     from scde_amd import api
     from scde_amd.models import model_matrix
@@ -185,7 +192,7 @@ def main():
         # before any HIP call: the workers are forked from this process
         par = cpu_baseline_parallel(cfg, models, counts, groups, prior, cpu_sample * args.cpu_workers,
                                     args.cpu_workers)
-    ctx = api.Context(local_rank)
+    ctx = api.Context(device)
     dc = api.DeviceCounts(ctx, counts)
     mm, lt, sq = model_matrix(models)
     px = np.ascontiguousarray(prior["x"], np.float64)
@@ -214,11 +221,13 @@ def main():
                                                    res.ctypes.data_as(ctypes.c_void_p), None, None, None))
         if dist is not None:
             import torch
-            zt = torch.from_numpy(np.ascontiguousarray(res[:, 4])).cuda()
+            zt = torch.from_numpy(np.ascontiguousarray(res[:, 4]))
+            if args.dist_backend == "nccl":
+                zt = zt.cuda()
             gathered = [torch.empty_like(zt) for _ in range(world)] if rank == 0 else None
             dist.gather(zt, gathered, dst=0)
             if rank == 0:
-                zall = torch.cat(gathered)
+                zall = torch.cat(gathered).cuda()
                 cz = torch.empty_like(zall)
                 torch.cuda.current_stream().synchronize()
                 api.bh_cz_device(ctx, zall.data_ptr(), zall.numel(), cz.data_ptr())
@@ -245,7 +254,7 @@ def main():
     kt = ctx.kernel_times()
     if dist is not None:
         import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
 
