@@ -245,6 +245,158 @@ __device__ __forceinline__ double exp_tab(double d, const double* __restrict__ t
   return ldexp(fma(t, em1, t), k >> 6);
 }
 
+// log for positive normal x (other inputs fall back to the library log): x = m 2^e with
+// m in [0.75, 1.5); 97 intervals centred on c_j = 0.75 + j/128 (the one around 1 has
+// c = 1 exactly, so r = m - 1 is exact there and results near 0 keep full relative
+// accuracy); r = m/c_j - 1 in [-1/192, 1/192]; log1p(r) by its degree-8 Taylor
+// polynomial (truncation < 1e-20); log(c_j) as a double-double.  <= 2 ulp, ~25 VALU
+// slots against ~100 for the library log.  The tables are staged in LDS by the caller.
+__device__ __constant__ const double kLogInvC[97] = {
+    1.3333333333333333, 1.3195876288659794, 1.3061224489795917, 1.292929292929293,
+    1.28, 1.2673267326732673, 1.2549019607843137, 1.2427184466019416,
+    1.2307692307692308, 1.2190476190476192, 1.2075471698113207, 1.1962616822429906,
+    1.1851851851851851, 1.1743119266055047, 1.1636363636363636, 1.1531531531531531,
+    1.1428571428571428, 1.1327433628318584, 1.1228070175438596, 1.1130434782608696,
+    1.103448275862069, 1.0940170940170941, 1.0847457627118644, 1.0756302521008403,
+    1.0666666666666667, 1.0578512396694215, 1.0491803278688525, 1.0406504065040652,
+    1.032258064516129, 1.024, 1.0158730158730158, 1.0078740157480315,
+    1.0, 0.9922480620155039, 0.9846153846153847, 0.9770992366412213,
+    0.9696969696969697, 0.9624060150375939, 0.9552238805970149, 0.9481481481481482,
+    0.9411764705882353, 0.9343065693430657, 0.927536231884058, 0.920863309352518,
+    0.9142857142857143, 0.9078014184397163, 0.9014084507042254, 0.8951048951048951,
+    0.8888888888888888, 0.8827586206896552, 0.8767123287671232, 0.8707482993197279,
+    0.8648648648648649, 0.8590604026845637, 0.8533333333333334, 0.847682119205298,
+    0.8421052631578947, 0.8366013071895425, 0.8311688311688312, 0.8258064516129032,
+    0.8205128205128205, 0.8152866242038217, 0.810126582278481, 0.8050314465408805,
+    0.8, 0.7950310559006211, 0.7901234567901234, 0.7852760736196319,
+    0.7804878048780488, 0.7757575757575758, 0.7710843373493976, 0.7664670658682635,
+    0.7619047619047619, 0.757396449704142, 0.7529411764705882, 0.7485380116959064,
+    0.7441860465116279, 0.7398843930635838, 0.735632183908046, 0.7314285714285714,
+    0.7272727272727273, 0.7231638418079096, 0.7191011235955056, 0.7150837988826816,
+    0.7111111111111111, 0.7071823204419889, 0.7032967032967034, 0.6994535519125683,
+    0.6956521739130435, 0.6918918918918919, 0.6881720430107527, 0.6844919786096256,
+    0.6808510638297872, 0.6772486772486772, 0.6736842105263158, 0.6701570680628273,
+    0.6666666666666666};
+__device__ __constant__ const double kLogCHi[97] = {
+    -0.2876820724517809, -0.27731928541623435, -0.26706278524904525, -0.2569104137850272,
+    -0.24686007793152578, -0.2369097470783577, -0.22705745063534608, -0.2173012756899814,
+    -0.2076393647782445, -0.1980699137620938, -0.18859116980755003, -0.179201429457711,
+    -0.16989903679539747, -0.16068238169047347, -0.15154989812720093, -0.14250006260728304,
+    -0.13353139262452263, -0.1246424452072766, -0.1158318155251217, -0.1070981355563671,
+    -0.09844007281325252, -0.08985632912186105, -0.0813456394539524, -0.07290677080808779,
+    -0.06453852113757118, -0.05623971832287608, -0.048009219186360606, -0.039845908547199674,
+    -0.0317486983145803, -0.023716526617316044, -0.015748356968139168, -0.007843177461025893,
+    0.0, 0.007782140442054949, 0.015504186535965254, 0.02316705928153438,
+    0.030771658666753687, 0.0383188643021366, 0.0458095360312942, 0.053244514518812285,
+    0.06062462181643484, 0.06795066190850775, 0.07522342123758753, 0.08244366921107459,
+    0.08961215868968714, 0.09672962645855111, 0.10379679368164356, 0.11081436634029011,
+    0.11778303565638346, 0.12470347850095724, 0.13157635778871926, 0.13840232285911913,
+    0.1451820098444979, 0.15191604202584197, 0.15860503017663857, 0.16524957289530717,
+    0.17185025692665923, 0.1784076574728183, 0.184922338494012, 0.19139485299962947,
+    0.19782574332991987, 0.2042155414286909, 0.21056476910734964, 0.21687393830061436,
+    0.22314355131420976, 0.22937410106484582, 0.2355660713127669, 0.24171993688714516,
+    0.24783616390458127, 0.25391520998096345, 0.25995752443692605, 0.26596354849713794,
+    0.27193371548364176, 0.2778684510034563, 0.2837681731306446, 0.28963329258304266,
+    0.2954642128938359, 0.3012613305781618, 0.3070250352949119, 0.3127557100038969,
+    0.3184537311185346, 0.324119468654212, 0.329753286372468, 0.3353555419211378,
+    0.3409265869705932, 0.34646676734620857, 0.3519764231571782, 0.3574558889218038,
+    0.3629054936893685, 0.3683255611587076, 0.37371640979358406, 0.37907835293496944,
+    0.38441169891033206, 0.3897167511400252, 0.394993808240869, 0.4002431641270127,
+    0.4054651081081644};
+__device__ __constant__ const double kLogCLo[97] = {
+    -2.607160616442564e-17, 7.44528405583513e-18, 7.32891532732017e-18, -2.502843296152504e-17,
+    -1.361743371748368e-17, -1.9682402978398164e-18, -9.551415762738488e-18, -1.6168452453763015e-18,
+    -1.2053243216686129e-17, -3.742843482461439e-18, 7.432164219196925e-18, 1.0785017454858423e-17,
+    4.868008764439071e-19, 3.650183553047837e-18, -5.1669593684615594e-18, 9.926388234225749e-18,
+    3.664457663660085e-18, 5.808912678940971e-18, -4.338484369808096e-18, 1.73705104015906e-18,
+    4.439009633675136e-18, 6.273760163689594e-19, -5.07707635593117e-18, 6.306860257532778e-18,
+    6.470486661692933e-18, 3.2835149805605613e-18, -1.4390903347292205e-18, 3.129547680315208e-18,
+    -3.0382263084680858e-18, 1.5774243488668215e-18, -1.0021578630528974e-18, -2.764708154124904e-19,
+    0.0, -1.2819179123343845e-20, -3.278321022892429e-19, -1.1769544932063305e-18,
+    1.0431732029005968e-18, -2.357996157351286e-18, 1.902959866474257e-18, -1.665575816973663e-18,
+    2.6424025938726934e-18, -1.2802141240611733e-18, -5.930604196293241e-18, 5.700437773813987e-18,
+    -5.4268129336647135e-18, -5.597397486289965e-19, 5.47772415726659e-18, 1.183748342825649e-18,
+    -1.1971685747593677e-18, -4.6522609636496624e-18, 1.1123000879729588e-17, 4.447777301357527e-18,
+    8.242418783022475e-18, 6.4838631244022194e-18, 1.1257003872182592e-17, -1.0094935622322628e-17,
+    -6.0224538210113705e-18, -1.2432553788701131e-17, 3.0236614153574064e-18, -1.2129496905792884e-17,
+    1.2821194372980142e-17, 2.7338281018722773e-18, -4.249405314729895e-18, 4.551026193234283e-18,
+    -9.091270597324799e-18, 9.927671823978025e-18, -2.3943371495187355e-18, 8.900990022166643e-18,
+    -1.2432209578702523e-17, -8.048097394424201e-18, 2.069806938978935e-17, 5.3393802761314314e-18,
+    7.83319637697442e-19, -9.16018294909263e-19, -2.032665581126656e-17, 2.0535953219858174e-17,
+    -2.16461086040599e-17, -9.048511144048564e-18, -1.2319916200101964e-17, -1.451808353098951e-17,
+    2.7114779367326236e-17, -7.958214381893813e-18, 2.122020616196946e-18, 1.834564437059473e-17,
+    1.7467136443544747e-17, 1.028583585496265e-17, -1.2953893030191963e-17, -2.5136910072413547e-17,
+    -2.1492361455310972e-17, 2.690672380132659e-17, 2.1836211281198184e-17, 1.587939415338447e-17,
+    -1.612149700764673e-17, 2.734172667856699e-17, -1.5113724418336168e-17, -1.1349239205188711e-17,
+    -2.8811380259626426e-18};
+
+struct LogTab {
+  const double* inv;
+  const double* hi;
+  const double* lo;
+};
+
+__device__ __forceinline__ double log_tab(double x, const LogTab& t) {
+  if (!(x >= DBL_MIN && x < INFINITY)) return log(x);
+  int e;
+  double m = frexp(x, &e);  // [0.5, 1)
+  if (m < 0.75) {
+    m *= 2.0;
+    e -= 1;
+  }
+  const int j = (int)((m - 0.75) * 128.0 + 0.5);
+  const double r = fma(m, t.inv[j], -1.0);
+  double q = fma(r, -1.0 / 8.0, 1.0 / 7.0);
+  q = fma(q, r, -1.0 / 6.0);
+  q = fma(q, r, 1.0 / 5.0);
+  q = fma(q, r, -1.0 / 4.0);
+  q = fma(q, r, 1.0 / 3.0);
+  q = fma(q, r, -0.5);
+  const double p = fma(q * r, r, r);  // log1p(r)
+  const double ed = (double)e;
+  // e*ln2_hi is exact (ln2_hi has 11 trailing zero bits)
+  return (fma(ed, 0.6931471805598903, t.hi[j]) + (fma(ed, 5.497923018708371e-14, t.lo[j]) + p));
+}
+
+// bd0 with the table log in its non-series branch
+__device__ inline double bd0_t(double x, double np, const LogTab& lt) {
+  if (!isfinite(x) || !isfinite(np) || np == 0.0) return NAN;
+  if (fabs(x - np) < 0.1 * (x + np)) {
+    double v = (x - np) / (x + np);
+    double s = (x - np) * v;
+    if (fabs(s) < DBL_MIN) return s;
+    double ej = 2 * x * v;
+    v = v * v;
+    for (int j = 1; j < 1000; j++) {
+      ej *= v;
+      double s1 = s + ej / ((j << 1) + 1);
+      if (s1 == s) return s1;
+      s = s1;
+    }
+  }
+  return x * log_tab(x / np, lt) + np - x;
+}
+
+__device__ inline double dnbinom_log_ct(const NbConst& c, double x_in, double size_in, double prob, const LogTab& lt) {
+  if (c.trivial || isnan(prob)) return dnbinom_log(x_in, size_in, prob);
+  if (prob <= 0 || prob > 1) return NAN;
+  const double X = c.size, n = c.n, p = prob, q = 1 - prob;
+  double ans;
+  if (p == 0)
+    ans = (X == 0) ? 0.0 : -INFINITY;
+  else if (q == 0)
+    ans = (X == n) ? 0.0 : -INFINITY;
+  else if (X == 0)
+    ans = (n == 0) ? 0.0 : ((p < 0.1) ? -bd0_t(n, n * q, lt) - n * p : n * log_tab(q, lt));
+  else if (X == n)
+    ans = (q < 0.1) ? -bd0_t(n, n * p, lt) - n * q : n * log_tab(p, lt);
+  else {
+    const double lc = c.S - bd0_t(X, n * p, lt) - bd0_t(c.nx, n * q, lt);
+    ans = lc - 0.5 * c.lf;
+  }
+  return c.lp + ans;
+}
+
 // ---- double-double accumulation (emulates R's LDOUBLE rowSums / cumsum) ----
 struct dd {
   double hi, lo;

@@ -98,10 +98,17 @@ template <bool CT>
 __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   extern __shared__ double vrow[];  // [4 waves][GS]
   __shared__ double etab[64];
+  __shared__ double ltab[3][97];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const long long col = (long long)blockIdx.x * 4 + wid;
   if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
+  if (threadIdx.x < 97) {
+    ltab[0][threadIdx.x] = kLogInvC[threadIdx.x];
+    ltab[1][threadIdx.x] = kLogCHi[threadIdx.x];
+    ltab[2][threadIdx.x] = kLogCLo[threadIdx.x];
+  }
   __syncthreads();
+  const LogTab lt{ltab[0], ltab[1], ltab[2]};
   if (col >= a.ncols) return;
   int lo = 0, hi = a.ncells;
   while (hi - lo > 1) {
@@ -127,7 +134,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
     const double mnext = last ? 0.0 : mu[k + 1];
     if ((!last && x > muv && x < mnext) || (last && x > muv)) muv = x;
     const double t = th[k];
-    double nb = CT ? dnbinom_log_c(nc, x, t, t / (t + muv)) : dnbinom_log(x, t, t / (t + muv));
+    double nb = CT ? dnbinom_log_ct(nc, x, t, t / (t + muv), lt) : dnbinom_log(x, t, t / (t + muv));
     nb += lcfpr[k];
     v[k] = nb;
     lmax = gt_max(lmax, nb);
@@ -152,7 +159,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   double* out = a.T + col * a.GS;
 #pragma unroll 1
   for (int k = lane; k < G; k += 64) {
-    double r = log(v[k] / s);
+    double r = log_tab(v[k] / s, lt);
     if (r > bv) {
       bv = r;
       bi = k;
