@@ -110,7 +110,7 @@ struct NbConst {
   bool trivial;  // x == 0 && size == 0 -> 0; or non-finite inputs handled by dnbinom_log
 };
 
-__device__ inline NbConst nb_const(double x, double size) {
+__device__ __noinline__ NbConst nb_const(double x, double size) {  // once per column, out of line
   NbConst c;
   c.trivial = isnan(x) || isnan(size) || size < 0 || x < 0 || !isfinite(x) || (x == 0 && size == 0);
   x = rint(x);
@@ -162,6 +162,8 @@ __device__ inline double dpois_log(double x, double lambda) {
   if (lambda < x * DBL_MIN) return -lambda + x * log(lambda) - lgamma(x + 1);
   return -0.5 * log(k2Pi * x) + (-stirlerr(x) - bd0(x, lambda));
 }
+
+__device__ __noinline__ double dpois_log_cold(double x, double lambda) { return dpois_log(x, lambda); }
 
 // R qnorm(p, 0, 1, lower_tail, log.p = FALSE): Wichura's AS241 (PPND16)
 __device__ inline double qnorm(double p, bool lower_tail) {
@@ -330,6 +332,9 @@ __device__ __constant__ const double kLogCLo[97] = {
     -1.612149700764673e-17, 2.734172667856699e-17, -1.5113724418336168e-17, -1.1349239205188711e-17,
     -2.8811380259626426e-18};
 
+// cold paths kept out of line so they do not inflate the hot loops' register allocation
+__device__ __noinline__ double log_cold(double x) { return log(x); }
+
 struct LogTab {
   const double* inv;
   const double* hi;
@@ -337,7 +342,7 @@ struct LogTab {
 };
 
 __device__ __forceinline__ double log_tab(double x, const LogTab& t) {
-  if (!(x >= DBL_MIN && x < INFINITY)) return log(x);
+  if (!(x >= DBL_MIN && x < INFINITY)) return log_cold(x);
   int e;
   double m = frexp(x, &e);  // [0.5, 1)
   if (m < 0.75) {
@@ -377,8 +382,12 @@ __device__ inline double bd0_t(double x, double np, const LogTab& lt) {
   return x * log_tab(x / np, lt) + np - x;
 }
 
+__device__ __noinline__ double dnbinom_log_cold(double x, double size, double prob) {
+  return dnbinom_log(x, size, prob);
+}
+
 __device__ inline double dnbinom_log_ct(const NbConst& c, double x_in, double size_in, double prob, const LogTab& lt) {
-  if (c.trivial || isnan(prob)) return dnbinom_log(x_in, size_in, prob);
+  if (c.trivial || isnan(prob)) return dnbinom_log_cold(x_in, size_in, prob);
   if (prob <= 0 || prob > 1) return NAN;
   const double X = c.size, n = c.n, p = prob, q = 1 - prob;
   double ans;

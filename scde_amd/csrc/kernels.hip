@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const double* lcfpr = a.lcfpr + (long long)c * a.GS;
   const double* th = a.theta + (long long)c * a.GS;
   const double maxcfp = a.cellscal[2 * c];
-  const double fp = dpois_log(x, a.cellscal[2 * c + 1]);
+  const double fp = dpois_log_cold(x, a.cellscal[2 * c + 1]);
   const NbConst nc = CT ? nb_const(x, th[0]) : NbConst{};
   double* v = vrow + (long long)wid * a.GS;
   double lmax = -INFINITY;
