@@ -52,6 +52,9 @@ __device__ inline double stirlerr(double n) {
 }
 
 // deviance term bd0(x, np) = x log(x/np) + np - x, Taylor form near x == np
+#ifndef SCDE_BD0_SERIES_OOL
+#define SCDE_BD0_SERIES_OOL 1
+#endif
 #ifndef SCDE_TABLES_DIAG
 #define SCDE_TABLES_DIAG 0  // timing-only builds: 1 = bd0 without its series, 2 = trivial dnbinom
 #endif
@@ -363,9 +366,26 @@ __device__ __forceinline__ double log_tab(double x, const LogTab& t) {
   return (fma(ed, 0.6931471805598903, t.hi[j]) + (fma(ed, 5.497923018708371e-14, t.lo[j]) + p));
 }
 
+// bd0's Taylor series (|x - np| < 0.1 (x + np)), out of line
+__device__ __noinline__ double bd0_series(double x, double np) {
+  double v = (x - np) / (x + np);
+  double s = (x - np) * v;
+  if (fabs(s) < DBL_MIN) return s;
+  double ej = 2 * x * v;
+  v = v * v;
+  for (int j = 1; j < 1000; j++) {
+    ej *= v;
+    double s1 = s + ej / ((j << 1) + 1);
+    if (s1 == s) return s1;
+    s = s1;
+  }
+  return x * log(x / np) + np - x;  // not reached for |v| < 0.1
+}
+
 // bd0 with the table log in its non-series branch
 __device__ inline double bd0_t(double x, double np, const LogTab& lt) {
   if (!isfinite(x) || !isfinite(np) || np == 0.0) return NAN;
+  if (SCDE_BD0_SERIES_OOL && fabs(x - np) < 0.1 * (x + np)) return bd0_series(x, np);
   if (fabs(x - np) < 0.1 * (x + np)) {
     double v = (x - np) / (x + np);
     double s = (x - np) * v;
