@@ -282,32 +282,32 @@ def test_negative_counts_rejected(api):
         api.scde_posteriors(models, -np.ones((3, 4), np.int32), {"x": g["prior_x"], "y": g["prior_y"]}, n_cores=1)
 
 
-def test_batch_corrected_difference(api, oracle):
-    """Batch branch (R/functions.R:321-399) against the oracle's .Call restatements."""
+@pytest.mark.parametrize("ncores", [1, 3])
+def test_batch_corrected_difference(api, oracle, ncores):
+    """Batch branch (R/functions.R:321-399) end to end against the oracle's restatement:
+    batch.effect, results and batch.adjusted tables (lb/mle/ub/ce exact, Z/cZ per spec) and
+    every posterior (jp, batch ratio, ratio, 1601-column batch-adjusted ratio) within 1e-6."""
     g = golden("esmef500.npz")
     models, counts, groups = _frame_inputs(g)
     counts = counts.iloc[:120]
     prior = {"x": g["prior_x"], "y": g["prior_y"]}
     batch = np.array(["b1" if (i * 5) % 3 else "b2" for i in range(40)])
     out = api.scde_expression_difference(models, counts, prior, groups=groups, batch=batch, n_randomizations=10,
-                                         n_cores=1, return_posteriors=True)
-    # recompute the batch posteriors with the oracle
-    md = _models(g)
-    cnt = g["counts"][:120]
-    codes = g["groups"]
-    bjp = []
-    for lv in (0, 1):
-        ii = np.nonzero(codes == lv)[0]
-        comp = [int(np.sum(batch[ii] == b)) for b in ("b1", "b2")]
-        bjp.append(oracle.scde_posteriors(md, cnt, g["prior_x"], n_randomizations=10, batch=list(batch),
-                                          composition=comp, n_cores=1))
-    bratio = oracle.calculate_ratio_posterior(bjp[0], bjp[1], g["prior_y"])
-    ratio = out["difference.posterior"].values
-    a_ref = oracle.calculate_ratio_posterior(ratio, bratio, None, skip_prior_adjustment=True)
-    assert_posterior_close(out["batch.adjusted.difference.posterior"].values, a_ref, rel=1e-5, what="batch-adjusted")
-    s_ref = oracle.quick_distribution_summary(a_ref, oracle.ratio_grid(oracle.ratio_grid(g["prior_x"])))
-    for k in ("lb", "mle", "ub"):
-        assert np.mean(out["batch.adjusted"][k].to_numpy() == s_ref[k]) > 0.98, k
+                                         n_cores=ncores, return_posteriors=True)
+    ref = oracle.scde_expression_difference_batch(_models(g), g["counts"][:120], g["prior_x"], g["prior_y"],
+                                                  g["groups"], list(batch), n_randomizations=10, n_cores=ncores,
+                                                  return_posteriors=True)
+    for i in range(2):
+        assert_posterior_close(out["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"jp{i}")
+    assert_posterior_close(out["difference.posterior"].values, ref["difference.posterior"], what="ratio")
+    assert_posterior_close(out["batch.adjusted.difference.posterior"].values,
+                           ref["batch.adjusted.difference.posterior"], what="batch-adjusted ratio")
+    for table in ("batch.effect", "results", "batch.adjusted"):
+        got, want = out[table], ref[table]
+        for k in ("lb", "mle", "ub", "ce"):
+            np.testing.assert_array_equal(got[k].to_numpy(), want[k], err_msg=f"{table}.{k}")
+        assert_z_close(got["Z"].to_numpy(), want["Z"], what=f"{table}.Z")
+        assert_z_close(got["cZ"].to_numpy(), want["cZ"], what=f"{table}.cZ")
 
 
 @pytest.mark.parametrize("case", ["random", "ties_nan", "tiny"])
