@@ -154,6 +154,18 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
                                    const scde_de_params* p, double* results, double* jp1, double* jp2,
                                    double* ratio);
 
+/* Batch-corrected scde.expression.difference (R/functions.R:321-399) on device-resident
+ * counts: p as for scde_expression_difference_dev (compute_cz is implied), batch_models
+ * ncells x 12 col-major (NULL = p->models), batch_codes[ncells] in [0, nbatch) (level
+ * order).  results: host, three consecutive ngenes x 6 col-major blocks (lb, mle, ub, ce,
+ * Z, cZ) for batch.adjusted, results, batch.effect.  Optional host outputs, col-major:
+ * jp1/jp2 (the groups' joint posteriors, ngenes x ngrid), ratio (the group difference posterior, ngenes x (2*ngrid-1)), adj_ratio (the
+ * batch-adjusted posterior, ngenes x (4*ngrid-3)), batch_ratio (ngenes x (2*ngrid-1)). */
+int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes,
+                                         const scde_de_params* p, const double* batch_models,
+                                         const int* batch_codes, int nbatch, double* results, double* jp1,
+                                         double* jp2, double* ratio, double* adj_ratio, double* batch_ratio);
+
 /* scde.posteriors (R/functions.R:566-669) on device-resident counts for the cells
  * listed in cellidx (host, ncells_sel entries).  Outputs are host, col-major.
  * batch_* may be NULL (no batch).  return_post: R postflag (0..3). */

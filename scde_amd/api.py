@@ -444,33 +444,43 @@ def scde_expression_difference(models, counts, prior, groups=None, batch=None, n
 
 def _expression_difference_batch(models, mat, genes, prior, codes, batch, nrand, n_cores, batch_models,
                                  return_posteriors, expectation, ctx):
-    """Batch-corrected branch (R/functions.R:321-399)."""
-    counts = mat
+    """Batch-corrected branch (R/functions.R:321-399) as one device-resident call
+    (scde_expression_difference_batch_dev): batch posteriors over all cells with each
+    group's batch composition, the group posteriors, the three ratio posteriors and their
+    summaries with BH, all in HBM."""
+    N, C = mat.shape
     levels = sorted(set(batch.tolist()))
-    batch_jpl = []
-    for lv in (0, 1):
-        ii = np.nonzero(codes == lv)[0]
-        comp = {b: int(np.sum(batch[ii] == b)) for b in levels}
-        batch_jpl.append(scde_posteriors(batch_models, counts, prior, n_randomizations=nrand, batch=batch,
-                                         composition=comp, n_cores=n_cores, ctx=ctx))
-    batch_bdiffp = calculate_ratio_posterior(batch_jpl[0], batch_jpl[1], prior, n_cores=n_cores)
-    batch_rep = quick_distribution_summary(batch_bdiffp, 0.0, genes)
-    jpl = []
-    md = as_model_dict(models)
-    for lv in (0, 1):
-        ii = np.nonzero(codes == lv)[0]
-        sub = {k: v[ii] for k, v in md.items()}
-        jpl.append(scde_posteriors(sub, counts[:, ii], prior, n_randomizations=nrand, n_cores=n_cores, ctx=ctx))
-    bdiffp = calculate_ratio_posterior(jpl[0], jpl[1], prior, n_cores=n_cores)
-    bdiffp.rownames = genes
-    rep = quick_distribution_summary(bdiffp, expectation, genes)
-    uniform = {"x": bdiffp.columns, "y": np.full(bdiffp.shape[1], 1.0 / bdiffp.shape[1])}
-    a_bdiffp = calculate_ratio_posterior(bdiffp.values, batch_bdiffp.values, uniform, skip_prior_adjustment=True)
-    a_rep = quick_distribution_summary(a_bdiffp, expectation, genes)
-    out = {"batch.adjusted": a_rep, "results": rep, "batch.effect": batch_rep}
-    if return_posteriors:
-        out.update({"difference.posterior": bdiffp, "batch.adjusted.difference.posterior": a_bdiffp,
-                    "joint.posteriors": jpl})
+    bcodes = np.ascontiguousarray([levels.index(b) for b in batch.tolist()], np.int32)
+    mm, lt, sq = model_matrix(models)
+    bmm, blt, bsq = model_matrix(batch_models)
+    if (blt, bsq) != (lt, sq):
+        raise ValueError("batch.models must be of the same model type as models")
+    px = np.ascontiguousarray(prior["x"], np.float64)
+    py = np.ascontiguousarray(prior["y"], np.float64)
+    G = len(px)
+    codes = np.ascontiguousarray(codes, np.int32)
+    res = np.zeros((N, 18), order="F")
+    rp = return_posteriors
+    jp1 = np.zeros((N, G), order="F") if rp else None
+    jp2 = np.zeros((N, G), order="F") if rp else None
+    ratio = np.zeros((N, 2 * G - 1), order="F") if rp else None
+    adj = np.zeros((N, 4 * G - 3), order="F") if rp else None
+    dc = DeviceCounts(ctx, mat)
+    try:
+        params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
+                          int(nrand), int(n_cores), 0, N, float(expectation), get_rand_kind(), 1)
+        check(lib().scde_expression_difference_batch_dev(ctx.handle, dc.ptr, N, N, ctypes.byref(params), _p(bmm),
+                                                         _p(bcodes), len(levels), _p(res), _p(jp1), _p(jp2),
+                                                         _p(ratio), _p(adj), None))
+    finally:
+        dc.free()
+    tables = [_result_frame(res[:, 6 * k: 6 * k + 5], res[:, 6 * k + 5].copy(), genes) for k in range(3)]
+    out = {"batch.adjusted": tables[0], "results": tables[1], "batch.effect": tables[2]}
+    if rp:
+        cols = ratio_columns(px)
+        out.update({"difference.posterior": RatioPosterior(ratio, cols, genes),
+                    "batch.adjusted.difference.posterior": RatioPosterior(adj, ratio_columns(cols), genes),
+                    "joint.posteriors": [jp1, jp2]})
     return out
 
 

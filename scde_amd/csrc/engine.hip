@@ -165,7 +165,7 @@ struct scde_ctx {
       Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci};
       for (Buf* x : b) x->release();
     }
-  } us[2];
+  } us[3];
   // profiling
   bool profile = false;
   struct Pending {
@@ -1274,6 +1274,181 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
     HCHK(hipMemcpyAsync(tmp.data(), ctx->jpB.p, sizeof(double) * NG, hipMemcpyDeviceToHost, st));
     RCHK(ctx->sync());
     transpose_rows_to_colmajor(tmp.data(), ngenes, G, jp2);
+  }
+  return ctx->sync();
+}
+
+// Batch-corrected scde.expression.difference (R/functions.R:321-399), device resident:
+// batch posteriors over all cells with each group's batch composition, the group
+// posteriors, three ratio posteriors (batch, groups, and the 1601-column second level of
+// the two with skip.prior.adjustment) and their summaries with device BH.
+int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes,
+                                         const scde_de_params* p, const double* batch_models,
+                                         const int* batch_codes, int nbatch, double* results, double* jp1,
+                                         double* jp2, double* ratio, double* adj_ratio, double* batch_ratio) {
+  if (!ctx || !counts_dev || !p || !p->models || !p->groups || !p->prior_x || !p->prior_y || !batch_codes ||
+      !results)
+    return fail(SCDE_EARG, "null argument");
+  if (ngenes < 0 || p->ncells <= 0 || p->ngrid <= 1 || nbatch < 1) return fail(SCDE_EARG, "bad dimensions");
+  HCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const int C = p->ncells, G = p->ngrid, N = ngenes;
+  const double* bm = batch_models ? batch_models : p->models;
+  std::vector<int> idx[2];
+  for (int c = 0; c < C; ++c)
+    if (p->groups[c] == 0 || p->groups[c] == 1) idx[p->groups[c]].push_back(c);
+  if (idx[0].empty() || idx[1].empty()) return fail(SCDE_EARG, "both groups need at least one cell");
+  // BatchIL (0-based cell indices per batch level) and table(batch[ii]) per group
+  std::vector<int> bvals;
+  std::vector<int64_t> boff(nbatch + 1, 0);
+  for (int k = 0; k < nbatch; ++k) {
+    for (int c = 0; c < C; ++c) {
+      if (batch_codes[c] < 0 || batch_codes[c] >= nbatch) return fail(SCDE_EARG, "batch code out of range");
+      if (batch_codes[c] == k) bvals.push_back(c);
+    }
+    boff[k + 1] = (int64_t)bvals.size();
+  }
+  std::vector<int> comp[2];
+  for (int gi = 0; gi < 2; ++gi) {
+    comp[gi].assign(nbatch, 0);
+    for (int c : idx[gi]) comp[gi][batch_codes[c]]++;
+  }
+  const std::vector<double> mag = marginals(p->prior_x, G);
+  std::vector<int> seeds, wset;
+  seeding(p->n_cores, p->gene_offset, p->ngenes_total > 0 ? p->ngenes_total : N, N, seeds, wset);
+  const size_t NG = (size_t)N * G;
+  HCHK(ctx->jpA.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  HCHK(ctx->jpB.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  HCHK(ctx->in1.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  HCHK(ctx->in2.ensure(sizeof(double) * std::max<size_t>(1, NG)));
+  // model matrices with the slope clamp (R/functions.R:579-583)
+  auto clamp_mm = [](std::vector<double>& m, int n) {
+    for (int c = 0; c < n; ++c)
+      if (m[(size_t)c + (size_t)n * 4] < 1e-10) m[(size_t)c + (size_t)n * 4] = 1e-10;
+  };
+  std::vector<double> mm[2], mmb(bm, bm + (size_t)C * 12);
+  clamp_mm(mmb, C);
+  std::vector<int> allc(C);
+  for (int c = 0; c < C; ++c) allc[c] = c;
+  PostSpec sg[2], sb[2];
+  for (int gi = 0; gi < 2; ++gi) {
+    const int Cg = (int)idx[gi].size();
+    mm[gi].assign((size_t)Cg * 12, NAN);
+    for (int j = 0; j < 12; ++j)
+      for (int c = 0; c < Cg; ++c) mm[gi][(size_t)c + (size_t)Cg * j] = p->models[(size_t)idx[gi][c] + (size_t)C * j];
+    clamp_mm(mm[gi], Cg);
+    for (int pass = 0; pass < 2; ++pass) {
+      PostSpec& s = pass == 0 ? sg[gi] : sb[gi];
+      s.ncells = pass == 0 ? Cg : C;
+      s.models = pass == 0 ? mm[gi].data() : mmb.data();
+      s.localtheta = p->local_theta;
+      s.squarelogit = p->square_logit_conc;
+      s.mag = mag.data();
+      s.G = G;
+      s.nboot = p->nboot;
+      s.counts_dev = counts_dev;
+      s.ld = ld;
+      s.cellidx_host = pass == 0 ? idx[gi].data() : allc.data();
+      s.ngenes = N;
+      s.seeds = seeds;
+      s.wset = wset;
+      s.rand_kind = p->rand_kind;
+      s.jp_g = G;
+      s.jp_k = 1;
+      if (pass == 1) {
+        s.batch_call = true;
+        s.batch_vals = bvals.data();
+        s.batch_off = boff.data();
+        s.comp = comp[gi].data();
+        s.nbatch = nbatch;
+      }
+    }
+    sg[gi].jp = (gi == 0 ? ctx->jpA : ctx->jpB).as<double>();
+    sb[gi].jp = (gi == 0 ? ctx->in1 : ctx->in2).as<double>();
+  }
+  // unique tables: group 0 cells, group 1 cells, all cells (shared by both batch runs)
+  {
+    for (auto& u : ctx->us) u.ready = false;
+    const PostSpec* sp[3] = {&sg[0], &sg[1], &sb[0]};
+    UniqueSet* up[3] = {&ctx->us[0], &ctx->us[1], &ctx->us[2]};
+    RCHK(build_unique_sets(ctx, sp, up, 3));
+  }
+  RCHK(run_posterior(ctx, sb[0], ctx->us[2]));
+  ctx->us[2].ready = true;  // same cells, same counts: reuse for the second batch run
+  RCHK(run_posterior(ctx, sb[1], ctx->us[2]));
+  RCHK(run_posterior(ctx, sg[0], ctx->us[0]));
+  RCHK(run_posterior(ctx, sg[1], ctx->us[1]));
+  // three ratio posteriors + summaries
+  const std::vector<double> dv1 = ratio_diffv(p->prior_x, G);
+  const int m = 2 * G - 1, m2 = 2 * m - 1;
+  const std::vector<double> dv2 = ratio_diffv(dv1.data(), m);
+  RCHK(upload(ctx, ctx->prior_y, p->prior_y, sizeof(double) * G));
+  RCHK(upload(ctx, ctx->diffv, dv1.data(), sizeof(double) * m));
+  RCHK(upload(ctx, ctx->outbuf, dv2.data(), sizeof(double) * m2));
+  HCHK(ctx->ratio.ensure(sizeof(double) * std::max<size_t>(1, (size_t)N * m)));
+  HCHK(ctx->part.ensure(sizeof(double) * std::max<size_t>(1, (size_t)N * m)));  // batch ratio
+  if (adj_ratio) HCHK(ctx->E.ensure(sizeof(double) * std::max<size_t>(1, (size_t)N * m2)));
+  HCHK(ctx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)N * 18)));
+  double* res = ctx->res.as<double>();
+  size_t wb = 0;
+  HCHK(launch_bh_cz(nullptr, N, nullptr, nullptr, &wb, st));
+  HCHK(ctx->bhw.ensure(wb));
+  auto ratio_pass = [&](const double* a1, long long a1g, long long a1k, const double* a2, long long a2g,
+                        long long a2k, const double* py, int n, const double* dv, int zi, double* rout,
+                        double* rres) -> int {
+    RatioArgs ra{};
+    ra.jp1 = a1;
+    ra.j1g = a1g;
+    ra.j1k = a1k;
+    ra.jp2 = a2;
+    ra.j2g = a2g;
+    ra.j2k = a2k;
+    ra.prior_y = py;
+    ra.n = n;
+    ra.ngenes = N;
+    ra.normalize = 1;
+    ra.ratio = rout;
+    ra.rg = 1;
+    ra.ro = N;
+    ra.diffv = dv;
+    ra.zi = zi;
+    ra.res = rres;
+    ra.res_ld = N;
+    hipEvent_t ev = ctx->mark_begin(SLOT_RATIO);
+    HCHK(launch_ratio_summary(ra, st));
+    ctx->mark_end(SLOT_RATIO, ev);
+    if (N) HCHK(launch_bh_cz(rres + (size_t)4 * N, N, rres + (size_t)5 * N, ctx->bhw.p, &wb, st));
+    return SCDE_OK;
+  };
+  // results blocks: [0] batch.adjusted, [1] results, [2] batch.effect (each N x 6)
+  double* r_adj = res;
+  double* r_res = res + (size_t)6 * N;
+  double* r_bat = res + (size_t)12 * N;
+  const double* py = ctx->prior_y.as<double>();
+  RCHK(ratio_pass(ctx->in1.as<double>(), G, 1, ctx->in2.as<double>(), G, 1, py, G, ctx->diffv.as<double>(),
+                  expectation_index(dv1, 0.0), ctx->part.as<double>(), r_bat));
+  RCHK(ratio_pass(ctx->jpA.as<double>(), G, 1, ctx->jpB.as<double>(), G, 1, py, G, ctx->diffv.as<double>(),
+                  expectation_index(dv1, p->expectation), ctx->ratio.as<double>(), r_res));
+  RCHK(ratio_pass(ctx->ratio.as<double>(), 1, N, ctx->part.as<double>(), 1, N, nullptr, m,
+                  ctx->outbuf.as<double>(), expectation_index(dv2, p->expectation),
+                  adj_ratio ? ctx->E.as<double>() : nullptr, r_adj));
+  if (N) {
+    HCHK(hipMemcpyAsync(results, res, sizeof(double) * (size_t)N * 18, hipMemcpyDeviceToHost, st));
+    if (ratio) HCHK(hipMemcpyAsync(ratio, ctx->ratio.p, sizeof(double) * (size_t)N * m, hipMemcpyDeviceToHost, st));
+    if (batch_ratio)
+      HCHK(hipMemcpyAsync(batch_ratio, ctx->part.p, sizeof(double) * (size_t)N * m, hipMemcpyDeviceToHost, st));
+    if (adj_ratio)
+      HCHK(hipMemcpyAsync(adj_ratio, ctx->E.p, sizeof(double) * (size_t)N * m2, hipMemcpyDeviceToHost, st));
+  }
+  std::vector<double> tmp;
+  for (int gi = 0; gi < 2 && NG; ++gi) {
+    double* out = gi == 0 ? jp1 : jp2;
+    if (!out) continue;
+    tmp.resize(NG);
+    HCHK(hipMemcpyAsync(tmp.data(), (gi == 0 ? ctx->jpA : ctx->jpB).p, sizeof(double) * NG, hipMemcpyDeviceToHost,
+                        st));
+    RCHK(ctx->sync());
+    transpose_rows_to_colmajor(tmp.data(), N, G, out);
   }
   return ctx->sync();
 }

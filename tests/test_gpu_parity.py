@@ -282,8 +282,8 @@ def test_negative_counts_rejected(api):
         api.scde_posteriors(models, -np.ones((3, 4), np.int32), {"x": g["prior_x"], "y": g["prior_y"]}, n_cores=1)
 
 
-@pytest.mark.parametrize("ncores", [1, 3])
-def test_batch_corrected_difference(api, oracle, ncores):
+@pytest.mark.parametrize("ncores,nlev", [(1, 2), (3, 2), (2, 3)])
+def test_batch_corrected_difference(api, oracle, ncores, nlev):
     """Batch branch (R/functions.R:321-399) end to end against the oracle's restatement:
     batch.effect, results and batch.adjusted tables (lb/mle/ub/ce exact, Z/cZ per spec) and
     every posterior (jp, batch ratio, ratio, 1601-column batch-adjusted ratio) within 1e-6."""
@@ -291,7 +291,10 @@ def test_batch_corrected_difference(api, oracle, ncores):
     models, counts, groups = _frame_inputs(g)
     counts = counts.iloc[:120]
     prior = {"x": g["prior_x"], "y": g["prior_y"]}
-    batch = np.array(["b1" if (i * 5) % 3 else "b2" for i in range(40)])
+    if nlev == 2:
+        batch = np.array(["b1" if (i * 5) % 3 else "b2" for i in range(40)])
+    else:
+        batch = np.array([("b1", "b2", "b3")[(i * 7 + i // 5) % 3] for i in range(40)])
     out = api.scde_expression_difference(models, counts, prior, groups=groups, batch=batch, n_randomizations=10,
                                          n_cores=ncores, return_posteriors=True)
     ref = oracle.scde_expression_difference_batch(_models(g), g["counts"][:120], g["prior_x"], g["prior_y"],
@@ -308,6 +311,38 @@ def test_batch_corrected_difference(api, oracle, ncores):
             np.testing.assert_array_equal(got[k].to_numpy(), want[k], err_msg=f"{table}.{k}")
         assert_z_close(got["Z"].to_numpy(), want["Z"], what=f"{table}.Z")
         assert_z_close(got["cZ"].to_numpy(), want["cZ"], what=f"{table}.cZ")
+
+
+def test_batch_device_matches_composition(api):
+    """The one-call device batch pipeline equals the composition of the per-step calls
+    (batch scde.posteriors, calculate.ratio.posterior, quick.distribution.summary) on a
+    larger synthetic set with 3 batch levels and NA-group cells; every table bit-equal."""
+    from scde_amd.prior import expression_prior
+    rng = np.random.default_rng(11)
+    models, counts, _ = _synthetic(7011, 700, 90)
+    C = counts.shape[1]
+    codes = np.where(np.arange(C) % 9 == 4, -1, np.arange(C) % 2)
+    groups = [None if c < 0 else ("a", "b")[c] for c in codes]
+    batch = np.array(["x", "y", "z"])[rng.integers(0, 3, C)]
+    prior = expression_prior(models, counts, length_out=400)
+    out = api.scde_expression_difference(models, counts, prior, groups=groups, batch=batch, n_randomizations=40,
+                                         n_cores=4, return_posteriors=True)
+    bpost = []
+    for lv in (0, 1):
+        ii = np.nonzero(codes == lv)[0]
+        comp = {b: int(np.sum(batch[ii] == b)) for b in ("x", "y", "z")}
+        bpost.append(api.scde_posteriors(models, counts, prior, n_randomizations=40, batch=batch, composition=comp,
+                                         n_cores=4))
+    brat = api.calculate_ratio_posterior(bpost[0], bpost[1], prior)
+    np.testing.assert_array_equal(out["batch.effect"]["ce"].to_numpy(),
+                                  api.quick_distribution_summary(brat, 0.0)["ce"].to_numpy())
+    rat = out["difference.posterior"]
+    uniform = {"x": rat.columns, "y": np.full(rat.shape[1], 1.0 / rat.shape[1])}
+    adj = api.calculate_ratio_posterior(rat.values, brat.values, uniform, skip_prior_adjustment=True)
+    np.testing.assert_array_equal(out["batch.adjusted.difference.posterior"].values, adj.values)
+    want = api.quick_distribution_summary(adj, 0.0)
+    for k in ("lb", "mle", "ub", "ce", "Z", "cZ"):
+        np.testing.assert_array_equal(out["batch.adjusted"][k].to_numpy(), want[k].to_numpy(), err_msg=k)
 
 
 @pytest.mark.parametrize("case", ["random", "ties_nan", "tiny"])
