@@ -10,6 +10,10 @@ results to host.
 --config 3: 20,000 genes x 1,000 cells (500/500), the north_star's headline shape.
 --config 4: scde.posteriors(return.individual.posterior.modes = TRUE) on 30,000 genes x 2,000
 cells (one group); one step returns jp (N x 401) and modes (N x 2000) to the host.
+--config 2b: config 2 with batch correction: two batch levels across
+both groups; one step = batch posteriors over all 200 cells with each group's batch
+composition, both group posteriors, the batch, group and 1601-column batch-adjusted ratio
+posteriors with their summaries and BH (three result tables to the host).
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): genes shard across ranks
 with a fixed gene count per rank (weak scaling); the one exchange is a gather of per-gene Z
@@ -37,16 +41,28 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 METRIC = "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)"
 
 CONFIGS = {
-    2: dict(genes=20000, cells=200, seed=2002, kind="de", cpu_sample=5000,
+    "2": dict(genes=20000, cells=200, seed=2002, kind="de", cpu_sample=5000,
             workload="config2: synthetic 20000 genes x 200 cells (100/100), 401-pt grid, 100 bootstraps, "
                      "n.cores=1 seeding"),
-    3: dict(genes=20000, cells=1000, seed=2003, kind="de", cpu_sample=1000,
+    "3": dict(genes=20000, cells=1000, seed=2003, kind="de", cpu_sample=1000,
             workload="config3: synthetic 20000 genes x 1000 cells (500/500), 401-pt grid, 100 bootstraps, "
                      "n.cores=1 seeding"),
-    4: dict(genes=30000, cells=2000, seed=2004, kind="posteriors", cpu_sample=100,
+    "4": dict(genes=30000, cells=2000, seed=2004, kind="posteriors", cpu_sample=100,
             workload="config4: scde.posteriors, synthetic 30000 genes x 2000 cells (one group), 401-pt grid, "
                      "100 bootstraps, return.individual.posterior.modes, n.cores=1 seeding"),
+    "2b": dict(genes=20000, cells=200, seed=2002, kind="de_batch", cpu_sample=1500, nbatch=2,
+               workload="config2b: batch-corrected scde.expression.difference, synthetic 20000 genes x 200 cells "
+                        "(100/100 groups, 2 batch levels), 401-pt grid, 100 bootstraps, n.cores=1 seeding"),
 }
+METRIC_BATCH = ("genes/sec for batch-corrected scde.expression.difference (400-pt grid, 100 randomizations, "
+                "2 batches)")
+
+
+def synthetic_batch(seed: int, ncells: int, nbatch: int):
+    """Batch labels for the batch config: PCG64(seed + 7), uniform over nbatch levels, so
+    each group spans every batch."""
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    return np.array(["b%d" % k for k in rng.integers(0, nbatch, ncells)])
 
 
 def synthetic(seed: int, ngenes: int, ncells: int, two_groups: bool = True):
@@ -108,6 +124,10 @@ def _cpu_chunk(job):
     if cfg["kind"] == "de":
         O.scde_expression_difference(models, sub, prior["x"], prior["y"], groups, n_randomizations=NBOOT,
                                      n_cores=ncores, gene_offset=lo, ngenes_total=ntotal)
+    elif cfg["kind"] == "de_batch":
+        O.scde_expression_difference_batch(models, sub, prior["x"], prior["y"], groups, cfg["batch"],
+                                           n_randomizations=NBOOT, n_cores=ncores, gene_offset=lo,
+                                           ngenes_total=ntotal)
     else:
         O.scde_posteriors(models, sub, prior["x"], n_randomizations=NBOOT, return_individual_posterior_modes=True,
                           n_cores=ncores, gene_offset=lo, ngenes_total=ntotal)
@@ -140,6 +160,9 @@ def cpu_baseline(cfg, models, counts, groups, prior, sample_genes):
     t0 = time.perf_counter()
     if cfg["kind"] == "de":
         O.scde_expression_difference(models, sub, prior["x"], prior["y"], groups, n_randomizations=NBOOT, n_cores=1)
+    elif cfg["kind"] == "de_batch":
+        O.scde_expression_difference_batch(models, sub, prior["x"], prior["y"], groups, cfg["batch"],
+                                           n_randomizations=NBOOT, n_cores=1)
     else:
         O.scde_posteriors(models, sub, prior["x"], n_randomizations=NBOOT, return_individual_posterior_modes=True,
                           n_cores=1)
@@ -152,7 +175,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-sample", type=int, default=None, help="genes timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -160,7 +183,7 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="forked oracle workers for the parallel CPU baseline (0 = skip; the GPU box's share is 16)")
     args = ap.parse_args()
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
     NG, NC = cfg["genes"], cfg["cells"]
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
 
@@ -183,8 +206,11 @@ def main():
     from scde_amd.models import model_matrix
     from scde_amd.prior import expression_prior
 
-    de = cfg["kind"] == "de"
+    de = cfg["kind"] in ("de", "de_batch")
+    batched = cfg["kind"] == "de_batch"
     models, counts, groups = synthetic(cfg["seed"] + rank, NG, NC, two_groups=de)
+    if batched:
+        cfg["batch"] = synthetic_batch(cfg["seed"], NC, cfg["nbatch"])
     zero_frac = float(np.mean(counts == 0))
     prior = expression_prior(models, counts, length_out=LENGTH_OUT)
     par = None
@@ -206,6 +232,10 @@ def main():
         params = api.DEParams(NC, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
                               NBOOT, 1, rank * NG, world * NG, 0.0, api.get_rand_kind(), int(world == 1))
         res = np.zeros((NG, 6 if world == 1 else 5), order="F")
+        if batched:
+            blevels = sorted(set(cfg["batch"].tolist()))
+            bcodes = np.ascontiguousarray([blevels.index(x) for x in cfg["batch"].tolist()], np.int32)
+            res = np.zeros((NG, 18), order="F")  # batch.adjusted, results, batch.effect
     else:
         cellidx = np.arange(NC, dtype=np.int32)
         jp = np.zeros((NG, G), order="F")
@@ -217,21 +247,29 @@ def main():
                                             1, rank * NG, world * NG, 1, 0, None, None, None, 0, P(jp), P(modes),
                                             None))
             return
-        api.check(L.scde_expression_difference_dev(ctx.handle, dc.ptr, NG, NG, ctypes.byref(params),
-                                                   res.ctypes.data_as(ctypes.c_void_p), None, None, None))
+        if batched:
+            api.check(L.scde_expression_difference_batch_dev(ctx.handle, dc.ptr, NG, NG, ctypes.byref(params), P(mm),
+                                                             P(bcodes), len(blevels), P(res), None, None, None, None,
+                                                             None))
+        else:
+            api.check(L.scde_expression_difference_dev(ctx.handle, dc.ptr, NG, NG, ctypes.byref(params),
+                                                       res.ctypes.data_as(ctypes.c_void_p), None, None, None))
         if dist is not None:
             import torch
-            zt = torch.from_numpy(np.ascontiguousarray(res[:, 4]))
+            # Z of every table (1 or 3) to rank 0; BH over all genes there
+            zcols = [4, 10, 16] if batched else [4]
+            zt = torch.from_numpy(np.ascontiguousarray(res[:, zcols].T).reshape(-1))
             if args.dist_backend == "nccl":
                 zt = zt.cuda()
             gathered = [torch.empty_like(zt) for _ in range(world)] if rank == 0 else None
             dist.gather(zt, gathered, dst=0)
             if rank == 0:
-                zall = torch.cat(gathered).cuda()
+                zall = torch.stack([t.view(len(zcols), NG) for t in gathered], 1).reshape(len(zcols), -1).cuda()
                 cz = torch.empty_like(zall)
                 torch.cuda.current_stream().synchronize()
-                api.bh_cz_device(ctx, zall.data_ptr(), zall.numel(), cz.data_ptr())
-                cz_host = cz.cpu()  # noqa: F841  (the table's last column, on the host)
+                for k in range(len(zcols)):
+                    api.bh_cz_device(ctx, zall[k].data_ptr(), zall.shape[1], cz[k].data_ptr())
+                cz_host = cz.cpu()  # noqa: F841  (the tables' last columns, on the host)
 
     def barrier():
         ctx.synchronize()
@@ -263,13 +301,16 @@ def main():
     boot_ms, boot_n = kt["boot"]
     boot_avg_s = (boot_ms / max(boot_n, 1)) / 1e3
     cpg = NC // 2 if de else NC
-    per_launch_bytes = dominant_kernel_bytes(NG, cpg)
-    achieved = per_launch_bytes / boot_avg_s / 1e9 if boot_n else None
-    prof = profiled_traffic() if args.config == 2 else None
+    # bootstrap launches of one step and their cells: (per group) + (all cells, per group) if batched
+    launch_cells = ([cpg, cpg] if de else [NC]) + ([NC, NC] if batched else [])
+    step_bytes = sum(dominant_kernel_bytes(NG, c) for c in launch_cells)
+    per_launch_bytes = step_bytes / len(launch_cells)
+    achieved = step_bytes * args.steps / (boot_ms / 1e3) / 1e9 if boot_n else None
+    prof = profiled_traffic() if args.config == "2" else None
     # reference-formulation FP64 adds per launch: B x C x G x N
-    ref_adds = NBOOT * cpg * G * NG
+    ref_adds = NBOOT * sum(launch_cells) / len(launch_cells) * G * NG
     out = {
-        "metric": METRIC if de else "genes/sec for scde.posteriors with posterior modes (400-pt grid, "
+        "metric": (METRIC_BATCH if batched else METRIC) if de else "genes/sec for scde.posteriors with posterior modes (400-pt grid, "
                                     "100 randomizations)",
         "value": value,
         "unit": "genes/s",
@@ -299,15 +340,17 @@ def main():
         # PCIe-inclusive rate through the host-buffer API (counts uploaded, table incl. cZ
         # returned per call) -- reported beside `value`, never as it.
         ctx.set_profiling(False)
+        bkw = {"batch": cfg["batch"]} if batched else {}
         api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
-                                       n_cores=1, ctx=ctx)
+                                       n_cores=1, ctx=ctx, **bkw)
         t1 = time.perf_counter()
         for _ in range(3):
             api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
-                                           n_cores=1, ctx=ctx)
+                                           n_cores=1, ctx=ctx, **bkw)
         out["host_buffers_genes_per_s"] = 3 * NG / (time.perf_counter() - t1)
     if rank == 0 and world == 1 and cpu_sample > 0:
-        what = "both groups + ratio + summary + BH" if de else "posteriors + modes"
+        what = ("batch + group posteriors, 3 ratio posteriors + summaries + BH" if batched else
+                "both groups + ratio + summary + BH" if de else "posteriors + modes")
         gps, secs = cpu_baseline(cfg, models, counts, groups, prior, cpu_sample)
         single = {"value": gps, "unit": "genes/s", "cores": 1, "kind": "port",
                   "sample": f"oracle C restatement, first {cpu_sample} genes of the same batch, {what}, {secs:.1f}s"}

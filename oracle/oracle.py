@@ -365,7 +365,8 @@ def scde_expression_difference(models, counts, prior_x, prior_y, groups, n_rando
 
 
 def scde_expression_difference_batch(models, counts, prior_x, prior_y, groups, batch, batch_models=None,
-                                     n_randomizations=150, n_cores=10, expectation=0.0, return_posteriors=False):
+                                     n_randomizations=150, n_cores=10, expectation=0.0, return_posteriors=False,
+                                     gene_offset=0, ngenes_total=None):
     """Restates the batch-corrected branch of scde.expression.difference (R/functions.R:321-399):
     batch posteriors over all cells with each group's batch composition (table(batch[ii])),
     their ratio posterior and summary (batch.effect); the group posteriors, ratio and summary
@@ -382,14 +383,15 @@ def scde_expression_difference_batch(models, counts, prior_x, prior_y, groups, b
         ii = np.nonzero(groups == lv)[0]
         comp = [int(sum(1 for i in ii if batch[i] == b)) for b in levels]
         bjp.append(scde_posteriors(bm, cnt, prior_x, n_randomizations=n_randomizations, batch=batch, composition=comp,
-                                   n_cores=n_cores))
+                                   n_cores=n_cores, gene_offset=gene_offset, ngenes_total=ngenes_total))
     batch_bdiffp = calculate_ratio_posterior(bjp[0], bjp[1], prior_y)
     batch_rep = quick_distribution_summary(batch_bdiffp, diffv, 0.0)
     jpl = []
     for lv in (0, 1):
         ii = np.nonzero(groups == lv)[0]
         sub = {k: np.asarray(v)[ii] for k, v in models.items()}
-        jpl.append(scde_posteriors(sub, cnt[:, ii], prior_x, n_randomizations=n_randomizations, n_cores=n_cores))
+        jpl.append(scde_posteriors(sub, cnt[:, ii], prior_x, n_randomizations=n_randomizations, n_cores=n_cores,
+                                   gene_offset=gene_offset, ngenes_total=ngenes_total))
     bdiffp = calculate_ratio_posterior(jpl[0], jpl[1], prior_y)
     rep = quick_distribution_summary(bdiffp, diffv, expectation)
     a_bdiffp = calculate_ratio_posterior(bdiffp, batch_bdiffp, None, skip_prior_adjustment=True)
