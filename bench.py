@@ -117,10 +117,13 @@ def profiled_traffic():
 
 def _cpu_chunk(job):
     """One mclapply-style worker: the oracle on a contiguous gene chunk with the global
-    n.cores chunk seeds (gene_offset / ngenes_total), as scde.posteriors' forked workers."""
-    cfg, models, counts, groups, prior, lo, hi, ncores, ntotal = job
+    n.cores chunk seeds (gene_offset / ngenes_total), as scde.posteriors' forked workers.
+    Returns (genes, start, end) wall-clock stamps of the compute."""
+    cfg, models, sub, groups, prior, lo, hi, ncores, ntotal = job
     from oracle import oracle as O
-    sub = np.ascontiguousarray(counts[lo:hi])
+    O.lib()
+    t0 = time.time()
+    sub = np.ascontiguousarray(sub)
     if cfg["kind"] == "de":
         O.scde_expression_difference(models, sub, prior["x"], prior["y"], groups, n_randomizations=NBOOT,
                                      n_cores=ncores, gene_offset=lo, ngenes_total=ntotal)
@@ -131,25 +134,24 @@ def _cpu_chunk(job):
     else:
         O.scde_posteriors(models, sub, prior["x"], n_randomizations=NBOOT, return_individual_posterior_modes=True,
                           n_cores=ncores, gene_offset=lo, ngenes_total=ntotal)
-    return hi - lo
+    return hi - lo, t0, time.time()
 
 
 def cpu_baseline_parallel(cfg, models, counts, groups, prior, sample_genes, workers):
     """The reference's CPU path is fork-parallel (mclapply over n.cores gene chunks): the oracle
-    in `workers` forked processes on the first sample_genes genes.  Must run before the GPU
-    is initialised in this process (fork after HIP init is unsafe)."""
+    in `workers` worker processes on the first sample_genes genes.  The workers are spawned
+    (fresh interpreters, no GPU state), so this runs after the GPU work; the wall time is from
+    the first chunk's start to the last chunk's end (interpreter start-up excluded)."""
     import multiprocessing as mp
-    from oracle import oracle as O
-    O.lib()  # build/load before forking
     n = min(sample_genes, counts.shape[0])
     bounds = np.linspace(0, n, workers + 1).astype(int)
-    jobs = [(cfg, models, counts, groups, prior, int(bounds[i]), int(bounds[i + 1]), workers, n)
-            for i in range(workers) if bounds[i + 1] > bounds[i]]
-    ctx = mp.get_context("fork")
-    t0 = time.perf_counter()
-    with ctx.Pool(len(jobs)) as pool:
-        done = sum(pool.map(_cpu_chunk, jobs))
-    dt = time.perf_counter() - t0
+    prior_h = {"x": np.asarray(prior["x"]), "y": np.asarray(prior["y"])}
+    jobs = [(cfg, models, counts[int(bounds[i]):int(bounds[i + 1])], groups, prior_h, int(bounds[i]),
+             int(bounds[i + 1]), workers, n) for i in range(workers) if bounds[i + 1] > bounds[i]]
+    with mp.get_context("spawn").Pool(len(jobs)) as pool:
+        res = pool.map(_cpu_chunk, jobs)
+    done = sum(r[0] for r in res)
+    dt = max(r[2] for r in res) - min(r[1] for r in res)
     return done / dt, dt
 
 
@@ -181,7 +183,7 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the real path) or gloo (CPU gather; rehearsal with ranks sharing one GPU)")
     ap.add_argument("--cpu-workers", type=int, default=16,
-                    help="forked oracle workers for the parallel CPU baseline (0 = skip; the GPU box's share is 16)")
+                    help="oracle worker processes for the parallel CPU baseline (0 = skip; the GPU box's share is 16)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     NG, NC = cfg["genes"], cfg["cells"]
@@ -212,14 +214,10 @@ def main():
     if batched:
         cfg["batch"] = synthetic_batch(cfg["seed"], NC, cfg["nbatch"])
     zero_frac = float(np.mean(counts == 0))
-    prior = expression_prior(models, counts, length_out=LENGTH_OUT)
-    par = None
-    if rank == 0 and world == 1 and cpu_sample > 0 and args.cpu_workers > 0:
-        # before any HIP call: the workers are forked from this process
-        par = cpu_baseline_parallel(cfg, models, counts, groups, prior, cpu_sample * args.cpu_workers,
-                                    args.cpu_workers)
     ctx = api.Context(device)
     dc = api.DeviceCounts(ctx, counts)
+    # the prior is an input of the measured path: computed once, on the GPU
+    prior = expression_prior(models, dc, length_out=LENGTH_OUT, ctx=ctx)
     mm, lt, sq = model_matrix(models)
     px = np.ascontiguousarray(prior["x"], np.float64)
     py = np.ascontiguousarray(prior["y"], np.float64)
@@ -348,6 +346,10 @@ def main():
             api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
                                            n_cores=1, ctx=ctx, **bkw)
         out["host_buffers_genes_per_s"] = 3 * NG / (time.perf_counter() - t1)
+    par = None
+    if rank == 0 and world == 1 and cpu_sample > 0 and args.cpu_workers > 0:
+        par = cpu_baseline_parallel(cfg, models, counts, groups, prior, cpu_sample * args.cpu_workers,
+                                    args.cpu_workers)
     if rank == 0 and world == 1 and cpu_sample > 0:
         what = ("batch + group posteriors, 3 ratio posteriors + summaries + BH" if batched else
                 "both groups + ratio + summary + BH" if de else "posteriors + modes")
@@ -357,7 +359,7 @@ def main():
         if par is not None:
             n = min(cpu_sample * args.cpu_workers, NG)
             out["cpu_baseline"] = {"value": par[0], "unit": "genes/s", "cores": args.cpu_workers, "kind": "port",
-                                   "sample": f"oracle C restatement in {args.cpu_workers} forked workers "
+                                   "sample": f"oracle C restatement in {args.cpu_workers} worker processes "
                                              f"(mclapply-style gene chunks, n.cores={args.cpu_workers} seeding), "
                                              f"first {n} genes of the same batch, {what}, {par[1]:.1f}s wall"}
             out["cpu_baseline_1core"] = single

@@ -166,6 +166,18 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
                                          const int* batch_codes, int nbatch, double* results, double* jp1,
                                          double* jp2, double* ratio, double* adj_ratio, double* batch_ratio);
 
+/* scde.expression.prior (R/functions.R:225-254; replaces the R-level function, which has
+ * no .Call) on device-resident counts (ngenes x ncells int32, column stride ld).  models:
+ * ncells x 12 col-major (conc.b, conc.a, ..., corr.b, corr.a, ..., conc.a2 at column 11 when
+ * square_logit_conc).  max_value NULL = quantile(x[x < Inf], max_quantile) of the
+ * log10(FPM + 1) magnitudes (type 7).  Outputs (host, length_out + 1 each): x, y, lp,
+ * grid_weight (lp / grid_weight may be NULL); max_value_out (nullable) receives the
+ * max.value used.  length_out in [1, 4095]. */
+int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, int ncells,
+                              const double* models, int square_logit_conc, int length_out, double pseudo_count,
+                              double bw, double max_quantile, const double* max_value, double* x, double* y,
+                              double* lp, double* grid_weight, double* max_value_out);
+
 /* scde.posteriors (R/functions.R:566-669) on device-resident counts for the cells
  * listed in cellidx (host, ncells_sel entries).  Outputs are host, col-major.
  * batch_* may be NULL (no batch).  return_post: R postflag (0..3). */

@@ -21,7 +21,7 @@ EXPORTS = [
     "scde_ctx_kernel_times", "scde_ctx_reset_kernel_times",
     "scde_dev_alloc", "scde_dev_free", "scde_h2d", "scde_d2h",
     "scde_expression_difference_dev", "scde_posteriors_dev", "scde_bh_cz_dev",
-    "scde_expression_difference_batch_dev",
+    "scde_expression_difference_batch_dev", "scde_expression_prior_dev",
 ]
 
 
@@ -93,6 +93,7 @@ def lib():
     L.scde_expression_difference_dev.argtypes = [P, P, i64, i, ctypes.POINTER(DEParams), P, P, P, P]
     L.scde_expression_difference_batch_dev.argtypes = [P, P, i64, i, ctypes.POINTER(DEParams), P, P, i, P, P, P, P,
                                                        P, P]
+    L.scde_expression_prior_dev.argtypes = [P, P, i64, i, i, P, i, i, d, d, d, P, P, P, P, P, P]
     L.scde_posteriors_dev.argtypes = [P, P, i64, i, P, i, P, i, i, P, i, i, i, i64, i64, i, i, P, P, P, i, P, P, P]
     _lib = L
     return L

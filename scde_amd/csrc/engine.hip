@@ -154,6 +154,8 @@ struct scde_ctx {
   // workspace
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, T, E, maxi, has_clamp, base_col, ent, nnz, Wt, Z, draws,
       degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
+  // scde.expression.prior
+  Buf pr_cell, pr_part, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
   // unique tables can be built up front, with their host syncs, before the heavy kernels
   struct UniqueSet {
@@ -1454,6 +1456,86 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
 }
 
 // ------------------------------------------------------------------ BH (host)
+// scde.expression.prior (R/functions.R:225-254) on device-resident counts (prior.hip).
+int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, int ncells,
+                              const double* models, int square_logit_conc, int length_out, double pseudo_count,
+                              double bw, double max_quantile, const double* max_value, double* x, double* y,
+                              double* lp, double* grid_weight, double* max_value_out) {
+  if (!ctx || !counts_dev || !models || !x || !y) return fail(SCDE_EARG, "null argument");
+  if (ngenes <= 0 || ncells <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
+  if (length_out < 1 || length_out > 4095) return fail(SCDE_EARG, "length.out must be in [1, 4095]");
+  if (!(bw > 0)) return fail(SCDE_EARG, "bw must be positive");
+  if (!max_value && !(max_quantile >= 0 && max_quantile <= 1)) return fail(SCDE_EARG, "'probs' outside [0,1]");
+  if ((long long)ngenes * ncells > 0x7fffffffLL) return fail(SCDE_EARG, "ngenes x ncells too large");
+  HCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const int N = ngenes, C = ncells, L = length_out;
+  // per-cell constants: corr.b, corr.a, conc.b, conc.a, conc.a2 (model columns 3, 4, 0, 1, 11)
+  std::vector<double> cellp((size_t)5 * C);
+  const int mcol[5] = {3, 4, 0, 1, 11};
+  for (int j = 0; j < 5; ++j)
+    for (int c = 0; c < C; ++c)
+      cellp[(size_t)j * C + c] = (j == 4 && !square_logit_conc) ? 0.0 : models[(size_t)mcol[j] * C + c];
+  RCHK(upload(ctx, ctx->pr_cell, cellp.data(), sizeof(double) * cellp.size()));
+  const int nb = prior_blocks(N, C, 1024);
+  HCHK(ctx->pr_part.ensure(sizeof(double) * 6 * nb));
+  HCHK(ctx->pr_stats.ensure(sizeof(double) * 4));
+  const long long NC = (long long)N * C;
+  const bool need_sort = !max_value && max_quantile < 1.0;
+  if (need_sort) HCHK(ctx->pr_v.ensure(sizeof(double) * NC));
+  HCHK(launch_prior_stats(counts_dev, ld, N, C, ctx->pr_cell.as<double>(), square_logit_conc,
+                          need_sort ? ctx->pr_v.as<double>() : nullptr, ctx->pr_part.as<double>(), nb,
+                          ctx->pr_stats.as<double>(), st));
+  double stats[4];
+  HCHK(hipMemcpyAsync(stats, ctx->pr_stats.p, sizeof(stats), hipMemcpyDeviceToHost, st));
+  RCHK(ctx->sync());
+  const double wsum = stats[0];
+  const long long nfin = (long long)stats[3];
+  // totMass = sum(weights[is.finite(x)]) / sum(weights), 1 when every x is finite
+  const double tot_mass = nfin == NC ? 1.0 : stats[1] / stats[0];
+  double mv;
+  if (max_value) {
+    mv = *max_value;
+  } else if (nfin == 0) {
+    return fail(SCDE_EARG, "no finite expression magnitudes for quantile()");
+  } else if (!need_sort) {
+    mv = stats[2];  // quantile(x, 1) = max
+  } else {
+    // quantile(x[x < Inf], p, type = 7): the finite values sort first
+    size_t wb = 0;
+    HCHK(launch_sort_doubles(nullptr, nullptr, NC, nullptr, &wb, st));
+    HCHK(ctx->pr_sortw.ensure(wb));
+    HCHK(ctx->pr_sorted.ensure(sizeof(double) * NC));
+    HCHK(launch_sort_doubles(ctx->pr_v.as<double>(), ctx->pr_sorted.as<double>(), NC, ctx->pr_sortw.p, &wb, st));
+    const double index = 1 + (double)std::max<long long>(nfin - 1, 0) * max_quantile;
+    const long long lo = (long long)std::floor(index), hi = (long long)std::ceil(index);
+    double xl = 0, xh = 0;
+    HCHK(hipMemcpyAsync(&xl, ctx->pr_sorted.as<double>() + (lo - 1), sizeof(double), hipMemcpyDeviceToHost, st));
+    HCHK(hipMemcpyAsync(&xh, ctx->pr_sorted.as<double>() + (hi - 1), sizeof(double), hipMemcpyDeviceToHost, st));
+    RCHK(ctx->sync());
+    mv = xl;
+    if (index > lo && xh != xl) {
+      const double h = index - lo;
+      mv = (1 - h) * xl + h * xh;
+    }
+  }
+  if (!(mv > 0) || !std::isfinite(mv)) return fail(SCDE_EARG, "max.value must be positive and finite");
+  const int n = prior_grid_n(L);
+  HCHK(ctx->pr_hist.ensure(sizeof(unsigned long long) * (size_t)nb * n));
+  HCHK(ctx->pr_work.ensure(sizeof(double) * 4 * (size_t)n));
+  HCHK(ctx->pr_out.ensure(sizeof(double) * 4 * (size_t)(L + 1)));
+  HCHK(launch_prior_density(counts_dev, ld, N, C, ctx->pr_cell.as<double>(), square_logit_conc, wsum, tot_mass, mv,
+                            bw, L, pseudo_count / (double)N, ctx->pr_hist.as<unsigned long long>(), nb,
+                            ctx->pr_work.as<double>(), ctx->pr_out.as<double>(), st));
+  const size_t m = (size_t)L + 1;
+  double* outs[4] = {x, y, lp, grid_weight};
+  for (int k = 0; k < 4; ++k)
+    if (outs[k])
+      HCHK(hipMemcpyAsync(outs[k], ctx->pr_out.as<double>() + k * m, sizeof(double) * m, hipMemcpyDeviceToHost, st));
+  if (max_value_out) *max_value_out = mv;
+  return ctx->sync();
+}
+
 int scde_bh_cz_dev(scde_ctx* ctx, const double* z_dev, int64_t n, double* cz_dev) {
   if (!ctx || n < 0 || (n > 0 && (!z_dev || !cz_dev))) return fail(SCDE_EARG, "bad arguments");
   if (n > 0x7fffffff) return fail(SCDE_EARG, "n too large");

@@ -154,6 +154,20 @@ hipError_t launch_uci(const int* counts, long long ld, long long g0, int ngenes,
 hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int GS, double* dst, hipStream_t s);
 // device BH cZ (bh.hip); work == nullptr -> *work_bytes = required size
 hipError_t launch_bh_cz(const double* z, int n, double* cz, void* work, size_t* work_bytes, hipStream_t s);
+
+// scde.expression.prior (prior.hip).  cellp: 5 x C (corr.b, corr.a, conc.b, conc.a, conc.a2).
+// Stats: out[0..3] = sum w, sum w over finite v, max finite v, count of finite v.
+hipError_t launch_prior_stats(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
+                              double* vout, double* partials, int nb, double* out, hipStream_t s);
+int prior_blocks(int N, int C, int cap);
+int prior_grid_n(int L);
+// partial: nb x prior_grid_n(L) u64; work: 4 x prior_grid_n(L) doubles; out: 4 x (L+1)
+// (x, y, lp, grid.weight)
+hipError_t launch_prior_density(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
+                                double wsum, double tot_mass, double max_value, double bw, int L, double pc,
+                                unsigned long long* partial, int nb, double* work, double* out, hipStream_t s);
+hipError_t launch_sort_doubles(const double* in, double* out, long long n, void* work, size_t* work_bytes,
+                               hipStream_t s);
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s);
 
 }  // namespace scde

@@ -1,27 +1,28 @@
-"""Host-side producers of the hot path's inputs (numpy, float64).
+"""The producers of the DE path's inputs.
 
-These restate the R helpers that *feed* the DE path (SURVEY.md §8(f) "next"
-#2); they are not on the GPU hot path:
-
+  * ``expression_prior``      scde.expression.prior      R/functions.R:225-254, on the GPU
+                              (``scde_expression_prior_dev``, csrc/prior.hip); counts may be
+                              host arrays or a resident ``DeviceCounts``.
   * ``expression_magnitude``  scde.expression.magnitude  R/functions.R:694-697
   * ``failure_probability``   scde.failure.probability   R/functions.R:725-750
-  * ``expression_prior``      scde.expression.prior      R/functions.R:225-254
-      - ``r_density``  R's density.default (gaussian kernel, weights, pre-4.4
-        "old.coords" grid): BinDist linear binning + FFT convolution + approx()
-      - ``r_quantile7`` R's quantile(type = 7)
+    (elementwise R-API helpers returning genes x cells matrices, numpy on the host).
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
-from .models import as_model_dict
+from . import api
+from ._lib import check, lib
+from .models import as_model_dict, model_matrix
 
 
 def expression_magnitude(models, counts):
     """t((t(log(counts)) - corr.b) / corr.a)   (natural-log FPM; log(0) = -inf)."""
     m = as_model_dict(models)
     c = np.asarray(counts, np.float64)
-    with np.errstate(divide="ignore"):
+    with np.errstate(divide="ignore", invalid="ignore"):
         return (np.log(c) - m["corr.b"][None, :]) / m["corr.a"][None, :]
 
 
@@ -47,94 +48,32 @@ def failure_probability(models, magnitudes=None, counts=None):
     return x
 
 
-def r_quantile7(x, p):
-    xs = np.sort(np.asarray(x, np.float64))
-    n = len(xs)
-    index = 1 + max(n - 1, 0) * p
-    lo = int(np.floor(index))
-    hi = int(np.ceil(index))
-    qs = xs[lo - 1]
-    h = index - lo
-    if index > lo and xs[hi - 1] != qs:
-        qs = (1 - h) * qs + h * xs[hi - 1]
-    return qs
-
-
-def r_seq_len(frm, to, n):
-    """seq.int(from, to, length.out = n)."""
-    if n == 1:
-        return np.array([frm], np.float64)
-    by = (to - frm) / (n - 1)
-    out = frm + np.arange(n, dtype=np.float64) * by
-    out[-1] = to
-    return out
-
-
-def _bindist(x, w, lo, hi, n):
-    """R's C_BinDist (src/library/stats/src/massdist.c): linear binning into 2n cells."""
-    y = np.zeros(2 * n)
-    xdelta = (hi - lo) / (n - 1)
-    ok = np.isfinite(x)
-    x, w = x[ok], w[ok]
-    xpos = (x - lo) / xdelta
-    ix = np.floor(xpos).astype(np.int64)
-    fx = xpos - ix
-    ixmax = n - 2
-    mid = (ix >= 0) & (ix <= ixmax)
-    np.add.at(y, ix[mid], w[mid] * (1 - fx[mid]))
-    np.add.at(y, ix[mid] + 1, w[mid] * fx[mid])
-    left = ix == -1
-    np.add.at(y, np.zeros(left.sum(), np.int64), w[left] * fx[left])
-    right = ix == ixmax + 1
-    np.add.at(y, ix[right], w[right] * (1 - fx[right]))
-    return y
-
-
-def r_density(x, bw, weights, n_user, frm, to, cut=3):
-    """density.default(x, bw, weights=, n=, from=, to=) with the gaussian kernel (R < 4.4 grid)."""
-    x = np.asarray(x, np.float64)
-    w = np.asarray(weights, np.float64)
-    fin = np.isfinite(x)
-    wsum = w.sum()
-    tot_mass = w[fin].sum() / wsum if not fin.all() else 1.0
-    n = max(n_user, 512)
-    if n > 512:
-        n = int(2 ** np.ceil(np.log2(n)))
-    lo = frm - 4 * bw
-    up = to + 4 * bw
-    y = _bindist(x, w, lo, up, n) * tot_mass
-    kords = r_seq_len(0.0, 2 * (up - lo), 2 * n)
-    kords[n + 1:2 * n] = -kords[n - 1:0:-1]
-    kords = np.exp(-0.5 * (kords / bw) ** 2) / (bw * np.sqrt(2 * np.pi))
-    conv = np.fft.ifft(np.fft.fft(y) * np.conj(np.fft.fft(kords)))
-    kords = np.maximum(0.0, conv.real[:n])
-    xords = r_seq_len(lo, up, n)
-    xo = r_seq_len(frm, to, n_user)
-    yo = np.interp(xo, xords, kords, left=np.nan, right=np.nan)
-    return xo, yo
-
-
-def expression_prior(models, counts, length_out=400, pseudo_count=1, bw=0.1, max_quantile=1.0,
-                     max_value=None):
-    """scde.expression.prior (R/functions.R:225-254).  Returns dict x, y, lp, grid_weight."""
-    fpkm = expression_magnitude(models, counts)
-    fail = failure_probability(models, counts=counts)
-    with np.errstate(over="ignore"):
-        fpkm = np.log10(np.exp(fpkm) + 1)
-    wts = (1 - fail).ravel(order="F")
-    wts = wts / wts.sum()
-    if max_value is None:
-        xv = fpkm.ravel(order="F")
-        max_value = r_quantile7(xv[xv < np.inf], max_quantile)
-    xs = fpkm.ravel(order="F")
-    mx, my = r_density(np.concatenate([-xs, xs]), bw, np.concatenate([wts / 2, wts / 2]),
-                       2 * length_out + 1, -max_value, max_value)
-    gx = mx[length_out:]
-    gy = my[length_out:].copy()
-    gy[np.isnan(gy)] = 0
-    gy = gy + pseudo_count / fpkm.shape[0]
-    gy = gy / gy.sum()
-    lp = np.log(gy)
-    xe = np.concatenate([[gx[0]], gx + np.concatenate([np.diff(gx) / 2, [0.0]])])
-    gw = np.diff(10.0 ** xe - 1)
-    return {"x": gx, "y": gy, "lp": lp, "grid.weight": gw, "max.value": max_value}
+def expression_prior(models, counts, length_out=400, show_plot=False, pseudo_count=1, bw=0.1, max_quantile=1.0,
+                     max_value=None, ctx: api.Context | None = None):
+    """scde.expression.prior (R/functions.R:225-254) -> dict x, y, lp, grid.weight (and
+    max.value, the value used).  Computed on the GPU; ``counts`` is a genes x cells matrix
+    (columns matched to the model rows) or a ``DeviceCounts`` already in HBM."""
+    ctx = ctx or api.default_context()
+    mm, _, sq = model_matrix(models)
+    own = not isinstance(counts, api.DeviceCounts)
+    if own:
+        mat, _ = api._align_counts(models, counts)
+        dc = api.DeviceCounts(ctx, mat)
+    else:
+        dc = counts
+    N, C = dc.ngenes, dc.ncells
+    if C != mm.shape[0]:
+        raise ValueError("counts and models disagree on the number of cells")
+    L = int(length_out)
+    out = np.zeros((4, L + 1))
+    mv_out = ctypes.c_double()
+    mv_in = None if max_value is None else ctypes.byref(ctypes.c_double(float(max_value)))
+    try:
+        check(lib().scde_expression_prior_dev(ctx.handle, dc.ptr, N, N, C, api._p(mm), sq, L, float(pseudo_count),
+                                              float(bw), float(max_quantile), mv_in, api._p(out[0]), api._p(out[1]),
+                                              api._p(out[2]), api._p(out[3]), ctypes.byref(mv_out)))
+    finally:
+        if own:
+            dc.free()
+    return {"x": out[0].copy(), "y": out[1].copy(), "lp": out[2].copy(), "grid.weight": out[3].copy(),
+            "max.value": mv_out.value}

@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 import rdata  # noqa: E402
 from oracle import oracle as O  # noqa: E402
-from scde_amd.prior import expression_prior  # noqa: E402
+from oracle.prior import expression_prior  # noqa: E402
 
 REF = "/root/reference/data"
 GOLD = os.path.join(ROOT, "tests", "golden")
