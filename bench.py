@@ -10,6 +10,8 @@ results to host.
 --config 3: 20,000 genes x 1,000 cells (500/500), the north_star's headline shape.
 --config 4: scde.posteriors(return.individual.posterior.modes = TRUE) on 30,000 genes x 2,000
 cells (one group); one step returns jp (N x 401) and modes (N x 2000) to the host.
+--config prior: scde.expression.prior on config 3's 20,000 x 1,000
+counts, resident; one step = the whole prior (x, y, lp, grid.weight) to the host.
 --config 2b: config 2 with batch correction: two batch levels across
 both groups; one step = batch posteriors over all 200 cells with each group's batch
 composition, both group posteriors, the batch, group and 1601-column batch-adjusted ratio
@@ -54,6 +56,10 @@ CONFIGS = {
                workload="config2b: batch-corrected scde.expression.difference, synthetic 20000 genes x 200 cells "
                         "(100/100 groups, 2 batch levels), 401-pt grid, 100 bootstraps, n.cores=1 seeding"),
 }
+CONFIGS["prior"] = dict(genes=20000, cells=1000, seed=2003, kind="prior", cpu_sample=20000,
+                        workload="prior: scde.expression.prior, synthetic 20000 genes x 1000 cells (config 3 counts), "
+                                 "length.out 400, max.quantile 1")
+METRIC_PRIOR = "genes/sec for scde.expression.prior (length.out 400, 1000 cells)"
 METRIC_BATCH = ("genes/sec for batch-corrected scde.expression.difference (400-pt grid, 100 randomizations, "
                 "2 batches)")
 
@@ -172,6 +178,57 @@ def cpu_baseline(cfg, models, counts, groups, prior, sample_genes):
     return sample_genes / dt, dt
 
 
+def bench_prior(args, cfg, rank, world, device):
+    """--config prior: scde.expression.prior on resident counts.  Roofline of the element
+    pass that bins (k_prior_bin): it must read each count once (4 B per gene x cell)."""
+    from scde_amd import api
+    from scde_amd.prior import expression_prior
+    NG, NC = cfg["genes"], cfg["cells"]
+    models, counts, _ = synthetic(cfg["seed"] + rank, NG, NC)
+    ctx = api.Context(device)
+    dc = api.DeviceCounts(ctx, counts)
+    for _ in range(args.warmup):
+        prior = expression_prior(models, dc, length_out=LENGTH_OUT, ctx=ctx)
+    ctx.set_profiling(True)
+    ctx.reset_kernel_times()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        prior = expression_prior(models, dc, length_out=LENGTH_OUT, ctx=ctx)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    kt = ctx.kernel_times()
+    bin_ms, bin_n = kt["prior_bin"]
+    bin_s = bin_ms / max(bin_n, 1) / 1e3
+    per_launch = 4 * NG * NC
+    achieved = per_launch / bin_s / 1e9 if bin_n else None
+    out = {"metric": METRIC_PRIOR, "value": NG * args.steps / dt, "unit": "genes/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": f"synthetic (PCG64 seed {cfg['seed']}; o.ifm-resampled models)",
+           "config": {"workload": cfg["workload"], "genes_per_gpu": NG, "cells": NC, "length_out": LENGTH_OUT,
+                      "parallelism": "single GPU"},
+           "roofline": {"bound": "hbm", "kernel": "k_prior_bin (magnitudes, weights, binning)",
+                        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+                        "avg_launch_ms": bin_s * 1e3, "launches": bin_n, "algorithmic_bytes_per_launch": per_launch},
+           "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
+    cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
+    if rank == 0 and cpu_sample > 0:
+        from oracle import prior as OP
+        n = min(cpu_sample, NG)
+        t1 = time.perf_counter()
+        OP.expression_prior(models, counts[:n], LENGTH_OUT)
+        secs = time.perf_counter() - t1
+        out["cpu_baseline"] = {"value": n / secs, "unit": "genes/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle numpy restatement (oracle/prior.py) on the first {n} genes, "
+                                         f"{secs:.1f}s"}
+    if rank == 0:
+        print(json.dumps(out))
+    dc.free()
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -208,6 +265,8 @@ def main():
     from scde_amd.models import model_matrix
     from scde_amd.prior import expression_prior
 
+    if cfg["kind"] == "prior":
+        return bench_prior(args, cfg, rank, world, device)
     de = cfg["kind"] in ("de", "de_batch")
     batched = cfg["kind"] == "de_batch"
     models, counts, groups = synthetic(cfg["seed"] + rank, NG, NC, two_groups=de)
@@ -332,7 +391,7 @@ def main():
                      "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
                      "algorithmic_bytes_per_launch": per_launch_bytes,
                      "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None},
-        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items()},
+        "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
     }
     if rank == 0 and world == 1 and de and not args.no_profile:
         # PCIe-inclusive rate through the host-buffer API (counts uploaded, table incl. cZ

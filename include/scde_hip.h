@@ -111,7 +111,8 @@ void scde_ctx_destroy(scde_ctx* ctx);
 int scde_ctx_synchronize(scde_ctx* ctx);
 /* Per-kernel HIP-event timing on the context's stream (0 = off). */
 int scde_ctx_set_profiling(scde_ctx* ctx, int on);
-/* slot names: 0 tables, 1 boot, 2 ratio_summary, 3 unique, 4 other; ms totals and launch counts */
+/* slot names: 0 tables, 1 boot, 2 ratio_summary, 3 unique, 4 other, 5 prior_stats,
+ * 6 prior_bin, 7 prior_tail; ms totals and launch counts */
 int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslots);
 int scde_ctx_reset_kernel_times(scde_ctx* ctx);
 
@@ -172,7 +173,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
  * square_logit_conc).  max_value NULL = quantile(x[x < Inf], max_quantile) of the
  * log10(FPM + 1) magnitudes (type 7).  Outputs (host, length_out + 1 each): x, y, lp,
  * grid_weight (lp / grid_weight may be NULL); max_value_out (nullable) receives the
- * max.value used.  length_out in [1, 4095]. */
+ * max.value used.  length_out in [1, 1023]. */
 int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, int ncells,
                               const double* models, int square_logit_conc, int length_out, double pseudo_count,
                               double bw, double max_quantile, const double* max_value, double* x, double* y,

@@ -228,11 +228,14 @@ class Context:
     def set_profiling(self, on: bool):
         check(lib().scde_ctx_set_profiling(self.handle, int(bool(on))))
 
+    SLOT_NAMES = ["tables", "boot", "ratio_summary", "unique", "other", "prior_stats", "prior_bin", "prior_tail"]
+
     def kernel_times(self):
-        ms = np.zeros(5)
-        n = np.zeros(5, np.int64)
-        check(lib().scde_ctx_kernel_times(self.handle, _p(ms), _p(n), 5))
-        names = ["tables", "boot", "ratio_summary", "unique", "other"]
+        """{slot: (total ms, launches)} from HIP events on the context's stream."""
+        names = self.SLOT_NAMES
+        ms = np.zeros(len(names))
+        n = np.zeros(len(names), np.int64)
+        check(lib().scde_ctx_kernel_times(self.handle, _p(ms), _p(n), len(names)))
         return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(names)}
 
     def reset_kernel_times(self):

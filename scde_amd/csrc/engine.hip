@@ -146,7 +146,17 @@ std::vector<long long> r_chunk_starts(long long N, int n) {
 
 }  // namespace
 
-enum { SLOT_TABLES = 0, SLOT_BOOT = 1, SLOT_RATIO = 2, SLOT_UNIQUE = 3, SLOT_OTHER = 4, NSLOTS = 5 };
+enum {
+  SLOT_TABLES = 0,
+  SLOT_BOOT = 1,
+  SLOT_RATIO = 2,
+  SLOT_UNIQUE = 3,
+  SLOT_OTHER = 4,
+  SLOT_PRIOR_STATS = 5,
+  SLOT_PRIOR_BIN = 6,
+  SLOT_PRIOR_TAIL = 7,
+  NSLOTS = 8
+};
 
 struct scde_ctx {
   int device = 0;
@@ -155,7 +165,7 @@ struct scde_ctx {
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, T, E, maxi, has_clamp, base_col, ent, nnz, Wt, Z, draws,
       degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
   // scde.expression.prior
-  Buf pr_cell, pr_part, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
+  Buf pr_cell, pr_part, pr_occ, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
   // unique tables can be built up front, with their host syncs, before the heavy kernels
   struct UniqueSet {
@@ -1463,7 +1473,7 @@ int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, 
                               double* lp, double* grid_weight, double* max_value_out) {
   if (!ctx || !counts_dev || !models || !x || !y) return fail(SCDE_EARG, "null argument");
   if (ngenes <= 0 || ncells <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
-  if (length_out < 1 || length_out > 4095) return fail(SCDE_EARG, "length.out must be in [1, 4095]");
+  if (length_out < 1 || length_out > 1023) return fail(SCDE_EARG, "length.out must be in [1, 1023]");
   if (!(bw > 0)) return fail(SCDE_EARG, "bw must be positive");
   if (!max_value && !(max_quantile >= 0 && max_quantile <= 1)) return fail(SCDE_EARG, "'probs' outside [0,1]");
   if ((long long)ngenes * ncells > 0x7fffffffLL) return fail(SCDE_EARG, "ngenes x ncells too large");
@@ -1477,15 +1487,19 @@ int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, 
     for (int c = 0; c < C; ++c)
       cellp[(size_t)j * C + c] = (j == 4 && !square_logit_conc) ? 0.0 : models[(size_t)mcol[j] * C + c];
   RCHK(upload(ctx, ctx->pr_cell, cellp.data(), sizeof(double) * cellp.size()));
-  const int nb = prior_blocks(N, C, 1024);
+  const int nb = prior_blocks(N, C, 2048);
   HCHK(ctx->pr_part.ensure(sizeof(double) * 6 * nb));
+  HCHK(ctx->pr_occ.ensure(sizeof(int) * 256 * (size_t)prior_items(N, C)));
   HCHK(ctx->pr_stats.ensure(sizeof(double) * 4));
   const long long NC = (long long)N * C;
   const bool need_sort = !max_value && max_quantile < 1.0;
   if (need_sort) HCHK(ctx->pr_v.ensure(sizeof(double) * NC));
+  hipEvent_t ev = ctx->mark_begin(SLOT_PRIOR_STATS);
   HCHK(launch_prior_stats(counts_dev, ld, N, C, ctx->pr_cell.as<double>(), square_logit_conc,
-                          need_sort ? ctx->pr_v.as<double>() : nullptr, ctx->pr_part.as<double>(), nb,
+                          need_sort ? ctx->pr_v.as<double>() : nullptr, ctx->pr_occ.as<int>(),
+                          ctx->pr_part.as<double>(), nb,
                           ctx->pr_stats.as<double>(), st));
+  ctx->mark_end(SLOT_PRIOR_STATS, ev);
   double stats[4];
   HCHK(hipMemcpyAsync(stats, ctx->pr_stats.p, sizeof(stats), hipMemcpyDeviceToHost, st));
   RCHK(ctx->sync());
@@ -1521,12 +1535,17 @@ int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, 
   }
   if (!(mv > 0) || !std::isfinite(mv)) return fail(SCDE_EARG, "max.value must be positive and finite");
   const int n = prior_grid_n(L);
-  HCHK(ctx->pr_hist.ensure(sizeof(unsigned long long) * (size_t)nb * n));
-  HCHK(ctx->pr_work.ensure(sizeof(double) * 4 * (size_t)n));
+  HCHK(ctx->pr_hist.ensure(sizeof(unsigned long long) * (size_t)n));
+  HCHK(ctx->pr_work.ensure(sizeof(double) * 3 * (size_t)n));
   HCHK(ctx->pr_out.ensure(sizeof(double) * 4 * (size_t)(L + 1)));
-  HCHK(launch_prior_density(counts_dev, ld, N, C, ctx->pr_cell.as<double>(), square_logit_conc, wsum, tot_mass, mv,
-                            bw, L, pseudo_count / (double)N, ctx->pr_hist.as<unsigned long long>(), nb,
-                            ctx->pr_work.as<double>(), ctx->pr_out.as<double>(), st));
+  ev = ctx->mark_begin(SLOT_PRIOR_BIN);
+  HCHK(launch_prior_bin(counts_dev, ld, N, C, ctx->pr_cell.as<double>(), square_logit_conc, ctx->pr_occ.as<int>(),
+                        wsum, mv, bw, L, ctx->pr_hist.as<unsigned long long>(), nb, st));
+  ctx->mark_end(SLOT_PRIOR_BIN, ev);
+  ev = ctx->mark_begin(SLOT_PRIOR_TAIL);
+  HCHK(launch_prior_tail(tot_mass, mv, bw, L, pseudo_count / (double)N, ctx->pr_hist.as<unsigned long long>(),
+                         ctx->pr_work.as<double>(), ctx->pr_out.as<double>(), st));
+  ctx->mark_end(SLOT_PRIOR_TAIL, ev);
   const size_t m = (size_t)L + 1;
   double* outs[4] = {x, y, lp, grid_weight};
   for (int k = 0; k < 4; ++k)

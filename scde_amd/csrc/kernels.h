@@ -156,16 +156,21 @@ hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int 
 hipError_t launch_bh_cz(const double* z, int n, double* cz, void* work, size_t* work_bytes, hipStream_t s);
 
 // scde.expression.prior (prior.hip).  cellp: 5 x C (corr.b, corr.a, conc.b, conc.a, conc.a2).
-// Stats: out[0..3] = sum w, sum w over finite v, max finite v, count of finite v.
+// Stats: out[0..3] = sum w, sum w over finite v, max finite v, count of finite v; occ:
+// prior_items(N, C) x 256 count multiplicities (read back by launch_prior_bin); vout (nullable)
+// = v per element in R order.
 hipError_t launch_prior_stats(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
-                              double* vout, double* partials, int nb, double* out, hipStream_t s);
+                              double* vout, int* occ, double* partials, int nb, double* out, hipStream_t s);
+long long prior_items(int N, int C);
 int prior_blocks(int N, int C, int cap);
 int prior_grid_n(int L);
-// partial: nb x prior_grid_n(L) u64; work: 4 x prior_grid_n(L) doubles; out: 4 x (L+1)
+// hist: prior_grid_n(L) u64 (zeroed here); work: 3 x prior_grid_n(L) doubles; out: 4 x (L+1)
 // (x, y, lp, grid.weight)
-hipError_t launch_prior_density(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
-                                double wsum, double tot_mass, double max_value, double bw, int L, double pc,
-                                unsigned long long* partial, int nb, double* work, double* out, hipStream_t s);
+hipError_t launch_prior_bin(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
+                            const int* occ, double wsum, double max_value, double bw, int L,
+                            unsigned long long* hist, int nb, hipStream_t s);
+hipError_t launch_prior_tail(double tot_mass, double max_value, double bw, int L, double pc,
+                             const unsigned long long* hist, double* work, double* out, hipStream_t s);
 hipError_t launch_sort_doubles(const double* in, double* out, long long n, void* work, size_t* work_bytes,
                                hipStream_t s);
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s);

@@ -9,14 +9,19 @@
 // normalised; lp and grid.weight.
 //
 // Kernels:
-//   k_prior_stats  element pass: double-double sums of w (all, finite v), max of finite v,
-//                  count of finite v; optionally v itself (for quantile(max.quantile < 1)).
-//   k_prior_bin    element pass: C_BinDist linear binning of +-v.  Each bin term w_i (1 - fx)
-//                  is rounded to a 2^-60 fixed point and summed in int64 (LDS histogram per
-//                  block, one partial histogram per block): deterministic, order-independent.
-//   k_prior_hist   partial histograms -> y = sum * 2^-60 * totMass.
+//   k_prior_occ    element pass 1.  v and w depend only on (cell, count): per (cell, gene
+//                  tile) the counts < 256 are histogrammed in LDS (zeros by ballot) and each
+//                  (cell, count) present is evaluated once; larger counts per element.
+//                  Double-double sums of w (all, finite v; exact w * multiplicity), max and
+//                  count of finite v.  k_prior_vals writes v itself for quantile(p < 1).
+//   k_prior_bin    element pass 2: C_BinDist linear binning of +-v from the same (cell,
+//                  count) multiplicities (+ the large counts per element).  Each bin term
+//                  w_i (1 - fx) is rounded to a 2^-60 fixed point and summed in int64 (LDS
+//                  histogram per block, integer atomics into the global one): deterministic
+//                  and order-independent, so k copies add exactly k times one term.
 //   k_prior_kords  dnorm(kords, sd = bw) on the 2n circular lags (nmath dnorm4).
-//   k_prior_conv   the FFT cross-correlation of R, as the direct sum over the n nonzero bins.
+//   k_prior_conv   the FFT cross-correlation of R as the direct sum over the n nonzero bins
+//                  (y = histogram * 2^-60 * totMass), LDS-staged.
 //   k_prior_final  approx(rule = 1) at the upper-half output points, pseudo count,
 //                  double-double normalisation, lp, grid.weight.
 // Work items of the element passes are (cell, 2048-gene tile): cell constants are
@@ -35,7 +40,8 @@ namespace scde {
 namespace {
 
 constexpr int kPriorBlock = 256;
-constexpr int kPriorGenesPerThread = 8;
+constexpr int kPriorGenesPerThread = 16;
+constexpr int kPriorSmall = kPriorBlock;  // counts below this are histogrammed per (cell, tile)
 constexpr int kPriorTile = kPriorBlock * kPriorGenesPerThread;
 constexpr double kFix = 1152921504606846976.0;  // 2^60
 constexpr double kInvFix = 1.0 / 1152921504606846976.0;
@@ -64,36 +70,26 @@ __device__ inline PriorCell load_cell(const double* cellp, int C, int c) {
   return p;
 }
 
-// Per-block partials: [S_all.hi, S_all.lo, S_fin.hi, S_fin.lo, max finite v, n finite v].
-__global__ __launch_bounds__(kPriorBlock) void k_prior_stats(const int* __restrict__ counts, long long ld, int N,
-                                                             int C, const double* __restrict__ cellp, int sq,
-                                                             double* __restrict__ vout,
-                                                             double* __restrict__ partials) {
-  const int tid = threadIdx.x;
-  const int ntiles = (N + kPriorTile - 1) / kPriorTile;
-  const long long items = (long long)ntiles * C;
-  dd sa{0.0, 0.0}, sf{0.0, 0.0};
-  double vmax = -INFINITY, nfin = 0.0;
-  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
-    const int c = (int)(it / ntiles), tile = (int)(it % ntiles);
-    const PriorCell p = load_cell(cellp, C, c);
-    const int* col = counts + (long long)c * ld;
-#pragma unroll 2
-    for (int k = 0; k < kPriorGenesPerThread; ++k) {
-      const int g = tile * kPriorTile + k * kPriorBlock + tid;
-      if (g >= N) break;
-      double v, w;
-      prior_elem(col[g], p, sq, v, w);
-      sa = dd_add_d(sa, w);
-      if (v < INFINITY) {
-        sf = dd_add_d(sf, w);
-        vmax = fmax(vmax, v);
-        nfin += 1.0;
-      }
-      if (vout) vout[(long long)c * N + g] = v;
-    }
+// exact w * k as a double-double (k < 2^31)
+__device__ inline dd dd_mul_int(double w, int k) {
+  const double kk = (double)k;
+  const double hi = __dmul_rn(w, kk);
+  return dd{hi, fma(w, kk, -hi)};
+}
+
+__device__ inline void stats_add(dd& sa, dd& sf, double& vmax, double& nfin, double v, double w, int k) {
+  const dd t = k == 1 ? dd{w, 0.0} : dd_mul_int(w, k);
+  sa = dd_add(sa, t);
+  if (v < INFINITY) {
+    sf = dd_add(sf, t);
+    vmax = fmax(vmax, v);
+    nfin += (double)k;
   }
+}
+
+__device__ inline void block_stats_out(dd sa, dd sf, double vmax, double nfin, double* __restrict__ out6) {
   __shared__ double red[6][kPriorBlock];
+  const int tid = threadIdx.x;
   red[0][tid] = sa.hi;
   red[1][tid] = sa.lo;
   red[2][tid] = sf.hi;
@@ -114,10 +110,94 @@ __global__ __launch_bounds__(kPriorBlock) void k_prior_stats(const int* __restri
     }
     __syncthreads();
   }
-  if (tid < 6) partials[(long long)blockIdx.x * 6 + tid] = red[tid][0];
+  if (tid < 6) out6[tid] = red[tid][0];
 }
 
-// One block: partials (nb x 6) -> out[0..5] = S_all, S_fin (rounded dd), max, nfinite.
+// Appends `cnt` to the block's LDS queue on the lanes where `take` holds (wave-aggregated:
+// one LDS atomic per wave, slots by mbcnt).  Call from wave-uniform control flow.
+__device__ inline void queue_push(bool take, int cnt, int* queue, int* qn) {
+  const unsigned long long m = __ballot(take);
+  if (!m) return;
+  int base = 0;
+  if (__lane_id() == 0) base = atomicAdd(qn, __popcll(m));
+  base = __builtin_amdgcn_readfirstlane(base);
+  const int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+  if (take) queue[base + r] = cnt;
+}
+
+// Element pass 1.  Per work item (cell c, tile of kPriorTile genes): occurrences of each
+// count < kPriorSmall in LDS (zeros by ballot), written to occ[item][kPriorSmall]; larger
+// (or negative) counts are evaluated per element.  Then each (c, count) present is evaluated
+// once and enters the sums with its multiplicity.  Per-block partials:
+// [S_all.hi, S_all.lo, S_fin.hi, S_fin.lo, max finite v, n finite v].
+__global__ __launch_bounds__(kPriorBlock) void k_prior_occ(const int* __restrict__ counts, long long ld, int N,
+                                                           int C, const double* __restrict__ cellp, int sq,
+                                                           int* __restrict__ occ_out,
+                                                           double* __restrict__ partials) {
+  __shared__ int occ[kPriorSmall];
+  __shared__ int queue[kPriorTile];
+  __shared__ int qn;
+  const int tid = threadIdx.x;
+  const int ntiles = (N + kPriorTile - 1) / kPriorTile;
+  const long long items = (long long)ntiles * C;
+  dd sa{0.0, 0.0}, sf{0.0, 0.0};
+  double vmax = -INFINITY, nfin = 0.0;
+  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
+    const int c = (int)(it / ntiles), tile = (int)(it % ntiles);
+    const PriorCell p = load_cell(cellp, C, c);
+    const int* col = counts + (long long)c * ld;
+    occ[tid] = 0;
+    if (tid == 0) qn = 0;
+    __syncthreads();
+    int zeros = 0;
+    const int g0 = tile * kPriorTile + tid;
+    int cv[kPriorGenesPerThread];  // all loads in flight before any LDS atomic
+#pragma unroll
+    for (int k = 0; k < kPriorGenesPerThread; ++k) {
+      const int g = g0 + k * kPriorBlock;
+      cv[k] = g < N ? __builtin_nontemporal_load(col + g) : 1;
+    }
+#pragma unroll
+    for (int k = 0; k < kPriorGenesPerThread; ++k) {
+      const int g = g0 + k * kPriorBlock;
+      const int cnt = cv[k];
+      zeros += __popcll(__ballot(cnt == 0));
+      if (g < N && cnt != 0 && (unsigned)cnt < (unsigned)kPriorSmall) atomicAdd(&occ[cnt], 1);
+      // large (or negative) counts: queued, then evaluated by full waves
+      queue_push(g < N && (unsigned)cnt >= (unsigned)kPriorSmall, cnt, queue, &qn);
+    }
+    if (zeros && __lane_id() == 0) atomicAdd(&occ[0], zeros);
+    __syncthreads();
+    for (int q = tid; q < qn; q += kPriorBlock) {
+      double v, w;
+      prior_elem(queue[q], p, sq, v, w);
+      stats_add(sa, sf, vmax, nfin, v, w, 1);
+    }
+    const int o = occ[tid];
+    occ_out[it * kPriorSmall + tid] = o;
+    if (o) {
+      double v, w;
+      prior_elem(tid, p, sq, v, w);
+      stats_add(sa, sf, vmax, nfin, v, w, o);
+    }
+    __syncthreads();
+  }
+  block_stats_out(sa, sf, vmax, nfin, partials + (long long)blockIdx.x * 6);
+}
+
+// v per element in R order (the quantile path only)
+__global__ __launch_bounds__(kPriorBlock) void k_prior_vals(const int* __restrict__ counts, long long ld, int N, int C,
+                                                            const double* __restrict__ cellp, int sq,
+                                                            double* __restrict__ vout) {
+  const long long e = (long long)blockIdx.x * kPriorBlock + threadIdx.x;
+  if (e >= (long long)N * C) return;
+  const int c = (int)(e / N), g = (int)(e % N);
+  double v, w;
+  prior_elem(counts[(long long)c * ld + g], load_cell(cellp, C, c), sq, v, w);
+  vout[e] = v;
+}
+
+// One block: partials (nb x 6) -> out[0..3] = S_all, S_fin (rounded dd), max, nfinite.
 __global__ __launch_bounds__(kPriorBlock) void k_prior_stats_reduce(const double* __restrict__ partials, int nb,
                                                                     double* __restrict__ out) {
   const int tid = threadIdx.x;
@@ -130,42 +210,26 @@ __global__ __launch_bounds__(kPriorBlock) void k_prior_stats_reduce(const double
     vmax = fmax(vmax, q[4]);
     nfin += q[5];
   }
-  __shared__ double red[6][kPriorBlock];
-  red[0][tid] = sa.hi;
-  red[1][tid] = sa.lo;
-  red[2][tid] = sf.hi;
-  red[3][tid] = sf.lo;
-  red[4][tid] = vmax;
-  red[5][tid] = nfin;
+  __shared__ double fin[6];
+  block_stats_out(sa, sf, vmax, nfin, fin);
   __syncthreads();
-  for (int s = kPriorBlock / 2; s > 0; s >>= 1) {
-    if (tid < s) {
-      const dd a = dd_add(dd{red[0][tid], red[1][tid]}, dd{red[0][tid + s], red[1][tid + s]});
-      const dd b = dd_add(dd{red[2][tid], red[3][tid]}, dd{red[2][tid + s], red[3][tid + s]});
-      red[0][tid] = a.hi;
-      red[1][tid] = a.lo;
-      red[2][tid] = b.hi;
-      red[3][tid] = b.lo;
-      red[4][tid] = fmax(red[4][tid], red[4][tid + s]);
-      red[5][tid] += red[5][tid + s];
-    }
-    __syncthreads();
-  }
   if (tid == 0) {
-    out[0] = dd_to_d(dd{red[0][0], red[1][0]});
-    out[1] = dd_to_d(dd{red[2][0], red[3][0]});
-    out[2] = red[4][0];
-    out[3] = red[5][0];
+    out[0] = dd_to_d(dd{fin[0], fin[1]});
+    out[1] = dd_to_d(dd{fin[2], fin[3]});
+    out[2] = fin[4];
+    out[3] = fin[5];
   }
 }
 
-__device__ inline void fix_add(unsigned long long* h, int i, double t) {
+__device__ inline void fix_add(unsigned long long* h, int i, double t, unsigned long long mult) {
   const unsigned long long q = __double2ull_rn(t * kFix);
-  if (q) atomicAdd(h + i, q);
+  if (q) atomicAdd(h + i, q * mult);
 }
 
-// C_BinDist (stats/src/massdist.c) for one value; xpos outside [-1, n) contributes nothing.
-__device__ inline void bin_one(double x, double wi, double lo, double xdelta, int n, unsigned long long* h) {
+// C_BinDist (stats/src/massdist.c) for `mult` copies of one value: each copy's terms are
+// rounded to the fixed point, so mult copies add exactly mult times that integer.
+__device__ inline void bin_one(double x, double wi, double lo, double xdelta, int n, unsigned long long* h,
+                               unsigned long long mult) {
   if (!isfinite(x)) return;
   const double xpos = (x - lo) / xdelta;
   if (!(xpos >= -1.0 && xpos < (double)n)) return;
@@ -173,76 +237,67 @@ __device__ inline void bin_one(double x, double wi, double lo, double xdelta, in
   const double fx = xpos - ix;
   const int ixmax = n - 2;
   if (ix >= 0 && ix <= ixmax) {
-    fix_add(h, ix, wi * (1 - fx));
-    fix_add(h, ix + 1, wi * fx);
+    fix_add(h, ix, wi * (1 - fx), mult);
+    fix_add(h, ix + 1, wi * fx, mult);
   } else if (ix == -1) {
-    fix_add(h, 0, wi * fx);
+    fix_add(h, 0, wi * fx, mult);
   } else if (ix == ixmax + 1) {
-    fix_add(h, ix, wi * (1 - fx));
+    fix_add(h, ix, wi * (1 - fx), mult);
   }
 }
 
+// Element pass 2: the same work items; each (cell, small count) present bins with its
+// multiplicity from pass 1, the large counts are re-read and binned per element.  LDS
+// histogram per block, integer-added into the global histogram (exact, order-free).
 __global__ __launch_bounds__(kPriorBlock) void k_prior_bin(const int* __restrict__ counts, long long ld, int N, int C,
-                                                           const double* __restrict__ cellp, int sq, double wsum,
-                                                           double lo, double xdelta, int n,
-                                                           unsigned long long* __restrict__ partial) {
+                                                           const double* __restrict__ cellp, int sq,
+                                                           const int* __restrict__ occ_in, double wsum, double lo,
+                                                           double xdelta, int n,
+                                                           unsigned long long* __restrict__ hist_out) {
   extern __shared__ unsigned long long hist[];
+  __shared__ int queue[kPriorTile];
+  __shared__ int qn;
   const int tid = threadIdx.x;
   for (int j = tid; j < n; j += kPriorBlock) hist[j] = 0ull;
-  __syncthreads();
-  // v == 0 (every zero count) lands in the same two bins for every cell: summed in
-  // registers (the same fixed-point terms, exact integer sums) instead of contended atomics
-  const double xpos0 = (0.0 - lo) / xdelta;
-  const int ix0 = (int)floor(xpos0);
-  const double fx0 = xpos0 - ix0;
-  const bool zero_mid = ix0 >= 0 && ix0 <= n - 2;
-  unsigned long long z0 = 0ull, z1 = 0ull;
   const int ntiles = (N + kPriorTile - 1) / kPriorTile;
   const long long items = (long long)ntiles * C;
   for (long long it = blockIdx.x; it < items; it += gridDim.x) {
     const int c = (int)(it / ntiles), tile = (int)(it % ntiles);
     const PriorCell p = load_cell(cellp, C, c);
-    const int* col = counts + (long long)c * ld;
-    for (int k = 0; k < kPriorGenesPerThread; ++k) {
-      const int g = tile * kPriorTile + k * kPriorBlock + tid;
-      if (g >= N) break;
+    if (tid == 0) qn = 0;
+    __syncthreads();
+    const int o = occ_in[it * kPriorSmall + tid];
+    if (o) {
       double v, w;
-      prior_elem(col[g], p, sq, v, w);
+      prior_elem(tid, p, sq, v, w);
       const double wi = (w / wsum) * 0.5;  // c(wts/2, wts/2), wts = w / sum(w)
-      if (v == 0.0 && zero_mid) {
-        const unsigned long long a = __double2ull_rn(wi * (1 - fx0) * kFix);
-        const unsigned long long b = __double2ull_rn(wi * fx0 * kFix);
-        z0 += 2 * a;  // -0 and +0
-        z1 += 2 * b;
-        continue;
-      }
-      bin_one(-v, wi, lo, xdelta, n, hist);
-      bin_one(v, wi, lo, xdelta, n, hist);
+      bin_one(-v, wi, lo, xdelta, n, hist, (unsigned long long)o);
+      bin_one(v, wi, lo, xdelta, n, hist, (unsigned long long)o);
     }
-  }
-  if (zero_mid) {
-    if (z0) atomicAdd(hist + ix0, z0);
-    if (z1) atomicAdd(hist + ix0 + 1, z1);
+    const int* col = counts + (long long)c * ld;
+    const int g0 = tile * kPriorTile + tid;
+    int cv[kPriorGenesPerThread];
+#pragma unroll
+    for (int k = 0; k < kPriorGenesPerThread; ++k) {
+      const int g = g0 + k * kPriorBlock;
+      cv[k] = g < N ? __builtin_nontemporal_load(col + g) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPriorGenesPerThread; ++k)
+      queue_push(g0 + k * kPriorBlock < N && (unsigned)cv[k] >= (unsigned)kPriorSmall, cv[k], queue, &qn);
+    __syncthreads();
+    for (int q = tid; q < qn; q += kPriorBlock) {
+      double v, w;
+      prior_elem(queue[q], p, sq, v, w);
+      const double wi = (w / wsum) * 0.5;
+      bin_one(-v, wi, lo, xdelta, n, hist, 1ull);
+      bin_one(v, wi, lo, xdelta, n, hist, 1ull);
+    }
+    __syncthreads();
   }
   __syncthreads();
-  for (int j = tid; j < n; j += kPriorBlock) partial[(long long)blockIdx.x * n + j] = hist[j];
-}
-
-// y[j] = (sum over blocks of partial[b][j]) * 2^-60 * totMass   (BinDist(...) * totMass)
-__global__ __launch_bounds__(kPriorBlock) void k_prior_hist(const unsigned long long* __restrict__ partial, int nb,
-                                                            int n, double tot_mass, double* __restrict__ y) {
-  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int part = threadIdx.x >> 6;  // 4 waves split the blocks
-  unsigned long long s = 0ull;
-  if (j < n)
-    for (int b = part; b < nb; b += 4) s += partial[(long long)b * n + j];
-  __shared__ unsigned long long red[4][64];
-  red[part][threadIdx.x & 63] = s;
-  __syncthreads();
-  if (part == 0 && j < n) {
-    const unsigned long long t = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    y[j] = ((double)t * kInvFix) * tot_mass;
-  }
+  for (int j = tid; j < n; j += kPriorBlock)
+    if (hist[j]) atomicAdd(hist_out + j, hist[j]);
 }
 
 // seq.int(from, to, length.out = len)[i]
@@ -272,17 +327,30 @@ __global__ void k_prior_kords(int n, double span, double bw, double* __restrict_
   K[j] = r_dnorm0(k, bw);
 }
 
-// Re(fft(fft(y) * Conj(fft(kords)), inverse = TRUE))[k] / (2n) = sum_a y[a] kords[(a - k) mod 2n];
-// y is zero beyond n-1.  pmax(0, .)
-__global__ __launch_bounds__(kPriorBlock) void k_prior_conv(const double* __restrict__ y,
-                                                            const double* __restrict__ K, int n,
+// Re(fft(fft(y) * Conj(fft(kords)), inverse = TRUE))[k] / (2n) = sum_a y[a] kords[(a - k) mod 2n],
+// y = BinDist(...) * totMass (zero beyond n-1); pmax(0, .).  A direct sum instead of R's FFT:
+// y and kords staged in LDS, 64 outputs per block (one per lane), the 4 waves split the
+// lags and combine in a fixed order.
+__global__ __launch_bounds__(kPriorBlock) void k_prior_conv(const unsigned long long* __restrict__ hist,
+                                                            double tot_mass, const double* __restrict__ K, int n,
                                                             double* __restrict__ dens) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= n) return;
-  const int mask = 2 * n - 1;
+  extern __shared__ double sm[];
+  double* y = sm;
+  double* Ks = sm + n;
+  const int tid = threadIdx.x;
+  for (int j = tid; j < n; j += kPriorBlock) y[j] = ((double)hist[j] * kInvFix) * tot_mass;
+  for (int j = tid; j < 2 * n; j += kPriorBlock) Ks[j] = K[j];
+  __syncthreads();
+  const int lane = tid & 63, part = tid >> 6;
+  const int k = blockIdx.x * 64 + lane;
+  const int mask = 2 * n - 1, q = n / 4;
   double s = 0.0;
-  for (int a = 0; a < n; ++a) s = fma(y[a], K[(a - k) & mask], s);
-  dens[k] = fmax(0.0, s);
+  if (k < n)
+    for (int a = part * q; a < (part + 1) * q; ++a) s = fma(y[a], Ks[(a - k) & mask], s);
+  __shared__ double red[4][64];
+  red[part][lane] = s;
+  __syncthreads();
+  if (part == 0 && k < n) dens[k] = fmax(0.0, ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane]);
 }
 
 // approx(xords, dens, xout = x, rule = 1) at the upper-half points x[L..2L]; NA -> 0;
@@ -351,36 +419,22 @@ __global__ __launch_bounds__(1024) void k_prior_final(const double* __restrict__
 }  // namespace
 
 hipError_t launch_prior_stats(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
-                              double* vout, double* partials, int nb, double* out, hipStream_t s) {
-  k_prior_stats<<<nb, kPriorBlock, 0, s>>>(counts, ld, N, C, cellp, sq, vout, partials);
+                              double* vout, int* occ, double* partials, int nb, double* out, hipStream_t s) {
+  k_prior_occ<<<nb, kPriorBlock, 0, s>>>(counts, ld, N, C, cellp, sq, occ, partials);
+  if (vout) {
+    const long long e = (long long)N * C;
+    k_prior_vals<<<(unsigned)((e + kPriorBlock - 1) / kPriorBlock), kPriorBlock, 0, s>>>(counts, ld, N, C, cellp, sq,
+                                                                                       vout);
+  }
   k_prior_stats_reduce<<<1, kPriorBlock, 0, s>>>(partials, nb, out);
   return hipGetLastError();
 }
 
+long long prior_items(int N, int C) { return (long long)((N + kPriorTile - 1) / kPriorTile) * C; }
+
 int prior_blocks(int N, int C, int cap) {
   const long long items = (long long)((N + kPriorTile - 1) / kPriorTile) * C;
   return (int)std::max<long long>(1, std::min<long long>(items, cap));
-}
-
-hipError_t launch_prior_density(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
-                                double wsum, double tot_mass, double max_value, double bw, int L, double pc,
-                                unsigned long long* partial, int nb, double* work, double* out, hipStream_t s) {
-  const int nu = 2 * L + 1;
-  int n = std::max(nu, 512);
-  if (n > 512) n = 1 << (int)std::ceil(std::log2((double)n));
-  const double from = -max_value, to = max_value;
-  const double lo = from - 4 * bw, up = to + 4 * bw;
-  const double xdelta = (up - lo) / (n - 1);
-  double* y = work;
-  double* K = work + n;
-  double* dens = K + 2 * n;
-  k_prior_bin<<<nb, kPriorBlock, sizeof(unsigned long long) * n, s>>>(counts, ld, N, C, cellp, sq, wsum, lo, xdelta,
-                                                                      n, partial);
-  k_prior_hist<<<(n + 63) / 64, kPriorBlock, 0, s>>>(partial, nb, n, tot_mass, y);
-  k_prior_kords<<<(2 * n + 255) / 256, 256, 0, s>>>(n, 2 * (up - lo), bw, K);
-  k_prior_conv<<<(n + kPriorBlock - 1) / kPriorBlock, kPriorBlock, 0, s>>>(y, K, n, dens);
-  k_prior_final<<<1, 1024, 0, s>>>(dens, n, lo, up, from, to, L, pc, out);
-  return hipGetLastError();
 }
 
 // density's internal grid size for n.user = 2L + 1 points
@@ -389,6 +443,32 @@ int prior_grid_n(int L) {
   int n = std::max(nu, 512);
   if (n > 512) n = 1 << (int)std::ceil(std::log2((double)n));
   return n;
+}
+
+hipError_t launch_prior_bin(const int* counts, long long ld, int N, int C, const double* cellp, int sq,
+                            const int* occ, double wsum, double max_value, double bw, int L,
+                            unsigned long long* hist, int nb, hipStream_t s) {
+  const int n = prior_grid_n(L);
+  const double lo = -max_value - 4 * bw, up = max_value + 4 * bw;
+  const double xdelta = (up - lo) / (n - 1);
+  hipError_t e = hipMemsetAsync(hist, 0, sizeof(unsigned long long) * n, s);
+  if (e != hipSuccess) return e;
+  k_prior_bin<<<nb, kPriorBlock, sizeof(unsigned long long) * n, s>>>(counts, ld, N, C, cellp, sq, occ, wsum, lo,
+                                                                      xdelta, n, hist);
+  return hipGetLastError();
+}
+
+hipError_t launch_prior_tail(double tot_mass, double max_value, double bw, int L, double pc,
+                             const unsigned long long* hist, double* work, double* out, hipStream_t s) {
+  const int n = prior_grid_n(L);
+  const double from = -max_value, to = max_value;
+  const double lo = from - 4 * bw, up = to + 4 * bw;
+  double* K = work;
+  double* dens = work + 2 * n;
+  k_prior_kords<<<(2 * n + 255) / 256, 256, 0, s>>>(n, 2 * (up - lo), bw, K);
+  k_prior_conv<<<(n + 63) / 64, kPriorBlock, sizeof(double) * 3 * n, s>>>(hist, tot_mass, K, n, dens);
+  k_prior_final<<<1, 1024, 0, s>>>(dens, n, lo, up, from, to, L, pc, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_sort_doubles(const double* in, double* out, long long n, void* work, size_t* work_bytes,
