@@ -1473,7 +1473,8 @@ int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, 
                               double* lp, double* grid_weight, double* max_value_out) {
   if (!ctx || !counts_dev || !models || !x || !y) return fail(SCDE_EARG, "null argument");
   if (ngenes <= 0 || ncells <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
-  if (length_out < 1 || length_out > 1023) return fail(SCDE_EARG, "length.out must be in [1, 1023]");
+  // density grid n <= 4096: k_prior_conv stages y and the 2n kernel values in LDS (96 KiB of 160)
+  if (length_out < 1 || length_out > 2047) return fail(SCDE_EARG, "length.out must be in [1, 2047]");
   if (!(bw > 0)) return fail(SCDE_EARG, "bw must be positive");
   if (!max_value && !(max_quantile >= 0 && max_quantile <= 1)) return fail(SCDE_EARG, "'probs' outside [0,1]");
   if ((long long)ngenes * ncells > 0x7fffffffLL) return fail(SCDE_EARG, "ngenes x ncells too large");
