@@ -12,6 +12,9 @@ results to host.
 cells (one group); one step returns jp (N x 401) and modes (N x 2000) to the host.
 --config prior: scde.expression.prior on config 3's 20,000 x 1,000
 counts, resident; one step = the whole prior (x, y, lp, grid.weight) to the host.
+--config 5: pagoda.pathway.wPCA (BASELINE config 5) on a resident
+synthetic varinfo of 20,000 genes x 3,000 cells; one step = every gene set's bwpca (10 starts),
+its 10 random gene sets and the orientation / normalisation glue, results to the host.
 --config 2b: config 2 with batch correction: two batch levels across
 both groups; one step = batch posteriors over all 200 cells with each group's batch
 composition, both group posteriors, the batch, group and 1601-column batch-adjusted ratio
@@ -59,7 +62,12 @@ CONFIGS = {
 CONFIGS["prior"] = dict(genes=20000, cells=1000, seed=2003, kind="prior", cpu_sample=20000,
                         workload="prior: scde.expression.prior, synthetic 20000 genes x 1000 cells (config 3 counts), "
                                  "length.out 400, max.quantile 1")
+CONFIGS["5"] = dict(genes=20000, cells=3000, seed=2005, kind="wpca", nsets=200, cpu_sample=4,
+                    workload="config5: pagoda.pathway.wPCA on a synthetic varinfo of 20000 genes x 3000 cells, "
+                             "200 gene sets (10-500 genes, log-uniform), n.components 2, n.randomizations 10, "
+                             "n.starts 10, em.tol 1e-6, em.maxiter 25")
 METRIC_PRIOR = "genes/sec for scde.expression.prior (length.out 400, 1000 cells)"
+METRIC_WPCA = "gene sets/sec for pagoda.pathway.wPCA (n.components 2, 10 randomizations, 10 starts, 3000 cells)"
 METRIC_BATCH = ("genes/sec for batch-corrected scde.expression.difference (400-pt grid, 100 randomizations, "
                 "2 batches)")
 
@@ -229,6 +237,123 @@ def bench_prior(args, cfg, rank, world, device):
     ctx.close()
 
 
+def synthetic_varinfo(seed: int, ngenes: int, ncells: int, nsets: int):
+    """A pagoda varinfo stand-in: low-rank structure in gene blocks plus noise, weights in
+    (0, 1] with 15% near-zero (dropout-like); gene sets of log-uniform size 10..500, half
+    of them drawn from one structured block."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nf = 8
+    L = rng.normal(size=(ngenes, nf)) * (rng.uniform(size=(ngenes, 1)) < 0.3)
+    R = rng.normal(size=(nf, ncells)) * np.linspace(2.0, 0.5, nf)[:, None]
+    mat = L @ R
+    mat += rng.normal(size=(ngenes, ncells))
+    matw = rng.uniform(0.05, 1.0, size=(ngenes, ncells))
+    matw[rng.uniform(size=(ngenes, ncells)) < 0.15] = 1e-3
+    genes = [f"g{i}" for i in range(ngenes)]
+    block = np.nonzero(L[:, 0] != 0)[0]
+    sets = {}
+    for k in range(nsets):
+        size = int(round(10 * 50 ** rng.uniform()))
+        pool = block if (k % 2 == 0 and len(block) >= size) else np.arange(ngenes)
+        sets[f"SET:{k:05d}"] = [genes[i] for i in rng.choice(pool, size=size, replace=False)]
+    return {"mat": mat, "matw": matw, "genes": genes, "batch": None}, sets
+
+
+def bench_wpca(args, cfg, rank, world, device):
+    """--config 5: pagoda.pathway.wPCA, every bwpca call batched on the device (wpca.hip).
+    Roofline of k_wpca_em: each EM pass (the start's coefficients, then per iteration the
+    eigenvector pass and the fused fit + coefficient pass) reads the problem's value and
+    weight columns once: 16 B x cells x genes per pass."""
+    from scde_amd import api
+    from scde_amd import pagoda as PG
+    NG, NC = cfg["genes"], cfg["cells"]
+    vinfo, sets = synthetic_varinfo(cfg["seed"] + rank, NG, NC, cfg["nsets"])
+    ctx = api.Context(device)
+    pdev = PG.PagodaDevice(vinfo, ctx)
+    kw = dict(n_components=2, n_randomizations=10, n_starts=10, seed=1, device=pdev)
+    for _ in range(args.warmup):
+        PG.pagoda_pathway_wPCA(None, sets, **kw)
+    ctx.set_profiling(True)
+    ctx.reset_kernel_times()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = PG.pagoda_pathway_wPCA(None, sets, **kw)
+    ctx.synchronize()
+    dt = time.perf_counter() - t0
+    kt = ctx.kernel_times()
+    nsets = len(out)
+    em_ms, em_n = kt["wpca_em"]
+    # algorithmic bytes of one step's EM launches: replay the step's problems with iteration counts
+    ctx.set_profiling(False)
+    passes_bytes = _wpca_pass_bytes(PG, pdev, sets)
+    em_s = em_ms / max(em_n, 1) / 1e3
+    launches_per_step = em_n / args.steps
+    per_launch = passes_bytes / launches_per_step if launches_per_step else 0
+    achieved = per_launch / em_s / 1e9 if em_n else None
+    res = {"metric": METRIC_WPCA, "value": nsets * args.steps / dt, "unit": "gene sets/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+           "data": f"synthetic varinfo (PCG64 seed {cfg['seed']}): rank-8 gene-block structure + N(0,1) noise, "
+                   f"uniform weights with 15% at 1e-3",
+           "config": {"workload": cfg["workload"], "genes": NG, "cells": NC, "gene_sets": nsets,
+                      "parallelism": "single GPU"},
+           "roofline": {"bound": "hbm", "kernel": "k_wpca_em (EM iterations, one workgroup per set x start)",
+                        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
+                        "avg_launch_ms": em_s * 1e3, "launches": em_n, "algorithmic_bytes_per_launch": per_launch},
+           "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
+    cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
+    if rank == 0 and cpu_sample > 0:
+        from oracle import wpca as W
+        # sets near 40 genes keep the sample to ~10-30 s on one core
+        names = sorted(sorted(sets), key=lambda k: abs(len(sets[k]) - 40))[:cpu_sample]
+        sub = {k: sets[k] for k in names}
+        mat, matw = _prepared_host(vinfo)
+        t1 = time.perf_counter()
+        W.pagoda_pathway_wPCA(mat, matw, vinfo["genes"], sub, n_components=2, n_randomizations=10, n_starts=10,
+                              center=False, seed=1)
+        secs = time.perf_counter() - t1
+        sizes = [len(sets[k]) for k in names]
+        # scale to the whole workload's mix by gene count (EM work grows with set size)
+        mean_all = float(np.mean([len(v) for v in sets.values()]))
+        rate = cpu_sample / secs * (np.mean(sizes) / mean_all)
+        res["cpu_baseline"] = {"value": rate, "unit": "gene sets/s", "cores": 1, "kind": "port",
+                               "sample": f"oracle C restatement (oracle/bwpca_oracle.c) + R glue on {cpu_sample} "
+                                         f"gene sets of {sizes} genes ({secs:.1f}s), scaled by mean set size "
+                                         f"{mean_all:.0f}"}
+    if rank == 0:
+        print(json.dumps(res))
+    pdev.free()
+    ctx.close()
+
+
+def _prepared_host(vinfo):
+    from scde_amd.pagoda import weighted_mat_center
+    mat = weighted_mat_center(vinfo["mat"], vinfo["matw"], None)
+    return mat, np.asarray(vinfo["matw"], dtype=np.float64)
+
+
+def _wpca_pass_bytes(PG, pdev, sets):
+    """Replays one step's batch with iteration counts: sum over (problem, start) of
+    (1 + 2 x iterations) passes x 16 B x cells x genes."""
+    orig = PG.WpcaBatch.run
+    total = [0.0]
+
+    def run(self, dev, **kw):
+        kw["want_iterations"] = True
+        res = orig(self, dev, **kw)
+        for p, r in enumerate(res):
+            total[0] += float(np.sum(1 + 2 * r["iterations"])) * 16.0 * dev.ncells * self.d[p]
+        return res
+    PG.WpcaBatch.run = run
+    try:
+        PG.pagoda_pathway_wPCA(None, sets, n_components=2, n_randomizations=10, n_starts=10, seed=1, device=pdev)
+    finally:
+        PG.WpcaBatch.run = orig
+    return total[0]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -267,6 +392,8 @@ def main():
 
     if cfg["kind"] == "prior":
         return bench_prior(args, cfg, rank, world, device)
+    if cfg["kind"] == "wpca":
+        return bench_wpca(args, cfg, rank, world, device)
     de = cfg["kind"] in ("de", "de_batch")
     batched = cfg["kind"] == "de_batch"
     models, counts, groups = synthetic(cfg["seed"] + rank, NG, NC, two_groups=de)

@@ -173,7 +173,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
  * square_logit_conc).  max_value NULL = quantile(x[x < Inf], max_quantile) of the
  * log10(FPM + 1) magnitudes (type 7).  Outputs (host, length_out + 1 each): x, y, lp,
  * grid_weight (lp / grid_weight may be NULL); max_value_out (nullable) receives the
- * max.value used.  length_out in [1, 1023]. */
+ * max.value used.  length_out in [1, 2047]. */
 int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, int ncells,
                               const double* models, int square_logit_conc, int length_out, double pseudo_count,
                               double bw, double max_quantile, const double* max_value, double* x, double* y,
@@ -188,6 +188,52 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
                         int64_t ngenes_total, int return_post, int ensemble, const int* batch_vals,
                         const int64_t* batch_off, const int* composition, int nbatch, double* jp, double* modes,
                         double* post);
+
+/* ---------------------------------------------------------------- weighted PCA
+ * Bailey's EM weighted PCA behind bwpca() / pagoda.pathway.wPCA() (BASELINE config 5;
+ * SURVEY.md section 8(f) row 3).
+ *
+ * .Call("baileyWPCA", Mat, Matw, Npcs, Nstarts, Smooth, EMtol, EMmaxiter, Seed, Nshuffles)
+ * (src/bwpca.cpp:59-182; declared src/bwpca.h:8) on host buffers.  mat, matw: n (cells)
+ * x d (genes) col-major.  The reference's random inputs are arguments, produced by the
+ * caller exactly as the reference draws them (the .Call shim in INTEGRATION.md):
+ *   starts: (1 + nshuffles) x nstarts x (d x K) uniforms, K = min(npcs, d), in draw order
+ *           (arma::randu<arma::mat>(d, npcs) per start = R's unif_rand() stream;
+ *           src/bwpca.cpp:197-198; Seed is a no-op there);
+ *   perms:  nshuffles x d x n row indices (set_random_matrices' std::random_shuffle over
+ *           rand(); src/bwpca.cpp:41-57), see scde_shuffle_perms.
+ * Outputs: rotation d x K, scores n x K, scoreweights n x K (nullable), var K, totvar,
+ * randvar nshuffles (src/bwpca.cpp:164-180).  npcs <= 8. */
+int scde_baileyWPCA(const double* mat, const double* matw, int n, int d, int npcs, int nstarts, int smooth,
+                    double em_tol, int em_maxiter, const double* starts, int nshuffles, const int* perms,
+                    double* rotation, double* scores, double* scoreweights, double* var, double* totvar,
+                    double* randvar);
+
+/* A batch of baileyWPCA problems on one device-resident matrix pair: M_dev / W_dev are
+ * ncells x mcols col-major (column stride ld), i.e. pagoda's t(varinfo$mat) / t(matw).
+ * Problem p: d[p] columns cols[col_off[p] ..], npcs[p] (K = min(npcs, d) <= 8), nstarts[p]
+ * starts from starts[start_off[p] ..] (nstarts x d x K uniforms), rows permuted per column
+ * by perms[perm_off[p] ..] (d x ncells) when perm_off (nullable) is >= 0.  Outputs (host),
+ * concatenated in problem order: rotation d x K, scores / scoreweights / colmeans ncells x K
+ * (colmeans[j, k] = mean_g M[j, g] |rotation[g, k]|, pagoda's orientation statistic;
+ * scoreweights / colmeans nullable), stats K + 2 per problem (var[K], totvar, the residual
+ * of component 1 alone), iterations (nullable) per (problem, start). */
+int scde_bwpca_batch_dev(scde_ctx* ctx, const double* M_dev, const double* W_dev, int64_t ld, int ncells,
+                         int64_t mcols, int nprob, const int* d, const int* npcs, const int* nstarts,
+                         const int64_t* col_off, const int* cols, int64_t ncols, const int64_t* perm_off,
+                         const int* perms, int64_t nperms, const int64_t* start_off, const double* starts,
+                         int64_t nstart_vals, int smooth, double em_tol, int em_maxiter, double* rotation,
+                         double* scores, double* scoreweights, double* colmeans, double* stats, int* iterations);
+
+/* R's RNG (src/main/RNG.c), host side, for the mirror of the R glue: set.seed(seed) into
+ * a 625-word Mersenne-Twister state (word 0 = mti), unif_rand() draws, and R >= 3.6
+ * sample.int(n, k) without replacement (1-based, rejection sampling). */
+int scde_r_set_seed(uint32_t seed, uint32_t* state);
+int scde_r_unif_rand(uint32_t* state, int64_t n, double* out);
+int scde_r_sample(uint32_t* state, int n, int k, int* out);
+/* set_random_matrices' permutations (src/bwpca.cpp:41-57) after srand(seed) with the
+ * platform rand() (scde_set_rand_kind): nshuffles x d x n. */
+int scde_shuffle_perms(unsigned int seed, int nshuffles, int d, int n, int* perms);
 
 #ifdef __cplusplus
 }

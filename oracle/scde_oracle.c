@@ -45,10 +45,7 @@
 /* ------------------------------------------------------------------ */
 /* glibc TYPE_3 rand() (srandom_r / random_r), private state            */
 /* ------------------------------------------------------------------ */
-typedef struct {
-    int32_t tbl[31];
-    int f, r;
-} o_rng;
+#include "scde_oracle.h"
 
 /* Generator variant, for pinning against the published vignette table:
  * 0 = glibc TYPE_3 (Linux, the default); 1 = Park-Miller "minimal standard"

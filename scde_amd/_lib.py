@@ -22,6 +22,8 @@ EXPORTS = [
     "scde_dev_alloc", "scde_dev_free", "scde_h2d", "scde_d2h",
     "scde_expression_difference_dev", "scde_posteriors_dev", "scde_bh_cz_dev",
     "scde_expression_difference_batch_dev", "scde_expression_prior_dev",
+    "scde_baileyWPCA", "scde_bwpca_batch_dev", "scde_r_set_seed", "scde_r_unif_rand", "scde_r_sample",
+    "scde_shuffle_perms",
 ]
 
 
@@ -95,6 +97,13 @@ def lib():
                                                        P, P]
     L.scde_expression_prior_dev.argtypes = [P, P, i64, i, i, P, i, i, d, d, d, P, P, P, P, P, P]
     L.scde_posteriors_dev.argtypes = [P, P, i64, i, P, i, P, i, i, P, i, i, i, i64, i64, i, i, P, P, P, i, P, P, P]
+    L.scde_baileyWPCA.argtypes = [P, P, i, i, i, i, i, d, i, P, i, P, P, P, P, P, P, P]
+    L.scde_bwpca_batch_dev.argtypes = [P, P, P, i64, i, i64, i, P, P, P, P, P, i64, P, P, i64, P, P, i64, i, d, i,
+                                       P, P, P, P, P, P]
+    L.scde_r_set_seed.argtypes = [ctypes.c_uint32, P]
+    L.scde_r_unif_rand.argtypes = [P, i64, P]
+    L.scde_r_sample.argtypes = [P, i, i, P]
+    L.scde_shuffle_perms.argtypes = [ctypes.c_uint, i, i, i, P]
     _lib = L
     return L
 

@@ -228,7 +228,8 @@ class Context:
     def set_profiling(self, on: bool):
         check(lib().scde_ctx_set_profiling(self.handle, int(bool(on))))
 
-    SLOT_NAMES = ["tables", "boot", "ratio_summary", "unique", "other", "prior_stats", "prior_bin", "prior_tail"]
+    SLOT_NAMES = ["tables", "boot", "ratio_summary", "unique", "other", "prior_stats", "prior_bin", "prior_tail",
+                  "wpca_em", "wpca_final"]
 
     def kernel_times(self):
         """{slot: (total ms, launches)} from HIP events on the context's stream."""

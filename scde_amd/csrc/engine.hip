@@ -155,7 +155,9 @@ enum {
   SLOT_PRIOR_STATS = 5,
   SLOT_PRIOR_BIN = 6,
   SLOT_PRIOR_TAIL = 7,
-  NSLOTS = 8
+  SLOT_WPCA_EM = 8,
+  SLOT_WPCA_FINAL = 9,
+  NSLOTS = 10
 };
 
 struct scde_ctx {
@@ -166,6 +168,8 @@ struct scde_ctx {
       degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
   // scde.expression.prior
   Buf pr_cell, pr_part, pr_occ, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
+  // weighted PCA (bwpca)
+  Buf wp_probs, wp_blocks, wp_kidx, wp_cols, wp_perms, wp_starts, wp_scratch, wp_stat, wp_out, wp_smooth, wp_M, wp_W;
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
   // unique tables can be built up front, with their host syncs, before the heavy kernels
   struct UniqueSet {
@@ -232,6 +236,10 @@ struct scde_ctx {
                   &has_clamp, &base_col, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
                   &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw};
     for (Buf* b : all) b->release();
+    Buf* wp[] = {&wp_probs, &wp_blocks,  &wp_kidx, &wp_cols,   &wp_perms, &wp_starts, &wp_scratch,
+                 &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
+                 &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw};
+    for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
     for (auto& p : pending) {
@@ -1603,6 +1611,395 @@ int scde_bh_cz(const double* z, int64_t n, double* cz) {
   return SCDE_OK;
 }
 
+
+// ------------------------------------------------------------------ weighted PCA
+// R's RNG (src/main/RNG.c) for the host mirror of the R glue: set.seed scrambling,
+// Mersenne-Twister unif_rand (with fixup), R >= 3.6 rejection sample().
+int scde_r_set_seed(uint32_t seed, uint32_t* state) {
+  if (!state) return fail(SCDE_EARG, "null state");
+  for (int j = 0; j < 50; ++j) seed = 69069u * seed + 1u;
+  for (int j = 0; j < 625; ++j) {
+    seed = 69069u * seed + 1u;
+    state[j] = seed;
+  }
+  state[0] = 624;
+  return SCDE_OK;
+}
+
+static double r_mt_genrand(uint32_t* st) {
+  static const uint32_t mag01[2] = {0x0u, 0x9908b0dfu};
+  uint32_t* mt = st + 1;
+  int mti = (int)st[0];
+  uint32_t y;
+  if (mti >= 624) {
+    int kk;
+    for (kk = 0; kk < 624 - 397; ++kk) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk + 397] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    for (; kk < 623; ++kk) {
+      y = (mt[kk] & 0x80000000u) | (mt[kk + 1] & 0x7fffffffu);
+      mt[kk] = mt[kk - 227] ^ (y >> 1) ^ mag01[y & 1u];
+    }
+    y = (mt[623] & 0x80000000u) | (mt[0] & 0x7fffffffu);
+    mt[623] = mt[396] ^ (y >> 1) ^ mag01[y & 1u];
+    mti = 0;
+  }
+  y = mt[mti++];
+  y ^= (y >> 11);
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= (y >> 18);
+  st[0] = (uint32_t)mti;
+  return (double)y * 2.3283064365386963e-10;
+}
+
+static double r_unif_rand(uint32_t* st) {
+  const double i2_32m1 = 2.328306437080797e-10;
+  const double x = r_mt_genrand(st);
+  if (x <= 0.0) return 0.5 * i2_32m1;
+  if ((1.0 - x) <= 0.0) return 1.0 - 0.5 * i2_32m1;
+  return x;
+}
+
+int scde_r_unif_rand(uint32_t* state, int64_t n, double* out) {
+  if (!state || (n > 0 && !out)) return fail(SCDE_EARG, "null argument");
+  for (int64_t i = 0; i < n; ++i) out[i] = r_unif_rand(state);
+  return SCDE_OK;
+}
+
+int scde_r_sample(uint32_t* state, int n, int k, int* out) {
+  if (!state || (k > 0 && !out)) return fail(SCDE_EARG, "null argument");
+  if (k > n || k < 0) return fail(SCDE_EARG, "cannot take a sample larger than the population");
+  std::vector<int> x(std::max(n, 1));
+  for (int i = 0; i < n; ++i) x[i] = i;
+  for (int i = 0; i < k; ++i) {
+    double dv = 0;
+    const double dn = (double)n;
+    if (dn > 0) {
+      const int bits = (int)std::ceil(std::log2(dn));
+      do {
+        int64_t v = 0;
+        for (int b = 0; b <= bits; b += 16) v = 65536 * v + (int)std::floor(r_unif_rand(state) * 65536);
+        dv = (double)(v & ((((int64_t)1) << bits) - 1));
+      } while (dn <= dv);
+    }
+    const int j = (int)dv;
+    out[i] = x[j] + 1;
+    x[j] = x[--n];
+  }
+  return SCDE_OK;
+}
+
+// set_random_matrices (src/bwpca.cpp:41-57) over the platform rand() (srand(seed) first):
+// ind = 0..n-1 per shuffle; per column libstdc++ std::random_shuffle (j = rand() % (i+1)).
+int scde_shuffle_perms(unsigned int seed, int nshuffles, int d, int n, int* perms) {
+  if (nshuffles > 0 && d > 0 && n > 0 && !perms) return fail(SCDE_EARG, "null perms");
+  PlatformRand rng(seed, g_rand_kind);
+  std::vector<int> ind(std::max(n, 1));
+  for (int s = 0; s < nshuffles; ++s) {
+    for (int i = 0; i < n; ++i) ind[i] = i;
+    for (int c = 0; c < d; ++c) {
+      for (int i = 1; i < n; ++i) {
+        const int j = rng.next() % (i + 1);
+        if (i != j) std::swap(ind[i], ind[j]);
+      }
+      std::memcpy(perms + ((int64_t)s * d + c) * n, ind.data(), sizeof(int) * n);
+    }
+  }
+  return SCDE_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// smoothing coefficients (src/bwpca.cpp:86-100): A (2np+1) x 4, A[:, j] = x^j,
+// smoothc = A solve(A^T A, e_0); solved by partial-pivot LU like the K x K systems.
+std::vector<double> wpca_smooth_coef(int smooth) {
+  const int np = smooth / 2, L = 2 * np + 1;
+  std::vector<double> X((size_t)L * 4), sc(L);
+  for (int j = 0; j < 4; ++j)
+    for (int i = 0; i < L; ++i) X[i + j * L] = std::pow((double)(i - np), (double)j);
+  double A[16], b[4] = {1, 0, 0, 0};
+  for (int j = 0; j < 4; ++j)
+    for (int k = 0; k < 4; ++k) {
+      double s = 0;
+      for (int i = 0; i < L; ++i) s += X[i + k * L] * X[i + j * L];
+      A[k + j * 4] = s;
+    }
+  int piv[4];
+  for (int j = 0; j < 4; ++j) {
+    int p = j;
+    for (int i = j + 1; i < 4; ++i)
+      if (std::fabs(A[i + j * 4]) > std::fabs(A[p + j * 4])) p = i;
+    piv[j] = p;
+    if (p != j)
+      for (int l = 0; l < 4; ++l) std::swap(A[j + l * 4], A[p + l * 4]);
+    const double r = 1.0 / A[j + j * 4];
+    for (int i = j + 1; i < 4; ++i) A[i + j * 4] *= r;
+    for (int l = j + 1; l < 4; ++l)
+      for (int i = j + 1; i < 4; ++i) A[i + l * 4] -= A[i + j * 4] * A[j + l * 4];
+  }
+  for (int j = 0; j < 4; ++j)
+    if (piv[j] != j) std::swap(b[j], b[piv[j]]);
+  for (int l = 0; l < 4; ++l)
+    for (int i = l + 1; i < 4; ++i) b[i] -= b[l] * A[i + l * 4];
+  for (int l = 3; l >= 0; --l) {
+    b[l] /= A[l + l * 4];
+    for (int i = 0; i < l; ++i) b[i] -= b[l] * A[i + l * 4];
+  }
+  for (int i = 0; i < L; ++i) {
+    double s = 0;
+    for (int j = 0; j < 4; ++j) s += X[i + j * L] * b[j];
+    sc[i] = s;
+  }
+  return sc;
+}
+
+template <class T>
+hipError_t upload(Buf& b, const T* src, size_t n, hipStream_t st) {
+  hipError_t e = b.ensure(sizeof(T) * std::max<size_t>(n, 1));
+  if (e != hipSuccess || n == 0) return e;
+  return hipMemcpyAsync(b.p, src, sizeof(T) * n, hipMemcpyHostToDevice, st);
+}
+}  // namespace
+
+extern "C" {
+
+int scde_bwpca_batch_dev(scde_ctx* ctx, const double* M_dev, const double* W_dev, int64_t ld, int ncells,
+                         int64_t mcols, int nprob, const int* d, const int* npcs, const int* nstarts,
+                         const int64_t* col_off, const int* cols, int64_t ncols, const int64_t* perm_off,
+                         const int* perms, int64_t nperms, const int64_t* start_off, const double* starts,
+                         int64_t nstart_vals, int smooth, double em_tol, int em_maxiter, double* rotation,
+                         double* scores, double* scoreweights, double* colmeans, double* stats, int* iterations) {
+  if (!ctx || !M_dev || !W_dev) return fail(SCDE_EARG, "null argument");
+  if (nprob < 0 || ncells <= 0 || ld < ncells || mcols <= 0) return fail(SCDE_EARG, "bad dimensions");
+  if (nprob == 0) return SCDE_OK;
+  if (!d || !npcs || !nstarts || !col_off || !cols || !start_off || !starts || !rotation || !scores || !stats)
+    return fail(SCDE_EARG, "null problem array");
+  const int n = ncells;
+  for (int64_t i = 0; i < ncols; ++i)
+    if (cols[i] < 0 || cols[i] >= mcols) return fail(SCDE_EARG, "column index %d out of range", cols[i]);
+  for (int64_t i = 0; i < nperms; ++i)
+    if (perms[i] < 0 || perms[i] >= n) return fail(SCDE_EARG, "permutation index out of range");
+  std::vector<WpcaProb> P(nprob);
+  int64_t o_rot = 0, o_sc = 0, o_var = 0;
+  for (int p = 0; p < nprob; ++p) {
+    if (d[p] <= 0) return fail(SCDE_EARG, "problem %d: no columns", p);
+    if (nstarts[p] <= 0) return fail(SCDE_EARG, "problem %d: nstarts must be positive", p);
+    const int K = std::min(npcs[p], d[p]);
+    if (K < 1 || K > wpca_max_k()) return fail(SCDE_EARG, "problem %d: npcs must be in [1, %d]", p, wpca_max_k());
+    if (col_off[p] < 0 || col_off[p] + d[p] > ncols) return fail(SCDE_EARG, "problem %d: cols out of range", p);
+    if (perm_off && perm_off[p] >= 0 && perm_off[p] + (int64_t)d[p] * n > nperms)
+      return fail(SCDE_EARG, "problem %d: perms out of range", p);
+    if (start_off[p] < 0 || start_off[p] + (int64_t)nstarts[p] * d[p] * K > nstart_vals)
+      return fail(SCDE_EARG, "problem %d: starts out of range", p);
+    WpcaProb& q = P[p];
+    q.d = d[p];
+    q.K = K;
+    q.nstarts = nstarts[p];
+    q.pad = 0;
+    q.col_off = col_off[p];
+    q.perm_off = perm_off ? perm_off[p] : -1;
+    q.start_off = start_off[p];
+    q.out_rot = o_rot;
+    q.out_sc = o_sc;
+    q.out_var = o_var;
+    o_rot += (int64_t)d[p] * K;
+    o_sc += (int64_t)n * K;
+    o_var += K + 2;
+  }
+  const int64_t tot_sc = o_sc;
+  for (auto& q : P) {  // output layout: [rot | scores | scoreweights | colmeans | stats]
+    q.out_sc += o_rot;
+    q.out_pcw = q.out_sc + tot_sc;
+    q.out_cm = q.out_sc + 2 * tot_sc;
+    q.out_var += o_rot + 3 * tot_sc;
+  }
+  const int64_t out_total = o_rot + 3 * tot_sc + o_var;
+  const int L = smooth > 0 ? 2 * (smooth / 2) + 1 : 0;
+  std::vector<double> sc = L > 0 ? wpca_smooth_coef(smooth) : std::vector<double>(1, 0.0);
+  constexpr int kLdsCap = 160 * 1024 - 2048;
+  HCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  HCHK(upload(ctx->wp_cols, cols, (size_t)ncols, st));
+  HCHK(upload(ctx->wp_perms, perms, (size_t)(perms ? nperms : 0), st));
+  HCHK(upload(ctx->wp_starts, starts, (size_t)nstart_vals, st));
+  HCHK(upload(ctx->wp_smooth, sc.data(), sc.size(), st));
+  HCHK(ctx->wp_out.ensure(sizeof(double) * out_total));
+  // problems grouped by K; within a group by work (d x nstarts) descending, in chunks
+  // whose scratch stays under a budget
+  std::vector<int> order(nprob);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    if (P[a].K != P[b].K) return P[a].K < P[b].K;
+    return (int64_t)P[a].d * P[a].nstarts > (int64_t)P[b].d * P[b].nstarts;
+  });
+  const int64_t kScratchBudget = (int64_t)1 << 28;  // doubles (2 GiB)
+  std::vector<int64_t> iters_all;
+  std::vector<double> stat_h;
+  if (iterations) {
+    int64_t tot = 0;
+    for (auto& q : P) tot += q.nstarts;
+    iters_all.assign(tot, 0);
+  }
+  std::vector<int64_t> it_base(nprob, 0);
+  {
+    int64_t b = 0;
+    for (int p = 0; p < nprob; ++p) {
+      it_base[p] = b;
+      b += P[p].nstarts;
+    }
+  }
+  size_t pos = 0;
+  while (pos < order.size()) {
+    const int K = P[order[pos]].K;
+    const int NM = K + K * (K + 1) / 2;
+    // chunk: same K, scratch within budget
+    size_t end = pos;
+    int dmax = 0;
+    int64_t need = 0;
+    while (end < order.size() && P[order[end]].K == K) {
+      const WpcaProb& q = P[order[end]];
+      const int dm = std::max(dmax, q.d);
+      const bool cl = (size_t)(dm + n) * K * sizeof(double) <= (size_t)kLdsCap;
+      const int64_t per = (int64_t)q.nstarts * ((int64_t)q.d * K + 2LL * n * K + (cl ? 0 : (int64_t)n * K) +
+                                                (int64_t)q.d * (NM + 1));
+      if (end > pos && need + per > kScratchBudget) break;
+      need += per;
+      dmax = dm;
+      ++end;
+    }
+    const bool cl = (size_t)(dmax + n) * K * sizeof(double) <= (size_t)kLdsCap;
+    int64_t so = 0, stt = 0;
+    for (size_t i = pos; i < end; ++i) {
+      WpcaProb& q = P[order[i]];
+      q.sE_off = so;
+      so += (int64_t)q.nstarts * q.d * K;
+      q.sC_off = so;
+      so += (int64_t)q.nstarts * 2 * n * K;
+      q.sW_off = so;
+      if (!cl) so += (int64_t)q.nstarts * n * K;
+      q.mom_off = so;
+      so += (int64_t)q.nstarts * q.d * (NM + 1);
+      q.stat_off = stt;
+      stt += q.nstarts;
+    }
+    HCHK(ctx->wp_scratch.ensure(sizeof(double) * std::max<int64_t>(so, 1)));
+    HCHK(ctx->wp_stat.ensure(sizeof(double) * 4 * std::max<int64_t>(stt, 1)));
+    // block list: problems in groups of 8 (one per XCD under round-robin dispatch);
+    // the starts of a problem sit 8 blocks apart, on the same XCD, sharing its columns in L2
+    std::vector<int2> blocks;
+    std::vector<WpcaProb> chunk;
+    std::vector<int> kidx;
+    for (size_t i = pos; i < end; ++i) {
+      chunk.push_back(P[order[i]]);
+      kidx.push_back((int)(i - pos));
+    }
+    for (size_t g0 = 0; g0 < chunk.size(); g0 += 8) {
+      const size_t g1 = std::min(chunk.size(), g0 + 8);
+      int smax = 0;
+      for (size_t i = g0; i < g1; ++i) smax = std::max(smax, chunk[i].nstarts);
+      for (int s = 0; s < smax; ++s)
+        for (size_t x = 0; x < 8; ++x) {
+          const size_t i = g0 + x;
+          if (i < g1 && s < chunk[i].nstarts) blocks.push_back(make_int2((int)i, s));
+          else blocks.push_back(make_int2(-1, 0));  // keeps the 8-block stride
+        }
+    }
+    // drop trailing padding
+    while (!blocks.empty() && blocks.back().x < 0) blocks.pop_back();
+    HCHK(upload(ctx->wp_probs, chunk.data(), chunk.size(), st));
+    HCHK(upload(ctx->wp_blocks, blocks.data(), blocks.size(), st));
+    HCHK(upload(ctx->wp_kidx, kidx.data(), kidx.size(), st));
+    WpcaLaunch a;
+    a.M = M_dev;
+    a.W = W_dev;
+    a.ld = ld;
+    a.n = n;
+    a.dmax = dmax;
+    a.probs = ctx->wp_probs.as<WpcaProb>();
+    a.blocks = ctx->wp_blocks.as<int2>();
+    a.cols = ctx->wp_cols.as<int>();
+    a.perms = ctx->wp_perms.as<int>();
+    a.starts = ctx->wp_starts.as<double>();
+    a.maxiter = em_maxiter;
+    a.tol = em_tol;
+    a.smoothc = ctx->wp_smooth.as<double>();
+    a.L = L;
+    a.scratch = ctx->wp_scratch.as<double>();
+    a.stat = ctx->wp_stat.as<double>();
+    a.out = ctx->wp_out.as<double>();
+    a.lds_cap = kLdsCap;
+    hipEvent_t ev = ctx->mark_begin(SLOT_WPCA_EM);
+    if (!blocks.empty()) HCHK(launch_wpca_em(K, a, (int)blocks.size(), st));
+    ctx->mark_end(SLOT_WPCA_EM, ev);
+    ev = ctx->mark_begin(SLOT_WPCA_FINAL);
+    HCHK(launch_wpca_final(K, a, ctx->wp_kidx.as<int>(), (int)chunk.size(), st));
+    ctx->mark_end(SLOT_WPCA_FINAL, ev);
+    if (iterations) {
+      stat_h.resize((size_t)4 * stt);
+      HCHK(hipMemcpyAsync(stat_h.data(), a.stat, sizeof(double) * 4 * stt, hipMemcpyDeviceToHost, st));
+      RCHK(ctx->sync());
+      for (size_t i = 0; i < chunk.size(); ++i)
+        for (int s = 0; s < chunk[i].nstarts; ++s)
+          iters_all[it_base[order[pos + i]] + s] = (int64_t)stat_h[(size_t)4 * (chunk[i].stat_off + s) + 2];
+    }
+    pos = end;
+  }
+  std::vector<double> out_h(out_total);
+  HCHK(hipMemcpyAsync(out_h.data(), ctx->wp_out.p, sizeof(double) * out_total, hipMemcpyDeviceToHost, st));
+  RCHK(ctx->sync());
+  std::memcpy(rotation, out_h.data(), sizeof(double) * o_rot);
+  std::memcpy(scores, out_h.data() + o_rot, sizeof(double) * tot_sc);
+  if (scoreweights) std::memcpy(scoreweights, out_h.data() + o_rot + tot_sc, sizeof(double) * tot_sc);
+  if (colmeans) std::memcpy(colmeans, out_h.data() + o_rot + 2 * tot_sc, sizeof(double) * tot_sc);
+  std::memcpy(stats, out_h.data() + o_rot + 3 * tot_sc, sizeof(double) * o_var);
+  if (iterations)
+    for (size_t i = 0; i < iters_all.size(); ++i) iterations[i] = (int)iters_all[i];
+  return SCDE_OK;
+}
+
+// .Call("baileyWPCA", ...) (src/bwpca.cpp:59; bwpca.h:8) on host buffers.
+int scde_baileyWPCA(const double* mat, const double* matw, int n, int d, int npcs, int nstarts, int smooth,
+                    double em_tol, int em_maxiter, const double* starts, int nshuffles, const int* perms,
+                    double* rotation, double* scores, double* scoreweights, double* var, double* totvar,
+                    double* randvar) {
+  if (!mat || !matw || !starts || !rotation || !scores || !var || !totvar) return fail(SCDE_EARG, "null argument");
+  if (n <= 0 || d <= 0) return fail(SCDE_EARG, "bad dimensions");
+  if (nshuffles < 0 || (nshuffles > 0 && (!perms || !randvar))) return fail(SCDE_EARG, "bad shuffles");
+  if (nstarts <= 0) return fail(SCDE_EARG, "nstarts must be positive");
+  const int K = std::min(npcs, d);
+  if (K < 1) return fail(SCDE_EARG, "npcs must be positive");
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  const size_t nd = (size_t)n * d;
+  HCHK(upload(cx->wp_M, mat, nd, cx->stream));
+  HCHK(upload(cx->wp_W, matw, nd, cx->stream));
+  const int np = 1 + nshuffles;
+  std::vector<int> dv(np, d), kv(np, npcs), sv(np, nstarts), cols(d);
+  std::vector<int64_t> co(np, 0), po(np, -1), so(np);
+  std::iota(cols.begin(), cols.end(), 0);
+  for (int q = 0; q < np; ++q) {
+    so[q] = (int64_t)q * nstarts * d * K;
+    if (q > 0) po[q] = (int64_t)(q - 1) * d * n;
+  }
+  std::vector<double> rot((size_t)np * d * K), sco((size_t)np * n * K), pcw((size_t)np * n * K),
+      stats((size_t)np * (K + 2));
+  RCHK(scde_bwpca_batch_dev(cx, cx->wp_M.as<double>(), cx->wp_W.as<double>(), n, n, d, np, dv.data(), kv.data(),
+                            sv.data(), co.data(), cols.data(), d, po.data(), perms,
+                            nshuffles > 0 ? (int64_t)nshuffles * d * n : 0, so.data(), starts,
+                            (int64_t)np * nstarts * d * K, smooth, em_tol, em_maxiter, rot.data(), sco.data(),
+                            pcw.data(), nullptr, stats.data(), nullptr));
+  std::memcpy(rotation, rot.data(), sizeof(double) * d * K);
+  std::memcpy(scores, sco.data(), sizeof(double) * n * K);
+  if (scoreweights) std::memcpy(scoreweights, pcw.data(), sizeof(double) * n * K);
+  std::memcpy(var, stats.data(), sizeof(double) * K);
+  *totvar = stats[K];
+  for (int s = 0; s < nshuffles; ++s) randvar[s] = *totvar - stats[(size_t)(1 + s) * (K + 2) + K + 1];
+  return SCDE_OK;
+}
 }  // extern "C"
 
 namespace {

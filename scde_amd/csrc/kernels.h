@@ -175,4 +175,44 @@ hipError_t launch_sort_doubles(const double* in, double* out, long long n, void*
                                hipStream_t s);
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s);
 
+
+// ---- weighted PCA (wpca.hip; src/bwpca.cpp).  One problem = a column subset of the
+// resident cells x genes value/weight matrices (column g at M + col*ld), optionally
+// row-permuted per column (internal shuffles).  All offsets in elements.
+constexpr int kWpcaMaxK = 8;
+struct WpcaProb {
+  int d, K, nstarts, pad;
+  long long col_off;    // cols[col_off .. +d)
+  long long perm_off;   // perms[perm_off .. + d*n) or -1
+  long long start_off;  // starts[start_off .. + nstarts*d*K): randu(d, K) per start
+  long long sE_off;     // scratch: best eigenvectors, nstarts x d x K
+  long long sC_off;     // scratch: coefficient slots, nstarts x 2 x n x K
+  long long sW_off;     // scratch: working coefficients (when not in LDS), nstarts x n x K
+  long long mom_off;    // scratch: moments + smoothing row, nstarts x d x (NM + 1)
+  long long stat_off;   // stat rows (pres, bpres, iterations, best slot), one per start
+  long long out_rot, out_sc, out_pcw, out_cm, out_var;  // outputs (var: K + 2 doubles)
+};
+struct WpcaLaunch {
+  const double* M;
+  const double* W;
+  long long ld;
+  int n, dmax;
+  const WpcaProb* probs;
+  const int2* blocks;
+  const int* cols;
+  const int* perms;
+  const double* starts;
+  int maxiter;
+  double tol;
+  const double* smoothc;
+  int L;
+  double* scratch;
+  double* stat;
+  double* out;
+  int lds_cap;
+};
+int wpca_max_k();
+hipError_t launch_wpca_em(int K, const WpcaLaunch& a, int nblocks, hipStream_t s);
+hipError_t launch_wpca_final(int K, const WpcaLaunch& a, const int* kidx, int nprob, hipStream_t s);
+
 }  // namespace scde
