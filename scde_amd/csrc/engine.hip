@@ -1896,11 +1896,15 @@ int scde_bwpca_batch_dev(scde_ctx* ctx, const double* M_dev, const double* W_dev
       chunk.push_back(P[order[i]]);
       kidx.push_back((int)(i - pos));
     }
+    // npcs = 1 without smoothing: one workgroup per group of wpca_ms_group() starts
+    static const bool no_ms = getenv("SCDE_WPCA_NOMS") != nullptr;
+    const bool ms = K == 1 && L == 0 && wpca_ms_ok(n, dmax) && !no_ms;
+    const int sstep = ms ? wpca_ms_group() : 1;
     for (size_t g0 = 0; g0 < chunk.size(); g0 += 8) {
       const size_t g1 = std::min(chunk.size(), g0 + 8);
       int smax = 0;
       for (size_t i = g0; i < g1; ++i) smax = std::max(smax, chunk[i].nstarts);
-      for (int s = 0; s < smax; ++s)
+      for (int s = 0; s < smax; s += sstep)
         for (size_t x = 0; x < 8; ++x) {
           const size_t i = g0 + x;
           if (i < g1 && s < chunk[i].nstarts) blocks.push_back(make_int2((int)i, s));
@@ -1932,7 +1936,10 @@ int scde_bwpca_batch_dev(scde_ctx* ctx, const double* M_dev, const double* W_dev
     a.out = ctx->wp_out.as<double>();
     a.lds_cap = kLdsCap;
     hipEvent_t ev = ctx->mark_begin(SLOT_WPCA_EM);
-    if (!blocks.empty()) HCHK(launch_wpca_em(K, a, (int)blocks.size(), st));
+    if (!blocks.empty()) {
+      if (ms) HCHK(launch_wpca_ms(a, (int)blocks.size(), st));
+      else HCHK(launch_wpca_em(K, a, (int)blocks.size(), st));
+    }
     ctx->mark_end(SLOT_WPCA_EM, ev);
     ev = ctx->mark_begin(SLOT_WPCA_FINAL);
     HCHK(launch_wpca_final(K, a, ctx->wp_kidx.as<int>(), (int)chunk.size(), st));

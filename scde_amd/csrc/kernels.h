@@ -10,6 +10,9 @@
 #ifndef SCDE_BOOT_DIAG
 #define SCDE_BOOT_DIAG 0  // bit switches that remove parts of k_boot2 for timing studies
 #endif
+#ifndef SCDE_WPCA_BLOCK
+#define SCDE_WPCA_BLOCK 512  // wpca.hip workgroup size (8 waves)
+#endif
 #include <hip/hip_runtime.h>
 
 namespace scde {
@@ -212,6 +215,10 @@ struct WpcaLaunch {
   int lds_cap;
 };
 int wpca_max_k();
+int wpca_ms_group();
+bool wpca_ms_ok(int n, int dmax);
+// npcs = 1, em without smoothing: blocks = (problem, first start of a group of wpca_ms_group())
+hipError_t launch_wpca_ms(const WpcaLaunch& a, int nblocks, hipStream_t s);
 hipError_t launch_wpca_em(int K, const WpcaLaunch& a, int nblocks, hipStream_t s);
 hipError_t launch_wpca_final(int K, const WpcaLaunch& a, const int* kidx, int nprob, hipStream_t s);
 

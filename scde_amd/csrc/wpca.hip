@@ -33,7 +33,8 @@
 namespace scde {
 namespace {
 
-constexpr int kWB = 256;  // block size: 4 waves
+constexpr int kWB = SCDE_WPCA_BLOCK;  // block size (waves = kWB / 64)
+constexpr int kNW = kWB / 64;
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
@@ -46,20 +47,28 @@ __device__ __forceinline__ double wave_max_d(double v) {
   return v;
 }
 
-// Fixed-order block sum over 4 waves; every thread gets the total.  red: >= 4 doubles.
+// Fixed-order block sum over NW waves; every thread gets the total.  red: NW doubles.
+template <int NW = kNW>
 __device__ __forceinline__ double block_sum_d(double v, double* red) {
   v = wave_sum_d(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  return (red[0] + red[1]) + (red[2] + red[3]);
+  double t = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) t += red[w];
+  return t;
 }
+template <int NW = kNW>
 __device__ __forceinline__ double block_max_d(double v, double* red) {
   v = wave_max_d(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  return fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  double t = red[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) t = fmax(t, red[w]);
+  return t;
 }
 
 __device__ __forceinline__ double dlapy2(double x, double y) {
@@ -68,43 +77,44 @@ __device__ __forceinline__ double dlapy2(double x, double y) {
   return w * sqrt(1 + (z / w) * (z / w));
 }
 
-// Block-wide Householder QR of E (d x K, E[g*K+k]) -> its economical Q (LAPACK
+// Block-wide Householder QR of E (d x K, E[g*ldg+k]) -> its economical Q (LAPACK
 // dgeqr2 + dorg2r, as Armadillo's qr_econ; src/bwpca.cpp:199).  tau: K doubles of LDS.
-template <int K>
-__device__ void block_qr(double* E, int d, double* tau, double* red) {
+template <int K, int NT = kWB>
+__device__ void block_qr(double* E, int d, int ldg, double* tau, double* red) {
+  constexpr int NW = NT / 64;
   const int tid = threadIdx.x;
   for (int i = 0; i < K; ++i) {
     double mx = 0;
-    for (int g = i + 1 + tid; g < d; g += kWB) mx = fmax(mx, fabs(E[g * K + i]));
-    mx = block_max_d(mx, red);
+    for (int g = i + 1 + tid; g < d; g += NT) mx = fmax(mx, fabs(E[g * ldg + i]));
+    mx = block_max_d<NW>(mx, red);
     double ss = 0;
     if (mx > 0)
-      for (int g = i + 1 + tid; g < d; g += kWB) {
-        const double t = E[g * K + i] / mx;
+      for (int g = i + 1 + tid; g < d; g += NT) {
+        const double t = E[g * ldg + i] / mx;
         ss += t * t;
       }
-    ss = block_sum_d(ss, red);
+    ss = block_sum_d<NW>(ss, red);
     const double xnorm = mx * sqrt(ss);
-    const double alpha = E[i * K + i];
+    const double alpha = E[i * ldg + i];
     double t = 0;
     __syncthreads();
     if (d - i > 1 && xnorm != 0) {
       const double beta = -copysign(dlapy2(alpha, xnorm), alpha);
       t = (beta - alpha) / beta;
       const double sc = 1.0 / (alpha - beta);
-      for (int g = i + 1 + tid; g < d; g += kWB) E[g * K + i] *= sc;
-      if (tid == 0) E[i * K + i] = beta;
+      for (int g = i + 1 + tid; g < d; g += NT) E[g * ldg + i] *= sc;
+      if (tid == 0) E[i * ldg + i] = beta;
     }
     if (tid == 0) tau[i] = t;
     __syncthreads();
     // H(i) applied to columns i+1..K-1 (v = [1, E[i+1.., i]])
     for (int jj = i + 1; jj < K; ++jj) {
       double w = 0;
-      for (int g = i + tid; g < d; g += kWB) w += E[g * K + jj] * (g == i ? 1.0 : E[g * K + i]);
-      w = block_sum_d(w, red);
+      for (int g = i + tid; g < d; g += NT) w += E[g * ldg + jj] * (g == i ? 1.0 : E[g * ldg + i]);
+      w = block_sum_d<NW>(w, red);
       const double tw = -t * w;
       if (t != 0)
-        for (int g = i + tid; g < d; g += kWB) E[g * K + jj] += (g == i ? 1.0 : E[g * K + i]) * tw;
+        for (int g = i + tid; g < d; g += NT) E[g * ldg + jj] += (g == i ? 1.0 : E[g * ldg + i]) * tw;
       __syncthreads();
     }
   }
@@ -112,17 +122,17 @@ __device__ void block_qr(double* E, int d, double* tau, double* red) {
     const double t = tau[i];
     for (int jj = i + 1; jj < K; ++jj) {
       double w = 0;
-      for (int g = i + tid; g < d; g += kWB) w += E[g * K + jj] * (g == i ? 1.0 : E[g * K + i]);
-      w = block_sum_d(w, red);
+      for (int g = i + tid; g < d; g += NT) w += E[g * ldg + jj] * (g == i ? 1.0 : E[g * ldg + i]);
+      w = block_sum_d<NW>(w, red);
       const double tw = -t * w;
       if (t != 0)
-        for (int g = i + tid; g < d; g += kWB) E[g * K + jj] += (g == i ? 1.0 : E[g * K + i]) * tw;
+        for (int g = i + tid; g < d; g += NT) E[g * ldg + jj] += (g == i ? 1.0 : E[g * ldg + i]) * tw;
       __syncthreads();
     }
-    for (int g = tid; g < d; g += kWB) {
-      if (g > i) E[g * K + i] *= -t;
-      else if (g == i) E[g * K + i] = 1 - t;
-      else E[g * K + i] = 0;
+    for (int g = tid; g < d; g += NT) {
+      if (g > i) E[g * ldg + i] *= -t;
+      else if (g == i) E[g * ldg + i] = 1 - t;
+      else E[g * ldg + i] = 0;
     }
     __syncthreads();
   }
@@ -305,7 +315,7 @@ __global__ __launch_bounds__(kWB) void k_wpca_em(const double* __restrict__ M, c
                                                  int maxiter, double tol, const double* __restrict__ smoothc, int L,
                                                  double* __restrict__ scratch, double* __restrict__ stat) {
   extern __shared__ double lds[];
-  __shared__ double red[8];
+  __shared__ double red[kNW];
   __shared__ double tau[K];
   constexpr int NM = K + K * (K + 1) / 2;
   const int2 bs = blocks[blockIdx.x];
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(kWB) void k_wpca_em(const double* __restrict__ M, c
     E[g * K + k] = X[e];
   }
   __syncthreads();
-  block_qr<K>(E, d, tau, red);
+  block_qr<K>(E, d, K, tau, red);
   // coefficients for the start (iteration 0's first step)
   (void)pass_ar<K, false>(P, M, Wm, ld, n, E, C, nullptr);
   __syncthreads();
@@ -335,7 +345,7 @@ __global__ __launch_bounds__(kWB) void k_wpca_em(const double* __restrict__ M, c
   int ii = 0, best = -1, cur = 0;
   while (ii < maxiter) {
     // ---- pass B: per-gene moments  P_k = sum_j (w c_k) m,  Q_kk' = sum_j (w c_k) c_k'
-    for (int g = wid; g < d; g += kWB / 64) {
+    for (int g = wid; g < d; g += kNW) {
       double acc[NM];
 #pragma unroll
       for (int q = 0; q < NM; ++q) acc[q] = 0;
@@ -438,7 +448,7 @@ __global__ __launch_bounds__(kWB) void k_wpca_final(const double* __restrict__ M
                                                     const int* __restrict__ perms,
                                                     const double* __restrict__ scratch,
                                                     const double* __restrict__ stat, double* __restrict__ out) {
-  __shared__ double red[8];
+  __shared__ double red[kNW];
   __shared__ int chosen_s;
   __shared__ int chosen_slot;
   const int p = kidx[blockIdx.x];
@@ -516,6 +526,306 @@ __global__ __launch_bounds__(kWB) void k_wpca_final(const double* __restrict__ M
   }
 }
 
+// ---- multi-start EM for npcs = 1 (pagoda's random gene sets; most of its EM work) ----
+// One workgroup of 1024 threads runs SG = 5 starts of one problem together, so every
+// value / weight element loaded serves 5 starts.  Thread t owns cells t + r * 1024
+// (r < R) in both passes, with the 5 coefficients of each owned cell in registers:
+//   * pass AR: loop over genes, E_g for the 5 starts broadcast from LDS;
+//   * pass B: per gene, each thread's partial moments (P_s, Q_s over its cells) are
+//     reduce-scattered across the wave on VALU (permlane swaps + DPP), the 16 waves'
+//     partials combined in LDS in a fixed order, 16 genes per barrier.
+// All 5 starts are computed until the last one stops; the finished ones' results are
+// discarded (their best model is already saved).
+constexpr int kMsNT = 1024, kMsNW = 16, kMsSG = 5, kMsGCH = 16;
+
+__device__ __forceinline__ void swap32d(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                   false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                   false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void swap16d(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                   false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                   false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+template <int CTRL>
+__device__ __forceinline__ double dppd(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// Sum reduce-scatter of 16 values over the wave: lane l ends with the wave total of
+// value (l >> 2) & 15.  Stages pair lanes by bit 5, 4 (permlane swaps), 3 (row mirror,
+// lane ^ 15), 2 (half mirror, lane ^ 7), then 1, 0 (quad perms).
+__device__ __forceinline__ double rs16_sum(double (&v)[16], int lane) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    swap32d(v[j], v[j + 8]);
+    v[j] = v[j] + v[j + 8];
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    swap16d(v[j], v[j + 4]);
+    v[j] = v[j] + v[j + 4];
+  }
+  {
+    const bool up = (lane & 8) != 0;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const double lo = v[j], hi = v[j + 2];
+      v[j] = (up ? hi : lo) + dppd<0x140>(up ? lo : hi);
+    }
+  }
+  {
+    const bool up = (lane & 4) != 0;
+    const double lo = v[0], hi = v[1];
+    v[0] = (up ? hi : lo) + dppd<0x141>(up ? lo : hi);
+  }
+  double x = v[0];
+  x = x + dppd<0x4E>(x);
+  x = x + dppd<0xB1>(x);
+  return x;
+}
+
+template <int NW, int V>
+__device__ __forceinline__ void block_sum_vec(double (&v)[V], double* red) {
+#pragma unroll
+  for (int i = 0; i < V; ++i) v[i] = wave_sum_d(v[i]);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int i = 0; i < V; ++i) red[(threadIdx.x >> 6) * V + i] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < V; ++i) {
+    double t = red[i];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) t += red[w * V + i];
+    v[i] = t;
+  }
+}
+
+// pass AR for the SG starts: fit of the old coefficients against E (FIT) and the new ones
+template <int R, bool FIT>
+__device__ __forceinline__ void ms_pass_ar(const ProbView& P, const double* __restrict__ M,
+                                           const double* __restrict__ Wm, long long ld, int n, const double* E,
+                                           double (&c)[R][kMsSG], double (&racc)[kMsSG], double* cbase, int nc,
+                                           unsigned amask, unsigned slots) {
+  constexpr int SG = kMsSG;
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int j = threadIdx.x + r * kMsNT;
+    const bool in = j < n;
+    const int jj = in ? j : 0;
+    double A[SG], b[SG];
+#pragma unroll
+    for (int s = 0; s < SG; ++s) A[s] = b[s] = 0;
+    int g = 0;
+    for (; g + 2 <= P.d; g += 2) {
+      double mv[2], wv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const long long e = elem(P, g + u, jj, P.cols[g + u], ld, n);
+        mv[u] = in ? M[e] : 0.0;
+        wv[u] = in ? Wm[e] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const double mw = mv[u] * wv[u];
+#pragma unroll
+        for (int s = 0; s < SG; ++s) {
+          const double eg = E[(g + u) * SG + s];
+          if (FIT) {
+            const double dl = c[r][s] * eg - mv[u];
+            racc[s] += (dl * dl) * wv[u];
+          }
+          b[s] += mw * eg;
+          A[s] += eg * (eg * wv[u]);
+        }
+      }
+    }
+    for (; g < P.d; ++g) {
+      const long long e = elem(P, g, jj, P.cols[g], ld, n);
+      const double mv = in ? M[e] : 0.0, wv = in ? Wm[e] : 0.0;
+      const double mw = mv * wv;
+#pragma unroll
+      for (int s = 0; s < SG; ++s) {
+        const double eg = E[g * SG + s];
+        if (FIT) {
+          const double dl = c[r][s] * eg - mv;
+          racc[s] += (dl * dl) * wv;
+        }
+        b[s] += mw * eg;
+        A[s] += eg * (eg * wv);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < SG; ++s) {
+      if (FIT && in && ((amask >> s) & 1u)) cbase[(long long)(2 * s + ((slots >> s) & 1u)) * nc + j] = c[r][s];
+      c[r][s] = A[s] == 0 ? 0.0 : b[s] / A[s];
+    }
+  }
+}
+
+template <int R>
+__global__ __launch_bounds__(kMsNT) void k_wpca_ms1(const double* __restrict__ M, const double* __restrict__ Wm,
+                                                    long long ld, int n, const WpcaProb* __restrict__ probs,
+                                                    const int2* __restrict__ blocks, const int* __restrict__ cols,
+                                                    const int* __restrict__ perms, const double* __restrict__ starts,
+                                                    int maxiter, double tol, double* __restrict__ scratch,
+                                                    double* __restrict__ stat) {
+  constexpr int SG = kMsSG, NW = kMsNW, NT = kMsNT, GCH = kMsGCH;
+  extern __shared__ double lds[];  // E[g * SG + s]
+  __shared__ double part[GCH][NW][2 * SG];
+  __shared__ double red[NW * SG];
+  __shared__ double tau[1];
+  // per-start EM state, kept by thread 0 (the block reads it after a barrier)
+  __shared__ double s_pres[SG], s_bpres[SG];
+  __shared__ int s_best[SG], s_cur[SG], s_iters[SG], s_impr[SG];
+  __shared__ unsigned s_amask;
+  const int2 bs = blocks[blockIdx.x];
+  if (bs.x < 0) return;
+  const WpcaProb Pr = probs[bs.x];
+  const int s0 = bs.y, d = Pr.d, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ns = Pr.nstarts - s0 < SG ? Pr.nstarts - s0 : SG;
+  ProbView P{d, Pr.nstarts, cols + Pr.col_off, Pr.perm_off >= 0 ? perms + Pr.perm_off : nullptr};
+  double* E = lds;
+  double* mom = scratch + Pr.mom_off + (long long)s0 * d * 3;  // d x 2 x ns (fits the group's d x 3 x ns)
+  double* cbase = scratch + Pr.sC_off + (long long)s0 * 2 * n;  // start s0+s, slot k: + (2 s + k) n
+  double* ebase = scratch + Pr.sE_off + (long long)s0 * d;      // start s0+s: + s d
+  for (int e = tid; e < d * SG; e += NT) {
+    const int g = e / SG, s = e % SG;
+    E[e] = s < ns ? starts[Pr.start_off + (long long)(s0 + s) * d + g] : 0.0;
+  }
+  if (tid < SG) {
+    s_pres[tid] = s_bpres[tid] = DBL_MAX;
+    s_best[tid] = -1;
+    s_cur[tid] = 0;
+    s_iters[tid] = 0;
+  }
+  if (tid == 0) s_amask = (1u << ns) - 1u;
+  __syncthreads();
+  for (int s = 0; s < ns; ++s) block_qr<1, NT>(E + s, d, SG, tau, red);
+  double c[R][SG];
+  double racc[SG];
+  ms_pass_ar<R, false>(P, M, Wm, ld, n, E, c, racc, nullptr, n, 0u, 0);
+  for (int it = 0; it < maxiter; ++it) {
+    __syncthreads();
+    const unsigned amask = s_amask;
+    if (amask == 0u) break;
+    // ---- pass B: moments P_s = sum_j (w c_s) m, Q_s = sum_j (w c_s) c_s, 16 genes per barrier
+    for (int g0 = 0; g0 < d; g0 += GCH) {
+      const int gn = d - g0 < GCH ? d - g0 : GCH;
+      for (int gi = 0; gi < gn; ++gi) {
+        const int g = g0 + gi;
+        const int col = P.cols[g];
+        double v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int j = tid + r * NT;
+          if (j < n) {
+            const long long e = elem(P, g, j, col, ld, n);
+            const double mv = M[e], wv = Wm[e];
+#pragma unroll
+            for (int s = 0; s < SG; ++s) {
+              const double t = wv * c[r][s];
+              v[s] += mv * t;
+              v[SG + s] += t * c[r][s];
+            }
+          }
+        }
+        const double x = rs16_sum(v, lane);
+        const int q = (lane >> 2) & 15;
+        if ((lane & 3) == 0 && q < 2 * SG) part[gi][wid][q] = x;
+      }
+      __syncthreads();
+      if (tid < gn * 2 * SG) {
+        const int gi = tid / (2 * SG), q = tid % (2 * SG);
+        double t = part[gi][0][q];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) t += part[gi][w][q];
+        const int s = q % SG;
+        if (s < ns) mom[(long long)(g0 + gi) * 2 * ns + (q / SG) * ns + s] = t;
+      }
+      __syncthreads();
+    }
+    // ---- new eigenvectors E = P / Q, then unit length
+    double dots[SG];
+#pragma unroll
+    for (int s = 0; s < SG; ++s) dots[s] = 0;
+    for (int g = tid; g < d; g += NT) {
+#pragma unroll
+      for (int s = 0; s < SG; ++s) {
+        if (s < ns) {
+          const double v = mom[(long long)g * 2 * ns + s] / mom[(long long)g * 2 * ns + ns + s];
+          E[g * SG + s] = v;
+          dots[s] += v * v;
+        }
+      }
+    }
+    block_sum_vec<NW, SG>(dots, red);
+    for (int g = tid; g < d; g += NT)
+#pragma unroll
+      for (int s = 0; s < SG; ++s)
+        if (s < ns) E[g * SG + s] /= sqrt(dots[s]);
+    __syncthreads();
+    // ---- fit of (C, E) fused with the next coefficients; old C -> the start's candidate slot
+#pragma unroll
+    for (int s = 0; s < SG; ++s) racc[s] = 0;
+    unsigned slots = 0;
+#pragma unroll
+    for (int s = 0; s < SG; ++s) slots |= (unsigned)(s_cur[s] & 1) << s;
+    ms_pass_ar<R, true>(P, M, Wm, ld, n, E, c, racc, cbase, n, amask, slots);
+    block_sum_vec<NW, SG>(racc, red);
+    if (tid == 0) {
+      unsigned am = amask;
+      for (int s = 0; s < SG; ++s) {
+        s_impr[s] = 0;
+        if ((am >> s) & 1u) {
+          const double npres = racc[s];
+          if (npres < s_bpres[s]) {
+            s_bpres[s] = npres;
+            s_best[s] = s_cur[s];
+            s_cur[s] ^= 1;
+            s_impr[s] = 1;
+          }
+          if (tol > 0 && it > 0 && (s_pres[s] - npres) / npres < tol && s_pres[s] > npres) {
+            s_pres[s] = npres;
+            s_iters[s] = it;
+            am &= ~(1u << s);
+          } else {
+            s_pres[s] = npres;
+            s_iters[s] = it + 1;
+          }
+        }
+      }
+      s_amask = am;
+    }
+    __syncthreads();
+    for (int e = tid; e < d * SG; e += NT) {
+      const int g = e / SG, s = e % SG;
+      if (s_impr[s]) ebase[(long long)s * d + g] = E[e];
+    }
+  }
+  __syncthreads();
+  if (tid < ns) {
+    double* st = stat + (Pr.stat_off + s0 + tid) * 4;
+    st[0] = s_pres[tid];
+    st[1] = s_bpres[tid];
+    st[2] = (double)s_iters[tid];
+    st[3] = (double)s_best[tid];
+  }
+}
+
 // ------------------------------------------------------------------ launchers
 namespace {
 template <int K>
@@ -546,6 +856,32 @@ hipError_t launch_final_k(const WpcaLaunch& a, const int* kidx, int nprob, hipSt
 }  // namespace
 
 int wpca_max_k() { return kWpcaMaxK; }
+
+int wpca_ms_group() { return kMsSG; }
+
+// npcs = 1, no smoothing, ncells <= 4096, E for 5 starts in LDS: the multi-start kernel
+bool wpca_ms_ok(int n, int dmax) {
+  return n <= 4 * kMsNT && (size_t)dmax * kMsSG * sizeof(double) <= (size_t)96 * 1024;
+}
+
+hipError_t launch_wpca_ms(const WpcaLaunch& a, int nblocks, hipStream_t st) {
+  const size_t need = (size_t)a.dmax * kMsSG * sizeof(double);
+  const int R = (a.n + kMsNT - 1) / kMsNT;
+  auto go = [&](auto fn) {
+    hipError_t e = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)need);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(fn, dim3(nblocks), dim3(kMsNT), need, st, a.M, a.W, a.ld, a.n, a.probs, a.blocks, a.cols,
+                       a.perms, a.starts, a.maxiter, a.tol, a.scratch, a.stat);
+    return hipGetLastError();
+  };
+  switch (R) {
+    case 1: return go(k_wpca_ms1<1>);
+    case 2: return go(k_wpca_ms1<2>);
+    case 3: return go(k_wpca_ms1<3>);
+    case 4: return go(k_wpca_ms1<4>);
+    default: return hipErrorInvalidValue;
+  }
+}
 
 hipError_t launch_wpca_em(int K, const WpcaLaunch& a, int nblocks, hipStream_t st) {
   switch (K) {
