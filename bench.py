@@ -43,6 +43,7 @@ sys.path.insert(0, ROOT)
 NBOOT = 100
 LENGTH_OUT = 400
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+FP64_VALU_PEAK_TF = 78.6  # FP64 vector spec = FP32 vector 157.3 TF (MI355X_MICROARCH.md) / 2; 67 TF measured (tools/micro)
 METRIC = "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)"
 
 CONFIGS = {
@@ -261,9 +262,9 @@ def synthetic_varinfo(seed: int, ngenes: int, ncells: int, nsets: int):
 
 def bench_wpca(args, cfg, rank, world, device):
     """--config 5: pagoda.pathway.wPCA, every bwpca call batched on the device (wpca.hip).
-    Roofline of k_wpca_em: each EM pass (the start's coefficients, then per iteration the
-    eigenvector pass and the fused fit + coefficient pass) reads the problem's value and
-    weight columns once: 16 B x cells x genes per pass."""
+    Roofline: FP64 VALU.  The starts of a problem share each loaded element on chip (5 per
+    workgroup for npcs = 1), so the EM kernels are compute-bound; achieved = the reference
+    formulation's flops (_wpca_work) / the EM launches' time."""
     from scde_amd import api
     from scde_amd import pagoda as PG
     NG, NC = cfg["genes"], cfg["cells"]
@@ -284,13 +285,11 @@ def bench_wpca(args, cfg, rank, world, device):
     kt = ctx.kernel_times()
     nsets = len(out)
     em_ms, em_n = kt["wpca_em"]
-    # algorithmic bytes of one step's EM launches: replay the step's problems with iteration counts
+    # algorithmic work of one step's EM launches: replay the step's problems with iteration counts
     ctx.set_profiling(False)
-    passes_bytes = _wpca_pass_bytes(PG, pdev, sets)
-    em_s = em_ms / max(em_n, 1) / 1e3
-    launches_per_step = em_n / args.steps
-    per_launch = passes_bytes / launches_per_step if launches_per_step else 0
-    achieved = per_launch / em_s / 1e9 if em_n else None
+    step_bytes, step_flops = _wpca_work(PG, pdev, sets)
+    em_s_step = em_ms / args.steps / 1e3
+    achieved = step_flops / em_s_step / 1e12 if em_n else None
     res = {"metric": METRIC_WPCA, "value": nsets * args.steps / dt, "unit": "gene sets/s", "n_gpus": world,
            "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3,
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -298,10 +297,14 @@ def bench_wpca(args, cfg, rank, world, device):
                    f"uniform weights with 15% at 1e-3",
            "config": {"workload": cfg["workload"], "genes": NG, "cells": NC, "gene_sets": nsets,
                       "parallelism": "single GPU"},
-           "roofline": {"bound": "hbm", "kernel": "k_wpca_em (EM iterations, one workgroup per set x start)",
-                        "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
-                        "avg_launch_ms": em_s * 1e3, "launches": em_n, "algorithmic_bytes_per_launch": per_launch},
+           "roofline": {"bound": "fp64-valu", "kernel": "k_wpca_ms1 + k_wpca_em (EM iterations)",
+                        "achieved": achieved, "peak": FP64_VALU_PEAK_TF, "unit": "TFLOP/s",
+                        "frac": achieved / FP64_VALU_PEAK_TF if achieved else None, "traffic": None,
+                        "em_ms_per_step": em_s_step * 1e3, "launches_per_step": em_n / args.steps,
+                        "algorithmic_flops_per_step": step_flops,
+                        "pass_bytes_per_step": step_bytes,
+                        "pass_bytes_note": "16 B x cells x genes per EM pass per start (the reference's reads); "
+                                           "starts share their columns on chip, so HBM sees a fraction"},
            "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
     if rank == 0 and cpu_sample > 0:
@@ -334,24 +337,31 @@ def _prepared_host(vinfo):
     return mat, np.asarray(vinfo["matw"], dtype=np.float64)
 
 
-def _wpca_pass_bytes(PG, pdev, sets):
-    """Replays one step's batch with iteration counts: sum over (problem, start) of
-    (1 + 2 x iterations) passes x 16 B x cells x genes."""
+def _wpca_work(PG, pdev, sets):
+    """Replays one step's batch with iteration counts.  Per (problem, start) with d genes,
+    n cells, npcs K and `it` EM iterations, the reference's loops (src/bwpca.cpp:221-294) do
+    per element: the start's coefficient step (1 + 2K + 3K^2 flops), then per iteration the
+    coefficient step, the eigenvector step (5K + 2(K-1)) and the fit (2K + 4):
+    3K^2 + 11K + 3 flops.  Each pass reads the value and weight columns: 16 B per element."""
     orig = PG.WpcaBatch.run
-    total = [0.0]
+    tot = [0.0, 0.0]
 
     def run(self, dev, **kw):
         kw["want_iterations"] = True
         res = orig(self, dev, **kw)
         for p, r in enumerate(res):
-            total[0] += float(np.sum(1 + 2 * r["iterations"])) * 16.0 * dev.ncells * self.d[p]
+            K = min(self.npcs[p], self.d[p])
+            el = float(dev.ncells) * self.d[p]
+            its = r["iterations"].astype(np.float64)
+            tot[0] += float(np.sum(1 + 2 * its)) * 16.0 * el
+            tot[1] += float(np.sum((1 + 2 * K + 3 * K * K) + its * (3 * K * K + 11 * K + 3))) * el
         return res
     PG.WpcaBatch.run = run
     try:
         PG.pagoda_pathway_wPCA(None, sets, n_components=2, n_randomizations=10, n_starts=10, seed=1, device=pdev)
     finally:
         PG.WpcaBatch.run = orig
-    return total[0]
+    return tot[0], tot[1]
 
 
 def main():
