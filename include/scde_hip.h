@@ -235,6 +235,29 @@ int scde_r_sample(uint32_t* state, int n, int k, int* out);
  * platform rand() (scde_set_rand_kind): nshuffles x d x n. */
 int scde_shuffle_perms(unsigned int seed, int nshuffles, int d, int n, int* perms);
 
+/* ---------------------------------------------------------------- PAGODA helpers
+ * The remaining .Call symbols of the package (src/pagoda.cpp; declared src/pagoda.h:5-8),
+ * SURVEY.md section 8(f) row 4.  Host buffers, R column-major. */
+
+/* .Call("winsorizeMatrix", Mat, Trim) (src/pagoda.cpp:6-31): per row, the round(ncol * trim)
+ * smallest values become the next smallest, the largest the next largest.  ncol <= 8192,
+ * or round(ncol * trim) <= 32. */
+int scde_winsorizeMatrix(const double* mat, int nrow, int ncol, double trim, double* out);
+
+/* .Call("matWCorr", Mat, Matw) (src/pagoda.cpp:41-65): weighted correlation of columns i < j
+ * with weights sqrt(w_i w_j) / sum; out ncol x ncol: 1 on the diagonal, c(j, i) below it,
+ * 0 above (as the reference fills it). */
+int scde_matWCorr(const double* mat, const double* matw, int nrow, int ncol, double* out);
+
+/* .Call("matCorr", X, Y) = arma::cor(x, y) (src/pagoda.cpp:33-38): x nrow x nx, y nrow x ny,
+ * out nx x ny. */
+int scde_matCorr(const double* x, int nrow, int nx, const double* y, int ny, double* out);
+
+/* .Call("plSemicompleteCor2", Pl) (src/pagoda.cpp:67-117): np sparse vectors (list element p
+ * = gene indices idx[off[p] .. off[p+1]) increasing, values val[...]); r = correlation over
+ * the shared genes (np x np, 1 on the diagonal), n = union sizes (np x np, 0 on it). */
+int scde_plSemicompleteCor2(int np, const int64_t* off, const int* idx, const double* val, double* r, int* n);
+
 #ifdef __cplusplus
 }
 #endif

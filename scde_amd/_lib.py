@@ -23,7 +23,7 @@ EXPORTS = [
     "scde_expression_difference_dev", "scde_posteriors_dev", "scde_bh_cz_dev",
     "scde_expression_difference_batch_dev", "scde_expression_prior_dev",
     "scde_baileyWPCA", "scde_bwpca_batch_dev", "scde_r_set_seed", "scde_r_unif_rand", "scde_r_sample",
-    "scde_shuffle_perms",
+    "scde_shuffle_perms", "scde_winsorizeMatrix", "scde_matWCorr", "scde_matCorr", "scde_plSemicompleteCor2",
 ]
 
 
@@ -104,6 +104,10 @@ def lib():
     L.scde_r_unif_rand.argtypes = [P, i64, P]
     L.scde_r_sample.argtypes = [P, i, i, P]
     L.scde_shuffle_perms.argtypes = [ctypes.c_uint, i, i, i, P]
+    L.scde_winsorizeMatrix.argtypes = [P, i, i, d, P]
+    L.scde_matWCorr.argtypes = [P, P, i, i, P]
+    L.scde_matCorr.argtypes = [P, i, i, P, i, P]
+    L.scde_plSemicompleteCor2.argtypes = [i, P, P, P, P, P]
     _lib = L
     return L
 

@@ -170,6 +170,8 @@ struct scde_ctx {
   Buf pr_cell, pr_part, pr_occ, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
   // weighted PCA (bwpca)
   Buf wp_probs, wp_blocks, wp_kidx, wp_cols, wp_perms, wp_starts, wp_scratch, wp_stat, wp_out, wp_smooth, wp_M, wp_W;
+  // PAGODA helpers
+  Buf pg_a, pg_b, pg_c, pg_d, pg_e;
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
   // unique tables can be built up front, with their host syncs, before the heavy kernels
   struct UniqueSet {
@@ -238,7 +240,8 @@ struct scde_ctx {
     for (Buf* b : all) b->release();
     Buf* wp[] = {&wp_probs, &wp_blocks,  &wp_kidx, &wp_cols,   &wp_perms, &wp_starts, &wp_scratch,
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
-                 &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw};
+                 &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
+                 &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
@@ -2006,6 +2009,100 @@ int scde_baileyWPCA(const double* mat, const double* matw, int n, int d, int npc
   *totvar = stats[K];
   for (int s = 0; s < nshuffles; ++s) randvar[s] = *totvar - stats[(size_t)(1 + s) * (K + 2) + K + 1];
   return SCDE_OK;
+}
+
+// ------------------------------------------------------------------ PAGODA helpers
+// .Call("winsorizeMatrix", Mat, Trim) (src/pagoda.cpp:6-31; pagoda.h:5).  mat: nrow x ncol.
+int scde_winsorizeMatrix(const double* mat, int nrow, int ncol, double trim, double* out) {
+  if (!mat || !out) return fail(SCDE_EARG, "null argument");
+  if (nrow < 0 || ncol < 0) return fail(SCDE_EARG, "bad dimensions");
+  const size_t nel = (size_t)nrow * ncol;
+  const int ntr = (int)std::round(ncol * trim);
+  if (nel == 0 || ntr == 0) {
+    if (nel) std::memcpy(out, mat, sizeof(double) * nel);
+    return SCDE_OK;
+  }
+  if (ntr < 0 || ntr > ncol - 1)  // the reference indexes sorted[ntr] and sorted[ncol - ntr - 1]
+    return fail(SCDE_EARG, "winsorizeMatrix: trim %g out of range for %d columns", trim, ncol);
+  int NP = 1;
+  while (NP < ncol) NP <<= 1;
+  if (NP > 8192 && ntr > 32) return fail(SCDE_EARG, "winsorizeMatrix: ncol > 8192 needs round(ncol * trim) <= 32");
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  HCHK(upload(cx->pg_a, mat, nel, cx->stream));
+  HCHK(cx->pg_b.ensure(sizeof(double) * nel));
+  HCHK(launch_winsorize(cx->pg_a.as<double>(), nrow, ncol, ntr, cx->pg_b.as<double>(), cx->stream));
+  HCHK(hipMemcpyAsync(out, cx->pg_b.p, sizeof(double) * nel, hipMemcpyDeviceToHost, cx->stream));
+  return cx->sync();
+}
+
+// .Call("matWCorr", Mat, Matw) (src/pagoda.cpp:41-65; pagoda.h:6).  mat, matw: nrow x ncol;
+// out: ncol x ncol (identity diagonal, c(j, i) for j > i, upper triangle 0).
+int scde_matWCorr(const double* mat, const double* matw, int nrow, int ncol, double* out) {
+  if (!mat || !matw || !out) return fail(SCDE_EARG, "null argument");
+  if (nrow < 0 || ncol < 0) return fail(SCDE_EARG, "bad dimensions");
+  if (ncol == 0) return SCDE_OK;
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  const size_t nel = (size_t)nrow * ncol, nout = (size_t)ncol * ncol;
+  HCHK(upload(cx->pg_a, mat, nel, cx->stream));
+  HCHK(upload(cx->pg_b, matw, nel, cx->stream));
+  HCHK(cx->pg_c.ensure(sizeof(double) * nout));
+  HCHK(launch_matwcorr(cx->pg_a.as<double>(), cx->pg_b.as<double>(), nrow, ncol, cx->pg_c.as<double>(),
+                       cx->stream));
+  HCHK(hipMemcpyAsync(out, cx->pg_c.p, sizeof(double) * nout, hipMemcpyDeviceToHost, cx->stream));
+  return cx->sync();
+}
+
+// .Call("matCorr", X, Y) = arma::cor(x, y) (src/pagoda.cpp:33-38; pagoda.h:8).  x: nrow x nx,
+// y: nrow x ny; out: nx x ny.
+int scde_matCorr(const double* x, int nrow, int nx, const double* y, int ny, double* out) {
+  if (!x || !y || !out) return fail(SCDE_EARG, "null argument");
+  if (nrow < 0 || nx < 0 || ny < 0) return fail(SCDE_EARG, "bad dimensions");
+  if ((size_t)nx * ny == 0) return SCDE_OK;
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  HCHK(upload(cx->pg_a, x, (size_t)nrow * nx, cx->stream));
+  HCHK(upload(cx->pg_b, y, (size_t)nrow * ny, cx->stream));
+  HCHK(cx->pg_c.ensure(sizeof(double) * (size_t)nx * ny));
+  HCHK(cx->pg_d.ensure(sizeof(double) * 2 * ((size_t)nx + ny)));
+  HCHK(launch_matcorr(cx->pg_a.as<double>(), nrow, nx, cx->pg_b.as<double>(), ny, cx->pg_d.as<double>(),
+                      cx->pg_c.as<double>(), cx->stream));
+  HCHK(hipMemcpyAsync(out, cx->pg_c.p, sizeof(double) * (size_t)nx * ny, hipMemcpyDeviceToHost, cx->stream));
+  return cx->sync();
+}
+
+// .Call("plSemicompleteCor2", Pl) (src/pagoda.cpp:67-117; pagoda.h:7).  List element p:
+// gene indices idx[off[p] .. off[p+1]) (increasing), values val[...].  r: np x np
+// correlations over the shared genes (1 on the diagonal); n: np x np union sizes (0 on it).
+int scde_plSemicompleteCor2(int np, const int64_t* off, const int* idx, const double* val, double* r, int* n) {
+  if (np < 0 || (np > 0 && (!off || !r || !n))) return fail(SCDE_EARG, "null argument");
+  if (np == 0) return SCDE_OK;
+  const int64_t tot = off[np];
+  if (off[0] != 0 || tot < 0) return fail(SCDE_EARG, "bad offsets");
+  for (int p = 0; p < np; ++p) {
+    if (off[p + 1] < off[p]) return fail(SCDE_EARG, "bad offsets");
+    for (int64_t e = off[p] + 1; e < off[p + 1]; ++e)
+      if (idx[e] <= idx[e - 1]) return fail(SCDE_EARG, "list %d: gene indices must increase", p);
+  }
+  scde_ctx* cx = nullptr;
+  RCHK(default_ctx(&cx));
+  HCHK(hipSetDevice(cx->device));
+  std::vector<long long> offl(off, off + np + 1);
+  HCHK(upload(cx->pg_a, offl.data(), offl.size(), cx->stream));
+  HCHK(upload(cx->pg_b, idx, (size_t)tot, cx->stream));
+  HCHK(upload(cx->pg_c, val, (size_t)tot, cx->stream));
+  const size_t nn = (size_t)np * np;
+  HCHK(cx->pg_d.ensure(sizeof(double) * nn));
+  HCHK(cx->pg_e.ensure(sizeof(int) * nn));
+  HCHK(launch_plcor(np, cx->pg_a.as<long long>(), cx->pg_b.as<int>(), cx->pg_c.as<double>(), cx->pg_d.as<double>(),
+                    cx->pg_e.as<int>(), cx->stream));
+  HCHK(hipMemcpyAsync(r, cx->pg_d.p, sizeof(double) * nn, hipMemcpyDeviceToHost, cx->stream));
+  HCHK(hipMemcpyAsync(n, cx->pg_e.p, sizeof(int) * nn, hipMemcpyDeviceToHost, cx->stream));
+  return cx->sync();
 }
 }  // extern "C"
 

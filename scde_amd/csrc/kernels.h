@@ -222,4 +222,16 @@ hipError_t launch_wpca_ms(const WpcaLaunch& a, int nblocks, hipStream_t s);
 hipError_t launch_wpca_em(int K, const WpcaLaunch& a, int nblocks, hipStream_t s);
 hipError_t launch_wpca_final(int K, const WpcaLaunch& a, const int* kidx, int nprob, hipStream_t s);
 
+// ---- PAGODA helpers (pagoda.hip; src/pagoda.cpp).  Matrices column-major.
+// winsorize: m k x n, ntr per side; n <= 8192, or ntr <= 32
+hipError_t launch_winsorize(const double* m, int k, int n, int ntr, double* out, hipStream_t s);
+// matWCorr: m, w k x n -> out n x n
+hipError_t launch_matwcorr(const double* m, const double* w, int k, int n, double* out, hipStream_t s);
+// matCorr: x k x nx, y k x ny -> out nx x ny; stats: 2 (nx + ny) doubles of scratch
+hipError_t launch_matcorr(const double* x, int k, int nx, const double* y, int ny, double* stats, double* out,
+                          hipStream_t s);
+// plSemicompleteCor2: np lists (off[np + 1], idx, val) -> r, cnt np x np
+hipError_t launch_plcor(int np, const long long* off, const int* idx, const double* val, double* r, int* cnt,
+                        hipStream_t s);
+
 }  // namespace scde

@@ -1,4 +1,6 @@
-"""Host-side mirror of scde's weighted-PCA path: ``bwpca()`` and ``pagoda.pathway.wPCA()``.
+"""Host-side mirror of scde's weighted-PCA path (``bwpca()``, ``pagoda.pathway.wPCA()``) and
+of the PAGODA helper ``.Call`` symbols (src/pagoda.cpp: ``winsorizeMatrix``, ``matWCorr``,
+``matCorr``, ``plSemicompleteCor2``).
 
 The EM iterations run in ``libscde_hip.so`` (``wpca.hip``: one workgroup per problem x
 random start, the whole EM loop on chip).  This module restates the R glue around the
@@ -376,3 +378,70 @@ def _pathway_wpca(pdev, setenv, n_components, min_pathway_size, max_pathway_size
         xv = xv / sds[:, None] * np.sqrt(avar)[:, None]
         out[go] = {"xv": xv, "xp": xp, "z": z, "sd": xp["sd"], "n": len(cols)}
     return out
+
+
+# ================================================================== PAGODA helpers (src/pagoda.cpp)
+def winsorizeMatrix(Mat, Trim):
+    """.Call("winsorizeMatrix", Mat, Trim) (src/pagoda.cpp:6-31)."""
+    m = np.asfortranarray(Mat, dtype=np.float64)
+    if m.ndim != 2:
+        raise ValueError("Mat must be a matrix")
+    out = np.empty_like(m, order="F")
+    check(lib().scde_winsorizeMatrix(_p(m), m.shape[0], m.shape[1], float(Trim), _p(out)))
+    return out
+
+
+def winsorize_matrix(mat, trim):
+    """winsorize.matrix (R/functions.R:1109-1115): trim > 0.5 is a count of values."""
+    rows = list(mat.index) if hasattr(mat, "index") else None
+    cols = list(mat.columns) if hasattr(mat, "columns") else None
+    m = np.asarray(mat, dtype=np.float64)
+    if trim > 0.5:
+        trim = trim / m.shape[1]
+    wm = winsorizeMatrix(m, trim)
+    if rows is not None or cols is not None:
+        import pandas as pd
+        return pd.DataFrame(wm, index=rows, columns=cols)
+    return wm
+
+
+def matWCorr(Mat, Matw):
+    """.Call("matWCorr", Mat, Matw) (src/pagoda.cpp:41-65): ncol x ncol, lower triangle."""
+    m = np.asfortranarray(Mat, dtype=np.float64)
+    w = np.asfortranarray(Matw, dtype=np.float64)
+    if m.shape != w.shape or m.ndim != 2:
+        raise ValueError("Mat and Matw must be matrices of the same dimensions")
+    out = np.empty((m.shape[1], m.shape[1]), order="F")
+    check(lib().scde_matWCorr(_p(m), _p(w), m.shape[0], m.shape[1], _p(out)))
+    return out
+
+
+def matCorr(X, Y):
+    """.Call("matCorr", X, Y) = arma::cor(X, Y) (src/pagoda.cpp:33-38)."""
+    x = np.asfortranarray(X, dtype=np.float64)
+    y = np.asarray(Y, dtype=np.float64)
+    if y.ndim == 1:
+        y = y[:, None]
+    y = np.asfortranarray(y)
+    if x.ndim != 2 or x.shape[0] != y.shape[0]:
+        raise ValueError("X and Y must have the same number of rows")
+    out = np.empty((x.shape[1], y.shape[1]), order="F")
+    check(lib().scde_matCorr(_p(x), x.shape[0], x.shape[1], _p(y), y.shape[1], _p(out)))
+    return out
+
+
+def plSemicompleteCor2(pl):
+    """.Call("plSemicompleteCor2", pl) (src/pagoda.cpp:67-117); pl: [(i, v), ...] with
+    increasing integer gene indices i.  Returns {"r", "n"}."""
+    npl = len(pl)
+    off = np.zeros(npl + 1, np.int64)
+    for k, (i, _) in enumerate(pl):
+        off[k + 1] = off[k] + len(i)
+    idx = np.ascontiguousarray(np.concatenate([np.asarray(i).astype(np.int32) for i, _ in pl]) if off[-1] else
+                               np.zeros(1, np.int32))
+    val = np.ascontiguousarray(np.concatenate([np.asarray(v, np.float64) for _, v in pl]) if off[-1] else
+                               np.zeros(1))
+    r = np.zeros((npl, npl), order="F")
+    n = np.zeros((npl, npl), np.int32, order="F")
+    check(lib().scde_plSemicompleteCor2(npl, _p(off), _p(idx), _p(val), _p(r), _p(n)))
+    return {"r": r, "n": n}
