@@ -10,6 +10,12 @@
 #ifndef SCDE_BOOT_DIAG
 #define SCDE_BOOT_DIAG 0  // bit switches that remove parts of k_boot2 for timing studies
 #endif
+#ifndef SCDE_RATIO_WPE
+#define SCDE_RATIO_WPE 1  // k_ratio_summary occupancy target (waves per SIMD; 1 = compiler's choice)
+#endif
+#ifndef SCDE_RATIO_DIAG
+#define SCDE_RATIO_DIAG 0  // timing-only builds: 1 skips the slide, 2 the summary (results wrong)
+#endif
 #ifndef SCDE_WPCA_BLOCK
 #define SCDE_WPCA_BLOCK 512  // wpca.hip workgroup size (8 waves)
 #endif

@@ -1246,58 +1246,139 @@ __device__ __forceinline__ void slide_group(const double* __restrict__ A, const 
   }
 }
 
+// Both sides of the slide in one form: X(d) = sum_t P[t] Q[t + d], t ascending, for R
+// adjacent lags d = d0 .. d0+R-1 (s >= 0: P = B, Q = A, d = s; s < 0: P = A, Q = B,
+// d = -s), so every lane runs the same instruction stream whichever side its group is on.
+// Products are commutative and the terms are summed in the same t order as above:
+// bit-identical to slide_group.  Q is zero-padded by >= R past n.
+template <int R>
+__device__ __forceinline__ void slide_lags(const double* P, const double* Q0, const double* Q1, int n, int d0,
+                                           double (&c)[R]) {
+  // P is 16-B aligned and t steps by 4: P[t..t+3] is two aligned 16-B reads.  Q0 / Q1 hold
+  // the row at an even / odd double offset; the one matching the parity of d0 + R puts
+  // Q[t + d0 + R] on a 16-B boundary (ds_read_b128: 16 B per lane in 4 LDS cycles, where
+  // ds_read2_b64 takes 16).
+  const double* Q = ((d0 + R) & 1) ? Q1 : Q0;
+  double w[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    c[r] = 0.0;
+    w[r] = Q[d0 + r];
+  }
+  const int len = n - d0;
+  auto step = [&](double p, double qnew) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[r] = __dadd_rn(c[r], __dmul_rn(w[r], p));
+#pragma unroll
+    for (int r = 0; r + 1 < R; ++r) w[r] = w[r + 1];
+    w[R - 1] = qnew;
+  };
+  int t = 0;
+  for (; t + 4 <= len; t += 4) {
+    const double2 pa = *reinterpret_cast<const double2*>(P + t);
+    const double2 pb = *reinterpret_cast<const double2*>(P + t + 2);
+    const double2 qa = *reinterpret_cast<const double2*>(Q + t + d0 + R);
+    const double2 qb = *reinterpret_cast<const double2*>(Q + t + d0 + R + 2);
+    step(pa.x, qa.x);
+    step(pa.y, qa.y);
+    step(pb.x, qb.x);
+    step(pb.y, qb.y);
+  }
+  for (; t < len; ++t) step(P[t], Q[t + d0 + R]);
+}
+
 // ------------------------------------------------------------------ K3: ratio posterior + summary
 template <int R>
-__global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
-  extern __shared__ double sh[];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_RATIO_WPE))) void k_ratio_summary(RatioArgs a) {
+  // All LDS is in the dynamic region, every array at a 16-B aligned offset (a static
+  // __shared__ in front would shift the base, and misaligned 16-B reads replay):
+  //   A, B        the prior-weighted rows at even double offsets, zero-padded to NA >= n + 8
+  //               (the sliding windows read past the end; a padded term adds +0 to a
+  //               non-negative sum: bit-identical);
+  //   A1, B1      the same rows at odd offsets: one of Q / Q1 puts a lane's window on a
+  //               16-B boundary, so every slide read is a ds_read_b128;
+  //   X           the 2n-1 outputs + 48 doubles of per-wave scratch;
+  //   red, red2   8 doubles each; ired, ired2, ired3 8 ints each.
+  extern __shared__ __attribute__((aligned(16))) double sh[];
   const int n = a.n, m = 2 * a.n - 1;
-  // A, B: prior-weighted rows, zero-padded by 8 so the sliding windows below may read past
-  // the end (a padded term adds +0 to a non-negative sum: bit-identical).  X: the row of
-  // 2n-1 outputs, then 48 doubles of per-wave scratch.
+  const int NA = (n + 9) & ~1;
   double* A = sh;
-  double* B = sh + (n + 8);
-  double* X = sh + 2 * (n + 8);
-  __shared__ double red[8];
-  __shared__ double red2[8];
-  __shared__ int ired[8];
-  __shared__ int ired2[8];
-  __shared__ int ired3[8];
+  double* B = sh + NA;
+  double* A1 = sh + 2 * NA + 1;
+  double* B1 = sh + 3 * NA + 1;
+  double* X = sh + 4 * NA + 2;
+  double* red = X + ((m + 49) & ~1);
+  double* red2 = red + 8;
+  int* ired = reinterpret_cast<int*>(red2 + 8);
+  int* ired2 = ired + 8;
+  int* ired3 = ired + 16;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
+  // Output groups q (R adjacent lags each): s0 = R q - (n-1) >= 0 ("pos": P = B, Q = A),
+  // s0 + R - 1 < 0 ("neg": P = A, Q = B), else the one group straddling s = 0.  Each
+  // side's groups go to its own waves (the shared operand P[t] is then one address per
+  // wave, a broadcast), longest first, so a wave's lanes run similar lengths.
+  const int NQ = (m + R - 1) / R;
+  const int qpos0 = (n - 1 + R - 1) / R;           // first pos group
+  const int NPOS = NQ - qpos0;
+  const int NNEG = n > R ? (n - R - 1) / R + 1 : 0;  // groups q < qneg0 with R q + R - 1 < n - 1
+  const int NSTR = qpos0 - NNEG;                     // 0 or 1
   for (int g = blockIdx.x; g < a.ngenes; g += gridDim.x) {
-    for (int k = tid; k < n + 8 && !a.xin; k += blockDim.x) {
-      if (k >= n) {
-        A[k] = 0.0;
-        B[k] = 0.0;
-        continue;
+    for (int k = tid; k < NA && !a.xin; k += blockDim.x) {
+      double va = 0.0, vb = 0.0;
+      if (k < n) {
+        const double y = a.prior_y ? a.prior_y[k] : 1.0;
+        const double p1 = a.jp1[(long long)g * a.j1g + (long long)k * a.j1k];
+        const double p2 = a.jp2[(long long)g * a.j2g + (long long)k * a.j2k];
+        va = a.prior_y ? __dmul_rn(p1, y) : p1;
+        vb = a.prior_y ? __dmul_rn(p2, y) : p2;
       }
-      const double y = a.prior_y ? a.prior_y[k] : 1.0;
-      const double p1 = a.jp1[(long long)g * a.j1g + (long long)k * a.j1k];
-      const double p2 = a.jp2[(long long)g * a.j2g + (long long)k * a.j2k];
-      A[k] = a.prior_y ? __dmul_rn(p1, y) : p1;
-      B[k] = a.prior_y ? __dmul_rn(p2, y) : p2;
+      A[k] = va;
+      B[k] = vb;
+      A1[k] = va;
+      B1[k] = vb;
     }
     __syncthreads();
     // matSlideMult (src/matSlideMult.cpp:12-20): X[o] = sum_t A[t + max(s,0)] * B[t + max(-s,0)],
-    // s = o - (n-1), t ascending, each product and sum rounded separately.  Four adjacent
-    // outputs per thread share one sliding register window: per t one new A (s >= 0) or
-    // B (s < 0) value and one shared operand feed four independent sums.
+    // s = o - (n-1), t ascending, each product and sum rounded separately.
     dd ls = {0.0, 0.0};
     for (int o = tid; o < m && a.xin; o += blockDim.x) X[o] = a.xin[(long long)g * a.xg + (long long)o * a.xo];
-    // Output groups q (R adjacent outputs each) have tent-shaped lengths; pairing q with
-    // q + ceil(NQ/2) gives every task ~n iterations, so no lane waits on a longer one.
-    const int NQ = (m + R - 1) / R, halfq = (NQ + 1) / 2;
-    for (int task = tid; task < halfq && !a.xin; task += blockDim.x) {
-      for (int h = 0; h < 2; ++h) {
-        const int q = task + h * halfq;
-        if (q >= NQ) break;
-        const int o0 = R * q;
-        double c[R];
-        slide_group<R>(A, B, n, o0 - (n - 1), c);
+    if (!a.xin && !(SCDE_RATIO_DIAG & 1)) {
+      const int side = nw >= 2 ? (wid & 1) : 0;
+      const int wstep = nw >= 2 ? 64 * (nw >> 1) : 64;
+      for (int pass = 0; pass < (nw >= 2 ? 1 : 2); ++pass) {
+        const int sd = nw >= 2 ? side : pass;
+        const int cnt = sd == 0 ? NPOS : NNEG + NSTR;
+        for (int i = (nw >= 2 ? (wid >> 1) * 64 : 0) + lane; i < cnt; i += wstep) {
+          double c[R];
+          if (sd == 0) {  // pos, longest first: q = qpos0 + i, lags d = s0 .. s0 + R - 1
+            const int q = qpos0 + i, o0 = R * q, s0 = o0 - (n - 1);
+            slide_lags<R>(B, A, A1, n, s0, c);
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          if (o0 + r < m) {
-            X[o0 + r] = c[r];
-            ls = dd_add_d(ls, c[r]);
+            for (int r = 0; r < R; ++r) {
+              if (o0 + r < m) {
+                X[o0 + r] = c[r];
+                ls = dd_add_d(ls, c[r]);
+              }
+            }
+          } else if (i < NNEG) {  // neg, longest first: q = NNEG - 1 - i, lags -s0 - R + 1 ..
+            const int q = NNEG - 1 - i, o0 = R * q, s0 = o0 - (n - 1);
+            slide_lags<R>(A, B, B1, n, -s0 - R + 1, c);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              const int o = o0 + R - 1 - r;
+              X[o] = c[r];
+              ls = dd_add_d(ls, c[r]);
+            }
+          } else {  // the group straddling s = 0 (only when (n - 1) % R != 0)
+            const int q = NNEG, o0 = R * q;
+            slide_group<R>(A, B, n, o0 - (n - 1), c);
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+              if (o0 + r < m) {
+                X[o0 + r] = c[r];
+                ls = dd_add_d(ls, c[r]);
+              }
+            }
           }
         }
       }
@@ -1325,7 +1406,7 @@ __global__ __launch_bounds__(256) void k_ratio_summary(RatioArgs a) {
       if (a.ratio) a.ratio[(long long)g * a.rg + (long long)o * a.ro] = p;
     }
     __syncthreads();
-    if (!a.res) continue;
+    if (!a.res || (SCDE_RATIO_DIAG & 2)) continue;
     // ---- quick.distribution.summary: contiguous chunk per thread ----
     const int per = (m + blockDim.x - 1) / blockDim.x;
     const int c0 = tid * per, c1 = min(m, c0 + per);
@@ -1695,20 +1776,26 @@ hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int 
 
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
-  const size_t shm = sizeof(double) * (size_t)(2 * (a.n + 8) + (2 * a.n - 1) + 48);
+  const int NA = (a.n + 9) & ~1;
+  const size_t shm = sizeof(double) * (size_t)(4 * NA + 2 + ((2 * a.n - 1 + 49) & ~1) + 16) + sizeof(int) * 24;
+  // R = 4 by default: a 4-step unrolled loop rotates the R-wide register window fully (no
+  // moves); measured fastest of R = 4, 5, 8 at n = 401
   const int grid = a.ngenes < 65536 ? a.ngenes : 65536;
   static int rsel = -1, bsel = -1;
   if (rsel < 0) {  // tuning overrides
     const char* r = getenv("SCDE_RATIO_R");
     const char* b = getenv("SCDE_RATIO_BLOCK");
-    rsel = (r && atoi(r) == 8) ? 8 : 4;
+    rsel = r ? atoi(r) : 4;
+    if (rsel != 4 && rsel != 5 && rsel != 7 && rsel != 8) rsel = 4;
     bsel = b ? atoi(b) : 128;
     if (bsel != 64 && bsel != 128 && bsel != 256) bsel = 128;
   }
-  if (rsel == 8)
-    hipLaunchKernelGGL(k_ratio_summary<8>, dim3(grid), dim3(bsel), shm, s, a);
-  else
-    hipLaunchKernelGGL(k_ratio_summary<4>, dim3(grid), dim3(bsel), shm, s, a);
+  switch (rsel) {
+    case 7: hipLaunchKernelGGL(k_ratio_summary<7>, dim3(grid), dim3(bsel), shm, s, a); break;
+    case 8: hipLaunchKernelGGL(k_ratio_summary<8>, dim3(grid), dim3(bsel), shm, s, a); break;
+    case 5: hipLaunchKernelGGL(k_ratio_summary<5>, dim3(grid), dim3(bsel), shm, s, a); break;
+    default: hipLaunchKernelGGL(k_ratio_summary<4>, dim3(grid), dim3(bsel), shm, s, a); break;
+  }
   return hipGetLastError();
 }
 
