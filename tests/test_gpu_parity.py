@@ -139,7 +139,9 @@ def test_logboot_degenerate_exact(api, oracle):
 
 def test_matSlideMult_bit_exact(api, oracle):
     rng = np.random.default_rng(11)
-    for nr, n in ((17, 401), (5, 801), (3, 1), (1, 2), (64, 33)):
+    # n - 1 not a multiple of the slide's 4-lag groups (10, 403, 7, 3, 2) exercises the group
+    # that straddles lag 0; n = 3 has no group entirely on the negative side
+    for nr, n in ((17, 401), (5, 801), (3, 1), (1, 2), (64, 33), (9, 10), (6, 403), (4, 7), (5, 3)):
         a = np.asfortranarray(rng.random((nr, n)))
         b = np.asfortranarray(rng.random((nr, n)) ** 3)
         np.testing.assert_array_equal(api.matSlideMult(a, b), oracle.matSlideMult(a, b))
@@ -423,7 +425,7 @@ def test_posteriors_modes_config4_shape(api, oracle):
     np.testing.assert_array_equal(got["modes"], ref["modes"])
 
 
-@pytest.mark.parametrize("length_out", [60, 700, 1200])
+@pytest.mark.parametrize("length_out", [60, 402, 700, 1200])
 def test_expression_difference_grid_sizes(api, oracle, length_out):
     """Grids other than 401 points: G = 61 (one wave), 701 (11-wave blocks, column stride
     768), 1201 (> 1024 lanes: the k_boot fallback), with wider tables and ratio rows."""
