@@ -264,31 +264,35 @@ __global__ __launch_bounds__(256) void k_delta(const double* __restrict__ T, con
   }
 }
 
-// Z[set][b][k] = sum over baseline cells of W[set][c][b] * T[base_col[c]][k]
-__global__ __launch_bounds__(512) void k_baseline_z(const double* __restrict__ T, int G, int GS,
+// Z[set][b][k] = sum over baseline cells of W[set][c][b] * T[base_col[c]][k].
+// One workgroup per (4 boots, 64-point tile of k, set): wave w takes the cells c = w
+// (mod 4), each lane one k with the 4 boots' partial sums (each baseline column read once
+// per 4 boots); the 4 waves' partials combine in a fixed order.  Bp is a multiple of 4.
+__global__ __launch_bounds__(256) void k_baseline_z(const double* __restrict__ T, int G, int GS,
                                                     const int* __restrict__ base_col, int ncells,
                                                     const double* __restrict__ Wt, int Bp,
                                                     double* __restrict__ Z) {
-  // four interleaved partial sums (cells c = 4i + r) keep four FMA chains in flight
-  const int b = blockIdx.x, set = blockIdx.y;
-  const double* W = Wt + (long long)set * ncells * Bp;
-  for (int k = threadIdx.x; k < GS; k += blockDim.x) {
-    double z[4] = {0.0, 0.0, 0.0, 0.0};
-    if (k < G) {
-      for (int c0 = 0; c0 < ncells; c0 += 4) {
+  __shared__ double part[4][4][64];  // [wave][boot][lane]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int b0 = blockIdx.x * 4, k = blockIdx.y * 64 + lane, set = blockIdx.z;
+  const double* W = Wt + (long long)set * ncells * Bp + b0;
+  double z[4] = {0.0, 0.0, 0.0, 0.0};
+  if (k < G) {
+    for (int c = wid; c < ncells; c += 4) {
+      const int bc = base_col[c];
+      if (bc < 0) continue;
+      const double t = T[(long long)bc * GS + k];
+      const double* w = W + (long long)c * Bp;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = c0 + r;
-          if (c >= ncells) break;
-          const int bc = base_col[c];
-          if (bc < 0) continue;
-          const double w = W[(long long)c * Bp + b];
-          if (w != 0.0) z[r] = fma(w, T[(long long)bc * GS + k], z[r]);
-        }
-      }
+      for (int r = 0; r < 4; ++r) z[r] = fma(w[r], t, z[r]);
     }
-    Z[((long long)set * Bp + b) * GS + k] = (z[0] + z[1]) + (z[2] + z[3]);
   }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) part[wid][r][lane] = z[r];
+  __syncthreads();
+  if (k < GS)
+    Z[((long long)set * Bp + b0 + wid) * GS + k] =
+        ((part[0][wid][lane] + part[1][wid][lane]) + part[2][wid][lane]) + part[3][wid][lane];
 }
 
 // ------------------------------------------------------------------ K2: bootstrap
@@ -1594,7 +1598,8 @@ hipError_t launch_delta(const double* T, const long long* ucl_off, int ncells, l
 
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
                              int Bp, int nsets, double* Z, hipStream_t s) {
-  hipLaunchKernelGGL(k_baseline_z, dim3(Bp, nsets), dim3(512), 0, s, T, G, GS, base_col, ncells, Wt, Bp, Z);
+  hipLaunchKernelGGL(k_baseline_z, dim3(Bp / 4, (GS + 63) / 64, nsets), dim3(256), 0, s, T, G, GS, base_col, ncells, Wt,
+                     Bp, Z);
   return hipGetLastError();
 }
 
