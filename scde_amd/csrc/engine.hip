@@ -164,7 +164,7 @@ struct scde_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   // workspace
-  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, T, E, maxi, has_clamp, base_col, ent, nnz, Wt, Z, draws,
+  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
       degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
   // scde.expression.prior
   Buf pr_cell, pr_part, pr_occ, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
@@ -235,7 +235,7 @@ struct scde_ctx {
   }
   ~scde_ctx() {
     Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &T,      &E,      &maxi,
-                  &has_clamp, &base_col, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
+                  &has_clamp, &base_col, &zcol, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
                   &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw};
     for (Buf* b : all) b->release();
     Buf* wp[] = {&wp_probs, &wp_blocks,  &wp_kidx, &wp_cols,   &wp_perms, &wp_starts, &wp_scratch,
@@ -470,7 +470,15 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   u.ready = false;  // consumed by this call
   const long long ncols = ucl_off_h[C];
   // ---- K1 tables
-  HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
+  // Bootstrap path with G <= 1024 (k_boot2): the tables kernel writes the baseline-delta
+  // columns D directly (phase 1: count-0 columns and base_col, phase 2: the rest); T itself
+  // is kept only when individual posteriors are returned.
+  const bool boot_path = s.nboot > 0 && (s.batch_call || !s.ensemble);
+  const bool fast = ((G + 63) / 64) * 64 <= 1024;
+  const bool fused = boot_path && fast;
+  const bool want_post = s.batch_call ? (s.postflag == 2) : (s.postflag == 2 || s.postflag == 3);
+  const bool keep_T = !fused || (want_post && s.post);
+  if (keep_T) HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
   HCHK(cx->maxi.ensure(sizeof(int) * std::max<long long>(1, ncols)));
   HCHK(cx->has_clamp.ensure(std::max<long long>(1, ncols)));
   const bool want_maxi = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
@@ -487,12 +495,28 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   ta.theta = cx->theta.as<double>();
   ta.cellscal = cx->cellscal.as<double>();
   ta.minlogprob = -1 * DBL_MAX / C / 1.1;
-  ta.T = cx->T.as<double>();
+  ta.T = keep_T ? cx->T.as<double>() : nullptr;
   ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
   ta.has_clamp = cx->has_clamp.as<unsigned char>();
   ta.const_theta = s.localtheta ? 0 : 1;
+  ta.use_baseline = s.use_baseline ? 1 : 0;
+  if (fused) {
+    HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
+    HCHK(cx->base_col.ensure(sizeof(int) * std::max(1, C)));
+    HCHK(cx->zcol.ensure(sizeof(int) * std::max(1, C)));
+    ta.D = cx->E.as<double>();
+    ta.zcol = cx->zcol.as<int>();
+    ta.base_col = cx->base_col.as<int>();
+  }
   ev = cx->mark_begin(SLOT_TABLES);
-  HCHK(launch_tables(ta, st));
+  if (fused) {
+    ta.phase = 1;
+    HCHK(launch_tables(ta, st));
+    ta.phase = 2;
+    HCHK(launch_tables(ta, st));
+  } else {
+    HCHK(launch_tables(ta, st));
+  }
   cx->mark_end(SLOT_TABLES, ev);
   // ---- joint posterior
   if (!s.batch_call && s.ensemble) {
@@ -509,7 +533,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     // logBootBatchPosterior with Nboot = 0 returns zeros (src/jpmatLogBoot.cpp:469-497)
     HCHK(hipMemsetAsync(s.jp, 0, sizeof(double) * (size_t)N * G, st));
   } else {
-    const bool fast = ((G + 63) / 64) * 64 <= 1024;
     int nb = fast ? boot2_nb(s.nboot) : 16;
     if (fast) {
       if (const char* ev_nb = getenv("SCDE_BOOT_NB")) {  // tuning override: a multiple of 4 in [4, 32]
@@ -525,20 +548,26 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     make_draws(s, Bp, draws, W, ndraw);
     RCHK(upload(cx, cx->Wt, W.data(), sizeof(double) * W.size()));
     RCHK(upload(cx, cx->draws, draws.data(), sizeof(int) * draws.size()));
-    HCHK(cx->base_col.ensure(sizeof(int) * C));
-    HCHK(launch_base_cols(u.ucl.as<int>(), u.ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
-                          s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
+    if (!fused) {
+      HCHK(cx->base_col.ensure(sizeof(int) * C));
+      HCHK(launch_base_cols(u.ucl.as<int>(), u.ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
+                            s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
+    }
     const int stride = (int)round_up(C, 8) + 8;  // + one look-ahead batch (k_boot2)
     HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * stride)));
     HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
     ev = cx->mark_begin(SLOT_OTHER);
-    HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
-    HCHK(launch_delta(cx->T.as<double>(), u.ucl_off.as<long long>(), C, ncols, cx->base_col.as<int>(), G, GS,
-                      cx->E.as<double>(), st));
+    if (!fused) {
+      HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
+      HCHK(launch_delta(cx->T.as<double>(), u.ucl_off.as<long long>(), C, ncols, cx->base_col.as<int>(), G, GS,
+                        cx->E.as<double>(), st));
+    }
+    // the baseline columns: T (slow path) or the fused D buffer, which holds T there
+    const double* Tbase = fused ? cx->E.as<double>() : cx->T.as<double>();
     HCHK(launch_ell(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->base_col.as<int>(), stride,
                     (int)ncols, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
-    HCHK(launch_baseline_z(cx->T.as<double>(), G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
+    HCHK(launch_baseline_z(Tbase, G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
                            cx->Z.as<double>(), st));
     cx->mark_end(SLOT_OTHER, ev);
     if (nsets > 1) {
@@ -605,7 +634,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     }
     cx->mark_end(SLOT_BOOT, ev);
     ExactArgs xa{};
-    xa.T = cx->T.as<double>();
+    xa.T = Tbase;
+    xa.base_col = fused ? cx->base_col.as<int>() : nullptr;
     xa.G = G;
     xa.GS = GS;
     xa.draws = cx->draws.as<int>();
@@ -625,7 +655,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   }
   // ---- individual outputs (src/jpmatLogBoot.cpp:277-328)
   const bool want_modes = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
-  const bool want_post = s.batch_call ? (s.postflag == 2) : (s.postflag == 2 || s.postflag == 3);
   if (want_modes && s.modes)
     HCHK(launch_modes(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->maxi.as<int>(),
                       cx->mag.as<double>(), s.modes, 1, N, st));

@@ -39,6 +39,17 @@ struct TablesArgs {
   int* maxi;                 // [ncols] argmax (nullable)
   unsigned char* has_clamp;  // [ncols]
   int const_theta;           // theta is the same at every grid point (no local theta fit)
+  // Fused baseline-delta output (bootstrap path; the k_delta pass folded into the tables):
+  //   phase 0: every column -> T (no D);
+  //   phase 1: one wave per cell, its count-0 column -> D (and T if non-null); writes
+  //            zcol[c] and base_col[c] (count-0 column when it has no clamp and use_baseline);
+  //   phase 2: every other column -> D = T - T[base_col] (T itself where the cell has no
+  //            baseline), pad lanes [G, GS) zeroed, column ncols all zero; T if non-null.
+  int phase;
+  int use_baseline;
+  double* D;      // [ncols + 1][GS]
+  int* zcol;      // [ncells] count-0 column or -1
+  int* base_col;  // [ncells]
 };
 
 struct BootArgs {
@@ -81,7 +92,8 @@ struct Boot2Args {
 };
 
 struct ExactArgs {
-  const double* T;
+  const double* T;  // log tables; or fused D columns when base_col is set (T = D + D[base])
+  const int* base_col;
   int G, GS;
   const int* draws;  // [nsets][nboot][ndraw] cell index per draw, reference order
   int ndraw, nboot;

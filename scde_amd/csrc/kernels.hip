@@ -100,7 +100,6 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   __shared__ double etab[64];
   __shared__ double ltab[3][97];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const long long col = (long long)blockIdx.x * 4 + wid;
   if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
   if (threadIdx.x < 97) {
     ltab[0][threadIdx.x] = kLogInvC[threadIdx.x];
@@ -109,13 +108,44 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   }
   __syncthreads();
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
-  if (col >= a.ncols) return;
-  int lo = 0, hi = a.ncells;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (a.ucl_off[mid] <= col) lo = mid; else hi = mid;
+  const int phase = a.phase;
+  long long col;
+  int c;
+  if (phase == 1) {
+    // one wave per cell: its count-0 column (unique within the cell), first match
+    c = blockIdx.x * 4 + wid;
+    if (c >= a.ncells) return;
+    const long long o1 = a.ucl_off[c + 1];
+    long long zc = -1;
+    for (long long i0 = a.ucl_off[c]; i0 < o1; i0 += 64) {
+      const long long i = i0 + lane;
+      const unsigned long long m = __ballot(i < o1 && a.ucl[i] == 0);
+      if (m) {
+        zc = i0 + __ffsll((long long)m) - 1;
+        break;
+      }
+    }
+    if (lane == 0) a.zcol[c] = (int)zc;
+    if (zc < 0) {
+      if (lane == 0) a.base_col[c] = -1;
+      return;
+    }
+    col = zc;
+  } else {
+    col = (long long)blockIdx.x * 4 + wid;
+    if (phase == 2 && col == a.ncols) {  // the ELL pad column
+      for (int k = lane; k < a.GS; k += 64) a.D[col * a.GS + k] = 0.0;
+      return;
+    }
+    if (col >= a.ncols) return;
+    int lo = 0, hi = a.ncells;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (a.ucl_off[mid] <= col) lo = mid; else hi = mid;
+    }
+    c = lo;
+    if (phase == 2 && col == a.zcol[c]) return;  // done in phase 1
   }
-  const int c = lo;
   const int G = a.G;
   const double x = (double)a.ucl[col];
   const double* mu = a.mu + (long long)c * a.GS;
@@ -156,7 +186,11 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   double bv = -INFINITY;
   int bi = 0x7fffffff;
   bool clamp = false;
-  double* out = a.T + col * a.GS;
+  double* out = a.T ? a.T + col * a.GS : nullptr;
+  // fused delta (phase 2): D = T - T[baseline column of the cell], as k_delta computes it
+  double* dout = phase ? a.D + col * a.GS : nullptr;
+  const int bc = (phase == 2) ? a.base_col[c] : -1;
+  const double* base = (bc >= 0) ? a.D + (long long)bc * a.GS : nullptr;
 #pragma unroll 1
   for (int k = lane; k < G; k += 64) {
     double r = log_tab(v[k] / s, lt);
@@ -168,8 +202,11 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
       r = a.minlogprob;
       clamp = true;
     }
-    out[k] = r;
+    if (out) out[k] = r;
+    if (dout) dout[k] = base ? r - base[k] : r;
   }
+  if (dout)
+    for (int k = G + lane; k < a.GS; k += 64) dout[k] = 0.0;
   if (a.maxi) {
     // first maximum over the grid (Armadillo max(index), strict '>')
 #pragma unroll
@@ -185,6 +222,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   }
   const unsigned long long anyc = __ballot(clamp);
   if (lane == 0) a.has_clamp[col] = anyc ? 1 : 0;
+  if (phase == 1 && lane == 0) a.base_col[c] = (a.use_baseline && !anyc) ? (int)col : -1;
 }
 
 // ------------------------------------------------------------------ baseline / ELL
@@ -938,9 +976,15 @@ __global__ __launch_bounds__(1024) void k_boot_exact(ExactArgs a) {
         col = a.ucl_off[cell] + a.uci[(long long)g + a.ld_uci * cell];
       else
         col = (long long)cell * a.ngenes + g;  // jpmat layout: matrix-major rows
+      // fused tables: T = D + D[baseline column] (<= 1 ulp of T; clamped values exact)
+      const int bc = a.base_col ? a.base_col[cell] : -1;
+      const double* base = (bc >= 0 && bc != col) ? a.T + (long long)bc * a.GS : nullptr;
       for (int j = 0; j < KPT; ++j) {
         const int k = tid + j * blockDim.x;
-        if (k < a.G) t[j] = __dadd_rn(t[j], a.T[col * a.GS + k]);
+        if (k < a.G) {
+          const double tv = base ? __dadd_rn(a.T[col * a.GS + k], base[k]) : a.T[col * a.GS + k];
+          t[j] = __dadd_rn(t[j], tv);
+        }
       }
     }
     double m = -INFINITY;
@@ -1562,8 +1606,11 @@ hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, con
 }
 
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
-  if (a.ncols <= 0) return hipSuccess;
-  const dim3 grid(div_up(a.ncols, 4)), block(256);
+  if (a.ncols <= 0 && a.phase != 2) return hipSuccess;
+  if (a.phase != 0 && (!a.D || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
+  const long long nwaves = a.phase == 1 ? a.ncells : a.phase == 2 ? a.ncols + 1 : a.ncols;
+  if (nwaves <= 0) return hipSuccess;
+  const dim3 grid(div_up(nwaves, 4)), block(256);
   const size_t shm = sizeof(double) * 4 * (size_t)a.GS;
   if (shm > 64 * 1024) return hipErrorInvalidValue;
   if (a.const_theta)
