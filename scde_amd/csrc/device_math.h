@@ -426,6 +426,79 @@ __device__ inline double dnbinom_log_ct(const NbConst& c, double x_in, double si
   return c.lp + ans;
 }
 
+// ---- fast constant-theta dnbinom (k_tables hot loop) ----
+// For a constant size theta, p_k = theta / (theta + mu_k), q_k = 1 - p_k and their logs
+// depend only on (cell, grid point) and are precomputed once per cell (k_cell_prep).  bd0's
+// non-series branch x log(x / np) + np - x is then evaluated as x (log x - log n - log p_k)
+// + np - x: no division and no log per grid point (the log of the ratio is exact to a few
+// ulps of its terms; outside the series region |log(x/np)| > 0.18, so the relative error
+// stays ~1e-15).  The series branch divides by the constant 2j+1 through a reciprocal
+// table.  Every case the reference routes elsewhere (p or q == 0, np or nq not a positive
+// finite number, x == 0 && size == 0, non-finite inputs) returns `false` and the caller
+// takes the exact dnbinom_log_ct path for that lane.
+__device__ __constant__ const double kInvOdd[40] = {
+    1.0,       1.0 / 3,  1.0 / 5,  1.0 / 7,  1.0 / 9,  1.0 / 11, 1.0 / 13, 1.0 / 15, 1.0 / 17, 1.0 / 19,
+    1.0 / 21,  1.0 / 23, 1.0 / 25, 1.0 / 27, 1.0 / 29, 1.0 / 31, 1.0 / 33, 1.0 / 35, 1.0 / 37, 1.0 / 39,
+    1.0 / 41,  1.0 / 43, 1.0 / 45, 1.0 / 47, 1.0 / 49, 1.0 / 51, 1.0 / 53, 1.0 / 55, 1.0 / 57, 1.0 / 59,
+    1.0 / 61,  1.0 / 63, 1.0 / 65, 1.0 / 67, 1.0 / 69, 1.0 / 71, 1.0 / 73, 1.0 / 75, 1.0 / 77, 1.0 / 79};
+
+// bd0 series (|x - np| < 0.1 (x + np)): |v| < 0.1, so v^2 < 0.01 and the terms fall by
+// 100x per step; 39 steps reach any double.
+__device__ __noinline__ double bd0_series_fast(double x, double np) {
+  double v = (x - np) / (x + np);
+  double s = (x - np) * v;
+  if (fabs(s) < DBL_MIN) return s;
+  double ej = 2 * x * v;
+  v = v * v;
+  for (int j = 1; j < 40; j++) {
+    ej *= v;
+    const double s1 = s + ej * kInvOdd[j];
+    if (s1 == s) return s1;
+    s = s1;
+  }
+  return s;
+}
+
+// L = log x - log np (precomputed as log x - log n - log p)
+__device__ __forceinline__ double bd0_fast(double x, double np, double L) {
+  if (fabs(x - np) < 0.1 * (x + np)) return bd0_series_fast(x, np);
+  return x * L + np - x;
+}
+
+struct NbFast {
+  double X, n, nx, S, hlf, lp;  // dbinom_raw's x (= size), n, n - x; stirlerr sum; 0.5 lf; log(size/(size+x))
+  double lXn, lnxn;             // log X - log n, log(n - X) - log n
+  bool ok;                      // the fast path applies to this column
+};
+
+__device__ __forceinline__ NbFast nb_fast(const NbConst& c) {
+  NbFast f;
+  f.X = c.size;
+  f.n = c.n;
+  f.nx = c.nx;
+  f.S = c.S;
+  f.hlf = 0.5 * c.lf;
+  f.lp = c.lp;
+  f.ok = !c.trivial && c.size > 0 && isfinite(c.size) && c.n > 0 && isfinite(c.n);
+  f.lXn = f.ok ? log(c.size) - log(c.n) : 0.0;
+  f.lnxn = (f.ok && c.nx > 0) ? log(c.nx) - log(c.n) : 0.0;
+  return f;
+}
+
+// returns false when the lane must take the exact path
+__device__ __forceinline__ bool dnbinom_fast(const NbFast& f, double p, double q, double lp, double lq, double& out) {
+  if (!(p > 0.0 && p <= 1.0 && q > 0.0)) return false;
+  const double np = f.n * p, nq = f.n * q;
+  if (!(np > 0.0 && np < INFINITY && nq > 0.0 && nq < INFINITY)) return false;
+  double ans;
+  if (f.X == f.n)  // count 0: dbinom_raw's x == n branch
+    ans = (q < 0.1) ? -bd0_fast(f.n, np, -lp) - f.n * q : f.n * lp;
+  else
+    ans = ((f.S - bd0_fast(f.X, np, f.lXn - lp)) - bd0_fast(f.nx, nq, f.lnxn - lq)) - f.hlf;
+  out = f.lp + ans;
+  return true;
+}
+
 // ---- double-double accumulation (emulates R's LDOUBLE rowSums / cumsum) ----
 struct dd {
   double hi, lo;

@@ -164,7 +164,7 @@ struct scde_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   // workspace
-  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
+  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, pq, colc, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
       degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
   // scde.expression.prior
   Buf pr_cell, pr_part, pr_occ, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
@@ -234,7 +234,7 @@ struct scde_ctx {
     return SCDE_OK;
   }
   ~scde_ctx() {
-    Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &T,      &E,      &maxi,
+    Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &pq, &colc, &T,      &E,      &maxi,
                   &has_clamp, &base_col, &zcol, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
                   &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw};
     for (Buf* b : all) b->release();
@@ -441,9 +441,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   HCHK(cx->theta.ensure(cg));
   HCHK(cx->cellscal.ensure(sizeof(double) * 2 * C));
   hipEvent_t ev = cx->mark_begin(SLOT_OTHER);
+  if (!s.localtheta) HCHK(cx->pq.ensure(4 * cg));
   HCHK(launch_cell_prep(cx->models.as<double>(), C, G, GS, cx->mag.as<double>(), s.localtheta, s.squarelogit,
                         cx->mu.as<double>(), cx->lcfp.as<double>(), cx->lcfpr.as<double>(), cx->theta.as<double>(),
-                        cx->cellscal.as<double>(), st));
+                        cx->cellscal.as<double>(), s.localtheta ? nullptr : cx->pq.as<double>(), st));
   cx->mark_end(SLOT_OTHER, ev);
   // ---- unique counts (prebuilt by build_unique_sets when u.ready)
   std::vector<long long>& ucl_off_h = u.ucl_off_h;
@@ -499,6 +500,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
   ta.has_clamp = cx->has_clamp.as<unsigned char>();
   ta.const_theta = s.localtheta ? 0 : 1;
+  ta.pq = s.localtheta ? nullptr : cx->pq.as<double>();
   ta.use_baseline = s.use_baseline ? 1 : 0;
   if (fused) {
     HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
@@ -509,6 +511,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     ta.base_col = cx->base_col.as<int>();
   }
   ev = cx->mark_begin(SLOT_TABLES);
+  if (!s.localtheta && ncols > 0) {
+    HCHK(cx->colc.ensure(sizeof(double) * 8 * (size_t)ncols));
+    HCHK(launch_col_consts(u.ucl.as<int>(), u.ucl_off.as<long long>(), ncols, C, cx->theta.as<double>(), GS,
+                           cx->cellscal.as<double>(), cx->colc.as<double>(), st));
+    ta.colc = cx->colc.as<double>();
+  }
   if (fused) {
     ta.phase = 1;
     HCHK(launch_tables(ta, st));

@@ -39,6 +39,8 @@ struct TablesArgs {
   int* maxi;                 // [ncols] argmax (nullable)
   unsigned char* has_clamp;  // [ncols]
   int const_theta;           // theta is the same at every grid point (no local theta fit)
+  const double* pq;          // [ncells][4][GS] p, q, log p, log q (const_theta), nullable
+  const double* colc;        // [ncols][8] k_col_consts output (with pq), nullable
   // Fused baseline-delta output (bootstrap path; the k_delta pass folded into the tables):
   //   phase 0: every column -> T (no D);
   //   phase 1: one wave per cell, its count-0 column -> D (and T if non-null); writes
@@ -140,7 +142,9 @@ struct RatioArgs {
 
 hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,
                             double* mu, double* lcfp, double* lcfpr, double* theta, double* cellscal,
-                            hipStream_t s);
+                            double* pq, hipStream_t s);
+hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long ncols, int ncells,
+                             const double* theta, int GS, const double* cellscal, double* colc, hipStream_t s);
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s);
 hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells, const unsigned char* has_clamp,
                             int use_baseline, int* base_col, hipStream_t s);

@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
                                                    const double* __restrict__ mag, int localtheta,
                                                    int squarelogit, double* __restrict__ mu,
                                                    double* __restrict__ lcfp, double* __restrict__ lcfpr,
-                                                   double* __restrict__ theta, double* __restrict__ cellscal) {
+                                                   double* __restrict__ theta, double* __restrict__ cellscal,
+                                                   double* __restrict__ pq) {
   const int c = blockIdx.x;
   auto M = [&](int col) { return models[(long long)c + (long long)ncells * col]; };
   const double concb = M(0), conca = M(1), failr = M(2), corrb = M(3), corra = M(4), corrt = M(5);
@@ -53,7 +54,8 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
   double lmax = -INFINITY;
   for (int k = threadIdx.x; k < G; k += blockDim.x) {
     const double m = mag[k];
-    mu[(long long)c * GS + k] = exp(m * corra + corrb);
+    const double muk = exp(m * corra + corrb);
+    mu[(long long)c * GS + k] = muk;
     double cf = squarelogit ? (conca + m * conca2) * m : m * conca;
     cf += concb;
     cf = 1.0 / (exp(cf) + 1.0);
@@ -75,6 +77,14 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
       th = t;
     }
     theta[(long long)c * GS + k] = th;
+    if (pq) {  // constant theta: the k_tables fast path's per-point terms (prob as k_tables forms it)
+      const double pr = th / (th + muk), qr = 1 - pr;
+      double* o = pq + (long long)c * 4 * GS + k;
+      o[0] = pr;
+      o[GS] = qr;
+      o[2 * GS] = log(pr);
+      o[3 * GS] = log(qr);
+    }
   }
   __shared__ double red[16];
   lmax = wave_max(lmax);
@@ -94,6 +104,38 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
 // one dnbinom body per kernel instead of one per unrolled point (the unrolled form was
 // ~12k instructions with lgamma inlined 8x).  CT: theta is the same at every grid point,
 // and the (theta, count)-only terms of dnbinom are computed once per column.
+// Per-column constants of the constant-theta fast path, one lane per column (k_tables
+// would otherwise evaluate them redundantly in all 64 lanes of the column's wave):
+// [n or -1, n - x, stirlerr sum, 0.5 lf, log(size/(size+x)), log X - log n,
+//  log(n - X) - log n, dpois_log(x, failure rate)].
+__global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl, const long long* __restrict__ ucl_off,
+                                                    long long ncols, int ncells, const double* __restrict__ theta,
+                                                    int GS, const double* __restrict__ cellscal,
+                                                    double* __restrict__ colc) {
+  const long long col = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (col >= ncols) return;
+  int lo = 0, hi = ncells;
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (ucl_off[mid] <= col) lo = mid; else hi = mid;
+  }
+  const double x = (double)ucl[col];
+  const NbConst nc = nb_const(x, theta[(long long)lo * GS]);
+  const NbFast f = nb_fast(nc);
+  double* o = colc + col * 8;
+  o[0] = f.ok ? f.n : -1.0;
+  o[1] = f.nx;
+  o[2] = f.S;
+  o[3] = f.hlf;
+  o[4] = f.lp;
+  o[5] = f.lXn;
+  o[6] = f.lnxn;
+  o[7] = dpois_log(x, cellscal[2 * lo + 1]);
+}
+
+#ifndef SCDE_KT_DIAG
+#define SCDE_KT_DIAG 0  // timing-only builds: 1 trivial dnbinom, 2 no exp, 4 no log, 8 no stores
+#endif
 template <bool CT>
 __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   extern __shared__ double vrow[];  // [4 waves][GS]
@@ -153,21 +195,69 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const double* lcfpr = a.lcfpr + (long long)c * a.GS;
   const double* th = a.theta + (long long)c * a.GS;
   const double maxcfp = a.cellscal[2 * c];
-  const double fp = dpois_log_cold(x, a.cellscal[2 * c + 1]);
-  const NbConst nc = CT ? nb_const(x, th[0]) : NbConst{};
+  double fp;
+  NbFast nf;
+  nf.ok = false;
+  if (CT && a.pq && a.colc) {
+    // per-column constants from k_col_consts (wave-uniform scalar loads)
+    const double* cc = a.colc + col * 8;
+    nf.n = cc[0];
+    nf.nx = cc[1];
+    nf.S = cc[2];
+    nf.hlf = cc[3];
+    nf.lp = cc[4];
+    nf.lXn = cc[5];
+    nf.lnxn = cc[6];
+    fp = cc[7];
+    nf.X = th[0];
+    nf.ok = nf.n > 0.0;  // k_col_consts stores n = -1 where the fast path does not apply
+  } else {
+    fp = dpois_log_cold(x, a.cellscal[2 * c + 1]);
+  }
   double* v = vrow + (long long)wid * a.GS;
   double lmax = -INFINITY;
+  if (CT && nf.ok) {
+    // fast path: per-point p, q, log p, log q from k_cell_prep; the lane whose mu is
+    // overridden by the count (R: x between mu[k] and mu[k+1]) forms its own; edge cases
+    // (p or q == 0, np or nq not finite and positive) take the reference dnbinom
+    const double* P = a.pq + (long long)c * 4 * a.GS;
 #pragma unroll 1
-  for (int k = lane; k < G; k += 64) {
-    double muv = mu[k];
-    const bool last = (k == G - 1);
-    const double mnext = last ? 0.0 : mu[k + 1];
-    if ((!last && x > muv && x < mnext) || (last && x > muv)) muv = x;
-    const double t = th[k];
-    double nb = CT ? dnbinom_log_ct(nc, x, t, t / (t + muv), lt) : dnbinom_log(x, t, t / (t + muv));
-    nb += lcfpr[k];
-    v[k] = nb;
-    lmax = gt_max(lmax, nb);
+    for (int k = lane; k < G; k += 64) {
+      const double muv = mu[k];
+      const bool last = (k == G - 1);
+      const double mnext = last ? 0.0 : mu[k + 1];
+      const bool over = (!last && x > muv && x < mnext) || (last && x > muv);
+      double pr = P[k], qr = P[a.GS + k], lpr = P[2 * a.GS + k], lqr = P[3 * a.GS + k];
+      if (over) {
+        const double t = th[k];
+        pr = t / (t + x);
+        qr = 1 - pr;
+        lpr = log_tab(pr, lt);
+        lqr = log_tab(qr, lt);
+      }
+      double nb;
+      if (SCDE_KT_DIAG & 1)  // timing diagnostic: trivial dnbinom
+        nb = lpr * x + lqr;
+      else if (!dnbinom_fast(nf, pr, qr, lpr, lqr, nb))
+        nb = dnbinom_log_cold(x, th[k], pr);  // out of line: the reference dnbinom as written
+      nb += lcfpr[k];
+      v[k] = nb;
+      lmax = gt_max(lmax, nb);
+    }
+  } else {
+    const NbConst nc = CT ? nb_const(x, th[0]) : NbConst{};
+#pragma unroll 1
+    for (int k = lane; k < G; k += 64) {
+      double muv = mu[k];
+      const bool last = (k == G - 1);
+      const double mnext = last ? 0.0 : mu[k + 1];
+      if ((!last && x > muv && x < mnext) || (last && x > muv)) muv = x;
+      const double t = th[k];
+      double nb = CT ? dnbinom_log_ct(nc, x, t, t / (t + muv), lt) : dnbinom_log(x, t, t / (t + muv));
+      nb += lcfpr[k];
+      v[k] = nb;
+      lmax = gt_max(lmax, nb);
+    }
   }
   double maxp = lmax;
 #pragma unroll
@@ -178,11 +268,13 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   for (int k = lane; k < G; k += 64) {
     // both arguments are <= 0 (maxp bounds them); exp_tab below -746 would underflow anyway
     const double d1 = v[k] - maxp, d2 = lcfp[k] + fp - maxp;
-    const double e = (d1 >= -746.0 ? exp_tab(d1, etab) : 0.0) + (d2 >= -746.0 ? exp_tab(d2, etab) : 0.0);
+    const double e = (SCDE_KT_DIAG & 2) ? (d1 + d2) * 1e-3 + 1.0
+                                        : (d1 >= -746.0 ? exp_tab(d1, etab) : 0.0) + (d2 >= -746.0 ? exp_tab(d2, etab) : 0.0);
     v[k] = e;
     ls += e;
   }
   const double s = wave_sum(ls);
+  const double lsum = log_tab(s, lt);  // s >= 1 (the maximum term is exp(0))
   double bv = -INFINITY;
   int bi = 0x7fffffff;
   bool clamp = false;
@@ -193,7 +285,10 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const double* base = (bc >= 0) ? a.D + (long long)bc * a.GS : nullptr;
 #pragma unroll 1
   for (int k = lane; k < G; k += 64) {
-    double r = log_tab(v[k] / s, lt);
+    // log(e / s) as log e - log s (no division); e / s could round differently only
+    // below DBL_MIN * s, where the reference's quotient is evaluated as written
+    const double e = v[k];
+    double r = (SCDE_KT_DIAG & 4) ? e - lsum : (e >= 0x1p-960) ? log_tab(e, lt) - lsum : log_tab(e / s, lt);
     if (r > bv) {
       bv = r;
       bi = k;
@@ -202,8 +297,12 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
       r = a.minlogprob;
       clamp = true;
     }
-    if (out) out[k] = r;
-    if (dout) dout[k] = base ? r - base[k] : r;
+    if (SCDE_KT_DIAG & 8) {
+      if (r == 12345.0) dout[k] = r;
+    } else {
+      if (out) out[k] = r;
+      if (dout) dout[k] = base ? r - base[k] : r;
+    }
   }
   if (dout)
     for (int k = G + lane; k < a.GS; k += 64) dout[k] = 0.0;
@@ -1598,10 +1697,18 @@ static inline int div_up(long long a, long long b) { return (int)((a + b - 1) / 
 
 hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,
                             double* mu, double* lcfp, double* lcfpr, double* theta, double* cellscal,
-                            hipStream_t s) {
+                            double* pq, hipStream_t s) {
   if (ncells <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_cell_prep, dim3(ncells), dim3(256), 0, s, models, ncells, G, GS, mag, lt, sq, mu, lcfp,
-                     lcfpr, theta, cellscal);
+                     lcfpr, theta, cellscal, lt ? nullptr : pq);
+  return hipGetLastError();
+}
+
+hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long ncols, int ncells,
+                             const double* theta, int GS, const double* cellscal, double* colc, hipStream_t s) {
+  if (ncols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_col_consts, dim3(div_up(ncols, 256)), dim3(256), 0, s, ucl, ucl_off, ncols, ncells, theta, GS,
+                     cellscal, colc);
   return hipGetLastError();
 }
 
