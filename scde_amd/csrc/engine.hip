@@ -178,9 +178,11 @@ struct scde_ctx {
     Buf cellidx, cmax, cmin, woff, bits, rank, nuniq, ucl, ucl_off, uci;
     std::vector<int> cmax_h, cmin_h, nuniq_h;
     std::vector<long long> woff_h, ucl_off_h;
+    std::vector<int4> tasks_h;  // cell-staged tables tasks (k_tables_cell)
+    Buf tasks;
     bool ready = false;
     void release() {
-      Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci};
+      Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci, &tasks};
       for (Buf* x : b) x->release();
     }
   } us[3];
@@ -509,6 +511,18 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     ta.D = cx->E.as<double>();
     ta.zcol = cx->zcol.as<int>();
     ta.base_col = cx->base_col.as<int>();
+  }
+  // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
+  if (G <= 448 && ncols > 0) {
+    constexpr long long kTaskCols = 64;
+    u.tasks_h.clear();
+    for (int c = 0; c < C; ++c)
+      for (long long b = ucl_off_h[c]; b < ucl_off_h[c + 1]; b += kTaskCols)
+        u.tasks_h.push_back(make_int4(c, (int)b, (int)std::min(b + kTaskCols, ucl_off_h[c + 1]), 0));
+    if (fused) u.tasks_h.push_back(make_int4(-1, 0, 0, 0));  // the ELL pad column
+    RCHK(upload(cx, u.tasks, u.tasks_h.data(), sizeof(int4) * u.tasks_h.size()));
+    ta.tasks = u.tasks.as<int4>();
+    ta.ntasks = (int)u.tasks_h.size();
   }
   ev = cx->mark_begin(SLOT_TABLES);
   if (!s.localtheta && ncols > 0) {

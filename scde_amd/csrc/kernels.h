@@ -52,6 +52,11 @@ struct TablesArgs {
   double* D;      // [ncols + 1][GS]
   int* zcol;      // [ncells] count-0 column or -1
   int* base_col;  // [ncells]
+  // Cell-staged tables (phases 0 and 2, G <= 448): per block {cell, first column, end
+  // column, 0}; one task with cell -1 writes the ELL pad column (phase 2).  Null: the
+  // column-per-wave kernel.
+  const int4* tasks;
+  int ntasks;
 };
 
 struct BootArgs {

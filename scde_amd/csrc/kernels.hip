@@ -136,69 +136,23 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
 #ifndef SCDE_KT_DIAG
 #define SCDE_KT_DIAG 0  // timing-only builds: 1 trivial dnbinom, 2 no exp, 4 no log, 8 no stores
 #endif
+// One (cell, unique count) column, one wavefront, lanes over grid points.  The per-cell
+// grid vectors (mu, pq, lcfpr, lcfp, theta) and the baseline column come in as pointers:
+// global memory (k_tables) or an LDS copy staged once per cell (k_tables_cell).
 template <bool CT>
-__global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
-  extern __shared__ double vrow[];  // [4 waves][GS]
-  __shared__ double etab[64];
-  __shared__ double ltab[3][97];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
-  if (threadIdx.x < 97) {
-    ltab[0][threadIdx.x] = kLogInvC[threadIdx.x];
-    ltab[1][threadIdx.x] = kLogCHi[threadIdx.x];
-    ltab[2][threadIdx.x] = kLogCLo[threadIdx.x];
-  }
-  __syncthreads();
-  const LogTab lt{ltab[0], ltab[1], ltab[2]};
-  const int phase = a.phase;
-  long long col;
-  int c;
-  if (phase == 1) {
-    // one wave per cell: its count-0 column (unique within the cell), first match
-    c = blockIdx.x * 4 + wid;
-    if (c >= a.ncells) return;
-    const long long o1 = a.ucl_off[c + 1];
-    long long zc = -1;
-    for (long long i0 = a.ucl_off[c]; i0 < o1; i0 += 64) {
-      const long long i = i0 + lane;
-      const unsigned long long m = __ballot(i < o1 && a.ucl[i] == 0);
-      if (m) {
-        zc = i0 + __ffsll((long long)m) - 1;
-        break;
-      }
-    }
-    if (lane == 0) a.zcol[c] = (int)zc;
-    if (zc < 0) {
-      if (lane == 0) a.base_col[c] = -1;
-      return;
-    }
-    col = zc;
-  } else {
-    col = (long long)blockIdx.x * 4 + wid;
-    if (phase == 2 && col == a.ncols) {  // the ELL pad column
-      for (int k = lane; k < a.GS; k += 64) a.D[col * a.GS + k] = 0.0;
-      return;
-    }
-    if (col >= a.ncols) return;
-    int lo = 0, hi = a.ncells;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (a.ucl_off[mid] <= col) lo = mid; else hi = mid;
-    }
-    c = lo;
-    if (phase == 2 && col == a.zcol[c]) return;  // done in phase 1
-  }
+__device__ __forceinline__ void tables_column(const TablesArgs& a, long long col, int c, int phase,
+                                              const double* __restrict__ mu, const double* __restrict__ P,
+                                              const double* __restrict__ lcfpr, const double* __restrict__ lcfp,
+                                              const double* __restrict__ th, const double* __restrict__ base,
+                                              double* __restrict__ v, const double* etab, const LogTab& lt, int lane,
+                                              int PS) {
   const int G = a.G;
   const double x = (double)a.ucl[col];
-  const double* mu = a.mu + (long long)c * a.GS;
-  const double* lcfp = a.lcfp + (long long)c * a.GS;
-  const double* lcfpr = a.lcfpr + (long long)c * a.GS;
-  const double* th = a.theta + (long long)c * a.GS;
   const double maxcfp = a.cellscal[2 * c];
   double fp;
   NbFast nf;
   nf.ok = false;
-  if (CT && a.pq && a.colc) {
+  if (CT && P && a.colc) {
     // per-column constants from k_col_consts (wave-uniform scalar loads)
     const double* cc = a.colc + col * 8;
     nf.n = cc[0];
@@ -214,20 +168,18 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   } else {
     fp = dpois_log_cold(x, a.cellscal[2 * c + 1]);
   }
-  double* v = vrow + (long long)wid * a.GS;
   double lmax = -INFINITY;
   if (CT && nf.ok) {
     // fast path: per-point p, q, log p, log q from k_cell_prep; the lane whose mu is
     // overridden by the count (R: x between mu[k] and mu[k+1]) forms its own; edge cases
     // (p or q == 0, np or nq not finite and positive) take the reference dnbinom
-    const double* P = a.pq + (long long)c * 4 * a.GS;
 #pragma unroll 1
     for (int k = lane; k < G; k += 64) {
       const double muv = mu[k];
       const bool last = (k == G - 1);
       const double mnext = last ? 0.0 : mu[k + 1];
       const bool over = (!last && x > muv && x < mnext) || (last && x > muv);
-      double pr = P[k], qr = P[a.GS + k], lpr = P[2 * a.GS + k], lqr = P[3 * a.GS + k];
+      double pr = P[k], qr = P[PS + k], lpr = P[2 * PS + k], lqr = P[3 * PS + k];
       if (over) {
         const double t = th[k];
         pr = t / (t + x);
@@ -281,8 +233,6 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   double* out = a.T ? a.T + col * a.GS : nullptr;
   // fused delta (phase 2): D = T - T[baseline column of the cell], as k_delta computes it
   double* dout = phase ? a.D + col * a.GS : nullptr;
-  const int bc = (phase == 2) ? a.base_col[c] : -1;
-  const double* base = (bc >= 0) ? a.D + (long long)bc * a.GS : nullptr;
 #pragma unroll 1
   for (int k = lane; k < G; k += 64) {
     // log(e / s) as log e - log s (no division); e / s could round differently only
@@ -322,6 +272,128 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const unsigned long long anyc = __ballot(clamp);
   if (lane == 0) a.has_clamp[col] = anyc ? 1 : 0;
   if (phase == 1 && lane == 0) a.base_col[c] = (a.use_baseline && !anyc) ? (int)col : -1;
+}
+
+__device__ __forceinline__ void tables_tabs(double* etab, double (*ltab)[97]) {
+  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
+  if (threadIdx.x < 97) {
+    ltab[0][threadIdx.x] = kLogInvC[threadIdx.x];
+    ltab[1][threadIdx.x] = kLogCHi[threadIdx.x];
+    ltab[2][threadIdx.x] = kLogCLo[threadIdx.x];
+  }
+}
+
+// Column-per-wave form, grid vectors read from global memory: phase 1 (one wave per
+// cell, its count-0 column) and grids too wide for the staged kernel.
+template <bool CT>
+__global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
+  extern __shared__ double vrow[];  // [4 waves][GS]
+  __shared__ double etab[64];
+  __shared__ double ltab[3][97];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  tables_tabs(etab, ltab);
+  __syncthreads();
+  const LogTab lt{ltab[0], ltab[1], ltab[2]};
+  const int phase = a.phase;
+  long long col;
+  int c;
+  if (phase == 1) {
+    // one wave per cell: its count-0 column (unique within the cell), first match
+    c = blockIdx.x * 4 + wid;
+    if (c >= a.ncells) return;
+    const long long o1 = a.ucl_off[c + 1];
+    long long zc = -1;
+    for (long long i0 = a.ucl_off[c]; i0 < o1; i0 += 64) {
+      const long long i = i0 + lane;
+      const unsigned long long m = __ballot(i < o1 && a.ucl[i] == 0);
+      if (m) {
+        zc = i0 + __ffsll((long long)m) - 1;
+        break;
+      }
+    }
+    if (lane == 0) a.zcol[c] = (int)zc;
+    if (zc < 0) {
+      if (lane == 0) a.base_col[c] = -1;
+      return;
+    }
+    col = zc;
+  } else {
+    col = (long long)blockIdx.x * 4 + wid;
+    if (phase == 2 && col == a.ncols) {  // the ELL pad column
+      for (int k = lane; k < a.GS; k += 64) a.D[col * a.GS + k] = 0.0;
+      return;
+    }
+    if (col >= a.ncols) return;
+    int lo = 0, hi = a.ncells;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (a.ucl_off[mid] <= col) lo = mid; else hi = mid;
+    }
+    c = lo;
+    if (phase == 2 && col == a.zcol[c]) return;  // done in phase 1
+  }
+  const long long co = (long long)c * a.GS;
+  const int bc = (phase == 2) ? a.base_col[c] : -1;
+  const double* base = (bc >= 0) ? a.D + (long long)bc * a.GS : nullptr;
+  tables_column<CT>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co, a.lcfp + co,
+                    a.theta + co, base, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
+}
+
+// Cell-staged form (phases 0 and 2, G <= kTabStagedG): one 8-wave block per task
+// (cell c, columns [b, e)), the cell's grid vectors and baseline column copied into LDS
+// once and shared by the block's waves, which take the task's columns round-robin.
+// Without the staging every column's wave re-reads ~9 grid vectors from L2 with a
+// dependent-load latency per 64-point step.  LDS rows have stride G (not GS) so two
+// blocks fit a CU: (8 + 9) * G * 8 B = 54.5 KB at G = 401.
+constexpr int kTabStagedG = 448;
+constexpr int kTabWaves = 8;
+template <bool CT>
+__global__ __launch_bounds__(64 * kTabWaves) void k_tables_cell(TablesArgs a) {
+  extern __shared__ double dyn[];  // vrow [8][G] | mu | P[4] | lcfpr | lcfp | th | base, each G
+  __shared__ double etab[64];
+  __shared__ double ltab[3][97];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int GS = a.GS, G = a.G;
+  tables_tabs(etab, ltab);
+  const int4 task = a.tasks[blockIdx.x];
+  const int c = task.x;
+  const int phase = a.phase;
+  if (c < 0) {  // the ELL pad column (phase 2)
+    if (wid == 0)
+      for (int k = lane; k < GS; k += 64) a.D[a.ncols * GS + k] = 0.0;
+    return;
+  }
+  const bool haveP = CT && a.pq;
+  double* smu = dyn + kTabWaves * G;
+  double* sP = smu + G;
+  double* slr = sP + 4 * G;
+  double* slc = slr + G;
+  double* sth = slc + G;
+  double* sbase = sth + G;
+  const long long co = (long long)c * GS;
+  const int bc = (phase == 2) ? a.base_col[c] : -1;
+  for (int k = threadIdx.x; k < G; k += 64 * kTabWaves) {
+    smu[k] = a.mu[co + k];
+    slr[k] = a.lcfpr[co + k];
+    slc[k] = a.lcfp[co + k];
+    sth[k] = a.theta[co + k];
+    if (haveP) {
+      const double* P = a.pq + 4 * co;
+      sP[k] = P[k];
+      sP[G + k] = P[GS + k];
+      sP[2 * G + k] = P[2 * GS + k];
+      sP[3 * G + k] = P[3 * GS + k];
+    }
+    if (bc >= 0) sbase[k] = a.D[(long long)bc * GS + k];
+  }
+  __syncthreads();
+  const LogTab lt{ltab[0], ltab[1], ltab[2]};
+  const int zc = (phase == 2) ? a.zcol[c] : -1;
+  for (int col = task.y + wid; col < task.z; col += kTabWaves) {
+    if (col == zc) continue;  // done in phase 1
+    tables_column<CT>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, slc, sth, bc >= 0 ? sbase : nullptr,
+                      dyn + wid * G, etab, lt, lane, G);
+  }
 }
 
 // ------------------------------------------------------------------ baseline / ELL
@@ -1715,6 +1787,14 @@ hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   if (a.ncols <= 0 && a.phase != 2) return hipSuccess;
   if (a.phase != 0 && (!a.D || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
+  if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG) {
+    const size_t shm = sizeof(double) * (kTabWaves + 9) * (size_t)a.G;
+    if (a.const_theta)
+      hipLaunchKernelGGL(k_tables_cell<true>, dim3(a.ntasks), dim3(64 * kTabWaves), shm, s, a);
+    else
+      hipLaunchKernelGGL(k_tables_cell<false>, dim3(a.ntasks), dim3(64 * kTabWaves), shm, s, a);
+    return hipGetLastError();
+  }
   const long long nwaves = a.phase == 1 ? a.ncells : a.phase == 2 ? a.ncols + 1 : a.ncols;
   if (nwaves <= 0) return hipSuccess;
   const dim3 grid(div_up(nwaves, 4)), block(256);
