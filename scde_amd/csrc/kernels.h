@@ -4,6 +4,9 @@
 #ifndef SCDE_BOOT_WPE
 #define SCDE_BOOT_WPE 8  // k_boot2 (NB <= 20) occupancy target: 8 waves per SIMD = 64 VGPRs
 #endif
+#ifndef SCDE_BOOT_ASMLD
+#define SCDE_BOOT_ASMLD 1  // k_boot2 column look-ahead issued from asm with explicit vmcnt waits
+#endif
 #ifndef SCDE_BOOT_EB
 #define SCDE_BOOT_EB 4  // ELL entries per k_boot2 batch (rows are padded to a multiple of 8, plus 8)
 #endif

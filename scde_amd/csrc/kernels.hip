@@ -919,11 +919,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
       }
     }
   };
-  load_batch(0, cell, v);
-  for (int e0 = 0; e0 < n; e0 += EB) {
-    int celln[EB];
-    double vn[EB];
-    load_batch(e0 + EB, celln, vn);
+  auto accumulate = [&](const int (&c)[EB], const double (&x)[EB]) {
 #pragma unroll
     for (int i0 = 0; i0 < NB; i0 += 2) {
       double2 w[EB];
@@ -932,22 +928,74 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
         if (diag & 1) {  // timing diagnostic: every entry reads the first entry's multiplicities
           w[j] = *reinterpret_cast<const double2*>(W + (long long)cell0 * Bp + b0 + i0);
         } else {
-          w[j] = *reinterpret_cast<const double2*>(W + (long long)__builtin_amdgcn_readfirstlane(cell[j]) * Bp +
-                                                   b0 + i0);
+          w[j] = *reinterpret_cast<const double2*>(W + (long long)__builtin_amdgcn_readfirstlane(c[j]) * Bp + b0 +
+                                                   i0);
         }
       }
 #pragma unroll
       for (int j = 0; j < EB; ++j) {
-        acc[i0] = fma(w[j].x, v[j], acc[i0]);
-        acc[i0 + 1] = fma(w[j].y, v[j], acc[i0 + 1]);
+        acc[i0] = fma(w[j].x, x[j], acc[i0]);
+        acc[i0 + 1] = fma(w[j].y, x[j], acc[i0 + 1]);
       }
     }
+  };
+#if SCDE_BOOT_ASMLD
+  // The column loads are issued from inline asm and waited with explicit vmcnt: left to
+  // itself the compiler sinks the look-ahead loads into the iteration that consumes them
+  // (to fit the 64-VGPR occupancy target), which exposes their latency every batch.  Two
+  // register buffers alternate (loop unrolled by 2) so no in-flight register is ever
+  // copied; the wait asm ties the consumed buffer, so no FMA is hoisted above it.  Rows
+  // are padded to a multiple of 8 plus 8 zero-column entries: the 2 x EB = 8 entries per
+  // iteration and the EB look-ahead stay inside the row.
+  static_assert(EB == 4, "the asm look-ahead assumes 4-entry batches");
+  auto issue = [&](int e0, int (&c)[EB], double (&x)[EB]) {
+    const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
+#pragma unroll
+    for (int j = 0; j < EB / 2; ++j) {
+      const int4 t = E4[j];
+      c[2 * j] = t.x;
+      c[2 * j + 1] = t.z;
+      const double* p0 = D + (long long)((diag & 2) ? col0 : t.y) * GS + tid;
+      const double* p1 = D + (long long)((diag & 2) ? col0 : t.w) * GS + tid;
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j]) : "v"(p0));
+      asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j + 1]) : "v"(p1));
+    }
+  };
+  auto ready = [&](double (&x)[EB]) {  // all but the EB youngest column loads have landed
+    asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
+  };
+  (void)load_batch;
+  int cellb[EB];
+  double vb[EB];
+  // the baseline loads into acc complete here: otherwise the compiler's wait for them
+  // lands at the first FMA inside the loop, as a vmcnt(0) executed every iteration
+#pragma unroll
+  for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));
+  issue(0, cell, v);
+  for (int e0 = 0; e0 < n; e0 += 2 * EB) {
+    issue(e0 + EB, cellb, vb);
+    ready(v);
+    accumulate(cell, v);
+    issue(e0 + 2 * EB, cell, v);
+    ready(vb);
+    accumulate(cellb, vb);
+  }
+  // drain the last look-ahead before its registers can be reused
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+#else
+  load_batch(0, cell, v);
+  for (int e0 = 0; e0 < n; e0 += EB) {
+    int celln[EB];
+    double vn[EB];
+    load_batch(e0 + EB, celln, vn);
+    accumulate(cell, v);
 #pragma unroll
     for (int j = 0; j < EB; ++j) {
       cell[j] = celln[j];
       v[j] = vn[j];
     }
   }
+#endif
   // ---- per-boot softmax over the grid: max, exp, sum (one LDS round each) ----
   if (diag & 8) {  // timing diagnostic: no reductions
     if (tid < NB) fin[tid] = acc[0];
