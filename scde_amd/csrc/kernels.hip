@@ -945,8 +945,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
   // (to fit the 64-VGPR occupancy target), which exposes their latency every batch.  Two
   // register buffers alternate (loop unrolled by 2) so no in-flight register is ever
   // copied; the wait asm ties the consumed buffer, so no FMA is hoisted above it.  Rows
-  // are padded to a multiple of 8 plus 8 zero-column entries: the 2 x EB = 8 entries per
-  // iteration and the EB look-ahead stay inside the row.
+  // are padded to a multiple of 8 plus 8 zero-column entries: every look-ahead batch
+  // stays inside the row.
   static_assert(EB == 4, "the asm look-ahead assumes 4-entry batches");
   auto issue = [&](int e0, int (&c)[EB], double (&x)[EB]) {
     const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
@@ -972,13 +972,23 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
 #pragma unroll
   for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));
   issue(0, cell, v);
-  for (int e0 = 0; e0 < n; e0 += 2 * EB) {
+  // whole pairs of batches, then at most one odd batch: the padding work stays < EB
+  // entries (rows of ~40 entries at config 2 would otherwise pad to a multiple of 8)
+  const int n4 = (n + EB - 1) & ~(EB - 1);
+  int e0 = 0;
+  for (; e0 + 2 * EB <= n4; e0 += 2 * EB) {
     issue(e0 + EB, cellb, vb);
     ready(v);
     accumulate(cell, v);
     issue(e0 + 2 * EB, cell, v);
     ready(vb);
     accumulate(cellb, vb);
+  }
+  if (e0 < n4) {
+    issue(e0 + EB, cellb, vb);  // look-ahead slot, unused: keeps the vmcnt bookkeeping uniform
+    ready(v);
+    accumulate(cell, v);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]));
   }
   // drain the last look-ahead before its registers can be reused
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
