@@ -855,6 +855,8 @@ __device__ __forceinline__ void block_max_f32(const double (&x)[NB], float* redf
   __syncthreads();
 }
 
+constexpr double kBootExpCut = -50.0;  // k_boot2 softmax terms below e^-50 are dropped
+
 // One block per (gene, boot slab of NB).  Lanes over grid points (k = threadIdx.x,
 // G <= blockDim <= GS); NB bootstrap accumulators per lane in VGPRs.  Per ELL entry
 // the NB draw multiplicities are wave-uniform (scalar loads, the FMA's SGPR operand)
@@ -1014,15 +1016,22 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
     block_max_f32<NB>(acc, reinterpret_cast<float*>(red), fin, lane, wid, nw);
   }
   if (tid < NB && b0 + tid < nboot && !(fabs(fin[tid]) <= degen_thresh)) degen[g] = 1;
+  // Softmax terms below e^kBootExpCut (1.9e-22) are dropped: a jp entry loses at most
+  // that much (each boot's row sums to >= 1 before the 1/B weighting), far below the
+  // 1e-18 absolute floor of SURVEY 8(d)'s tolerance.  Rows are sharply peaked, so for most
+  // (wave, boot) pairs no lane of the 64-point stretch is above the cut and the whole
+  // wave skips the exp (a wave-uniform branch); inside an active wave the lanes below
+  // the cut are zeroed as before.
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     const double d = acc[i] - fin[i];
-    // exp(d) underflows to exactly 0 for d < -745.14; skip the call there
+    const bool need = live && d >= kBootExpCut;
     if (diag & 4)  // timing diagnostic: no exp
       acc[i] = live ? d : 0.0;
+    else if (__builtin_amdgcn_ballot_w64(need))
+      acc[i] = need ? exp_tab(d, etab) : 0.0;
     else
-      acc[i] = (live && d >= -746.0) ? exp_tab(d, etab) : 0.0;
-    if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+      acc[i] = 0.0;
   }
   if (diag & 8) {
     if (tid < NB) fin[tid] = acc[1];
