@@ -165,6 +165,7 @@ struct scde_ctx {
   hipStream_t stream = nullptr;
   // workspace
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, pq, colc, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
+      ubound, zubound, smask, subuf, sredo,
       degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
   // scde.expression.prior
   Buf pr_cell, pr_part, pr_occ, pr_stats, pr_hist, pr_work, pr_out, pr_v, pr_sorted, pr_sortw;
@@ -238,7 +239,7 @@ struct scde_ctx {
   ~scde_ctx() {
     Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &pq, &colc, &T,      &E,      &maxi,
                   &has_clamp, &base_col, &zcol, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
-                  &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw};
+                  &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw, &ubound, &zubound, &smask, &subuf, &sredo};
     for (Buf* b : all) b->release();
     Buf* wp[] = {&wp_probs, &wp_blocks,  &wp_kidx, &wp_cols,   &wp_perms, &wp_starts, &wp_scratch,
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
@@ -504,6 +505,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   ta.const_theta = s.localtheta ? 0 : 1;
   ta.pq = s.localtheta ? nullptr : cx->pq.as<double>();
   ta.use_baseline = s.use_baseline ? 1 : 0;
+  // k_boot2 grid-stretch skipping (G <= 448: at most 7 stretches of 64 points); the
+  // tables kernel emits the per-column stretch maxima.  SCDE_BOOT_SKIP=0 disables it.
+  bool stretch_skip = fused && G <= 448;
+  if (const char* e = getenv("SCDE_BOOT_SKIP")) stretch_skip = stretch_skip && atoi(e) != 0;
   if (fused) {
     HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
     HCHK(cx->base_col.ensure(sizeof(int) * std::max(1, C)));
@@ -511,6 +516,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     ta.D = cx->E.as<double>();
     ta.zcol = cx->zcol.as<int>();
     ta.base_col = cx->base_col.as<int>();
+    if (stretch_skip) {
+      HCHK(cx->ubound.ensure(sizeof(double) * 8 * (size_t)(ncols + 1)));
+      ta.U = cx->ubound.as<double>();
+    }
   }
   // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
   if (G <= 448 && ncols > 0) {
@@ -591,6 +600,11 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
     HCHK(launch_baseline_z(Tbase, G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
                            cx->Z.as<double>(), st));
+    if (stretch_skip) {
+      HCHK(cx->zubound.ensure(sizeof(double) * 8 * (size_t)nsets * Bp));
+      HCHK(launch_stretch_zu(cx->ubound.as<double>(), cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
+                             cx->zubound.as<double>(), st));
+    }
     cx->mark_end(SLOT_OTHER, ev);
     if (nsets > 1) {
       if ((int)s.wset.size() != N) return fail(SCDE_EINTERNAL, "wset size mismatch");
@@ -629,7 +643,31 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       b2.out_k = s.jp_k;
       b2.degen = cx->degen.as<int>();
       b2.ngenes = N;
+      b2.U = stretch_skip ? cx->ubound.as<double>() : nullptr;
+      b2.ZU = stretch_skip ? cx->zubound.as<double>() : nullptr;
+      if (stretch_skip) {
+        HCHK(cx->smask.ensure(sizeof(int) * std::max<size_t>(1, (size_t)P * N)));
+        HCHK(cx->subuf.ensure(sizeof(double) * 8 * nb * std::max<size_t>(1, (size_t)P * N)));
+        HCHK(cx->sredo.ensure(sizeof(int) * ((size_t)P * N + 1)));
+        b2.mask = cx->smask.as<int>();
+        b2.ubuf = cx->subuf.as<double>();
+        b2.redo = cx->sredo.as<int>();
+      }
       HCHK(launch_boot2(b2, st));
+      if (stretch_skip && getenv("SCDE_DEBUG_SKIP")) {  // diagnostics: skipped stretches, redo slabs
+        std::vector<int> m((size_t)P * N), r((size_t)P * N);
+        HCHK(hipMemcpyAsync(m.data(), cx->smask.p, sizeof(int) * m.size(), hipMemcpyDeviceToHost, st));
+        HCHK(hipMemcpyAsync(r.data(), cx->sredo.p, sizeof(int) * r.size(), hipMemcpyDeviceToHost, st));
+        HCHK(hipStreamSynchronize(st));
+        const int nst = (G + 63) / 64;
+        long long kept = 0, redo = 0;
+        for (size_t i = 0; i < m.size(); ++i) {
+          kept += __builtin_popcount((unsigned)m[i]);
+          redo += r[i] != 0;
+        }
+        fprintf(stderr, "[scde skip] C=%d slabs=%zu stretches kept %.3f, redo slabs %lld\n", C, m.size(),
+                (double)kept / (double)(m.size() * nst), redo);
+      }
     } else {
       BootArgs ba{};
       ba.T = cx->T.as<double>();

@@ -60,6 +60,10 @@ struct TablesArgs {
   // column-per-wave kernel.
   const int4* tasks;
   int ntasks;
+  // Stretch bounds for k_boot2's grid-stretch skipping (nullable): per column and 64-point
+  // stretch j, max_j T (phase 1) or max_j T - max_j T[baseline column] (phase 2; the
+  // maximum itself where the cell has no baseline); 0 for the pad column.  [ncols + 1][8]
+  double* U;
 };
 
 struct BootArgs {
@@ -99,6 +103,13 @@ struct Boot2Args {
   long long out_g, out_k;
   int* degen;
   int ngenes;
+  // Grid-stretch skipping (nullable U disables it; needs G <= 448, nb <= 20): stretch
+  // bounds of the columns (TablesArgs::U) and their baseline part ZU [nsets][Bp][8]
+  const double* U;
+  const double* ZU;
+  int* mask;     // [ngenes][P] needed-stretch bits (k_stretch_mask output)
+  double* ubuf;  // [ngenes][P][8][nb] stretch upper bounds (k_stretch_mask output)
+  int* redo;     // [ngenes][P] slabs whose skipped stretches failed the post-check
 };
 
 struct ExactArgs {
@@ -154,6 +165,8 @@ hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, con
 hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long ncols, int ncells,
                              const double* theta, int GS, const double* cellscal, double* colc, hipStream_t s);
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s);
+hipError_t launch_stretch_zu(const double* U, const int* base_col, int ncells, const double* Wt, int Bp, int nsets,
+                             double* ZU, hipStream_t s);
 hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells, const unsigned char* has_clamp,
                             int use_baseline, int* base_col, hipStream_t s);
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,

@@ -136,6 +136,9 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
 #ifndef SCDE_KT_DIAG
 #define SCDE_KT_DIAG 0  // timing-only builds: 1 trivial dnbinom, 2 no exp, 4 no log, 8 no stores
 #endif
+constexpr int kStretchSlots = 8;  // per-column stretch bounds: ceil(G / 64) <= 7 used
+__device__ __forceinline__ float gt_maxf(float a, float b) { return (b > a) ? b : a; }
+
 // One (cell, unique count) column, one wavefront, lanes over grid points.  The per-cell
 // grid vectors (mu, pq, lcfpr, lcfp, theta) and the baseline column come in as pointers:
 // global memory (k_tables) or an LDS copy staged once per cell (k_tables_cell).
@@ -233,25 +236,43 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   double* out = a.T ? a.T + col * a.GS : nullptr;
   // fused delta (phase 2): D = T - T[baseline column of the cell], as k_delta computes it
   double* dout = phase ? a.D + col * a.GS : nullptr;
+  const int bc_u = (phase == 2) ? a.base_col[c] : -1;
+  // per 64-point stretch j (grid points 64j .. 64j+63, one k_boot2 wave each): the
+  // column's maximum, for k_boot2's stretch bounds (U: raw maxima for phase-1 columns,
+  // maxima minus the cell's baseline-column maxima for phase-2 columns)
+  const double* ubase = (a.U && bc_u >= 0) ? a.U + (long long)bc_u * kStretchSlots : nullptr;
 #pragma unroll 1
-  for (int k = lane; k < G; k += 64) {
-    // log(e / s) as log e - log s (no division); e / s could round differently only
-    // below DBL_MIN * s, where the reference's quotient is evaluated as written
-    const double e = v[k];
-    double r = (SCDE_KT_DIAG & 4) ? e - lsum : (e >= 0x1p-960) ? log_tab(e, lt) - lsum : log_tab(e / s, lt);
-    if (r > bv) {
-      bv = r;
-      bi = k;
+  for (int j = 0; 64 * j < G; ++j) {
+    const int k = lane + 64 * j;
+    double r = -INFINITY;
+    if (k < G) {
+      // log(e / s) as log e - log s (no division); e / s could round differently only
+      // below DBL_MIN * s, where the reference's quotient is evaluated as written
+      const double e = v[k];
+      r = (SCDE_KT_DIAG & 4) ? e - lsum : (e >= 0x1p-960) ? log_tab(e, lt) - lsum : log_tab(e / s, lt);
+      if (r > bv) {
+        bv = r;
+        bi = k;
+      }
+      if (r < a.minlogprob) {
+        r = a.minlogprob;
+        clamp = true;
+      }
+      if (SCDE_KT_DIAG & 8) {
+        if (r == 12345.0) dout[k] = r;
+      } else {
+        if (out) out[k] = r;
+        if (dout) dout[k] = base ? r - base[k] : r;
+      }
     }
-    if (r < a.minlogprob) {
-      r = a.minlogprob;
-      clamp = true;
-    }
-    if (SCDE_KT_DIAG & 8) {
-      if (r == 12345.0) dout[k] = r;
-    } else {
-      if (out) out[k] = r;
-      if (dout) dout[k] = base ? r - base[k] : r;
+    if (a.U) {
+      // in f32 (one permute per step), then widened by 2^-23 |m|: (float)r can round down
+      // by at most that, so the stored value is still an upper bound
+      float mf = (float)r;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) mf = gt_maxf(mf, __shfl_xor(mf, o, 64));
+      const double m = (double)mf + 0x1p-23 * fabs((double)mf);
+      if (lane == 0) a.U[col * kStretchSlots + j] = ubase ? m - ubase[j] : m;
     }
   }
   if (dout)
@@ -321,6 +342,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
     col = (long long)blockIdx.x * 4 + wid;
     if (phase == 2 && col == a.ncols) {  // the ELL pad column
       for (int k = lane; k < a.GS; k += 64) a.D[col * a.GS + k] = 0.0;
+      if (a.U && lane < kStretchSlots) a.U[col * kStretchSlots + lane] = 0.0;
       return;
     }
     if (col >= a.ncols) return;
@@ -359,8 +381,10 @@ __global__ __launch_bounds__(64 * kTabWaves) void k_tables_cell(TablesArgs a) {
   const int c = task.x;
   const int phase = a.phase;
   if (c < 0) {  // the ELL pad column (phase 2)
-    if (wid == 0)
+    if (wid == 0) {
       for (int k = lane; k < GS; k += 64) a.D[a.ncols * GS + k] = 0.0;
+      if (a.U && lane < kStretchSlots) a.U[a.ncols * kStretchSlots + lane] = 0.0;
+    }
     return;
   }
   const bool haveP = CT && a.pq;
@@ -502,6 +526,23 @@ __global__ __launch_bounds__(256) void k_baseline_z(const double* __restrict__ T
   if (k < GS)
     Z[((long long)set * Bp + b0 + wid) * GS + k] =
         ((part[0][wid][lane] + part[1][wid][lane]) + part[2][wid][lane]) + part[3][wid][lane];
+}
+
+// ZU[set][b][j] = sum over baseline cells of W[set][c][b] * U[base_col[c]][j]: the
+// baseline part of k_boot2's stretch upper bounds (U holds the baseline columns' raw
+// stretch maxima).  One thread per (set, boot, stretch).
+__global__ void k_stretch_zu(const double* __restrict__ U, const int* __restrict__ base_col, int ncells,
+                             const double* __restrict__ Wt, int Bp, int nsets, double* __restrict__ ZU) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nsets * Bp * kStretchSlots) return;
+  const int j = t % kStretchSlots, b = (t / kStretchSlots) % Bp, set = t / (kStretchSlots * Bp);
+  const double* W = Wt + (long long)set * ncells * Bp + b;
+  double z = 0.0;
+  for (int c = 0; c < ncells; ++c) {
+    const int bc = base_col[c];
+    if (bc >= 0) z = fma(W[(long long)c * Bp], U[(long long)bc * kStretchSlots + j], z);
+  }
+  ZU[t] = z;
 }
 
 // ------------------------------------------------------------------ K2: bootstrap
@@ -790,7 +831,6 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
 }
-__device__ __forceinline__ float gt_maxf(float a, float b) { return (b > a) ? b : a; }
 
 // f32 twin of wave_reduce_scatter_v (same lane -> index mapping), max only.
 template <int BC>
@@ -855,6 +895,112 @@ __device__ __forceinline__ void block_max_f32(const double (&x)[NB], float* redf
   __syncthreads();
 }
 
+// Variants for blocks whose waves outside `wmask` have exited (k_boot2 stretch
+// skipping): s_barrier waits only for the surviving waves, the combine reads only their
+// slots, and the first surviving wave (`lead`) does it.
+template <int NB>
+__device__ __forceinline__ void block_max_f32_m(const double (&x)[NB], float* redf, double* fin, int lane, int wid,
+                                                int nw, unsigned wmask, int lead) {
+#pragma unroll
+  for (int i0 = 0; i0 + 16 <= NB; i0 += 16) wave_max_partials<16, NB>(x, i0, redf, lane, wid);
+  if constexpr ((NB % 16) >= 8) wave_max_partials<8, NB>(x, NB - (NB % 16), redf, lane, wid);
+  if constexpr ((NB % 8) >= 4) wave_max_partials<4, NB>(x, NB - (NB % 8), redf, lane, wid);
+  __syncthreads();
+  if (wid == lead && lane < NB) {
+    float r = -INFINITY;
+    for (int w = 0; w < nw; ++w)
+      if ((wmask >> w) & 1) r = gt_maxf(r, redf[w * 32 + lane]);
+    fin[lane] = (double)r;
+  }
+  __syncthreads();
+}
+template <int NB>
+__device__ __forceinline__ void block_sum_m(const double (&x)[NB], bool live, double* red, double* fin, int lane,
+                                            int wid, int nw, unsigned wmask, int lead) {
+#pragma unroll
+  for (int i0 = 0; i0 + 16 <= NB; i0 += 16) wave_partials<16, false, NB>(x, i0, live, red, lane, wid);
+  if constexpr ((NB % 16) >= 8) wave_partials<8, false, NB>(x, NB - (NB % 16), live, red, lane, wid);
+  if constexpr ((NB % 8) >= 4) wave_partials<4, false, NB>(x, NB - (NB % 8), live, red, lane, wid);
+  __syncthreads();
+  if (wid == lead && lane < NB) {
+    double r = 0.0;
+    for (int w = 0; w < nw; ++w)
+      if ((wmask >> w) & 1) r += red[w * 32 + lane];
+    fin[lane] = r;
+  }
+  __syncthreads();
+}
+
+// Grid-stretch masks for k_boot2 (one wave per (gene, boot slab of NB <= 32)).
+// A boot's row is Z_b + sum_e W_be D_e; over stretch s (grid points 64s .. 64s+63, one
+// k_boot2 wave) it is bounded by the per-column stretch maxima of k_tables (U) and their
+// baseline part (ZU):
+//   UB_bs = ZU_bs + sum_e W_be U_e,s  >=  every row value in the stretch,
+// a (boots x entries) . (entries x stretches) product, done here on the FP64 matrix
+// cores (v_mfma_f64_16x16x4: 16 boots x 16 stretch slots x 4 entries per instruction;
+// two boot tiles).  Heuristic mask: stretch s is kept when some live boot has
+// UB_bs >= max_s' UB_bs' - 50 - slack.  Rigour comes from k_boot2's post-check, which
+// compares each skipped stretch's UB with the exact row maximum and sends the slab to
+// the redo launch when UB_bs >= max_b - 50 (the softmax cut): skipped stretches only ever
+// hold terms the cut zeroes anyway.  Writes UB [gene][slab][8][NB] and mask [gene][slab].
+typedef double d4_t __attribute__((ext_vector_type(4)));
+template <int NB>
+__global__ __launch_bounds__(64) void k_stretch_mask(const int2* __restrict__ ent, const int* __restrict__ nnz,
+                                                     int ent_stride, const double* __restrict__ Wt, int Bp,
+                                                     int ncells, const int* __restrict__ wset, int G, int P,
+                                                     int nboot, const double* __restrict__ U,
+                                                     const double* __restrict__ ZU, double slack,
+                                                     double* __restrict__ ub_out, int* __restrict__ mask,
+                                                     int ngenes) {
+  static_assert(NB <= 32, "two 16-boot tiles");
+  __shared__ double ubs[kStretchSlots][32];
+  const int lane = threadIdx.x;
+  const int g = blockIdx.x / P, p = blockIdx.x % P;
+  if (g >= ngenes) return;
+  const int b0 = p * NB, n = nnz[g];
+  const int nst = (G + 63) / 64;
+  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  const int set = wset ? wset[g] : 0;
+  const double* __restrict__ W = Wt + (long long)set * ncells * Bp + b0;
+  const int r = lane & 15, k4 = lane >> 4;  // A: boot r, entry k4; B: entry k4, stretch r
+  const bool a1ok = 16 + r < NB, bok = r < nst;
+  d4_t c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
+  // rows are padded with zero-column entries to a multiple of 8 (U of the pad column is 0)
+  const int n4 = (n + 3) & ~3;
+#pragma unroll 4
+  for (int e0 = 0; e0 < n4; e0 += 4) {
+    const int2 x = E[e0 + k4];
+    const double* w = W + (long long)x.x * Bp;
+    const double a0 = w[r];
+    const double a1 = a1ok ? w[16 + r] : 0.0;
+    const double bb = bok ? U[(long long)x.y * kStretchSlots + r] : 0.0;
+    c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bb, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bb, c1, 0, 0, 0);
+  }
+  // C/D (f64 16x16x4): column = lane & 15 (stretch), rows (lane >> 4) + 4 j (boots)
+  if (r < nst) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i0 = k4 + 4 * j, i1 = 16 + k4 + 4 * j;
+      if (i0 < NB) ubs[r][i0] = c0[j] + ZU[((long long)set * Bp + b0 + i0) * kStretchSlots + r];
+      if (i1 < NB) ubs[r][i1] = c1[j] + ZU[((long long)set * Bp + b0 + i1) * kStretchSlots + r];
+    }
+  }
+  __syncthreads();
+  double* o = ub_out + (long long)blockIdx.x * kStretchSlots * NB;
+  for (int t = lane; t < nst * NB; t += 64) o[t] = ubs[t / NB][t % NB];
+  unsigned need = 0;
+  if (lane < NB && b0 + lane < nboot) {
+    double m = -INFINITY;
+    for (int st = 0; st < nst; ++st) m = gt_max(m, ubs[st][lane]);
+    for (int st = 0; st < nst; ++st)
+      if (!(ubs[st][lane] < m - 50.0 - slack)) need |= 1u << st;
+  }
+#pragma unroll
+  for (int o2 = 32; o2 >= 1; o2 >>= 1) need |= (unsigned)__shfl_xor((int)need, o2, 64);
+  if (lane == 0) mask[blockIdx.x] = (int)need;
+}
+
 constexpr double kBootExpCut = -50.0;  // k_boot2 softmax terms below e^-50 are dropped
 
 // One block per (gene, boot slab of NB).  Lanes over grid points (k = threadIdx.x,
@@ -871,14 +1017,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
                                                 const int* __restrict__ wset, const double* __restrict__ Z, int G,
                                                 int GS, int P, int nboot, double norm_mult, double degen_thresh,
                                                 double* __restrict__ part, long long part_stride,
-                                                int* __restrict__ degen, int ngenes) {
+                                                int* __restrict__ degen, int ngenes,
+                                                const int* __restrict__ smask, const double* __restrict__ sub,
+                                                int* __restrict__ redo, int redo_pass) {
   static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
   constexpr int diag = SCDE_BOOT_DIAG;  // timing-only builds (tools/); 0 in production
   __shared__ double red[16 * 32];
   __shared__ double fin[32];
   __shared__ double etab[64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
-  if (tid < 64) etab[tid] = kExp2Frac64[tid];  // visible after the first reduction's barrier
   const bool live = tid < G;
   const int within = blockIdx.x % (8 * P);
   const int p = within >> 3;
@@ -890,16 +1037,38 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
   const int set = wset ? wset[g] : 0;
   const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
   const double* __restrict__ Zs = Z ? Z + (long long)set * Bp * GS : nullptr;
-  double acc[NB];
-  // lanes past the grid start at -inf: their pad columns are 0, so they stay -inf, never
-  // win a max and exp to 0 -- the reductions need no per-lane select
-#pragma unroll
-  for (int i = 0; i < NB; ++i) acc[i] = !live ? -INFINITY : (Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0);
+  // Grid-stretch skipping (smask/sub from k_stretch_mask): this wave's 64 points are
+  // left out when its mask bit is clear.  After the row maxima are known, every skipped
+  // stretch checks UB_bs < max_b - 51 for its live boots (1 covers the f32 maxima); a
+  // failure sends the slab to the redo pass (redo_pass: only flagged slabs, no skipping),
+  // so a stretch is only ever left out when all its softmax terms fall below the e^-50
+  // cut that zeroes them anyway -- the output is the same as without skipping.
+  if (redo_pass == 1 && !redo[(long long)g * P + p]) return;
+  const unsigned wmask = smask ? (unsigned)__builtin_amdgcn_readfirstlane(smask[(long long)g * P + p]) : ~0u;
+  const int wsid = __builtin_amdgcn_readfirstlane(wid);
+  const bool run = (wmask >> wsid) & 1;
+  const int lw = __builtin_ffs((int)wmask) - 1;  // first surviving wave: does the combines
+  if (wsid == lw) etab[lane] = kExp2Frac64[lane];  // visible after the first reduction's barrier
+  if (!run) {
+    // a left-out stretch: its partial row is zero; the wave exits (the block's barriers
+    // then wait only for the surviving waves, and the combines skip its slots)
+    if (live) part[(long long)p * part_stride + (long long)g * GS + tid] = 0.0;
+    __builtin_amdgcn_s_waitcnt(0);
+    return;
+  }
   // Entries in batches of EB, double-buffered in registers: batch e+1's column loads are
   // in flight while batch e accumulates.  ELL rows are padded to a multiple of EB plus
   // one extra batch of zero-column entries, so the look-ahead load is unconditional.
   // The multiplicities come in two boots x EB entries per scalar-load round.
   constexpr int EB = SCDE_BOOT_EB;
+  double acc[NB];
+  // lanes past the grid start at -inf: their pad columns are 0, so they stay -inf, never
+  // win a max and exp to 0 -- the reductions need no per-lane select.  A skipped
+  // stretch is set to -inf: its softmax terms are exactly the zeros the cut would give.
+#pragma unroll
+  for (int i = 0; i < NB; ++i)
+    acc[i] = (!live || !run) ? -INFINITY : (Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0);
+  if (run) {
   const int cell0 = __builtin_amdgcn_readfirstlane(E[0].x), col0 = __builtin_amdgcn_readfirstlane(E[0].y);
   (void)cell0;
   (void)col0;
@@ -1008,14 +1177,22 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
     }
   }
 #endif
+    }
   // ---- per-boot softmax over the grid: max, exp, sum (one LDS round each) ----
   if (diag & 8) {  // timing diagnostic: no reductions
     if (tid < NB) fin[tid] = acc[0];
     __syncthreads();
   } else {
-    block_max_f32<NB>(acc, reinterpret_cast<float*>(red), fin, lane, wid, nw);
+    block_max_f32_m<NB>(acc, reinterpret_cast<float*>(red), fin, lane, wid, nw, wmask, lw);
   }
-  if (tid < NB && b0 + tid < nboot && !(fabs(fin[tid]) <= degen_thresh)) degen[g] = 1;
+  if (wsid == lw && lane < NB && b0 + lane < nboot) {
+    if (!(fabs(fin[lane]) <= degen_thresh)) degen[g] = 1;
+    // post-check of the left-out stretches against the exact row maxima
+    if (smask)
+      for (int w = 0; w < nw; ++w)
+        if (!((wmask >> w) & 1) && !(sub[((long long)(g * P + p) * kStretchSlots + w) * NB + lane] < fin[lane] - 51.0))
+          redo[(long long)g * P + p] = 1;
+  }
   // Softmax terms below e^kBootExpCut (1.9e-22) are dropped: a jp entry loses at most
   // that much (each boot's row sums to >= 1 before the 1/B weighting), far below the
   // 1e-18 absolute floor of SURVEY 8(d)'s tolerance.  Rows are sharply peaked, so for most
@@ -1037,9 +1214,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
     if (tid < NB) fin[tid] = acc[1];
     __syncthreads();
   } else {
-    block_reduce_all<false, NB>(acc, live, red, fin, lane, wid, nw);
+    block_sum_m<NB>(acc, live, red, fin, lane, wid, nw, wmask, lw);
   }
-  if (tid < NB) fin[tid] = (b0 + tid < nboot) ? 1.0 / (fin[tid] * norm_mult) : 0.0;
+  if (wsid == lw && lane < NB) fin[lane] = (b0 + lane < nboot) ? 1.0 / (fin[lane] * norm_mult) : 0.0;
   __syncthreads();
   double jpv = 0.0;
 #pragma unroll
@@ -1904,6 +2081,14 @@ hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col
   return hipGetLastError();
 }
 
+hipError_t launch_stretch_zu(const double* U, const int* base_col, int ncells, const double* Wt, int Bp, int nsets,
+                             double* ZU, hipStream_t s) {
+  const int n = nsets * Bp * kStretchSlots;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_stretch_zu, dim3(div_up(n, 256)), dim3(256), 0, s, U, base_col, ncells, Wt, Bp, nsets, ZU);
+  return hipGetLastError();
+}
+
 static inline int block_for_grid(int G, int* kpt) {
   int b = ((G + 63) / 64) * 64;
   *kpt = 1;
@@ -1946,14 +2131,36 @@ int boot2_nb(int nboot) {
 hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const int block = ((a.G + 63) / 64) * 64;
-  if (block > 1024 || block > a.GS) return hipErrorInvalidValue;
   const int P = (a.nboot + a.nb - 1) / a.nb;
+  // stretch skipping: at most 8 stretches (U slots); mask kernel, skipping launch, redo launch
+  const int* smask = nullptr;
+  const double* sub = nullptr;
+  if (a.U && a.ZU && a.mask && a.ubuf && a.redo && block <= 64 * kStretchSlots && !a.lds_stage) {
+    // slack of the heuristic: UB's looseness grows with the draws per boot (~0.1 per cell)
+    const double slack = 30.0 + 0.25 * a.ncells;
+#define SCDE_SM(NBV)                                                                                              \
+  case NBV:                                                                                                        \
+    hipLaunchKernelGGL(k_stretch_mask<NBV>, dim3(a.ngenes * P), dim3(64), 0, s, a.ent, a.nnz, a.ent_stride, a.Wt, \
+                       a.Bp, a.ncells, a.wset, a.G, P, a.nboot, a.U, a.ZU, slack, a.ubuf, a.mask, a.ngenes);      \
+    break;
+    switch (a.nb) {
+      SCDE_SM(4) SCDE_SM(8) SCDE_SM(12) SCDE_SM(16) SCDE_SM(20) SCDE_SM(24) SCDE_SM(28) SCDE_SM(32)
+      default: return hipErrorInvalidValue;
+    }
+#undef SCDE_SM
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(a.redo, 0, sizeof(int) * ((size_t)a.ngenes * P + 1), s);
+    if (e != hipSuccess) return e;
+    smask = a.mask;
+    sub = a.ubuf;
+  }
   const int grid = (a.ngenes + 7) / 8 * 8 * P;
 #define SCDE_B2(NBV)                                                                                              \
   case NBV:                                                                                                        \
     hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid), dim3(block), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
                        a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
-                       a.part_stride, a.degen, a.ngenes);                                                         \
+                       a.part_stride, a.degen, a.ngenes, smask, sub, a.redo, RP);                             \
     break;
 #define SCDE_B3(NBV)                                                                                              \
   case NBV:                                                                                                        \
@@ -1967,9 +2174,14 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
       default: return hipErrorInvalidValue;
     }
   } else {
-    switch (a.nb) {
-      SCDE_B2(4) SCDE_B2(8) SCDE_B2(12) SCDE_B2(16) SCDE_B2(20) SCDE_B2(24) SCDE_B2(28) SCDE_B2(32)
-      default: return hipErrorInvalidValue;
+    // pass 0: with skipping (when set up); pass 1: the slabs the post-check flagged
+    const int npass = smask ? 2 : 1;
+    for (int RP = 0; RP < npass; ++RP) {
+      switch (a.nb) {
+        SCDE_B2(4) SCDE_B2(8) SCDE_B2(12) SCDE_B2(16) SCDE_B2(20) SCDE_B2(24) SCDE_B2(28) SCDE_B2(32)
+        default: return hipErrorInvalidValue;
+      }
+      if (RP == 0) smask = nullptr;  // the redo launch recomputes whole slabs
     }
   }
 #undef SCDE_B2
