@@ -264,15 +264,24 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         if (out) out[k] = r;
         if (dout) dout[k] = base ? r - base[k] : r;
       }
+      if (a.U) v[k] = r;  // the row of final values, for the stretch maxima below
     }
-    if (a.U) {
-      // in f32 (one permute per step), then widened by 2^-23 |m|: (float)r can round down
-      // by at most that, so the stored value is still an upper bound
-      float mf = (float)r;
+  }
+  if (a.U) {
+    // per-stretch maxima from the LDS row: lane l < 8 * stretches takes 8 points of
+    // stretch l >> 3, then a 3-step max over its group of 8 lanes; in f32, widened by
+    // 2^-23 |m| (the f32 rounding of the values) so the stored value is an upper bound
+    const int nst = (G + 63) / 64;
+    const int j = lane >> 3, k0 = 64 * j + 8 * (lane & 7);
+    float mf = -INFINITY;
+    if (j < nst)
+      for (int t = 0; t < 8; ++t)
+        if (k0 + t < G) mf = gt_maxf(mf, (float)v[k0 + t]);
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) mf = gt_maxf(mf, __shfl_xor(mf, o, 64));
+    for (int o = 1; o <= 4; o <<= 1) mf = gt_maxf(mf, __shfl_xor(mf, o, 64));
+    if ((lane & 7) == 0 && j < nst) {
       const double m = (double)mf + 0x1p-23 * fabs((double)mf);
-      if (lane == 0) a.U[col * kStretchSlots + j] = ubase ? m - ubase[j] : m;
+      a.U[col * kStretchSlots + j] = ubase ? m - ubase[j] : m;
     }
   }
   if (dout)
@@ -983,7 +992,7 @@ __global__ __launch_bounds__(64) void k_stretch_mask(const int2* __restrict__ en
   d4_t c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
   // rows are padded with zero-column entries to a multiple of 8 (U of the pad column is 0)
   const int n4 = (n + 3) & ~3;
-#pragma unroll 4
+#pragma unroll 8
   for (int e0 = 0; e0 < n4; e0 += 4) {
     const int2 x = E[e0 + k4];
     const double* w = W + (long long)x.x * Bp;
