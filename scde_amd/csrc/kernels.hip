@@ -978,13 +978,20 @@ __global__ __launch_bounds__(64) void k_stretch_mask(const int2* __restrict__ en
                                                      double* __restrict__ ub_out, int* __restrict__ mask,
                                                      int ngenes) {
   static_assert(NB <= 32, "two 16-boot tiles");
+  extern __shared__ int2 es[];  // the gene's entries: each step's gathers then wait on LDS only
   __shared__ double ubs[kStretchSlots][32];
   const int lane = threadIdx.x;
   const int g = blockIdx.x / P, p = blockIdx.x % P;
   if (g >= ngenes) return;
   const int b0 = p * NB, n = nnz[g];
   const int nst = (G + 63) / 64;
-  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  {
+    const int2* __restrict__ Eg = ent + (long long)g * ent_stride;
+    const int n4s = (n + 3) & ~3;
+    for (int e = lane; e < n4s; e += 64) es[e] = Eg[e];
+    __syncthreads();
+  }
+  const int2* E = es;
   const int set = wset ? wset[g] : 0;
   const double* __restrict__ W = Wt + (long long)set * ncells * Bp + b0;
   const int r = lane & 15, k4 = lane >> 4;  // A: boot r, entry k4; B: entry k4, stretch r
@@ -2163,10 +2170,12 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
     // slack of the heuristic: UB's looseness grows with the draws per boot (~0.1 per cell)
     double slack = 30.0 + 0.25 * a.ncells;
     if (const char* e = getenv("SCDE_SKIP_SLACK")) slack = atof(e);  // tests: force post-check failures
+    const size_t eshm = sizeof(int2) * (size_t)a.ent_stride;
+    if (eshm > 60 * 1024) return hipErrorInvalidValue;
 #define SCDE_SM(NBV)                                                                                              \
   case NBV:                                                                                                        \
-    hipLaunchKernelGGL(k_stretch_mask<NBV>, dim3(a.ngenes * P), dim3(64), 0, s, a.ent, a.nnz, a.ent_stride, a.Wt, \
-                       a.Bp, a.ncells, a.wset, a.G, P, a.nboot, a.U, a.ZU, slack, a.ubuf, a.mask, a.ngenes);      \
+    hipLaunchKernelGGL(k_stretch_mask<NBV>, dim3(a.ngenes * P), dim3(64), eshm, s, a.ent, a.nnz, a.ent_stride,    \
+                       a.Wt, a.Bp, a.ncells, a.wset, a.G, P, a.nboot, a.U, a.ZU, slack, a.ubuf, a.mask, a.ngenes); \
     break;
     switch (a.nb) {
       SCDE_SM(4) SCDE_SM(8) SCDE_SM(12) SCDE_SM(16) SCDE_SM(20) SCDE_SM(24) SCDE_SM(28) SCDE_SM(32)
