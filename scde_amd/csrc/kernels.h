@@ -7,6 +7,9 @@
 #ifndef SCDE_BOOT_ASMLD
 #define SCDE_BOOT_ASMLD 1  // k_boot2 column look-ahead issued from asm with explicit vmcnt waits
 #endif
+#ifndef SCDE_TAB_WPE
+#define SCDE_TAB_WPE 4  // k_tables_cell occupancy target (waves per SIMD)
+#endif
 #ifndef SCDE_BOOT_EB
 #define SCDE_BOOT_EB 4  // ELL entries per k_boot2 batch (rows are padded to a multiple of 8, plus 8)
 #endif

@@ -379,7 +379,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
 constexpr int kTabStagedG = 448;
 constexpr int kTabWaves = 8;
 template <bool CT>
-__global__ __launch_bounds__(64 * kTabWaves) void k_tables_cell(TablesArgs a) {
+__global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TAB_WPE))) void k_tables_cell(TablesArgs a) {
   extern __shared__ double dyn[];  // vrow [8][G] | mu | P[4] | lcfpr | lcfp | th | base, each G
   __shared__ double etab[64];
   __shared__ double ltab[3][97];
@@ -999,7 +999,7 @@ __global__ __launch_bounds__(64) void k_stretch_mask(const int2* __restrict__ en
   d4_t c0 = {0, 0, 0, 0}, c1 = {0, 0, 0, 0};
   // rows are padded with zero-column entries to a multiple of 8 (U of the pad column is 0)
   const int n4 = (n + 3) & ~3;
-#pragma unroll 8
+#pragma unroll 2
   for (int e0 = 0; e0 < n4; e0 += 4) {
     const int2 x = E[e0 + k4];
     const double* w = W + (long long)x.x * Bp;
@@ -2166,12 +2166,13 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   // stretch skipping: at most 8 stretches (U slots); mask kernel, skipping launch, redo launch
   const int* smask = nullptr;
   const double* sub = nullptr;
-  if (a.U && a.ZU && a.mask && a.ubuf && a.redo && block <= 64 * kStretchSlots && !a.lds_stage) {
+  // (the mask kernel stages a gene's entry list in LDS: up to ~7,600 cells)
+  if (a.U && a.ZU && a.mask && a.ubuf && a.redo && block <= 64 * kStretchSlots && !a.lds_stage &&
+      sizeof(int2) * (size_t)a.ent_stride <= 60 * 1024) {
     // slack of the heuristic: UB's looseness grows with the draws per boot (~0.1 per cell)
     double slack = 30.0 + 0.25 * a.ncells;
     if (const char* e = getenv("SCDE_SKIP_SLACK")) slack = atof(e);  // tests: force post-check failures
     const size_t eshm = sizeof(int2) * (size_t)a.ent_stride;
-    if (eshm > 60 * 1024) return hipErrorInvalidValue;
 #define SCDE_SM(NBV)                                                                                              \
   case NBV:                                                                                                        \
     hipLaunchKernelGGL(k_stretch_mask<NBV>, dim3(a.ngenes * P), dim3(64), eshm, s, a.ent, a.nnz, a.ent_stride,    \
