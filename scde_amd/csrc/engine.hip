@@ -618,6 +618,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     if (fast) {
       Boot2Args b2{};
       b2.D = cx->E.as<double>();
+      b2.ncols_p1 = ncols + 1;
       b2.ent = cx->ent.as<int2>();
       b2.nnz = cx->nnz.as<int>();
       b2.ent_stride = stride;

@@ -90,6 +90,7 @@ struct BootArgs {
 
 struct Boot2Args {
   const double* D;  // [ncols + 1][GS] baseline-delta columns (k_delta)
+  long long ncols_p1;  // columns of D (ncols + 1)
   const int2* ent;  // [ngenes][ent_stride] (cell, column) -- the k_ell list
   const int* nnz;
   int ent_stride;

@@ -1131,7 +1131,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
         if (diag & 1) {  // timing diagnostic: every entry reads the first entry's multiplicities
           w[j] = *reinterpret_cast<const double2*>(W + (long long)cell0 * Bp + b0 + i0);
         } else {
-          w[j] = *reinterpret_cast<const double2*>(W + (long long)__builtin_amdgcn_readfirstlane(c[j]) * Bp + b0 +
+          // 32-bit row offsets (cells x Bp < 2^31): one s_mul_i32 instead of a 64-bit product
+          w[j] = *reinterpret_cast<const double2*>(W + (unsigned)(__builtin_amdgcn_readfirstlane(c[j]) * Bp) + b0 +
                                                    i0);
         }
       }
@@ -1158,8 +1159,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
       const int4 t = E4[j];
       c[2 * j] = t.x;
       c[2 * j + 1] = t.z;
-      const double* p0 = D + (long long)((diag & 2) ? col0 : t.y) * GS + tid;
-      const double* p1 = D + (long long)((diag & 2) ? col0 : t.w) * GS + tid;
+      // 32-bit column offsets: launch_boot2 checks (ncols + 1) x GS < 2^31
+      const double* p0 = D + (unsigned)(((diag & 2) ? col0 : t.y) * GS) + tid;
+      const double* p1 = D + (unsigned)(((diag & 2) ? col0 : t.w) * GS) + tid;
       asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j]) : "v"(p0));
       asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j + 1]) : "v"(p1));
     }
@@ -2161,6 +2163,9 @@ int boot2_nb(int nboot) {
 
 hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
+  // k_boot2 forms column and multiplicity-row offsets in 32 bits
+  if ((long long)a.ncols_p1 * a.GS >= (1LL << 31) || (long long)a.ncells * a.Bp >= (1LL << 31))
+    return hipErrorInvalidValue;
   const int block = ((a.G + 63) / 64) * 64;
   const int P = (a.nboot + a.nb - 1) / a.nb;
   // stretch skipping: at most 8 stretches (U slots); mask kernel, skipping launch, redo launch
