@@ -1750,19 +1750,30 @@ __device__ __forceinline__ void slide_group(const double* __restrict__ A, const 
 // bit-identical to slide_group.  Q is zero-padded by >= R past n.
 template <int R>
 __device__ __forceinline__ void slide_lags(const double* P, const double* Q0, const double* Q1, int n, int d0,
-                                           double (&c)[R]) {
+                                           double (&c)[R], int pl = 0, int ph = 1 << 30, int ql = 0,
+                                           int qh = 1 << 30) {
   // P is 16-B aligned and t steps by 4: P[t..t+3] is two aligned 16-B reads.  Q0 / Q1 hold
   // the row at an even / odd double offset; the one matching the parity of d0 + R puts
   // Q[t + d0 + R] on a 16-B boundary (ds_read_b128: 16 B per lane in 4 LDS cycles, where
   // ds_read2_b64 takes 16).
   const double* Q = ((d0 + R) & 1) ? Q1 : Q0;
+  // Support restriction (bit-identical): a term P[t] Q[t + d] with P[t] == 0 or Q[t + d] ==
+  // 0 is +0 (both rows are finite and >= 0; the caller passes full ranges otherwise), and
+  // adding +0 to a non-negative partial sum changes nothing, so t only needs to cover
+  // [pl, ph] (P nonzero) intersected with the t where some lag's Q[t + d] is nonzero,
+  // starting on a multiple of 4 so the aligned reads stay aligned.
+  const int tlo = max(max(0, pl), ql - d0 - R + 1);
+  const int tend0 = min(min(n - d0, ph + 1), qh - d0 + 1);
+  const bool any = tlo < tend0;  // else every term is +0 and so is every sum
+  const int t0 = any ? (tlo & ~3) : 0;
+  const int tend = any ? tend0 : 0;
   double w[R];
 #pragma unroll
   for (int r = 0; r < R; ++r) {
     c[r] = 0.0;
-    w[r] = Q[d0 + r];
+    w[r] = Q[t0 + d0 + r];
   }
-  const int len = n - d0;
+  const int len = tend;
   auto step = [&](double p, double qnew) {
 #pragma unroll
     for (int r = 0; r < R; ++r) c[r] = __dadd_rn(c[r], __dmul_rn(w[r], p));
@@ -1770,7 +1781,7 @@ __device__ __forceinline__ void slide_lags(const double* P, const double* Q0, co
     for (int r = 0; r + 1 < R; ++r) w[r] = w[r + 1];
     w[R - 1] = qnew;
   };
-  int t = 0;
+  int t = t0;
   for (; t + 4 <= len; t += 4) {
     const double2 pa = *reinterpret_cast<const double2*>(P + t);
     const double2 pb = *reinterpret_cast<const double2*>(P + t + 2);
@@ -1819,7 +1830,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_RATIO_
   const int NPOS = NQ - qpos0;
   const int NNEG = n > R ? (n - R - 1) / R + 1 : 0;  // groups q < qneg0 with R q + R - 1 < n - 1
   const int NSTR = qpos0 - NNEG;                     // 0 or 1
+  int* sup = ired + 24;  // [pl, ph, ql, qh, nonfinite] of the current gene's rows
   for (int g = blockIdx.x; g < a.ngenes; g += gridDim.x) {
+    if (tid == 0) {
+      sup[0] = 1 << 30;
+      sup[1] = -1;
+      sup[2] = 1 << 30;
+      sup[3] = -1;
+      sup[4] = 0;
+    }
+    __syncthreads();
     for (int k = tid; k < NA && !a.xin; k += blockDim.x) {
       double va = 0.0, vb = 0.0;
       if (k < n) {
@@ -1833,8 +1853,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_RATIO_
       B[k] = vb;
       A1[k] = va;
       B1[k] = vb;
+      if (k < n) {
+        // supports of the two rows (nonzero entries); any non-finite value turns the
+        // restriction off (0 * inf is not +0)
+        if (va != 0.0) {
+          atomicMin(&sup[0], k);
+          atomicMax(&sup[1], k);
+        }
+        if (vb != 0.0) {
+          atomicMin(&sup[2], k);
+          atomicMax(&sup[3], k);
+        }
+        if (!isfinite(va) || !isfinite(vb) || va < 0.0 || vb < 0.0) sup[4] = 1;
+      }
     }
     __syncthreads();
+    int al = 0, ah = 1 << 30, bl = 0, bh = 1 << 30;
+    if (!a.xin && !sup[4]) {
+      al = sup[0];
+      ah = sup[1];
+      bl = sup[2];
+      bh = sup[3];
+    }
     // matSlideMult (src/matSlideMult.cpp:12-20): X[o] = sum_t A[t + max(s,0)] * B[t + max(-s,0)],
     // s = o - (n-1), t ascending, each product and sum rounded separately.
     dd ls = {0.0, 0.0};
@@ -1849,7 +1889,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_RATIO_
           double c[R];
           if (sd == 0) {  // pos, longest first: q = qpos0 + i, lags d = s0 .. s0 + R - 1
             const int q = qpos0 + i, o0 = R * q, s0 = o0 - (n - 1);
-            slide_lags<R>(B, A, A1, n, s0, c);
+            slide_lags<R>(B, A, A1, n, s0, c, bl, bh, al, ah);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               if (o0 + r < m) {
@@ -1859,7 +1899,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_RATIO_
             }
           } else if (i < NNEG) {  // neg, longest first: q = NNEG - 1 - i, lags -s0 - R + 1 ..
             const int q = NNEG - 1 - i, o0 = R * q, s0 = o0 - (n - 1);
-            slide_lags<R>(A, B, B1, n, -s0 - R + 1, c);
+            slide_lags<R>(A, B, B1, n, -s0 - R + 1, c, al, ah, bl, bh);
 #pragma unroll
             for (int r = 0; r < R; ++r) {
               const int o = o0 + R - 1 - r;
@@ -2335,7 +2375,7 @@ hipError_t launch_colmajor_to_rows(const double* src, int nrows, int ncols, int 
 hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const int NA = (a.n + 9) & ~1;
-  const size_t shm = sizeof(double) * (size_t)(4 * NA + 2 + ((2 * a.n - 1 + 49) & ~1) + 16) + sizeof(int) * 24;
+  const size_t shm = sizeof(double) * (size_t)(4 * NA + 2 + ((2 * a.n - 1 + 49) & ~1) + 16) + sizeof(int) * 32;
   // R = 4 by default: a 4-step unrolled loop rotates the R-wide register window fully (no
   // moves); measured fastest of R = 4, 5, 8 at n = 401
   const int grid = a.ngenes < 65536 ? a.ngenes : 65536;
