@@ -2215,7 +2215,7 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (a.U && a.ZU && a.mask && a.ubuf && a.redo && block <= 64 * kStretchSlots && !a.lds_stage &&
       sizeof(int2) * (size_t)a.ent_stride <= 60 * 1024) {
     // slack of the heuristic: UB's looseness grows with the draws per boot (~0.1 per cell)
-    double slack = 30.0 + 0.25 * a.ncells;
+    double slack = 30.0 + 0.4 * a.ncells;
     if (const char* e = getenv("SCDE_SKIP_SLACK")) slack = atof(e);  // tests: force post-check failures
     const size_t eshm = sizeof(int2) * (size_t)a.ent_stride;
 #define SCDE_SM(NBV)                                                                                              \
