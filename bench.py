@@ -1,13 +1,15 @@
 """bench.py -- genes/sec for scde.expression.difference (401-pt grid, 100 randomizations).
 
-Default workload (BASELINE.json configs[1] = SURVEY.md §8(d) config 2): synthetic 20,000 genes
-x 200 cells (100/100 groups), 400-point prior (G = 401 grid points), n.randomizations = 100,
-reference seeding n.cores = 1.  One step = one scde.expression.difference pass over the batch
-on counts resident in HBM: unique-count tables, per-cell NB/Poisson log-posterior tables,
-bootstrap joint posteriors for both groups, ratio posterior + lb/mle/ub/ce/Z summary, BH cZ,
-results to host.
+Default workload (north_star's headline = BASELINE.json configs[2] = SURVEY.md §8(d) config 3):
+synthetic 20,000 genes x 1,000 cells (500/500 groups), 400-point prior (G = 401 grid points),
+n.randomizations = 100, reference seeding n.cores = 1.  One step = one scde.expression.difference
+call as the R shim makes it: the host count matrix is uploaded, then unique-count tables,
+per-cell NB/Poisson log-posterior tables, bootstrap joint posteriors for both groups, ratio
+posterior + lb/mle/ub/ce/Z summary, BH cZ, and the result table lands in host memory
+(SURVEY.md §8(d)'s wall time).  The same pass on counts already resident in HBM is reported
+beside it as device_resident_genes_per_s.
 
---config 3: 20,000 genes x 1,000 cells (500/500), the north_star's headline shape.
+--config 2: 20,000 genes x 200 cells (100/100), BASELINE configs[1].
 --config 4: scde.posteriors(return.individual.posterior.modes = TRUE) on 30,000 genes x 2,000
 cells (one group); one step returns jp (N x 401) and modes (N x 2000) to the host.
 --config prior: scde.expression.prior on config 3's 20,000 x 1,000
@@ -20,9 +22,10 @@ both groups; one step = batch posteriors over all 200 cells with each group's ba
 composition, both group posteriors, the batch, group and 1601-column batch-adjusted ratio
 posteriors with their summaries and BH (three result tables to the host).
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): genes shard across ranks
-with a fixed gene count per rank (weak scaling); the one exchange is a gather of per-gene Z
-to rank 0 (RCCL) for the global BH adjustment, done there on the device.
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU.  Configs
+3 and 4 scale strongly by default (the fixed gene set split into contiguous shards, global
+seeding offsets); --scaling weak gives every rank a full gene set.  The one exchange is a gather
+of per-gene Z to rank 0 (RCCL) for the global BH adjustment, done there on the device.
 
 Prints ONE JSON line on rank 0.
 """
@@ -110,24 +113,27 @@ def dominant_kernel_bytes(ngenes, cells_per_group):
     return ngenes * (cells_per_group * (4 + 8 * G) + 8 * G)
 
 
-def profiled_traffic():
+BOOT_STAGE = "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum_partials)"
+
+
+def profiled_traffic(config: str):
     """HBM-side bytes per launch of the bootstrap stage from the newest committed rocprofv3
-    summary (profiles/rNN_summary.json, written by tools/profile.sh + tools/pmc_summary.py from
-    separate --pmc passes of this same command; FETCH_SIZE x2 per MI355X_MICROARCH.md).  The
-    stage is what bench times as one bootstrap launch: k_stretch_mask, the k_boot2 pass and
-    its redo pass, k_sum_partials; bytes and durations are summed over its kernels and
-    divided by the number of stages (the k_sum_partials calls)."""
+    summary of this config (profiles/rNN_config<C>_summary.json, written by tools/profile.sh +
+    tools/pmc_summary.py from separate --pmc passes of this same command; FETCH_SIZE x2 per
+    MI355X_MICROARCH.md).  The stage is what bench times as one bootstrap launch; bytes and
+    durations are summed over its kernels and divided by the number of stages (launches of
+    the stage's last kernel)."""
     d = os.path.join(ROOT, "profiles")
     if not os.path.isdir(d):
         return None
-    cands = sorted(f for f in os.listdir(d) if f.endswith("_summary.json"))
+    tag = f"_config{config}_summary.json"
+    cands = sorted(f for f in os.listdir(d) if f.endswith(tag))
     if not cands:
         return None
     with open(os.path.join(d, cands[-1])) as f:
         ks = json.load(f)["kernels"]
-    stage = {k: v for k, v in ks.items()
-             if (k.startswith("k_boot") and "exact" not in k) or k.startswith("k_stretch_mask") or k == "k_sum_partials"}
-    n = ks.get("k_sum_partials", {}).get("calls")
+    stage = {k: v for k, v in ks.items() if stage_kernel(k)}
+    n = max((v.get("calls") or 0 for k, v in stage.items() if stage_last(k)), default=0)
     if not stage or not n:
         return None
     if any(v.get("traffic_bytes") is None for v in stage.values()):
@@ -135,6 +141,16 @@ def profiled_traffic():
     return {"file": "profiles/" + cands[-1], "kernel": " + ".join(sorted(stage)),
             "avg_ms": sum(v["avg_ms"] * v["calls"] for v in stage.values()) / n,
             "traffic_bytes": sum(v["traffic_bytes"] * v["calls"] for v in stage.values()) / n}
+
+
+def stage_kernel(name: str) -> bool:
+    """Kernels of the bootstrap stage (bench's 'boot' slot)."""
+    return ((name.startswith("k_boot") and "exact" not in name) or name.startswith("k_stretch_mask")
+            or name == "k_sum_partials")
+
+
+def stage_last(name: str) -> bool:
+    return name == "k_sum_partials"
 
 
 def _cpu_chunk(job):
@@ -371,12 +387,27 @@ def _wpca_work(PG, pdev, sets):
     return tot[0], tot[1]
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="2", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="3", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", default=None, choices=["strong", "weak"],
+                    help="multi-GPU: strong = one fixed gene set split over the ranks (configs 3/4 default), "
+                         "weak = a full gene set per rank")
     ap.add_argument("--cpu-sample", type=int, default=None, help="genes timed on the CPU baseline (0 = skip)")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -385,7 +416,6 @@ def main():
                     help="oracle worker processes for the parallel CPU baseline (0 = skip; the GPU box's share is 16)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
-    NG, NC = cfg["genes"], cfg["cells"]
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -406,6 +436,7 @@ def main():
     from scde_amd import api
     from scde_amd.models import model_matrix
     from scde_amd.prior import expression_prior
+    from scde_amd.sharded import shard_range
 
     if cfg["kind"] == "prior":
         return bench_prior(args, cfg, rank, world, device)
@@ -413,14 +444,29 @@ def main():
         return bench_wpca(args, cfg, rank, world, device)
     de = cfg["kind"] in ("de", "de_batch")
     batched = cfg["kind"] == "de_batch"
-    models, counts, groups = synthetic(cfg["seed"] + rank, NG, NC, two_groups=de)
+    scaling = args.scaling or ("strong" if args.config in ("3", "4") else "weak")
+    if scaling == "strong":
+        # one data set of cfg genes, split by shard_range; global gene offsets keep the seeding
+        NTOT = cfg["genes"]
+        models, counts_all, groups = synthetic(cfg["seed"], NTOT, cfg["cells"], two_groups=de)
+        g0, g1 = shard_range(NTOT, world, rank)
+        counts = np.asfortranarray(counts_all[g0:g1])
+    else:
+        NTOT = cfg["genes"] * world
+        models, counts, groups = synthetic(cfg["seed"] + rank, cfg["genes"], cfg["cells"], two_groups=de)
+        counts_all = counts
+        g0 = rank * cfg["genes"]
+    NG, NC = counts.shape
     if batched:
         cfg["batch"] = synthetic_batch(cfg["seed"], NC, cfg["nbatch"])
     zero_frac = float(np.mean(counts == 0))
     ctx = api.Context(device)
-    dc = api.DeviceCounts(ctx, counts)
-    # the prior is an input of the measured path: computed once, on the GPU
-    prior = expression_prior(models, dc, length_out=LENGTH_OUT, ctx=ctx)
+    # the prior is an input of the measured path: computed once, on the GPU,
+    # from the whole data set (so every rank of a strong-scaling run holds the same grid)
+    dcp = api.DeviceCounts(ctx, counts_all)
+    prior = expression_prior(models, dcp, length_out=LENGTH_OUT, ctx=ctx)
+    dcp.free()
+    del counts_all
     mm, lt, sq = model_matrix(models)
     px = np.ascontiguousarray(prior["x"], np.float64)
     py = np.ascontiguousarray(prior["y"], np.float64)
@@ -428,10 +474,11 @@ def main():
     G = len(px)
     L = api.lib()
     P = api._p
+    counts_p = P(counts)
     if de:
         # one rank: cZ (BH) in the same call on device; several: Z gathered to rank 0, BH there
         params = api.DEParams(NC, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
-                              NBOOT, 1, rank * NG, world * NG, 0.0, api.get_rand_kind(), int(world == 1))
+                              NBOOT, 1, g0, NTOT, 0.0, api.get_rand_kind(), int(world == 1))
         res = np.zeros((NG, 6 if world == 1 else 5), order="F")
         if batched:
             blevels = sorted(set(cfg["batch"].tolist()))
@@ -442,34 +489,56 @@ def main():
         jp = np.zeros((NG, G), order="F")
         modes = np.zeros((NG, NC), order="F")
 
-    def step():
+    def run(dev_counts=None):
+        """One pass of the path.  dev_counts None: from the host count matrix (the timed
+        value: counts uploaded, every kernel, table back on the host); else the counts
+        already resident in HBM (the device-resident rate, reported beside it)."""
         if not de:
-            api.check(L.scde_posteriors_dev(ctx.handle, dc.ptr, NG, NG, P(cellidx), NC, P(mm), lt, sq, P(px), G, NBOOT,
-                                            1, rank * NG, world * NG, 1, 0, None, None, None, 0, P(jp), P(modes),
-                                            None))
+            if dev_counts is None:
+                api.check(L.scde_posteriors_host(ctx.handle, counts_p, NG, NG, NC, P(cellidx), NC, P(mm), lt, sq,
+                                                 P(px), G, NBOOT, 1, g0, NTOT, 1, 0, None, None, None, 0, P(jp),
+                                                 P(modes), None))
+            else:
+                api.check(L.scde_posteriors_dev(ctx.handle, dev_counts, NG, NG, P(cellidx), NC, P(mm), lt, sq, P(px),
+                                                G, NBOOT, 1, g0, NTOT, 1, 0, None, None, None, 0, P(jp), P(modes),
+                                                None))
             return
         if batched:
-            api.check(L.scde_expression_difference_batch_dev(ctx.handle, dc.ptr, NG, NG, ctypes.byref(params), P(mm),
-                                                             P(bcodes), len(blevels), P(res), None, None, None, None,
-                                                             None))
+            if dev_counts is None:
+                api.check(L.scde_expression_difference_batch_host(ctx.handle, counts_p, NG, NG, ctypes.byref(params),
+                                                                  P(mm), P(bcodes), len(blevels), P(res), None, None,
+                                                                  None, None, None))
+            else:
+                api.check(L.scde_expression_difference_batch_dev(ctx.handle, dev_counts, NG, NG,
+                                                                 ctypes.byref(params), P(mm), P(bcodes), len(blevels),
+                                                                 P(res), None, None, None, None, None))
+        elif dev_counts is None:
+            api.check(L.scde_expression_difference_host(ctx.handle, counts_p, NG, NG, ctypes.byref(params), P(res),
+                                                        None, None, None))
         else:
-            api.check(L.scde_expression_difference_dev(ctx.handle, dc.ptr, NG, NG, ctypes.byref(params),
-                                                       res.ctypes.data_as(ctypes.c_void_p), None, None, None))
+            api.check(L.scde_expression_difference_dev(ctx.handle, dev_counts, NG, NG, ctypes.byref(params), P(res),
+                                                       None, None, None))
         if dist is not None:
             import torch
-            # Z of every table (1 or 3) to rank 0; BH over all genes there
+            # Z of every table (1 or 3) to rank 0; BH over all genes there, cZ to the host
             zcols = [4, 10, 16] if batched else [4]
-            zt = torch.from_numpy(np.ascontiguousarray(res[:, zcols].T).reshape(-1))
+            per = -(-NTOT // world) if scaling == "strong" else NG
+            zt = torch.zeros((len(zcols), per), dtype=torch.float64)
+            zt[:, :NG] = torch.from_numpy(np.ascontiguousarray(res[:, zcols].T))
+            zt = zt.reshape(-1)
             if args.dist_backend == "nccl":
                 zt = zt.cuda()
             gathered = [torch.empty_like(zt) for _ in range(world)] if rank == 0 else None
             dist.gather(zt, gathered, dst=0)
             if rank == 0:
-                zall = torch.stack([t.view(len(zcols), NG) for t in gathered], 1).reshape(len(zcols), -1).cuda()
+                sizes = [(lambda b: b[1] - b[0])(shard_range(NTOT, world, r)) if scaling == "strong" else NG
+                         for r in range(world)]
+                zall = torch.cat([t.view(len(zcols), per)[:, :n] for t, n in zip(gathered, sizes)], 1).cuda()
                 cz = torch.empty_like(zall)
                 torch.cuda.current_stream().synchronize()
                 for k in range(len(zcols)):
                     api.bh_cz_device(ctx, zall[k].data_ptr(), zall.shape[1], cz[k].data_ptr())
+                ctx.synchronize()
                 cz_host = cz.cpu()  # noqa: F841  (the tables' last columns, on the host)
 
     def barrier():
@@ -479,25 +548,34 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
-    if not args.no_profile:
-        ctx.set_profiling(True)
-    ctx.reset_kernel_times()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    barrier()
-    dt = time.perf_counter() - t0
-    kt = ctx.kernel_times()
-    if dist is not None:
-        import torch
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
+    def timed(dev_counts=None, steps=args.steps, profile=False):
+        for _ in range(args.warmup):
+            run(dev_counts)
+        if profile:
+            ctx.set_profiling(True)
+        ctx.reset_kernel_times()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run(dev_counts)
+        barrier()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            import torch
+            tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            dt = float(tt.item())
+        return dt
 
-    total_genes = NG * world * args.steps
+    # the metric: host-resident counts -> host-resident result table
+    dt = timed()
+    # device-resident rate and per-kernel HIP-event times (counts already in HBM)
+    dc = api.DeviceCounts(ctx, counts)
+    dt_dev = timed(dc.ptr, profile=not args.no_profile)
+    kt = ctx.kernel_times()
+    ctx.set_profiling(False)
+
+    total_genes = NTOT * args.steps
     value = total_genes / dt
     boot_ms, boot_n = kt["boot"]
     boot_avg_s = (boot_ms / max(boot_n, 1)) / 1e3
@@ -507,12 +585,24 @@ def main():
     step_bytes = sum(dominant_kernel_bytes(NG, c) for c in launch_cells)
     per_launch_bytes = step_bytes / len(launch_cells)
     achieved = step_bytes * args.steps / (boot_ms / 1e3) / 1e9 if boot_n else None
-    prof = profiled_traffic() if args.config == "2" else None
+    prof = profiled_traffic(args.config)
     # reference-formulation FP64 adds per launch: B x C x G x N
     ref_adds = NBOOT * sum(launch_cells) / len(launch_cells) * G * NG
+    roof = {"bound": "hbm", "kernel": BOOT_STAGE,
+            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
+            "traffic": prof["traffic_bytes"] if prof else None,
+            "traffic_source": (f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"
+                               if prof else None),
+            "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
+            "algorithmic_bytes_per_launch": per_launch_bytes,
+            "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None}
+    if prof:
+        # what the stage really moves: counter bytes per stage over the rocprof stage time
+        roof["counter_bytes_frac"] = prof["traffic_bytes"] / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
     out = {
-        "metric": (METRIC_BATCH if batched else METRIC) if de else "genes/sec for scde.posteriors with posterior modes (400-pt grid, "
-                                    "100 randomizations)",
+        "metric": (METRIC_BATCH if batched else METRIC) if de else "genes/sec for scde.posteriors with posterior modes "
+                                                                   "(400-pt grid, 100 randomizations)",
         "value": value,
         "unit": "genes/s",
         "n_gpus": world,
@@ -520,35 +610,21 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
-        "data": f"synthetic (PCG64 seed {cfg['seed']}+rank; o.ifm-resampled models; zero fraction {zero_frac:.3f})",
-        "config": {"workload": cfg["workload"], "genes_per_gpu": NG, "cells": NC, "grid": G,
-                   "n_randomizations": NBOOT, "parallelism": f"gene-shard x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum_partials)",
-                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-                     "traffic": prof["traffic_bytes"] if prof else None,
-                     "traffic_source": (f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms)"
-                                        if prof else None),
-                     "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
-                     "algorithmic_bytes_per_launch": per_launch_bytes,
-                     "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None},
+        "data": f"synthetic (PCG64 seed {cfg['seed']}{'+rank' if scaling == 'weak' else ''}; o.ifm-resampled models; "
+                f"zero fraction {zero_frac:.3f})",
+        "config": {"workload": cfg["workload"], "genes_total": NTOT, "genes_per_gpu": NG, "cells": NC, "grid": G,
+                   "n_randomizations": NBOOT, "parallelism": f"gene-shard x{world} ({scaling})",
+                   "timed_region": "host counts -> upload -> unique tables, posteriors, ratio, summary, BH -> "
+                                   "host result table"},
+        "device_resident_genes_per_s": NTOT * args.steps / dt_dev,
+        "device_resident_ms_per_step": dt_dev / args.steps * 1e3,
+        "roofline": roof,
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
     }
-    if rank == 0 and world == 1 and de and not args.no_profile:
-        # PCIe-inclusive rate through the host-buffer API (counts uploaded, table incl. cZ
-        # returned per call) -- reported beside `value`, never as it.
-        ctx.set_profiling(False)
-        bkw = {"batch": cfg["batch"]} if batched else {}
-        api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
-                                       n_cores=1, ctx=ctx, **bkw)
-        t1 = time.perf_counter()
-        for _ in range(3):
-            api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NBOOT,
-                                           n_cores=1, ctx=ctx, **bkw)
-        out["host_buffers_genes_per_s"] = 3 * NG / (time.perf_counter() - t1)
+    dc.free()
     par = None
     if rank == 0 and world == 1 and cpu_sample > 0 and args.cpu_workers > 0:
         par = cpu_baseline_parallel(cfg, models, counts, groups, prior, cpu_sample * args.cpu_workers,
@@ -557,11 +633,13 @@ def main():
         what = ("batch + group posteriors, 3 ratio posteriors + summaries + BH" if batched else
                 "both groups + ratio + summary + BH" if de else "posteriors + modes")
         gps, secs = cpu_baseline(cfg, models, counts, groups, prior, cpu_sample)
-        single = {"value": gps, "unit": "genes/s", "cores": 1, "kind": "port",
+        cpu = cpu_model()
+        single = {"value": gps, "unit": "genes/s", "cores": 1, "kind": "port", "cpu": cpu,
                   "sample": f"oracle C restatement, first {cpu_sample} genes of the same batch, {what}, {secs:.1f}s"}
         if par is not None:
             n = min(cpu_sample * args.cpu_workers, NG)
             out["cpu_baseline"] = {"value": par[0], "unit": "genes/s", "cores": args.cpu_workers, "kind": "port",
+                                   "cpu": cpu,
                                    "sample": f"oracle C restatement in {args.cpu_workers} worker processes "
                                              f"(mclapply-style gene chunks, n.cores={args.cpu_workers} seeding), "
                                              f"first {n} genes of the same batch, {what}, {par[1]:.1f}s wall"}
@@ -570,7 +648,6 @@ def main():
             out["cpu_baseline"] = single
     if rank == 0:
         print(json.dumps(out))
-    dc.free()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -115,6 +115,18 @@ int scde_ctx_set_profiling(scde_ctx* ctx, int on);
  * 6 prior_bin, 7 prior_tail; ms totals and launch counts */
 int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslots);
 int scde_ctx_reset_kernel_times(scde_ctx* ctx);
+/* Tuning and test options of a context (defaults are the product settings; nothing is read
+ * from the environment on the compute path):
+ *   "boot_skip"     1/0  grid-stretch skipping in the bootstrap (output unchanged either way)
+ *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
+ *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
+ *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
+ *   "ratio_window"  k_ratio_summary register window 4, 5, 7 or 8;  "ratio_block" 64, 128, 256
+ *   "wpca_ms"       1/0  the multi-start npcs = 1 weighted-PCA kernel
+ * Statistics: "skip_slabs", "skip_stretches", "skip_kept", "skip_redo" (with skip_stats). */
+int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);
+int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
+int scde_ctx_reset_stats(scde_ctx* ctx);
 
 /* device buffers owned by the context's allocator */
 int scde_dev_alloc(scde_ctx* ctx, int64_t bytes, void** dptr);
@@ -166,6 +178,27 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
                                          const scde_de_params* p, const double* batch_models,
                                          const int* batch_codes, int nbatch, double* results, double* jp1,
                                          double* jp2, double* ratio, double* adj_ratio, double* batch_ratio);
+
+/* The same three calls on the caller's HOST count matrix, as the R shim makes them
+ * (R/functions.R:304 scde.expression.difference, :566 scde.posteriors; the R glue hands
+ * the count matrix to the native side once per call): counts int32 column-major with
+ * leading dimension ld >= ngenes and p->ncells (scde_posteriors_host: ncells_total)
+ * columns, staged into the context's device buffer on its stream, then the resident
+ * pipeline above.  ctx may be NULL: the process-wide default context (device
+ * $SCDE_DEVICE, created lazily on first use, i.e. after any fork). */
+int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes,
+                                    const scde_de_params* p, double* results, double* jp1, double* jp2,
+                                    double* ratio);
+int scde_expression_difference_batch_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes,
+                                          const scde_de_params* p, const double* batch_models,
+                                          const int* batch_codes, int nbatch, double* results, double* jp1,
+                                          double* jp2, double* ratio, double* adj_ratio, double* batch_ratio);
+int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes, int ncells_total,
+                         const int* cellidx, int ncells_sel, const double* models_sel, int local_theta,
+                         int square_logit_conc, const double* prior_x, int ngrid, int nboot, int n_cores,
+                         int64_t gene_offset, int64_t ngenes_total, int return_post, int ensemble,
+                         const int* batch_vals, const int64_t* batch_off, const int* composition, int nbatch,
+                         double* jp, double* modes, double* post);
 
 /* scde.expression.prior (R/functions.R:225-254; replaces the R-level function, which has
  * no .Call) on device-resident counts (ngenes x ncells int32, column stride ld).  models:

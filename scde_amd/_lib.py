@@ -18,10 +18,12 @@ EXPORTS = [
     "scde_logBootPosterior", "scde_logBootBatchPosterior", "scde_jpmatLogBoot", "scde_jpmatLogBatchBoot",
     "scde_matSlideMult", "scde_ratio_summary", "scde_distribution_summary", "scde_bh_cz",
     "scde_ctx_create", "scde_ctx_destroy", "scde_ctx_synchronize", "scde_ctx_set_profiling",
-    "scde_ctx_kernel_times", "scde_ctx_reset_kernel_times",
+    "scde_ctx_kernel_times", "scde_ctx_reset_kernel_times", "scde_ctx_set_option", "scde_ctx_get_stat",
+    "scde_ctx_reset_stats",
     "scde_dev_alloc", "scde_dev_free", "scde_h2d", "scde_d2h",
     "scde_expression_difference_dev", "scde_posteriors_dev", "scde_bh_cz_dev",
     "scde_expression_difference_batch_dev", "scde_expression_prior_dev",
+    "scde_expression_difference_host", "scde_expression_difference_batch_host", "scde_posteriors_host",
     "scde_baileyWPCA", "scde_bwpca_batch_dev", "scde_r_set_seed", "scde_r_unif_rand", "scde_r_sample",
     "scde_shuffle_perms", "scde_winsorizeMatrix", "scde_matWCorr", "scde_matCorr", "scde_plSemicompleteCor2",
 ]
@@ -87,6 +89,9 @@ def lib():
     L.scde_ctx_set_profiling.argtypes = [P, i]
     L.scde_ctx_kernel_times.argtypes = [P, P, P, i]
     L.scde_ctx_reset_kernel_times.argtypes = [P]
+    L.scde_ctx_set_option.argtypes = [P, ctypes.c_char_p, d]
+    L.scde_ctx_get_stat.argtypes = [P, ctypes.c_char_p, P]
+    L.scde_ctx_reset_stats.argtypes = [P]
     L.scde_dev_alloc.argtypes = [P, i64, ctypes.POINTER(P)]
     L.scde_dev_free.argtypes = [P, P]
     L.scde_h2d.argtypes = [P, P, P, i64]
@@ -95,6 +100,11 @@ def lib():
     L.scde_expression_difference_dev.argtypes = [P, P, i64, i, ctypes.POINTER(DEParams), P, P, P, P]
     L.scde_expression_difference_batch_dev.argtypes = [P, P, i64, i, ctypes.POINTER(DEParams), P, P, i, P, P, P, P,
                                                        P, P]
+    L.scde_expression_difference_host.argtypes = [P, P, i64, i, ctypes.POINTER(DEParams), P, P, P, P]
+    L.scde_expression_difference_batch_host.argtypes = [P, P, i64, i, ctypes.POINTER(DEParams), P, P, i, P, P, P, P,
+                                                        P, P]
+    L.scde_posteriors_host.argtypes = [P, P, i64, i, i, P, i, P, i, i, P, i, i, i, i64, i64, i, i, P, P, P, i, P, P,
+                                       P]
     L.scde_expression_prior_dev.argtypes = [P, P, i64, i, i, P, i, i, d, d, d, P, P, P, P, P, P]
     L.scde_posteriors_dev.argtypes = [P, P, i64, i, P, i, P, i, i, P, i, i, i, i64, i64, i, i, P, P, P, i, P, P, P]
     L.scde_baileyWPCA.argtypes = [P, P, i, i, i, i, i, d, i, P, i, P, P, P, P, P, P, P]

@@ -242,6 +242,18 @@ class Context:
     def reset_kernel_times(self):
         check(lib().scde_ctx_reset_kernel_times(self.handle))
 
+    def set_option(self, name: str, value: float):
+        """Tuning / test switches (include/scde_hip.h scde_ctx_set_option)."""
+        check(lib().scde_ctx_set_option(self.handle, name.encode(), float(value)))
+
+    def stat(self, name: str) -> float:
+        v = ctypes.c_double()
+        check(lib().scde_ctx_get_stat(self.handle, name.encode(), ctypes.byref(v)))
+        return v.value
+
+    def reset_stats(self):
+        check(lib().scde_ctx_reset_stats(self.handle))
+
 
 class DeviceCounts:
     """An int32 genes x cells count matrix resident in HBM (R column-major layout)."""
@@ -291,7 +303,8 @@ def _align_counts(models, counts):
             raise ValueError("ERROR: provided count data does not cover all of the cells specified in the model matrix")
         pos = {c: i for i, c in enumerate(cells)}
         mat = mat[:, [pos[r] for r in rn]]
-    if np.any(np.asarray(mat) != np.round(np.asarray(mat))):
+    mat = np.asarray(mat)
+    if not np.issubdtype(mat.dtype, np.integer) and np.any(mat != np.round(mat)):
         raise ValueError("counts must be integers")
     return np.asfortranarray(mat, dtype=np.int32), genes
 
@@ -327,21 +340,17 @@ def scde_posteriors(models, counts, prior, n_randomizations=100, batch=None, com
         else:
             comp = np.ascontiguousarray(composition, np.int32)
         nbatch = len(levels)
-    dc = DeviceCounts(ctx, mat)
-    try:
-        jp = np.zeros((N, G), order="F")
-        bt = batch is not None
-        want_modes = postflag == 1 if bt else postflag in (1, 3)
-        want_post = postflag == 2 if bt else postflag in (2, 3)
-        modes = np.zeros((N, C), order="F") if want_modes else None
-        post = np.zeros(C * N * G) if want_post else None
-        cellidx = np.arange(C, dtype=np.int32)
-        check(lib().scde_posteriors_dev(ctx.handle, dc.ptr, N, N, _p(cellidx), C, _p(mm), lt, sq, _p(prior_x), G,
-                                        int(n_randomizations), int(n_cores), 0, N, postflag,
-                                        int(bool(ensemble_posterior)), _p(bvals), _p(boff), _p(comp), nbatch,
-                                        _p(jp), _p(modes), _p(post)))
-    finally:
-        dc.free()
+    jp = np.zeros((N, G), order="F")
+    bt = batch is not None
+    want_modes = postflag == 1 if bt else postflag in (1, 3)
+    want_post = postflag == 2 if bt else postflag in (2, 3)
+    modes = np.zeros((N, C), order="F") if want_modes else None
+    post = np.zeros(C * N * G) if want_post else None
+    cellidx = np.arange(C, dtype=np.int32)
+    check(lib().scde_posteriors_host(ctx.handle, _p(mat), N, N, C, _p(cellidx), C, _p(mm), lt, sq, _p(prior_x), G,
+                                     int(n_randomizations), int(n_cores), 0, N, postflag,
+                                     int(bool(ensemble_posterior)), _p(bvals), _p(boff), _p(comp), nbatch,
+                                     _p(jp), _p(modes), _p(post)))
     if postflag == 0 or (bt and postflag == 3):
         return jp
     out = {"jp": jp}
@@ -427,18 +436,14 @@ def scde_expression_difference(models, counts, prior, groups=None, batch=None, n
         return _expression_difference_batch(models, mat, genes, prior, codes, np.asarray(batch), n_randomizations,
                                             n_cores, batch_models if batch_models is not None else models,
                                             return_posteriors, expectation, ctx)
-    dc = DeviceCounts(ctx, mat)
-    try:
-        params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
-                          int(n_randomizations), int(n_cores), 0, N, float(expectation), get_rand_kind(), 1)
-        res = np.zeros((N, 6), order="F")  # lb, mle, ub, ce, Z, cZ (BH on device)
-        jp1 = np.zeros((N, G), order="F") if return_posteriors else None
-        jp2 = np.zeros((N, G), order="F") if return_posteriors else None
-        ratio = np.zeros((N, 2 * G - 1), order="F") if return_posteriors else None
-        check(lib().scde_expression_difference_dev(ctx.handle, dc.ptr, N, N, ctypes.byref(params), _p(res),
-                                                   _p(jp1), _p(jp2), _p(ratio)))
-    finally:
-        dc.free()
+    params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
+                      int(n_randomizations), int(n_cores), 0, N, float(expectation), get_rand_kind(), 1)
+    res = np.zeros((N, 6), order="F")  # lb, mle, ub, ce, Z, cZ (BH on device)
+    jp1 = np.zeros((N, G), order="F") if return_posteriors else None
+    jp2 = np.zeros((N, G), order="F") if return_posteriors else None
+    ratio = np.zeros((N, 2 * G - 1), order="F") if return_posteriors else None
+    check(lib().scde_expression_difference_host(ctx.handle, _p(mat), N, N, ctypes.byref(params), _p(res), _p(jp1),
+                                                _p(jp2), _p(ratio)))
     table = _result_frame(res[:, :5], res[:, 5].copy(), genes)
     if return_posteriors:
         return {"results": table, "difference.posterior": RatioPosterior(ratio, ratio_columns(px), genes),
@@ -469,15 +474,11 @@ def _expression_difference_batch(models, mat, genes, prior, codes, batch, nrand,
     jp2 = np.zeros((N, G), order="F") if rp else None
     ratio = np.zeros((N, 2 * G - 1), order="F") if rp else None
     adj = np.zeros((N, 4 * G - 3), order="F") if rp else None
-    dc = DeviceCounts(ctx, mat)
-    try:
-        params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
-                          int(nrand), int(n_cores), 0, N, float(expectation), get_rand_kind(), 1)
-        check(lib().scde_expression_difference_batch_dev(ctx.handle, dc.ptr, N, N, ctypes.byref(params), _p(bmm),
-                                                         _p(bcodes), len(levels), _p(res), _p(jp1), _p(jp2),
-                                                         _p(ratio), _p(adj), None))
-    finally:
-        dc.free()
+    params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
+                      int(nrand), int(n_cores), 0, N, float(expectation), get_rand_kind(), 1)
+    check(lib().scde_expression_difference_batch_host(ctx.handle, _p(mat), N, N, ctypes.byref(params), _p(bmm),
+                                                      _p(bcodes), len(levels), _p(res), _p(jp1), _p(jp2), _p(ratio),
+                                                      _p(adj), None))
     tables = [_result_frame(res[:, 6 * k: 6 * k + 5], res[:, 6 * k + 5].copy(), genes) for k in range(3)]
     out = {"batch.adjusted": tables[0], "results": tables[1], "batch.effect": tables[2]}
     if rp:

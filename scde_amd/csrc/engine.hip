@@ -173,6 +173,18 @@ struct scde_ctx {
   Buf wp_probs, wp_blocks, wp_kidx, wp_cols, wp_perms, wp_starts, wp_scratch, wp_stat, wp_out, wp_smooth, wp_M, wp_W;
   // PAGODA helpers
   Buf pg_a, pg_b, pg_c, pg_d, pg_e;
+  // host-count entry points: the call's counts staged here (grow-only, reused across calls)
+  Buf counts_in;
+  // options (scde_ctx_set_option): tuning and test switches, never read from the environment
+  int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
+  double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 30 + 0.4 C); tests force redo slabs
+  int opt_boot_nb = 0;           // "boot_nb": boots per slab (0 = automatic; a multiple of 4 in [4, 32])
+  int opt_skip_stats = 0;        // "skip_stats": count kept stretches / redo slabs (a host sync per launch)
+  int opt_ratio_window = 4;      // "ratio_window": k_ratio_summary register window (4, 5, 7, 8)
+  int opt_ratio_block = 128;     // "ratio_block": k_ratio_summary block size (64, 128, 256)
+  int opt_wpca_ms = 1;           // "wpca_ms": the multi-start npcs = 1 kernel (k_wpca_ms1)
+  // statistics (scde_ctx_get_stat)
+  double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0;
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
   // unique tables can be built up front, with their host syncs, before the heavy kernels
   struct UniqueSet {
@@ -244,7 +256,7 @@ struct scde_ctx {
     Buf* wp[] = {&wp_probs, &wp_blocks,  &wp_kidx, &wp_cols,   &wp_perms, &wp_starts, &wp_scratch,
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
-                 &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e};
+                 &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
@@ -417,8 +429,8 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
 
 int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
-  // column stride: >= the k_boot2 block (lanes never read past a column); 512 lets
-  // k_boot3 move a column as four whole 1 KB LDS-DMA pieces
+  // column stride: >= the k_boot2 block (lanes never read past a column); 512 keeps
+  // columns 4 KiB-aligned
   const int GS = G <= 448 ? 512 : (int)round_up(G, 64);
   hipStream_t st = cx->stream;
   if (C <= 0 || G <= 0) return fail(SCDE_EARG, "ncells and ngrid must be positive");
@@ -478,7 +490,9 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   // columns D directly (phase 1: count-0 columns and base_col, phase 2: the rest); T itself
   // is kept only when individual posteriors are returned.
   const bool boot_path = s.nboot > 0 && (s.batch_call || !s.ensemble);
-  const bool fast = ((G + 63) / 64) * 64 <= 1024;
+  // k_boot2 forms column and multiplicity-row offsets in 32 bits: past that, the general kernel
+  const bool fast = ((G + 63) / 64) * 64 <= 1024 && (ncols + 1) * (long long)GS < (1LL << 31) &&
+                    (long long)C * round_up(std::max(s.nboot, 1), 32) < (1LL << 31);
   const bool fused = boot_path && fast;
   const bool want_post = s.batch_call ? (s.postflag == 2) : (s.postflag == 2 || s.postflag == 3);
   const bool keep_T = !fused || (want_post && s.post);
@@ -507,8 +521,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   ta.use_baseline = s.use_baseline ? 1 : 0;
   // k_boot2 grid-stretch skipping (G <= 448: at most 7 stretches of 64 points); the
   // tables kernel emits the per-column stretch maxima.  SCDE_BOOT_SKIP=0 disables it.
-  bool stretch_skip = fused && G <= 448;
-  if (const char* e = getenv("SCDE_BOOT_SKIP")) stretch_skip = stretch_skip && atoi(e) != 0;
+  const bool stretch_skip = fused && G <= 448 && cx->opt_boot_skip;
   if (fused) {
     HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
     HCHK(cx->base_col.ensure(sizeof(int) * std::max(1, C)));
@@ -566,10 +579,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   } else {
     int nb = fast ? boot2_nb(s.nboot) : 16;
     if (fast) {
-      if (const char* ev_nb = getenv("SCDE_BOOT_NB")) {  // tuning override: a multiple of 4 in [4, 32]
-        const int v = atoi(ev_nb);
-        if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
-      }
+      const int v = cx->opt_boot_nb;  // tuning option: a multiple of 4 in [4, 32]
+      if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
     }
     const int Bp = (int)round_up(s.nboot, nb);
     const int nsets = (int)s.seeds.size();
@@ -631,8 +642,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       b2.GS = GS;
       b2.nboot = s.nboot;
       b2.nb = nb;
-      b2.lds_stage = 0;  // LDS-DMA staging measured slower than k_boot2 at config 2
-      if (const char* ls = getenv("SCDE_LDS_STAGE")) b2.lds_stage = atoi(ls) != 0;
       const int P = (s.nboot + nb - 1) / nb;
       b2.part_stride = (long long)N * GS;
       HCHK(cx->part.ensure(sizeof(double) * std::max<size_t>(1, (size_t)P * N * GS)));
@@ -644,6 +653,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       b2.out_k = s.jp_k;
       b2.degen = cx->degen.as<int>();
       b2.ngenes = N;
+      b2.slack = cx->opt_skip_slack;
       b2.U = stretch_skip ? cx->ubound.as<double>() : nullptr;
       b2.ZU = stretch_skip ? cx->zubound.as<double>() : nullptr;
       if (stretch_skip) {
@@ -655,7 +665,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         b2.redo = cx->sredo.as<int>();
       }
       HCHK(launch_boot2(b2, st));
-      if (stretch_skip && getenv("SCDE_DEBUG_SKIP")) {  // diagnostics: skipped stretches, redo slabs
+      if (stretch_skip && cx->opt_skip_stats) {  // diagnostics: kept stretches, redo slabs
         std::vector<int> m((size_t)P * N), r((size_t)P * N);
         HCHK(hipMemcpyAsync(m.data(), cx->smask.p, sizeof(int) * m.size(), hipMemcpyDeviceToHost, st));
         HCHK(hipMemcpyAsync(r.data(), cx->sredo.p, sizeof(int) * r.size(), hipMemcpyDeviceToHost, st));
@@ -666,8 +676,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
           kept += __builtin_popcount((unsigned)m[i]);
           redo += r[i] != 0;
         }
-        fprintf(stderr, "[scde skip] C=%d slabs=%zu stretches kept %.3f, redo slabs %lld\n", C, m.size(),
-                (double)kept / (double)(m.size() * nst), redo);
+        cx->st_skip_slabs += (double)m.size();
+        cx->st_skip_stretches += (double)(m.size() * nst);
+        cx->st_skip_kept += (double)kept;
+        cx->st_skip_redo += (double)redo;
       }
     } else {
       BootArgs ba{};
@@ -896,6 +908,37 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx) {
     ctx->ms[i] = 0;
     ctx->launches[i] = 0;
   }
+  return SCDE_OK;
+}
+
+int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
+  if (!ctx || !name) return fail(SCDE_EARG, "null argument");
+  const std::string n(name);
+  if (n == "boot_skip") ctx->opt_boot_skip = value != 0;
+  else if (n == "skip_slack") ctx->opt_skip_slack = value;
+  else if (n == "boot_nb") ctx->opt_boot_nb = (int)value;
+  else if (n == "skip_stats") ctx->opt_skip_stats = value != 0;
+  else if (n == "ratio_window") ctx->opt_ratio_window = (int)value;
+  else if (n == "ratio_block") ctx->opt_ratio_block = (int)value;
+  else if (n == "wpca_ms") ctx->opt_wpca_ms = value != 0;
+  else return fail(SCDE_EARG, "unknown option '%s'", name);
+  return SCDE_OK;
+}
+
+int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
+  if (!ctx || !name || !value) return fail(SCDE_EARG, "null argument");
+  const std::string n(name);
+  if (n == "skip_slabs") *value = ctx->st_skip_slabs;
+  else if (n == "skip_stretches") *value = ctx->st_skip_stretches;
+  else if (n == "skip_kept") *value = ctx->st_skip_kept;
+  else if (n == "skip_redo") *value = ctx->st_skip_redo;
+  else return fail(SCDE_EARG, "unknown statistic '%s'", name);
+  return SCDE_OK;
+}
+
+int scde_ctx_reset_stats(scde_ctx* ctx) {
+  if (!ctx) return fail(SCDE_EARG, "null argument");
+  ctx->st_skip_slabs = ctx->st_skip_kept = ctx->st_skip_stretches = ctx->st_skip_redo = 0;
   return SCDE_OK;
 }
 
@@ -1172,6 +1215,8 @@ static int ratio_common(const double* pmat1, const double* pmat2, int nrows, int
   ra.res = res ? cx->res.as<double>() : nullptr;
   ra.res_ld = nrows;
   hipEvent_t ev = cx->mark_begin(SLOT_RATIO);
+  ra.window = cx->opt_ratio_window;
+  ra.block = cx->opt_ratio_block;
   HCHK(launch_ratio_summary(ra, st));
   cx->mark_end(SLOT_RATIO, ev);
   if (ratio && nrows) HCHK(hipMemcpyAsync(ratio, ra.ratio, sizeof(double) * nrows * m, hipMemcpyDeviceToHost, st));
@@ -1200,6 +1245,8 @@ int scde_distribution_summary(const double* rpost, int nrows, int m, const doubl
   ra.zi = zi;
   ra.res = cx->res.as<double>();
   ra.res_ld = nrows;
+  ra.window = cx->opt_ratio_window;
+  ra.block = cx->opt_ratio_block;
   HCHK(launch_ratio_summary(ra, st));
   if (nrows) HCHK(hipMemcpyAsync(res, ra.res, sizeof(double) * nrows * 5, hipMemcpyDeviceToHost, st));
   return cx->sync();
@@ -1365,6 +1412,8 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
   ra.res = ctx->res.as<double>();
   ra.res_ld = ngenes;
   hipEvent_t ev = ctx->mark_begin(SLOT_RATIO);
+  ra.window = ctx->opt_ratio_window;
+  ra.block = ctx->opt_ratio_block;
   HCHK(launch_ratio_summary(ra, st));
   ctx->mark_end(SLOT_RATIO, ev);
   if (p->compute_cz && ngenes) {
@@ -1528,6 +1577,8 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     ra.res = rres;
     ra.res_ld = N;
     hipEvent_t ev = ctx->mark_begin(SLOT_RATIO);
+    ra.window = ctx->opt_ratio_window;
+    ra.block = ctx->opt_ratio_block;
     HCHK(launch_ratio_summary(ra, st));
     ctx->mark_end(SLOT_RATIO, ev);
     if (N) HCHK(launch_bh_cz(rres + (size_t)4 * N, N, rres + (size_t)5 * N, ctx->bhw.p, &wb, st));
@@ -1564,6 +1615,65 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     transpose_rows_to_colmajor(tmp.data(), N, G, out);
   }
   return ctx->sync();
+}
+
+// ------------------------------------------------------------------ host-count entry points
+// The R-level calls as the .Call shim makes them: counts are the caller's host matrix
+// (int32, column-major, leading dimension ld >= ngenes, ncols columns).  They are copied
+// into the context's staging buffer (dense, ld = ngenes) on its stream and the resident
+// pipeline runs on them; everything the caller gets back is host memory.
+static int stage_counts(scde_ctx*& ctx, const int* counts, int64_t ld, int ngenes, int ncols, const int** dev) {
+  if (!ctx) RCHK(default_ctx(&ctx));
+  if (!counts) return fail(SCDE_EARG, "null argument");
+  if (ngenes < 0 || ncols <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
+  HCHK(hipSetDevice(ctx->device));
+  const size_t row = sizeof(int) * (size_t)ngenes;
+  HCHK(ctx->counts_in.ensure(std::max<size_t>(1, row * ncols)));
+  if (ngenes > 0) {
+    if (ld == ngenes)
+      HCHK(hipMemcpyAsync(ctx->counts_in.p, counts, row * ncols, hipMemcpyHostToDevice, ctx->stream));
+    else
+      HCHK(hipMemcpy2DAsync(ctx->counts_in.p, row, counts, sizeof(int) * (size_t)ld, row, ncols,
+                            hipMemcpyHostToDevice, ctx->stream));
+  }
+  *dev = ctx->counts_in.as<int>();
+  return SCDE_OK;
+}
+
+int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes,
+                                    const scde_de_params* p, double* results, double* jp1, double* jp2,
+                                    double* ratio) {
+  if (!p) return fail(SCDE_EARG, "null argument");
+  const int* dev = nullptr;
+  RCHK(stage_counts(ctx, counts, ld, ngenes, p->ncells, &dev));
+  return scde_expression_difference_dev(ctx, dev, ngenes, ngenes, p, results, jp1, jp2, ratio);
+}
+
+int scde_expression_difference_batch_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes,
+                                          const scde_de_params* p, const double* batch_models,
+                                          const int* batch_codes, int nbatch, double* results, double* jp1,
+                                          double* jp2, double* ratio, double* adj_ratio, double* batch_ratio) {
+  if (!p) return fail(SCDE_EARG, "null argument");
+  const int* dev = nullptr;
+  RCHK(stage_counts(ctx, counts, ld, ngenes, p->ncells, &dev));
+  return scde_expression_difference_batch_dev(ctx, dev, ngenes, ngenes, p, batch_models, batch_codes, nbatch,
+                                              results, jp1, jp2, ratio, adj_ratio, batch_ratio);
+}
+
+int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes, int ncells_total,
+                         const int* cellidx, int ncells_sel, const double* models_sel, int local_theta,
+                         int square_logit_conc, const double* prior_x, int ngrid, int nboot, int n_cores,
+                         int64_t gene_offset, int64_t ngenes_total, int return_post, int ensemble,
+                         const int* batch_vals, const int64_t* batch_off, const int* composition, int nbatch,
+                         double* jp, double* modes, double* post) {
+  if (!cellidx) return fail(SCDE_EARG, "null argument");
+  for (int i = 0; i < ncells_sel; ++i)
+    if (cellidx[i] < 0 || cellidx[i] >= ncells_total) return fail(SCDE_EARG, "cell index %d out of range", cellidx[i]);
+  const int* dev = nullptr;
+  RCHK(stage_counts(ctx, counts, ld, ngenes, ncells_total, &dev));
+  return scde_posteriors_dev(ctx, dev, ngenes, ngenes, cellidx, ncells_sel, models_sel, local_theta,
+                             square_logit_conc, prior_x, ngrid, nboot, n_cores, gene_offset, ngenes_total,
+                             return_post, ensemble, batch_vals, batch_off, composition, nbatch, jp, modes, post);
 }
 
 // ------------------------------------------------------------------ BH (host)
@@ -1990,8 +2100,7 @@ int scde_bwpca_batch_dev(scde_ctx* ctx, const double* M_dev, const double* W_dev
       kidx.push_back((int)(i - pos));
     }
     // npcs = 1 without smoothing: one workgroup per group of wpca_ms_group() starts
-    static const bool no_ms = getenv("SCDE_WPCA_NOMS") != nullptr;
-    const bool ms = K == 1 && L == 0 && wpca_ms_ok(n, dmax) && !no_ms;
+    const bool ms = K == 1 && L == 0 && wpca_ms_ok(n, dmax) && ctx->opt_wpca_ms;
     const int sstep = ms ? wpca_ms_group() : 1;
     for (size_t g0 = 0; g0 < chunk.size(); g0 += 8) {
       const size_t g1 = std::min(chunk.size(), g0 + 8);

@@ -99,7 +99,6 @@ struct Boot2Args {
   const int* wset;
   const double* Z;  // [nsets][Bp][GS]
   int G, GS, nboot, nb;
-  int lds_stage;  // use the LDS-DMA staged kernel (needs GS == 512, G <= 448)
   double norm_mult, degen_thresh;
   double* part;  // [ceil(nboot/nb)][ngenes][GS] per-slab partial jp rows
   long long part_stride;
@@ -114,6 +113,7 @@ struct Boot2Args {
   int* mask;     // [ngenes][P] needed-stretch bits (k_stretch_mask output)
   double* ubuf;  // [ngenes][P][8][nb] stretch upper bounds (k_stretch_mask output)
   int* redo;     // [ngenes][P] slabs whose skipped stretches failed the post-check
+  double slack;  // heuristic slack of the mask (NaN: the default 30 + 0.4 C)
 };
 
 struct ExactArgs {
@@ -161,6 +161,7 @@ struct RatioArgs {
   int zi;
   double* res;  // nullable; column-major res_ld x 5 (lb, mle, ub, ce, Z)
   long long res_ld;
+  int window, block;  // register-window width R (4, 5, 7, 8) and block size (64/128/256); 0 = default
 };
 
 hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,

@@ -18,6 +18,7 @@
 //   unique-count builder (R/functions.R:609-610 done on device), ELL entry
 //   builder, modes/post gathers, ensemble and nboot==0 variants.
 #include <hip/hip_runtime.h>
+#include <cmath>
 #include <cstdint>
 
 #include "device_math.h"
@@ -1219,13 +1220,19 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
   } else {
     block_max_f32_m<NB>(acc, reinterpret_cast<float*>(red), fin, lane, wid, nw, wmask, lw);
   }
-  if (wsid == lw && lane < NB && b0 + lane < nboot) {
-    if (!(fabs(fin[lane]) <= degen_thresh)) degen[g] = 1;
+  if (wsid == lw) {
+    const bool lb = lane < NB && b0 + lane < nboot;
     // post-check of the left-out stretches against the exact row maxima
-    if (smask)
+    bool fails = false;
+    if (smask && lb)
       for (int w = 0; w < nw; ++w)
         if (!((wmask >> w) & 1) && !(sub[((long long)(g * P + p) * kStretchSlots + w) * NB + lane] < fin[lane] - 51.0))
-          redo[(long long)g * P + p] = 1;
+          fails = true;
+    const bool flagged = __builtin_amdgcn_ballot_w64(fails) != 0;
+    if (flagged && lane == 0) redo[(long long)g * P + p] = 1;
+    // a flagged slab's maxima cover the surviving stretches only: the redo pass, with every
+    // stretch, decides its degenerate flag
+    if (!flagged && lb && !(fabs(fin[lane]) <= degen_thresh)) degen[g] = 1;
   }
   // Softmax terms below e^kBootExpCut (1.9e-22) are dropped: a jp entry loses at most
   // that much (each boot's row sums to >= 1 before the 1/B weighting), far below the
@@ -1251,118 +1258,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
     block_sum_m<NB>(acc, live, red, fin, lane, wid, nw, wmask, lw);
   }
   if (wsid == lw && lane < NB) fin[lane] = (b0 + lane < nboot) ? 1.0 / (fin[lane] * norm_mult) : 0.0;
-  __syncthreads();
-  double jpv = 0.0;
-#pragma unroll
-  for (int i = 0; i < NB; ++i) jpv = fma(acc[i], fin[i], jpv);
-  if (live) part[(long long)p * part_stride + (long long)g * GS + tid] = jpv;
-}
-
-// ---- K2 with LDS-DMA staging (k_boot3) ----
-// Same slab decomposition as k_boot2, for G <= 448 with GS == 512: the block is 8
-// waves (512 lanes; lanes >= G only stage).  An 8-entry batch of baseline-delta
-// columns (8 x 4 KB) is moved HBM/L2 -> LDS by global_load_lds_dwordx4: each wave
-// issues exactly 4 lane-linear 1 KB pieces per batch, so a counted vmcnt(4) retires
-// the previous batch while the next one stays in flight across the raw s_barrier.
-template <int NB>
-__global__ __launch_bounds__(512, 2) void k_boot3(const double* __restrict__ D, const int2* __restrict__ ent,
-                                                  const int* __restrict__ nnz, int ent_stride,
-                                                  const double* __restrict__ Wt, int Bp, int ncells,
-                                                  const int* __restrict__ wset, const double* __restrict__ Z, int G,
-                                                  int P, int nboot, double norm_mult, double degen_thresh,
-                                                  double* __restrict__ part, long long part_stride,
-                                                  int* __restrict__ degen, int ngenes) {
-  __shared__ double etab[64];
-  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];  // read after the first barrier
-  static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
-  constexpr int GS = 512, EB = 8;
-  __shared__ __attribute__((aligned(16))) double stage[2][EB][GS];
-  __shared__ double red[16 * 32];
-  __shared__ double fin[32];
-  const int tid = threadIdx.x, lane = tid & 63, nw = blockDim.x >> 6;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar entry loads)
-  const bool live = tid < G;
-  const int within = blockIdx.x % (8 * P);
-  const int p = within >> 3;
-  const int g = (blockIdx.x / (8 * P)) * 8 + (within & 7);
-  if (g >= ngenes) return;  // uniform over the block
-  const int b0 = p * NB;
-  const int n = nnz[g];
-  const int2* __restrict__ E = ent + (long long)g * ent_stride;
-  const int set = wset ? wset[g] : 0;
-  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
-  const double* __restrict__ Zs = Z ? Z + (long long)set * Bp * GS : nullptr;
-  // wave w stages column (w >> 2) * 2 + {0,1}... simpler: piece q = w*4 + i covers
-  // column q >> 2, quarter q & 3 (EB * 4 = 32 pieces, 8 waves x 4)
-  // The DMA is issued from inline asm so the compiler's waitcnt pass does not see it
-  // (it would drain it with vmcnt(0) before every LDS read); this kernel counts it:
-  // every wave has exactly 4 pieces in flight per batch.
-  auto issue = [&](int e0, int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int q = wid * 4 + i;
-      const int j = q >> 2, quarter = q & 3;
-      const int col = __builtin_amdgcn_readfirstlane(E[e0 + j].y);
-      const double* src = D + (long long)col * GS + quarter * 128 + lane * 2;
-      const unsigned dst = __builtin_amdgcn_readfirstlane(
-          (unsigned)(unsigned long long)(const void*)&stage[buf][j][quarter * 128]);
-      unsigned keep;
-      asm volatile(
-          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-          : "=&s"(keep)
-          : "v"(src), "s"(dst)
-          : "memory");
-    }
-  };
-  double acc[NB];
-  // lanes past the grid start at -inf: their pad columns are 0, so they stay -inf, never
-  // win a max and exp to 0 -- the reductions need no per-lane select
-#pragma unroll
-  for (int i = 0; i < NB; ++i) acc[i] = !live ? -INFINITY : (Zs ? Zs[(long long)(b0 + i) * GS + tid] : 0.0);
-#pragma unroll
-  for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));  // materialise now: no compiler vmcnt in the loop
-  issue(0, 0);
-  int buf = 0;
-  for (int e0 = 0; e0 < n; e0 += EB) {
-    issue(e0 + EB, buf ^ 1);  // ELL rows carry one extra zero-column batch
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    int cell[EB];
-    double v[EB];
-#pragma unroll
-    for (int j = 0; j < EB; ++j) {
-      cell[j] = E[e0 + j].x;
-      v[j] = stage[buf][j][tid];
-    }
-#pragma unroll
-    for (int i0 = 0; i0 < NB; i0 += 2) {
-      double2 w[EB];
-#pragma unroll
-      for (int j = 0; j < EB; ++j)
-        w[j] = *reinterpret_cast<const double2*>(W + (long long)__builtin_amdgcn_readfirstlane(cell[j]) * Bp + b0 +
-                                                 i0);
-#pragma unroll
-      for (int j = 0; j < EB; ++j) {
-        acc[i0] = fma(w[j].x, v[j], acc[i0]);
-        acc[i0 + 1] = fma(w[j].y, v[j], acc[i0 + 1]);
-      }
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // everyone has read `buf` before it is refilled
-    buf ^= 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // ---- per-boot softmax over the grid: max, exp, sum (one LDS round each) ----
-  block_reduce_all<true, NB>(acc, live, red, fin, lane, wid, nw);
-  if (tid < NB && b0 + tid < nboot && !(fabs(fin[tid]) <= degen_thresh)) degen[g] = 1;
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const double d = acc[i] - fin[i];
-    acc[i] = (live && d >= -746.0) ? exp_tab(d, etab) : 0.0;
-    if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-  }
-  block_reduce_all<false, NB>(acc, live, red, fin, lane, wid, nw);
-  if (tid < NB) fin[tid] = (b0 + tid < nboot) ? 1.0 / (fin[tid] * norm_mult) : 0.0;
   __syncthreads();
   double jpv = 0.0;
 #pragma unroll
@@ -2212,11 +2107,10 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   const int* smask = nullptr;
   const double* sub = nullptr;
   // (the mask kernel stages a gene's entry list in LDS: up to ~7,600 cells)
-  if (a.U && a.ZU && a.mask && a.ubuf && a.redo && block <= 64 * kStretchSlots && !a.lds_stage &&
+  if (a.U && a.ZU && a.mask && a.ubuf && a.redo && block <= 64 * kStretchSlots &&
       sizeof(int2) * (size_t)a.ent_stride <= 60 * 1024) {
     // slack of the heuristic: UB's looseness grows with the draws per boot (~0.1 per cell)
-    double slack = 30.0 + 0.4 * a.ncells;
-    if (const char* e = getenv("SCDE_SKIP_SLACK")) slack = atof(e);  // tests: force post-check failures
+    const double slack = std::isnan(a.slack) ? 30.0 + 0.4 * a.ncells : a.slack;  // tests force post-check failures
     const size_t eshm = sizeof(int2) * (size_t)a.ent_stride;
 #define SCDE_SM(NBV)                                                                                              \
   case NBV:                                                                                                        \
@@ -2242,18 +2136,7 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
                        a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
                        a.part_stride, a.degen, a.ngenes, smask, sub, a.redo, RP);                             \
     break;
-#define SCDE_B3(NBV)                                                                                              \
-  case NBV:                                                                                                        \
-    hipLaunchKernelGGL(k_boot3<NBV>, dim3(grid), dim3(512), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,   \
-                       a.ncells, a.wset, a.Z, a.G, P, a.nboot, a.norm_mult, a.degen_thresh, a.part, a.part_stride, \
-                       a.degen, a.ngenes);                                                                         \
-    break;
-  if (a.GS == 512 && a.G <= 448 && a.lds_stage) {
-    switch (a.nb) {
-      SCDE_B3(4) SCDE_B3(8) SCDE_B3(12) SCDE_B3(16) SCDE_B3(20) SCDE_B3(24) SCDE_B3(28) SCDE_B3(32)
-      default: return hipErrorInvalidValue;
-    }
-  } else {
+  {
     // pass 0: with skipping (when set up); pass 1: the slabs the post-check flagged
     const int npass = smask ? 2 : 1;
     for (int RP = 0; RP < npass; ++RP) {
@@ -2265,7 +2148,6 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
     }
   }
 #undef SCDE_B2
-#undef SCDE_B3
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const long long n = (long long)a.ngenes * a.G;
@@ -2379,15 +2261,9 @@ hipError_t launch_ratio_summary(const RatioArgs& a, hipStream_t s) {
   // R = 4 by default: a 4-step unrolled loop rotates the R-wide register window fully (no
   // moves); measured fastest of R = 4, 5, 8 at n = 401
   const int grid = a.ngenes < 65536 ? a.ngenes : 65536;
-  static int rsel = -1, bsel = -1;
-  if (rsel < 0) {  // tuning overrides
-    const char* r = getenv("SCDE_RATIO_R");
-    const char* b = getenv("SCDE_RATIO_BLOCK");
-    rsel = r ? atoi(r) : 4;
-    if (rsel != 4 && rsel != 5 && rsel != 7 && rsel != 8) rsel = 4;
-    bsel = b ? atoi(b) : 128;
-    if (bsel != 64 && bsel != 128 && bsel != 256) bsel = 128;
-  }
+  int rsel = a.window, bsel = a.block;  // tuning options of the context (scde_ctx_set_option)
+  if (rsel != 4 && rsel != 5 && rsel != 7 && rsel != 8) rsel = 4;
+  if (bsel != 64 && bsel != 128 && bsel != 256) bsel = 128;
   switch (rsel) {
     case 7: hipLaunchKernelGGL(k_ratio_summary<7>, dim3(grid), dim3(bsel), shm, s, a); break;
     case 8: hipLaunchKernelGGL(k_ratio_summary<8>, dim3(grid), dim3(bsel), shm, s, a); break;

@@ -34,7 +34,7 @@ def _inputs():
     return models, counts, prior, g["groups"]
 
 
-def oracle_shard(models, counts_shard, prior, codes, nrand, n_cores, expectation, lo, N):
+def oracle_shard(models, counts_shard, prior, codes, nrand, n_cores, expectation, lo, N, ctx=None):
     """Per-shard compute for the CPU tests: the oracle restatement on rows [lo, lo+n)."""
     from oracle import oracle as O
     r = O.scde_expression_difference(models, counts_shard, prior["x"], prior["y"], codes, n_randomizations=nrand,
@@ -42,21 +42,37 @@ def oracle_shard(models, counts_shard, prior, codes, nrand, n_cores, expectation
     return np.column_stack([r[k] for k in ("lb", "mle", "ub", "ce", "Z")])
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, hip=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if hip:
+        os.environ["SCDE_SAME_DEVICE"] = "1"  # every rank on the one GPU of the box
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from scde_amd import sharded
+        from scde_amd import api, sharded
         models, counts, prior, groups = _inputs()
+        if hip:
+            api.set_rand("glibc")
         tab = sharded.expression_difference(models, counts, prior, list(groups), n_randomizations=NRAND,
-                                            n_cores=NCORES, compute=oracle_shard)
+                                            n_cores=NCORES, compute=None if hip else oracle_shard)
         if rank == 0:
             np.save(out_path, tab[["lb", "mle", "ub", "ce", "Z", "cZ"]].to_numpy())
         else:
             assert tab is None
     finally:
         dist.destroy_process_group()
+
+
+def test_rank_device(monkeypatch):
+    from scde_amd.sharded import rank_device
+    monkeypatch.delenv("SCDE_SAME_DEVICE", raising=False)
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert rank_device(13) == 5
+    monkeypatch.delenv("LOCAL_RANK")
+    assert rank_device(3) == 3
+    monkeypatch.setenv("SCDE_SAME_DEVICE", "1")
+    monkeypatch.setenv("LOCAL_RANK", "5")
+    assert rank_device(13) == 0
 
 
 def test_shard_range_partition():
@@ -113,3 +129,21 @@ def test_device_shards_match_unsharded():
     for j in range(4):
         np.testing.assert_array_equal(full[:, j], want[:, j])
     np.testing.assert_allclose(full[:, 4], want[:, 4], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_gloo_hip_shards_match_single_process(tmp_path):
+    """Two ranks, each running the HIP path on its shard (both on the box's one GPU), gather
+    to rank 0 with cZ there: the table equals the single-process HIP call."""
+    import torch.multiprocessing as mp
+    from scde_amd import api
+    out = str(tmp_path / "tab.npy")
+    mp.spawn(_worker, args=(2, _free_port(), out, True), nprocs=2, join=True)
+    got = np.load(out)
+    models, counts, prior, groups = _inputs()
+    api.set_rand("glibc")
+    ref = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NRAND,
+                                         n_cores=NCORES)
+    want = ref[["lb", "mle", "ub", "ce", "Z", "cZ"]].to_numpy()
+    np.testing.assert_array_equal(got[:, :4], want[:, :4])
+    np.testing.assert_allclose(got[:, 4:], want[:, 4:], rtol=1e-6, atol=1e-9)

@@ -4,11 +4,14 @@ The skipping is an optimisation that must not change results: a 64-point stretch
 left out of a boot slab when a rigorous upper bound of its row values stays more than 51
 below the exact row maximum (post-check), i.e. when every softmax term there falls under
 the e^-50 cut that zeroes it anyway; any slab that fails the check is recomputed whole.
-These tests run the same calls with skipping on (default), off (SCDE_BOOT_SKIP=0), and
-with a negative heuristic slack (SCDE_SKIP_SLACK) that makes the mask drop stretches the
-post-check must reject, so the redo launch carries real work -- and compare all three
-with the oracle at the SURVEY §8(d) bar.
+These tests run the same calls with skipping on (default), off (context option
+boot_skip = 0), and with a negative heuristic slack (skip_slack) that makes the mask drop
+stretches the post-check must reject, so the redo launch carries real work (its count is
+read back and must be > 0) -- and compare all three with the oracle at the SURVEY §8(d)
+bar, and with each other bit for bit.
 """
+import math
+
 import numpy as np
 import pytest
 
@@ -24,18 +27,26 @@ def api():
     return A
 
 
-def _run(api, monkeypatch, env, models, counts, prior, groups, nrand, ncores):
-    for k in ("SCDE_BOOT_SKIP", "SCDE_SKIP_SLACK"):
-        monkeypatch.delenv(k, raising=False)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+def _run(api, opts, models, counts, prior, groups, nrand, ncores):
+    ctx = api.default_context()
+    ctx.set_option("boot_skip", opts.get("boot_skip", 1))
+    ctx.set_option("skip_slack", opts.get("skip_slack", math.nan))
+    ctx.set_option("skip_stats", 1)
+    ctx.reset_stats()
     api.set_rand("glibc")
-    return api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=nrand,
-                                          n_cores=ncores, return_posteriors=True)
+    try:
+        out = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=nrand,
+                                             n_cores=ncores, return_posteriors=True)
+        stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo")}
+    finally:
+        ctx.set_option("boot_skip", 1)
+        ctx.set_option("skip_slack", math.nan)
+        ctx.set_option("skip_stats", 0)
+    return out, stats
 
 
 @pytest.mark.parametrize("seed,ngenes,ncells,nrand,ncores", [(8002, 300, 200, 100, 1), (8003, 120, 1000, 40, 3)])
-def test_skip_modes_match_oracle(api, oracle, monkeypatch, seed, ngenes, ncells, nrand, ncores):
+def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncores):
     import bench
     from scde_amd.prior import expression_prior
     models, counts, groups = bench.synthetic(seed, ngenes, ncells)
@@ -44,16 +55,32 @@ def test_skip_modes_match_oracle(api, oracle, monkeypatch, seed, ngenes, ncells,
                                             n_cores=ncores, return_posteriors=True)
     runs = {
         "skip": {},
-        "noskip": {"SCDE_BOOT_SKIP": "0"},
-        "forced-redo": {"SCDE_SKIP_SLACK": "-45"},
+        "noskip": {"boot_skip": 0},
+        "forced-redo": {"skip_slack": -45.0},
     }
-    for name, env in runs.items():
-        got = _run(api, monkeypatch, env, models, counts, prior, groups, nrand, ncores)
+    got = {}
+    for name, opts in runs.items():
+        got[name], stats = _run(api, opts, models, counts, prior, groups, nrand, ncores)
+        if name == "noskip":
+            assert stats["skip_slabs"] == 0
+        else:
+            assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
+        if name == "forced-redo":
+            assert stats["skip_redo"] > 0, stats  # the redo launch really recomputes slabs
+        g = got[name]
         for i in range(2):
-            assert_posterior_close(got["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"{name} jp{i}")
-        assert_posterior_close(got["difference.posterior"].values, ref["difference.posterior"], what=f"{name} ratio")
-        res = got["results"]
+            assert_posterior_close(g["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"{name} jp{i}")
+        assert_posterior_close(g["difference.posterior"].values, ref["difference.posterior"], what=f"{name} ratio")
+        res = g["results"]
         for k in ("lb", "mle", "ub", "ce"):
             np.testing.assert_array_equal(res[k].to_numpy(), ref["results"][k], err_msg=f"{name} {k}")
         assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"], what=f"{name} Z")
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
+    # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
+    for name in ("noskip", "forced-redo"):
+        for i in range(2):
+            np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got["skip"]["joint.posteriors"][i])
+        np.testing.assert_array_equal(got[name]["difference.posterior"].values,
+                                      got["skip"]["difference.posterior"].values)
+        for k in ("Z", "cZ"):
+            np.testing.assert_array_equal(got[name]["results"][k].to_numpy(), got["skip"]["results"][k].to_numpy())
