@@ -18,6 +18,7 @@
 //   unique-count builder (R/functions.R:609-610 done on device), ELL entry
 //   builder, modes/post gathers, ensemble and nboot==0 variants.
 #include <hip/hip_runtime.h>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 
@@ -148,8 +149,8 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
                                               const double* __restrict__ mu, const double* __restrict__ P,
                                               const double* __restrict__ lcfpr, const double* __restrict__ lcfp,
                                               const double* __restrict__ th, const double* __restrict__ base,
-                                              double* __restrict__ v, const double* etab, const LogTab& lt, int lane,
-                                              int PS) {
+                                              const long long* __restrict__ qbase, double* __restrict__ v,
+                                              const double* etab, const LogTab& lt, int lane, int PS) {
   const int G = a.G;
   const double x = (double)a.ucl[col];
   const double maxcfp = a.cellscal[2 * c];
@@ -236,12 +237,17 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   bool clamp = false;
   double* out = a.T ? a.T + col * a.GS : nullptr;
   // fused delta (phase 2): D = T - T[baseline column of the cell], as k_delta computes it
-  double* dout = phase ? a.D + col * a.GS : nullptr;
+  double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
   const int bc_u = (phase == 2) ? a.base_col[c] : -1;
   // per 64-point stretch j (grid points 64j .. 64j+63, one k_boot2 wave each): the
   // column's maximum, for k_boot2's stretch bounds (U: raw maxima for phase-1 columns,
   // maxima minus the cell's baseline-column maxima for phase-2 columns)
   const double* ubase = (a.U && bc_u >= 0) ? a.U + (long long)bc_u * kStretchSlots : nullptr;
+  // fixed-point output (k_bootq): q, or q - q[base] in phase 2; the row of final digits'
+  // values (int64) for the tile bounds
+  unsigned long long* qout = (phase && a.DQ) ? a.DQ + col * a.GS : nullptr;
+  long long* vq = reinterpret_cast<long long*>(v);
+  bool nanq = false;
 #pragma unroll 1
   for (int j = 0; 64 * j < G; ++j) {
     const int k = lane + 64 * j;
@@ -266,6 +272,37 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         if (dout) dout[k] = base ? r - base[k] : r;
       }
       if (a.U) v[k] = r;  // the row of final values, for the stretch maxima below
+      if (qout) {
+        long long q = 0;
+        if (r != r)
+          nanq = true;
+        else if (r < -kQSat)
+          q = -(1LL << kQSatLog2);
+        else if (r < 0.0)
+          q = __double2ll_rn(r * 0x1p36);  // exact scaling by 2^kQFrac, one rounding
+        const long long d = qbase ? q - qbase[k] : q;
+        qout[k] = packq(d);
+        vq[k] = d;
+      }
+    }
+  }
+  if (qout) {
+    if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
+    for (int k = G + lane; k < a.GS; k += 64) qout[k] = 0ull;
+    // per 16-point tile: the maximum of the stored values, rounded up to 2^-kQUFrac (two
+    // lanes per tile, 8 points each); tiles past the grid: 0
+    const int nt = (G + 15) / 16, t = lane >> 1;
+    long long m = LLONG_MIN;
+    if (t < nt)
+      for (int i = 0; i < 8; ++i) {
+        const int k = 16 * t + 8 * (lane & 1) + i;
+        if (k < G) m = vq[k] > m ? vq[k] : m;
+      }
+    const long long o = __shfl_xor(m, 1, 64);
+    m = o > m ? o : m;
+    if ((lane & 1) == 0) {
+      const int u = (t < nt) ? (int)(-((-m) >> (kQFrac - kQUFrac))) : 0;  // ceil(m / 2^28)
+      a.UQ[col * kQTiles + t] = packu(u);
     }
   }
   if (a.U) {
@@ -325,6 +362,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   tables_tabs(etab, ltab);
   __syncthreads();
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
+  if (a.gate && *a.gate == 0) return;
   const int phase = a.phase;
   long long col;
   int c;
@@ -351,8 +389,12 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   } else {
     col = (long long)blockIdx.x * 4 + wid;
     if (phase == 2 && col == a.ncols) {  // the ELL pad column
-      for (int k = lane; k < a.GS; k += 64) a.D[col * a.GS + k] = 0.0;
+      for (int k = lane; k < a.GS; k += 64) {
+        if (a.D) a.D[col * a.GS + k] = 0.0;
+        if (a.DQ) a.DQ[col * a.GS + k] = 0ull;
+      }
       if (a.U && lane < kStretchSlots) a.U[col * kStretchSlots + lane] = 0.0;
+      if (a.UQ && lane < kQTiles) a.UQ[col * kQTiles + lane] = 0u;
       return;
     }
     if (col >= a.ncols) return;
@@ -366,9 +408,9 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   }
   const long long co = (long long)c * a.GS;
   const int bc = (phase == 2) ? a.base_col[c] : -1;
-  const double* base = (bc >= 0) ? a.D + (long long)bc * a.GS : nullptr;
+  const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
   tables_column<CT>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co, a.lcfp + co,
-                    a.theta + co, base, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
+                    a.theta + co, base, nullptr, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
 }
 
 // Cell-staged form (phases 0 and 2, G <= kTabStagedG): one 8-wave block per task
@@ -387,13 +429,18 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int GS = a.GS, G = a.G;
   tables_tabs(etab, ltab);
+  if (a.gate && *a.gate == 0) return;
   const int4 task = a.tasks[blockIdx.x];
   const int c = task.x;
   const int phase = a.phase;
   if (c < 0) {  // the ELL pad column (phase 2)
     if (wid == 0) {
-      for (int k = lane; k < GS; k += 64) a.D[a.ncols * GS + k] = 0.0;
+      for (int k = lane; k < GS; k += 64) {
+        if (a.D) a.D[a.ncols * GS + k] = 0.0;
+        if (a.DQ) a.DQ[a.ncols * GS + k] = 0ull;
+      }
       if (a.U && lane < kStretchSlots) a.U[a.ncols * kStretchSlots + lane] = 0.0;
+      if (a.UQ && lane < kQTiles) a.UQ[a.ncols * kQTiles + lane] = 0u;
     }
     return;
   }
@@ -418,15 +465,22 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
       sP[2 * G + k] = P[2 * GS + k];
       sP[3 * G + k] = P[3 * GS + k];
     }
-    if (bc >= 0) sbase[k] = a.D[(long long)bc * GS + k];
+    if (bc >= 0) {
+      if (a.DQ)
+        reinterpret_cast<long long*>(sbase)[k] = unpackq(a.DQ[(long long)bc * GS + k]);
+      else
+        sbase[k] = a.D[(long long)bc * GS + k];
+    }
   }
   __syncthreads();
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
   const int zc = (phase == 2) ? a.zcol[c] : -1;
   for (int col = task.y + wid; col < task.z; col += kTabWaves) {
     if (col == zc) continue;  // done in phase 1
-    tables_column<CT>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, slc, sth, bc >= 0 ? sbase : nullptr,
-                      dyn + wid * G, etab, lt, lane, G);
+    tables_column<CT>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, slc, sth,
+                      (bc >= 0 && !a.DQ) ? sbase : nullptr,
+                      (bc >= 0 && a.DQ) ? reinterpret_cast<const long long*>(sbase) : nullptr, dyn + wid * G, etab,
+                      lt, lane, G);
   }
 }
 
@@ -459,7 +513,7 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
 __global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
                                              int ncells, const long long* __restrict__ ucl_off,
                                              const int* __restrict__ base_col, int stride, int pad_col,
-                                             int2* __restrict__ ent, int* __restrict__ nnz) {
+                                             int padto, int2* __restrict__ ent, int* __restrict__ nnz) {
   const int lane = threadIdx.x & 63;
   const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (g >= ngenes) return;
@@ -479,7 +533,7 @@ __global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long l
     n += __popcll(m);
   }
   if (lane == 0) nnz[g] = n;
-  const int end = ((n + 7) & ~7) + 8;
+  const int end = padto == 64 ? (n > 0 ? (n + 63) & ~63 : 64) : ((n + 7) & ~7) + 8;
   for (int p = n + lane; p < end && p < stride; p += 64) E[p] = make_int2(0, pad_col);
 }
 
@@ -1999,7 +2053,8 @@ hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long
 
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   if (a.ncols <= 0 && a.phase != 2) return hipSuccess;
-  if (a.phase != 0 && (!a.D || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
+  if (a.phase != 0 && ((!a.D && !a.DQ) || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
+  if (a.DQ && (!a.UQ || !a.nanflag || a.G > kTabStagedG)) return hipErrorInvalidValue;
   if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG) {
     const size_t shm = sizeof(double) * (kTabWaves + 9) * (size_t)a.G;
     if (a.const_theta)
@@ -2029,10 +2084,12 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 }
 
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
-                      const int* base_col, int stride, int pad_col, int2* ent, int* nnz, hipStream_t s) {
+                      const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s) {
   if (ngenes <= 0) return hipSuccess;
+  if (padto == 64 ? stride < ((ncells + 63) & ~63) || stride < 64 : stride < ((ncells + 7) & ~7) + 8)
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 4)), dim3(256), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
-                     base_col, stride, pad_col, ent, nnz);
+                     base_col, stride, pad_col, padto, ent, nnz);
   return hipGetLastError();
 }
 

@@ -7,7 +7,8 @@ Cases draw: genes 1-60, cells per group 1-35 (groups of unequal size), NA-group 
 counts from a zero-inflated negative binomial with occasional huge counts, models
 resampled from the es.mef (6-column) or knn (12-column: local theta, squared-logit
 concentration) fixtures, n.randomizations in {1, 2, 7, 20, 33}, n.cores in {1, 2, 5},
-prior length.out in {60, 401}.
+prior length.out in {60, 401}.  Every case runs through both bootstrap kernels: the FP64
+k_boot2 and the fixed-point int8-MFMA k_bootq (context option boot_q 0 / 2).
 """
 import numpy as np
 import pytest
@@ -41,8 +42,9 @@ def _case(seed):
         length_out=int(rng.choice([60, 400])))
 
 
+@pytest.mark.parametrize("boot_q", [0, 2])
 @pytest.mark.parametrize("seed", range(NCASES))
-def test_expression_difference_fuzz(seed):
+def test_expression_difference_fuzz(seed, boot_q):
     from oracle import oracle as O
     from oracle import prior as OP
     from scde_amd import api
@@ -50,9 +52,14 @@ def test_expression_difference_fuzz(seed):
     prior = OP.expression_prior(models, counts, kw["length_out"])
     api.set_rand("glibc")
     glist = list(groups)
-    got = api.scde_expression_difference(models, counts, {"x": prior["x"], "y": prior["y"]}, groups=glist,
-                                         n_randomizations=kw["n_randomizations"], n_cores=kw["n_cores"],
-                                         return_posteriors=True)
+    ctx = api.default_context()
+    ctx.set_option("boot_q", boot_q)
+    try:
+        got = api.scde_expression_difference(models, counts, {"x": prior["x"], "y": prior["y"]}, groups=glist,
+                                             n_randomizations=kw["n_randomizations"], n_cores=kw["n_cores"],
+                                             return_posteriors=True)
+    finally:
+        ctx.set_option("boot_q", 1)
     # the oracle takes factor codes (level order a < b, NA = -1), the api R-style labels
     codes = np.array([{"a": 0, "b": 1, None: -1}[v] for v in glist])
     ref = O.scde_expression_difference(models, counts, prior["x"], prior["y"], codes,

@@ -4,11 +4,12 @@ The skipping is an optimisation that must not change results: a 64-point stretch
 left out of a boot slab when a rigorous upper bound of its row values stays more than 51
 below the exact row maximum (post-check), i.e. when every softmax term there falls under
 the e^-50 cut that zeroes it anyway; any slab that fails the check is recomputed whole.
-These tests run the same calls with skipping on (default), off (context option
-boot_skip = 0), and with a negative heuristic slack (skip_slack) that makes the mask drop
-stretches the post-check must reject, so the redo launch carries real work (its count is
-read back and must be > 0) -- and compare all three with the oracle at the SURVEY §8(d)
-bar, and with each other bit for bit.
+These tests run the same calls, for both bootstrap kernels (the fixed-point k_bootq with
+16-point tiles, and the FP64 k_boot2 with 64-point stretches; context option boot_q = 2 / 0),
+with skipping on (default), off (boot_skip = 0), and with a negative heuristic slack
+(skip_slack) that makes the mask drop tiles the post-check must reject, so the extra work
+really happens (its count is read back and must be > 0) -- and compare every run with the
+oracle at the SURVEY §8(d) bar, and the runs of one kernel with each other bit for bit.
 """
 import math
 
@@ -29,6 +30,7 @@ def api():
 
 def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx = api.default_context()
+    ctx.set_option("boot_q", opts.get("boot_q", 2))
     ctx.set_option("boot_skip", opts.get("boot_skip", 1))
     ctx.set_option("skip_slack", opts.get("skip_slack", math.nan))
     ctx.set_option("skip_stats", 1)
@@ -39,6 +41,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
                                              n_cores=ncores, return_posteriors=True)
         stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo")}
     finally:
+        ctx.set_option("boot_q", 1)
         ctx.set_option("boot_skip", 1)
         ctx.set_option("skip_slack", math.nan)
         ctx.set_option("skip_stats", 0)
@@ -57,16 +60,21 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "skip": {},
         "noskip": {"boot_skip": 0},
         "forced-redo": {"skip_slack": -45.0},
+        "fp64": {"boot_q": 0},
+        "fp64-noskip": {"boot_q": 0, "boot_skip": 0},
+        "fp64-forced-redo": {"boot_q": 0, "skip_slack": -45.0},
     }
     got = {}
     for name, opts in runs.items():
         got[name], stats = _run(api, opts, models, counts, prior, groups, nrand, ncores)
-        if name == "noskip":
+        if name == "fp64-noskip":
             assert stats["skip_slabs"] == 0
+        elif name == "noskip":
+            assert stats["skip_slabs"] > 0 and stats["skip_kept"] == stats["skip_stretches"], stats
         else:
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
-        if name == "forced-redo":
-            assert stats["skip_redo"] > 0, stats  # the redo launch really recomputes slabs
+        if name.endswith("forced-redo"):
+            assert stats["skip_redo"] > 0, stats  # the post-check really adds work
         g = got[name]
         for i in range(2):
             assert_posterior_close(g["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"{name} jp{i}")
@@ -77,10 +85,11 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"], what=f"{name} Z")
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
-    for name in ("noskip", "forced-redo"):
-        for i in range(2):
-            np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got["skip"]["joint.posteriors"][i])
-        np.testing.assert_array_equal(got[name]["difference.posterior"].values,
-                                      got["skip"]["difference.posterior"].values)
-        for k in ("Z", "cZ"):
-            np.testing.assert_array_equal(got[name]["results"][k].to_numpy(), got["skip"]["results"][k].to_numpy())
+    for base, others in (("skip", ("noskip", "forced-redo")), ("fp64", ("fp64-noskip", "fp64-forced-redo"))):
+        for name in others:
+            for i in range(2):
+                np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got[base]["joint.posteriors"][i])
+            np.testing.assert_array_equal(got[name]["difference.posterior"].values,
+                                          got[base]["difference.posterior"].values)
+            for k in ("Z", "cZ"):
+                np.testing.assert_array_equal(got[name]["results"][k].to_numpy(), got[base]["results"][k].to_numpy())
