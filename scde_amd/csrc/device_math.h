@@ -459,10 +459,37 @@ __device__ __noinline__ double bd0_series_fast(double x, double np) {
   return s;
 }
 
-// L = log x - log np (precomputed as log x - log n - log p)
+// bd0's series as a fixed polynomial: with v = (x - np)/(x + np), |v| < 0.1, w = v^2 < 0.01,
+// bd0 = (x - np) v + 2 x v sum_{j>=1} w^j / (2j + 1) (src: R nmath bd0, the loop R runs until
+// the sum stops changing).  Nine terms leave a tail below 2e-17 of the first, so the result
+// matches the loop to rounding, with no loop, no early exit and no divergence.
+__device__ __forceinline__ double bd0_poly(double x, double np) {
+  const double d = x - np;
+  const double v = d / (x + np);
+  const double w = v * v;
+  double P = 1.0 / 19;
+  P = fma(P, w, 1.0 / 17);
+  P = fma(P, w, 1.0 / 15);
+  P = fma(P, w, 1.0 / 13);
+  P = fma(P, w, 1.0 / 11);
+  P = fma(P, w, 1.0 / 9);
+  P = fma(P, w, 1.0 / 7);
+  P = fma(P, w, 1.0 / 5);
+  P = fma(P, w, 1.0 / 3);
+  P *= w;
+  return fma(2.0 * x * v, P, d * v);
+}
+
+// L = log x - log np (precomputed as log x - log n - log p).  The series region is taken
+// with a wave-uniform branch: only waves with a lane in it evaluate the polynomial.
 __device__ __forceinline__ double bd0_fast(double x, double np, double L) {
-  if (fabs(x - np) < 0.1 * (x + np)) return bd0_series_fast(x, np);
-  return x * L + np - x;
+  const bool ser = fabs(x - np) < 0.1 * (x + np);
+  double b = x * L + np - x;
+  if (__builtin_amdgcn_ballot_w64(ser)) {
+    const double sv = bd0_poly(x, np);
+    b = ser ? sv : b;
+  }
+  return b;
 }
 
 struct NbFast {
