@@ -1,0 +1,135 @@
+# scde_hip.R -- R wrappers for the fused device path of libscde_hip (R/src/scde_hip_shim.c).
+#
+# With the shim installed, the reference's own scde.posteriors / scde.expression.difference
+# (R/functions.R:566, 304) already run on the GPU through the layer-1 .Call symbols.  These
+# functions keep exactly those signatures but hand the whole call to the device in one .Call:
+# unique-count tables, both groups' posteriors, the ratio posterior, the summary and BH run
+# in HBM (scde_expression_difference_host).  Arguments the fused path does not cover (batch
+# correction) go to the reference implementation, which is saved as .scde.ref.* first.
+
+.scde.model.matrix <- function(models) {
+    # R/functions.R:601-604 (mm), with the flags R/functions.R:595-598 derives
+    mm <- matrix(NA, nrow(models), 12)
+    cols <- c("conc.b", "conc.a", "fail.r", "corr.b", "corr.a", "corr.theta", "corr.ltheta.b", "corr.ltheta.t",
+              "corr.ltheta.m", "corr.ltheta.s", "corr.ltheta.r", "conc.a2")
+    for (j in seq_along(cols)) if (cols[j] %in% colnames(models)) mm[, j] <- models[, cols[j]]
+    list(mm = mm, localtheta = "corr.ltheta.b" %in% colnames(models), squarelogit = "conc.a2" %in% colnames(models))
+}
+
+if (!exists(".scde.ref.expression.difference")) .scde.ref.expression.difference <- scde.expression.difference
+if (!exists(".scde.ref.posteriors")) .scde.ref.posteriors <- scde.posteriors
+
+scde.expression.difference <- function(models, counts, prior, groups = NULL, batch = NULL, n.randomizations = 150,
+                                       n.cores = 10, batch.models = models, return.posteriors = FALSE,
+                                       expectation = 0, verbose = 0) {
+    if (!is.null(batch) && length(unique(batch)) > 1) {
+        return(.scde.ref.expression.difference(models, counts, prior, groups, batch, n.randomizations, n.cores,
+                                               batch.models, return.posteriors, expectation, verbose))
+    }
+    if (!all(rownames(models) %in% colnames(counts))) {
+        stop("ERROR: provided count data does not cover all of the cells specified in the model matrix")
+    }
+    counts <- as.matrix(counts[, match(rownames(models), colnames(counts))])
+    if (is.null(groups)) {
+        groups <- as.factor(attr(models, "groups"))
+        if (is.null(groups)) stop("ERROR: groups factor is not provided, and models structure is lacking groups attribute")
+        names(groups) <- rownames(models)
+    }
+    if (length(levels(groups)) != 2) {
+        stop(paste("ERROR: wrong number of levels in the grouping factor (", paste(levels(groups), collapse = " "),
+                   "), but must be two.", sep = ""))
+    }
+    storage.mode(counts) <- "integer"
+    m <- .scde.model.matrix(models)
+    m$mm[, 5] <- pmax(m$mm[, 5], 1e-10)  # R/functions.R:579-583
+    x <- .Call("scde_hip_expression_difference", m$mm, counts, prior$x, prior$y,
+               as.integer(groups[rownames(models)]), n.randomizations, n.cores, m$localtheta, m$squarelogit,
+               expectation, return.posteriors, PACKAGE = "scde")
+    res <- as.data.frame(x$results)
+    colnames(res) <- c("lb", "mle", "ub", "ce", "Z", "cZ")
+    rownames(res) <- rownames(counts)
+    if (!return.posteriors) return(res)
+    marginals <- log(pmax(10^prior$x - 1, 0))
+    jp <- lapply(list(x$jp1, x$jp2), function(j) {
+        rownames(j) <- rownames(counts)
+        colnames(j) <- as.character(exp(marginals))
+        j
+    })
+    names(jp) <- levels(groups)
+    rv <- seq(prior$x[1] - prior$x[length(prior$x)], prior$x[length(prior$x)] - prior$x[1],
+              length = length(prior$x) * 2 - 1)
+    ratio <- x$ratio
+    rownames(ratio) <- rownames(counts)
+    colnames(ratio) <- as.character(rv)
+    list(results = res, difference.posterior = ratio, joint.posteriors = jp)
+}
+
+scde.posteriors <- function(models, counts, prior, n.randomizations = 100, batch = NULL, composition = NULL,
+                            return.individual.posteriors = FALSE, return.individual.posterior.modes = FALSE,
+                            ensemble.posterior = FALSE, n.cores = 20) {
+    if (!is.null(batch)) {
+        return(.scde.ref.posteriors(models, counts, prior, n.randomizations, batch, composition,
+                                    return.individual.posteriors, return.individual.posterior.modes,
+                                    ensemble.posterior, n.cores))
+    }
+    if (!all(rownames(models) %in% colnames(counts))) {
+        stop("ERROR: provided count data does not cover all of the cells specified in the model matrix")
+    }
+    counts <- as.matrix(counts[, match(rownames(models), colnames(counts)), drop = FALSE])
+    storage.mode(counts) <- "integer"
+    marginals <- log(pmax(10^prior$x - 1, 0))
+    postflag <- 0
+    if (return.individual.posteriors) {
+        postflag <- if (return.individual.posterior.modes) 3 else 2
+    } else if (return.individual.posterior.modes) {
+        postflag <- 1
+    }
+    m <- .scde.model.matrix(models)
+    m$mm[, 5] <- pmax(m$mm[, 5], 1e-10)
+    x <- .Call("scde_hip_posteriors", m$mm, counts, prior$x, n.randomizations, n.cores, m$localtheta, m$squarelogit,
+               postflag, ensemble.posterior, PACKAGE = "scde")
+    name.jp <- function(j) {
+        rownames(j) <- rownames(counts)
+        colnames(j) <- as.character(exp(marginals))
+        j
+    }
+    if (postflag == 0) return(name.jp(x))
+    x$jp <- name.jp(x$jp)
+    if (!is.null(x$modes)) {
+        rownames(x$modes) <- rownames(counts)
+        colnames(x$modes) <- rownames(models)
+    }
+    if (!is.null(x$post)) {
+        names(x$post) <- rownames(models)
+        x$post <- lapply(x$post, name.jp)
+    }
+    x
+}
+
+# pagoda.varnorm's mode and weight computation (R/functions.R:1414-1507) in one call; returns
+# list(avmodes, modes (one column per batch level, or NULL), matw, bmatw)
+scde.hip.varnorm.weights <- function(models, counts, prior, batch = NULL, n.randomizations = 100, n.cores = 1,
+                                     use.expected.value = TRUE) {
+    counts <- as.matrix(counts[, match(rownames(models), colnames(counts)), drop = FALSE])
+    storage.mode(counts) <- "integer"
+    m <- .scde.model.matrix(models)
+    nb <- 0
+    codes <- integer(0)
+    if (!is.null(batch)) {
+        batch <- as.factor(batch)
+        bt <- table(batch)
+        if (any(bt < 2)) batch[batch %in% names(bt)[bt < 2]] <- names(bt)[which.max(bt)]  # R/functions.R:1404-1410
+        batch <- droplevels(batch)
+        nb <- length(levels(batch))
+        codes <- as.integer(batch)
+    }
+    x <- .Call("scde_hip_varnorm_weights", m$mm, counts, prior$x, n.randomizations, n.cores, m$localtheta,
+               m$squarelogit, codes, nb, use.expected.value, PACKAGE = "scde")
+    avmodes <- x$modes[, 1]
+    names(avmodes) <- rownames(counts)
+    modes <- if (nb > 1) x$modes[, -1, drop = FALSE] else NULL
+    if (!is.null(modes)) dimnames(modes) <- list(rownames(counts), levels(batch))
+    dimnames(x$matw) <- list(rownames(counts), rownames(models))
+    if (!is.null(x$bmatw)) dimnames(x$bmatw) <- list(rownames(counts), rownames(models))
+    list(avmodes = avmodes, modes = modes, matw = x$matw, bmatw = x$bmatw)
+}

@@ -200,6 +200,24 @@ int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngene
                          const int* batch_vals, const int64_t* batch_off, const int* composition, int nbatch,
                          double* jp, double* modes, double* post);
 
+/* pagoda.varnorm's posterior-mode consumer (R/functions.R:1414-1507; SURVEY.md section 8(f)
+ * row 4).  Runs scde.posteriors (n.cores seeding, nboot randomizations) over all cells and,
+ * with a batch (batch_codes[ncells] in [0, nbatch), nbatch > 1), over each level's cells; the
+ * modes are jp %*% as.numeric(colnames(jp)) (use_expected_value) or the magnitude of each row's
+ * maximum.  Outputs (host): modes (1 [+ nbatch]) x ngenes (dataset-wide, then per level);
+ * matw ngenes x ncells = 1 - mfp * sfp with mfp = scde.failure.probability at log(dataset
+ * modes) and sfp = ppois(count - 1, exp(fail.r), lower.tail = FALSE) (1466-1474); bmatw (with
+ * a batch) the same with each cell's level modes (1485-1506).  models: ncells x 12 col-major. */
+int scde_pagoda_varnorm_weights_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, int ncells,
+                                    const double* models, int local_theta, int square_logit_conc,
+                                    const double* prior_x, int ngrid, int nboot, int n_cores, const int* batch_codes,
+                                    int nbatch, int use_expected_value, double* modes, double* matw, double* bmatw);
+int scde_pagoda_varnorm_weights_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes, int ncells,
+                                     const double* models, int local_theta, int square_logit_conc,
+                                     const double* prior_x, int ngrid, int nboot, int n_cores,
+                                     const int* batch_codes, int nbatch, int use_expected_value, double* modes,
+                                     double* matw, double* bmatw);
+
 /* scde.expression.prior (R/functions.R:225-254; replaces the R-level function, which has
  * no .Call) on device-resident counts (ngenes x ncells int32, column stride ld).  models:
  * ncells x 12 col-major (conc.b, conc.a, ..., corr.b, corr.a, ..., conc.a2 at column 11 when

@@ -27,7 +27,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+# SCDE_ORACLE_LIB: another build of the same sources (the sanitizer build, oracle/Makefile)
+_LIB_PATH = os.environ.get("SCDE_ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
 
 MODEL_COLUMNS = ["conc.b", "conc.a", "fail.r", "corr.b", "corr.a", "corr.theta",
                  "corr.ltheta.b", "corr.ltheta.t", "corr.ltheta.m", "corr.ltheta.s",

@@ -24,6 +24,7 @@ EXPORTS = [
     "scde_expression_difference_dev", "scde_posteriors_dev", "scde_bh_cz_dev",
     "scde_expression_difference_batch_dev", "scde_expression_prior_dev",
     "scde_expression_difference_host", "scde_expression_difference_batch_host", "scde_posteriors_host",
+    "scde_pagoda_varnorm_weights_dev", "scde_pagoda_varnorm_weights_host",
     "scde_baileyWPCA", "scde_bwpca_batch_dev", "scde_r_set_seed", "scde_r_unif_rand", "scde_r_sample",
     "scde_shuffle_perms", "scde_winsorizeMatrix", "scde_matWCorr", "scde_matCorr", "scde_plSemicompleteCor2",
 ]
@@ -64,10 +65,11 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ScdeError(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                         " or `make -C scde_amd/csrc`")
-    try:  # share torch's HIP runtime when torch is present (same SONAME)
-        import torch  # noqa: F401
-    except Exception:  # pragma: no cover - torch is optional plumbing
-        pass
+    if not os.environ.get("SCDE_SKIP_TORCH"):  # host-only sanitizer runs load the library alone
+        try:  # share torch's HIP runtime when torch is present (same SONAME)
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is optional plumbing
+            pass
     L = ctypes.CDLL(LIB_PATH)
     P, i, i64, d = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
     L.scde_last_error.restype = ctypes.c_char_p
@@ -105,6 +107,8 @@ def lib():
                                                         P, P]
     L.scde_posteriors_host.argtypes = [P, P, i64, i, i, P, i, P, i, i, P, i, i, i, i64, i64, i, i, P, P, P, i, P, P,
                                        P]
+    L.scde_pagoda_varnorm_weights_dev.argtypes = [P, P, i64, i, i, P, i, i, P, i, i, i, P, i, i, P, P, P]
+    L.scde_pagoda_varnorm_weights_host.argtypes = [P, P, i64, i, i, P, i, i, P, i, i, i, P, i, i, P, P, P]
     L.scde_expression_prior_dev.argtypes = [P, P, i64, i, i, P, i, i, d, d, d, P, P, P, P, P, P]
     L.scde_posteriors_dev.argtypes = [P, P, i64, i, P, i, P, i, i, P, i, i, i, i64, i64, i, i, P, P, P, i, P, P, P]
     L.scde_baileyWPCA.argtypes = [P, P, i, i, i, i, i, d, i, P, i, P, P, P, P, P, P, P]

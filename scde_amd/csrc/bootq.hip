@@ -64,6 +64,8 @@ __device__ __forceinline__ void tr4(unsigned a, unsigned b, unsigned c, unsigned
   p3 = __builtin_amdgcn_perm(cd13, ab13, 0x07060302u);
 }
 
+constexpr int kZChunk = 64;  // cells per baseline-sum block
+
 __device__ __forceinline__ int sbyte(unsigned long long p, int l) { return (int)(signed char)(p >> (8 * l)); }
 
 // sum_l d_l 256^l 2^-36 from seven digit sums (|d_l| < 2^22): pairs exact in int32, then
@@ -78,14 +80,17 @@ __device__ __forceinline__ double qcombine(int d0, int d1, int d2, int d3, int d
 
 // ------------------------------------------------------------------ baseline digit sums
 // Zq[set][l][k][Bp] = sum over cells with a baseline column of W8[set][c][b] * digit_l(DQ[bc][k]).
-// Block: 64 grid points (lanes) x 8 boots, 4 waves over cells (c = wave mod 4); exact
-// integer partials combine by LDS atomics (order-free).
+// Block: 64 grid points (lanes) x 8 boots x a chunk of kZChunk cells, 4 waves over the chunk's
+// cells (c = wave mod 4); exact integer partials combine by LDS then global atomics (order-free;
+// Zq is zeroed first).
 __global__ __launch_bounds__(256) void k_zq(const unsigned long long* __restrict__ DQ, int G, int GS,
                                             const int* __restrict__ base_col, int ncells,
                                             const unsigned char* __restrict__ W8, int Bp, int* __restrict__ Zq) {
   __shared__ int part[7][8][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int b0 = blockIdx.x * 8, k = blockIdx.y * 64 + lane, set = blockIdx.z;
+  const int nch = (ncells + kZChunk - 1) / kZChunk;
+  const int b0 = blockIdx.x * 8, k = blockIdx.y * 64 + lane, set = blockIdx.z / nch;
+  const int c0 = (blockIdx.z % nch) * kZChunk, c1 = min(ncells, c0 + kZChunk);
   for (int i = threadIdx.x; i < 7 * 8 * 64; i += 256) (&part[0][0][0])[i] = 0;
   __syncthreads();
   int acc[8][7];
@@ -95,7 +100,7 @@ __global__ __launch_bounds__(256) void k_zq(const unsigned long long* __restrict
     for (int l = 0; l < 7; ++l) acc[r][l] = 0;
   const unsigned char* W = W8 + (long long)set * ncells * Bp + b0;
   if (k < GS) {
-    for (int c = wid; c < ncells; c += 4) {
+    for (int c = c0 + wid; c < c1; c += 4) {
       const int bc = base_col[c];
       if (bc < 0) continue;
       const unsigned long long p = DQ[(long long)bc * GS + k];
@@ -113,25 +118,26 @@ __global__ __launch_bounds__(256) void k_zq(const unsigned long long* __restrict
 #pragma unroll
     for (int l = 0; l < 7; ++l) atomicAdd(&part[l][r][lane], acc[r][l]);
   __syncthreads();
-  if (k < GS && wid == 0)
-#pragma unroll
-    for (int l = 0; l < 7; ++l) {
-      int* o = Zq + (((long long)set * 7 + l) * GS + k) * Bp + b0;
-      *reinterpret_cast<int4*>(o) = make_int4(part[l][0][lane], part[l][1][lane], part[l][2][lane], part[l][3][lane]);
-      *reinterpret_cast<int4*>(o + 4) =
-          make_int4(part[l][4][lane], part[l][5][lane], part[l][6][lane], part[l][7][lane]);
+  if (k < GS)
+    for (int i = wid; i < 7 * 8; i += 4) {
+      const int l = i >> 3, rr = i & 7;
+      const int v = part[l][rr][lane];
+      if (v) atomicAdd(Zq + (((long long)set * 7 + l) * GS + k) * Bp + b0 + rr, v);
     }
 }
 
 // ZUq[set][l][t][Bp] = sum over baseline cells of W8[set][c][b] * digit_l(UQ[bc][t]), l < 4.
-// Block per (set, 32 boots); thread = (tile, boot).
+// Block per (set, 32 boots, chunk of kZChunk cells); thread = (tile, boot); global atomics
+// (exact; ZUq is zeroed first).
 __global__ __launch_bounds__(1024) void k_zuq(const unsigned* __restrict__ UQ, const int* __restrict__ base_col,
                                               int ncells, const unsigned char* __restrict__ W8, int Bp,
                                               int* __restrict__ ZUq) {
-  const int t = threadIdx.x >> 5, b = blockIdx.x * 32 + (threadIdx.x & 31), set = blockIdx.y;
+  const int nch = (ncells + kZChunk - 1) / kZChunk;
+  const int t = threadIdx.x >> 5, b = blockIdx.x * 32 + (threadIdx.x & 31), set = blockIdx.y / nch;
+  const int c0 = (blockIdx.y % nch) * kZChunk, c1 = min(ncells, c0 + kZChunk);
   const unsigned char* W = W8 + (long long)set * ncells * Bp + b;
   int acc[4] = {0, 0, 0, 0};
-  for (int c = 0; c < ncells; ++c) {
+  for (int c = c0; c < c1; ++c) {
     const int bc = base_col[c];
     if (bc < 0) continue;
     const int w = W[(long long)c * Bp];
@@ -140,7 +146,8 @@ __global__ __launch_bounds__(1024) void k_zuq(const unsigned* __restrict__ UQ, c
     for (int l = 0; l < 4; ++l) acc[l] += w * (int)(signed char)(u >> (8 * l));
   }
 #pragma unroll
-  for (int l = 0; l < 4; ++l) ZUq[(((long long)set * 4 + l) * kQTiles + t) * Bp + b] = acc[l];
+  for (int l = 0; l < 4; ++l)
+    if (acc[l]) atomicAdd(ZUq + (((long long)set * 4 + l) * kQTiles + t) * Bp + b, acc[l]);
 }
 
 // ------------------------------------------------------------------ the bootstrap
@@ -456,14 +463,21 @@ size_t bootq_lds_bytes(int ent_stride) { return (size_t)ent_stride * 8 + (size_t
 hipError_t launch_zq(const unsigned long long* DQ, int G, int GS, const int* base_col, int ncells,
                      const unsigned char* W8, int Bp, int nsets, int* Zq, hipStream_t s) {
   if (Bp % 8 || GS % 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_zq, dim3(Bp / 8, GS / 64, nsets), dim3(256), 0, s, DQ, G, GS, base_col, ncells, W8, Bp, Zq);
+  hipError_t e = hipMemsetAsync(Zq, 0, sizeof(int) * (size_t)nsets * 7 * GS * Bp, s);
+  if (e != hipSuccess) return e;
+  const int nch = (ncells + kZChunk - 1) / kZChunk;
+  hipLaunchKernelGGL(k_zq, dim3(Bp / 8, GS / 64, nsets * nch), dim3(256), 0, s, DQ, G, GS, base_col, ncells, W8, Bp,
+                     Zq);
   return hipGetLastError();
 }
 
 hipError_t launch_zuq(const unsigned* UQ, const int* base_col, int ncells, const unsigned char* W8, int Bp, int nsets,
                       int* ZUq, hipStream_t s) {
   if (Bp % 32) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_zuq, dim3(Bp / 32, nsets), dim3(1024), 0, s, UQ, base_col, ncells, W8, Bp, ZUq);
+  hipError_t e = hipMemsetAsync(ZUq, 0, sizeof(int) * (size_t)nsets * 4 * kQTiles * Bp, s);
+  if (e != hipSuccess) return e;
+  const int nch = (ncells + kZChunk - 1) / kZChunk;
+  hipLaunchKernelGGL(k_zuq, dim3(Bp / 32, nsets * nch), dim3(1024), 0, s, UQ, base_col, ncells, W8, Bp, ZUq);
   return hipGetLastError();
 }
 

@@ -1831,6 +1831,121 @@ int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngene
                              return_post, ensemble, batch_vals, batch_off, composition, nbatch, jp, modes, post);
 }
 
+// pagoda.varnorm's posterior-mode consumer (R/functions.R:1414-1507): modes from
+// scde.posteriors' joint posteriors -- dataset-wide and per batch level -- and the weight
+// matrices 1 - mfp * sfp.  The magnitudes are as.numeric(colnames(jp)) = exp(marginals)
+// through R's 15-significant-digit as.character (R/functions.R:640-643).
+static int vn_posterior_jp(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const int* cellidx, int C,
+                           const double* models, int mld, int local_theta, int sq, const double* prior_x, int G,
+                           int nboot, int n_cores, double* jp_dev) {
+  std::vector<double> mm((size_t)C * 12);
+  for (int j = 0; j < 12; ++j)
+    for (int c = 0; c < C; ++c) mm[(size_t)c + (size_t)C * j] = models[(size_t)cellidx[c] + (size_t)mld * j];
+  for (int c = 0; c < C; ++c) {
+    double& ca = mm[(size_t)c + (size_t)C * 4];
+    if (ca < 1e-10) ca = 1e-10;  // R/functions.R:579-583
+  }
+  const std::vector<double> mag = marginals(prior_x, G);
+  PostSpec s;
+  s.ncells = C;
+  s.models = mm.data();
+  s.localtheta = local_theta;
+  s.squarelogit = sq;
+  s.mag = mag.data();
+  s.G = G;
+  s.nboot = nboot;
+  s.postflag = 0;
+  s.counts_dev = counts_dev;
+  s.ld = ld;
+  s.cellidx_host = cellidx;
+  s.ngenes = ngenes;
+  seeding(n_cores, 0, ngenes, ngenes, s.seeds, s.wset);
+  s.rand_kind = g_rand_kind;
+  s.jp = jp_dev;
+  s.jp_g = 1;
+  s.jp_k = ngenes;
+  ctx->us[0].ready = false;
+  return run_posterior(ctx, s, ctx->us[0]);
+}
+
+int scde_pagoda_varnorm_weights_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, int ncells,
+                                    const double* models, int local_theta, int square_logit_conc,
+                                    const double* prior_x, int ngrid, int nboot, int n_cores, const int* batch_codes,
+                                    int nbatch, int use_expected_value, double* modes, double* matw,
+                                    double* bmatw) {
+  if (!ctx || !counts_dev || !models || !prior_x || !modes || !matw) return fail(SCDE_EARG, "null argument");
+  if (ngenes < 0 || ncells <= 0 || ngrid <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
+  const bool batch = batch_codes && nbatch > 1;
+  if (batch && !bmatw) return fail(SCDE_EARG, "bmatw required with a batch");
+  HCHK(hipSetDevice(ctx->device));
+  hipStream_t st = ctx->stream;
+  const int N = ngenes, C = ncells, G = ngrid;
+  // as.numeric(colnames(jp)): exp(marginals) with 15 significant digits
+  const std::vector<double> marg = marginals(prior_x, G);
+  std::vector<double> mag(G);
+  for (int k = 0; k < G; ++k) {
+    char buf[64];
+    snprintf(buf, sizeof(buf), "%.15g", std::exp(marg[k]));
+    mag[k] = strtod(buf, nullptr);
+  }
+  RCHK(upload(ctx, ctx->diffv, mag.data(), sizeof(double) * G));
+  const int nm = batch ? 1 + nbatch : 1;
+  HCHK(ctx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)N * nm)));
+  HCHK(ctx->jpB.ensure(sizeof(double) * std::max<size_t>(1, (size_t)N * G)));
+  double* dmodes = ctx->res.as<double>();
+  std::vector<int> allc(C);
+  for (int c = 0; c < C; ++c) allc[c] = c;
+  // dataset-wide modes, then one set per batch level
+  for (int m = 0; m < nm; ++m) {
+    std::vector<int> cells;
+    if (m == 0) {
+      cells = allc;
+    } else {
+      for (int c = 0; c < C; ++c) {
+        if (batch_codes[c] < 0 || batch_codes[c] >= nbatch) return fail(SCDE_EARG, "batch code out of range");
+        if (batch_codes[c] == m - 1) cells.push_back(c);
+      }
+      if (cells.empty()) return fail(SCDE_EARG, "batch level %d has no cells", m - 1);
+    }
+    if (N > 0) {
+      RCHK(vn_posterior_jp(ctx, counts_dev, ld, N, cells.data(), (int)cells.size(), models, C, local_theta,
+                           square_logit_conc, prior_x, G, nboot, n_cores, ctx->jpB.as<double>()));
+      HCHK(launch_vn_modes(ctx->jpB.as<double>(), 1, N, N, G, ctx->diffv.as<double>(), use_expected_value,
+                           dmodes + (size_t)m * N, st));
+    }
+  }
+  // weight matrices
+  RCHK(upload(ctx, ctx->models, models, sizeof(double) * (size_t)C * 12));
+  RCHK(upload(ctx, ctx->in1, allc.data(), sizeof(int) * C));
+  HCHK(ctx->outbuf.ensure(sizeof(double) * std::max<size_t>(1, (size_t)N * C)));
+  std::vector<long long> off(C, 0);
+  for (int pass = 0; pass < (batch ? 2 : 1); ++pass) {
+    if (pass == 1)
+      for (int c = 0; c < C; ++c) off[c] = (long long)(1 + batch_codes[c]) * N;
+    RCHK(upload(ctx, ctx->in2, off.data(), sizeof(long long) * C));
+    HCHK(launch_vn_matw(counts_dev, ld, N, ctx->in1.as<int>(), C, ctx->models.as<double>(), C, square_logit_conc,
+                        dmodes, ctx->in2.as<long long>(), ctx->outbuf.as<double>(), st));
+    if ((size_t)N * C)
+      HCHK(hipMemcpyAsync(pass == 0 ? matw : bmatw, ctx->outbuf.p, sizeof(double) * (size_t)N * C,
+                          hipMemcpyDeviceToHost, st));
+    RCHK(ctx->sync());  // outbuf / in2 are reused by the next pass
+  }
+  if (N) HCHK(hipMemcpyAsync(modes, dmodes, sizeof(double) * (size_t)N * nm, hipMemcpyDeviceToHost, st));
+  return ctx->sync();
+}
+
+int scde_pagoda_varnorm_weights_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes, int ncells,
+                                     const double* models, int local_theta, int square_logit_conc,
+                                     const double* prior_x, int ngrid, int nboot, int n_cores,
+                                     const int* batch_codes, int nbatch, int use_expected_value, double* modes,
+                                     double* matw, double* bmatw) {
+  const int* dev = nullptr;
+  RCHK(stage_counts(ctx, counts, ld, ngenes, ncells, &dev));
+  return scde_pagoda_varnorm_weights_dev(ctx, dev, ngenes, ngenes, ncells, models, local_theta, square_logit_conc,
+                                         prior_x, ngrid, nboot, n_cores, batch_codes, nbatch, use_expected_value,
+                                         modes, matw, bmatw);
+}
+
 // ------------------------------------------------------------------ BH (host)
 // scde.expression.prior (R/functions.R:225-254) on device-resident counts (prior.hip).
 int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, int ncells,

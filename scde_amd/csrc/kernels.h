@@ -338,5 +338,12 @@ hipError_t launch_matcorr(const double* x, int k, int nx, const double* y, int n
 // plSemicompleteCor2: np lists (off[np + 1], idx, val) -> r, cnt np x np
 hipError_t launch_plcor(int np, const long long* off, const int* idx, const double* val, double* r, int* cnt,
                         hipStream_t s);
+// pagoda.varnorm's mode consumer: modes from jp (expected value or row-maximum magnitude);
+// the weight matrix 1 - mfp * sfp for cells cellidx (matw: ngenes x ncells col-major)
+hipError_t launch_vn_modes(const double* jp, long long jg, long long jk, int ngenes, int G, const double* mag,
+                           int expected, double* modes, hipStream_t s);
+hipError_t launch_vn_matw(const int* counts, long long ld, int ngenes, const int* cellidx, int ncells,
+                          const double* models, int mld, int sq, const double* modes, const long long* mode_off,
+                          double* matw, hipStream_t s);
 
 }  // namespace scde

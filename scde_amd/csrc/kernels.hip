@@ -144,7 +144,7 @@ __device__ __forceinline__ float gt_maxf(float a, float b) { return (b > a) ? b 
 // One (cell, unique count) column, one wavefront, lanes over grid points.  The per-cell
 // grid vectors (mu, pq, lcfpr, lcfp, theta) and the baseline column come in as pointers:
 // global memory (k_tables) or an LDS copy staged once per cell (k_tables_cell).
-template <bool CT>
+template <bool CT, bool Q>
 __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col, int c, int phase,
                                               const double* __restrict__ mu, const double* __restrict__ P,
                                               const double* __restrict__ lcfpr, const double* __restrict__ lcfp,
@@ -237,15 +237,16 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   bool clamp = false;
   double* out = a.T ? a.T + col * a.GS : nullptr;
   // fused delta (phase 2): D = T - T[baseline column of the cell], as k_delta computes it
-  double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
+  double* dout = (!Q && phase && a.D) ? a.D + col * a.GS : nullptr;
   const int bc_u = (phase == 2) ? a.base_col[c] : -1;
   // per 64-point stretch j (grid points 64j .. 64j+63, one k_boot2 wave each): the
   // column's maximum, for k_boot2's stretch bounds (U: raw maxima for phase-1 columns,
   // maxima minus the cell's baseline-column maxima for phase-2 columns)
-  const double* ubase = (a.U && bc_u >= 0) ? a.U + (long long)bc_u * kStretchSlots : nullptr;
+  double* const U = Q ? nullptr : a.U;
+  const double* ubase = (U && bc_u >= 0) ? U + (long long)bc_u * kStretchSlots : nullptr;
   // fixed-point output (k_bootq): q, or q - q[base] in phase 2; the row of final digits'
   // values (int64) for the tile bounds
-  unsigned long long* qout = (phase && a.DQ) ? a.DQ + col * a.GS : nullptr;
+  unsigned long long* qout = (Q && phase) ? a.DQ + col * a.GS : nullptr;
   long long* vq = reinterpret_cast<long long*>(v);
   bool nanq = false;
 #pragma unroll 1
@@ -271,7 +272,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         if (out) out[k] = r;
         if (dout) dout[k] = base ? r - base[k] : r;
       }
-      if (a.U) v[k] = r;  // the row of final values, for the stretch maxima below
+      if (U) v[k] = r;  // the row of final values, for the stretch maxima below
       if (qout) {
         long long q = 0;
         if (r != r)
@@ -305,7 +306,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
       a.UQ[col * kQTiles + t] = packu(u);
     }
   }
-  if (a.U) {
+  if (U) {
     // per-stretch maxima from the LDS row: lane l < 8 * stretches takes 8 points of
     // stretch l >> 3, then a 3-step max over its group of 8 lanes; in f32, widened by
     // 2^-23 |m| (the f32 rounding of the values) so the stored value is an upper bound
@@ -319,7 +320,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
     for (int o = 1; o <= 4; o <<= 1) mf = gt_maxf(mf, __shfl_xor(mf, o, 64));
     if ((lane & 7) == 0 && j < nst) {
       const double m = (double)mf + 0x1p-23 * fabs((double)mf);
-      a.U[col * kStretchSlots + j] = ubase ? m - ubase[j] : m;
+      U[col * kStretchSlots + j] = ubase ? m - ubase[j] : m;
     }
   }
   if (dout)
@@ -353,7 +354,7 @@ __device__ __forceinline__ void tables_tabs(double* etab, double (*ltab)[97]) {
 
 // Column-per-wave form, grid vectors read from global memory: phase 1 (one wave per
 // cell, its count-0 column) and grids too wide for the staged kernel.
-template <bool CT>
+template <bool CT, bool Q>
 __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   extern __shared__ double vrow[];  // [4 waves][GS]
   __shared__ double etab[64];
@@ -409,8 +410,8 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const long long co = (long long)c * a.GS;
   const int bc = (phase == 2) ? a.base_col[c] : -1;
   const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
-  tables_column<CT>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co, a.lcfp + co,
-                    a.theta + co, base, nullptr, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
+  tables_column<CT, Q>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
+                       a.lcfp + co, a.theta + co, base, nullptr, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
 }
 
 // Cell-staged form (phases 0 and 2, G <= kTabStagedG): one 8-wave block per task
@@ -421,7 +422,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
 // blocks fit a CU: (8 + 9) * G * 8 B = 54.5 KB at G = 401.
 constexpr int kTabStagedG = 448;
 constexpr int kTabWaves = 8;
-template <bool CT>
+template <bool CT, bool Q>
 __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TAB_WPE))) void k_tables_cell(TablesArgs a) {
   extern __shared__ double dyn[];  // vrow [8][G] | mu | P[4] | lcfpr | lcfp | th | base, each G
   __shared__ double etab[64];
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
       sP[3 * G + k] = P[3 * GS + k];
     }
     if (bc >= 0) {
-      if (a.DQ)
+      if (Q)
         reinterpret_cast<long long*>(sbase)[k] = unpackq(a.DQ[(long long)bc * GS + k]);
       else
         sbase[k] = a.D[(long long)bc * GS + k];
@@ -477,10 +478,10 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   const int zc = (phase == 2) ? a.zcol[c] : -1;
   for (int col = task.y + wid; col < task.z; col += kTabWaves) {
     if (col == zc) continue;  // done in phase 1
-    tables_column<CT>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, slc, sth,
-                      (bc >= 0 && !a.DQ) ? sbase : nullptr,
-                      (bc >= 0 && a.DQ) ? reinterpret_cast<const long long*>(sbase) : nullptr, dyn + wid * G, etab,
-                      lt, lane, G);
+    tables_column<CT, Q>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, slc, sth,
+                         (bc >= 0 && !Q) ? sbase : nullptr,
+                         (bc >= 0 && Q) ? reinterpret_cast<const long long*>(sbase) : nullptr, dyn + wid * G, etab,
+                         lt, lane, G);
   }
 }
 
@@ -2057,10 +2058,18 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   if (a.DQ && (!a.UQ || !a.nanflag || a.G > kTabStagedG)) return hipErrorInvalidValue;
   if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG) {
     const size_t shm = sizeof(double) * (kTabWaves + 9) * (size_t)a.G;
-    if (a.const_theta)
-      hipLaunchKernelGGL(k_tables_cell<true>, dim3(a.ntasks), dim3(64 * kTabWaves), shm, s, a);
-    else
-      hipLaunchKernelGGL(k_tables_cell<false>, dim3(a.ntasks), dim3(64 * kTabWaves), shm, s, a);
+    const dim3 grid(a.ntasks), block(64 * kTabWaves);
+    if (a.const_theta) {
+      if (a.DQ)
+        hipLaunchKernelGGL((k_tables_cell<true, true>), grid, block, shm, s, a);
+      else
+        hipLaunchKernelGGL((k_tables_cell<true, false>), grid, block, shm, s, a);
+    } else {
+      if (a.DQ)
+        hipLaunchKernelGGL((k_tables_cell<false, true>), grid, block, shm, s, a);
+      else
+        hipLaunchKernelGGL((k_tables_cell<false, false>), grid, block, shm, s, a);
+    }
     return hipGetLastError();
   }
   const long long nwaves = a.phase == 1 ? a.ncells : a.phase == 2 ? a.ncols + 1 : a.ncols;
@@ -2068,10 +2077,17 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   const dim3 grid(div_up(nwaves, 4)), block(256);
   const size_t shm = sizeof(double) * 4 * (size_t)a.GS;
   if (shm > 64 * 1024) return hipErrorInvalidValue;
-  if (a.const_theta)
-    hipLaunchKernelGGL(k_tables<true>, grid, block, shm, s, a);
-  else
-    hipLaunchKernelGGL(k_tables<false>, grid, block, shm, s, a);
+  if (a.const_theta) {
+    if (a.DQ)
+      hipLaunchKernelGGL((k_tables<true, true>), grid, block, shm, s, a);
+    else
+      hipLaunchKernelGGL((k_tables<true, false>), grid, block, shm, s, a);
+  } else {
+    if (a.DQ)
+      hipLaunchKernelGGL((k_tables<false, true>), grid, block, shm, s, a);
+    else
+      hipLaunchKernelGGL((k_tables<false, false>), grid, block, shm, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -3,6 +3,10 @@
 //   matCorr         (src/pagoda.cpp:33-38)    k_colstats + k_matcorr
 //   matWCorr        (src/pagoda.cpp:41-65)    k_matwcorr
 //   plSemicompleteCor2 (src/pagoda.cpp:67-117) k_plcor
+//   pagoda.varnorm's posterior-mode consumer (R/functions.R:1423-1450, 1466-1474):
+//     k_vn_modes (jp %*% magnitudes, or the magnitude of the row maximum), k_vn_matw
+//     (matw = 1 - mfp * sfp: scde.failure.probability at log(modes) times ppois(count - 1,
+//     exp(fail.r), lower.tail = FALSE))
 // All FP64.  Reductions run lane-parallel in a fixed tree order, so sums differ from the
 // reference's sequential BLAS/Armadillo order by rounding only.
 #include <hip/hip_runtime.h>
@@ -295,6 +299,103 @@ __global__ void k_pl_diag(int np, double* __restrict__ r, int* __restrict__ cnt)
 }
 
 // ------------------------------------------------------------------ launchers
+// ---- pagoda.varnorm: dataset (or batch) modes from a joint posterior, R/functions.R:1426-1430.
+// jp: ngenes x G, element (g, k) at jp[g * jg + k * jk].  mode 1: sum_k jp[g, k] mag[k] in k
+// order, multiply then add (R's %*%, a reference-BLAS dgemv column sweep); mode 0: mag at the
+// first row maximum (R's max.col breaks ties at random; ties do not occur on posterior rows).
+__global__ __launch_bounds__(256) void k_vn_modes(const double* __restrict__ jp, long long jg, long long jk, int ngenes,
+                                                  int G, const double* __restrict__ mag, int expected,
+                                                  double* __restrict__ modes) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= ngenes) return;
+  const double* row = jp + (long long)g * jg;
+  if (expected) {
+    double s = 0.0;
+    for (int k = 0; k < G; ++k) s = __dadd_rn(s, __dmul_rn(row[(long long)k * jk], mag[k]));
+    modes[g] = s;
+  } else {
+    double bv = row[0];
+    int bi = 0;
+    for (int k = 1; k < G; ++k) {
+      const double v = row[(long long)k * jk];
+      if (v > bv) {
+        bv = v;
+        bi = k;
+      }
+    }
+    modes[g] = mag[bi];
+  }
+}
+
+// upper Poisson tail P(X >= c), X ~ Poisson(lambda): R's ppois(c - 1, lambda, lower.tail =
+// FALSE) = pgamma(lambda, c) (nmath ppois_raw).  c <= 0: 1.  Otherwise the first term
+// e^-lambda lambda^c / c! times sum_j lambda^j / ((c+1)...(c+j)), summed until it stops
+// changing (lambda <= c: terms fall at least geometrically); for lambda > c the complement of
+// the lower sum.
+__device__ double pois_upper(int c, double lambda) {
+  if (c <= 0) return 1.0;
+  if (!(lambda > 0.0)) return lambda == 0.0 ? 0.0 : NAN;
+  if (lambda <= (double)c) {
+    const double lt = -lambda + c * log(lambda) - lgamma((double)c + 1.0);
+    double term = 1.0, s = 1.0;
+    for (int j = 1; j < 10000; ++j) {
+      term *= lambda / ((double)c + j);
+      const double s1 = s + term;
+      if (s1 == s) break;
+      s = s1;
+    }
+    return exp(lt) * s;
+  }
+  double term = exp(-lambda), s = term;  // P(X <= c - 1)
+  for (int k = 1; k < c; ++k) {
+    term *= lambda / k;
+    s += term;
+  }
+  return 1.0 - s;
+}
+
+// matw[g, j] = 1 - mfp[g, j] * sfp[g, j] for the cells j of one call (R/functions.R:1466-1474,
+// and the batch columns 1490-1500 with each cell's batch modes): mfp = 1 / (exp(conc.a m (+
+// conc.a2 m^2) + conc.b) + 1) at m = log(mode) (scde.failure.probability, 725-748; NaN -> 0),
+// sfp = ppois(count - 1, exp(fail.r), lower.tail = FALSE).  models: ncells x 12 col-major.
+// modes: per cell j, modes + mode_off[j] (the cell's batch's mode vector).
+__global__ __launch_bounds__(256) void k_vn_matw(const int* __restrict__ counts, long long ld, int ngenes,
+                                                 const int* __restrict__ cellidx, int ncells,
+                                                 const double* __restrict__ models, int mld, int sq,
+                                                 const double* __restrict__ modes, const long long* __restrict__ mode_off,
+                                                 double* __restrict__ matw) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)ngenes * ncells) return;
+  const int g = (int)(i % ngenes), j = (int)(i / ngenes);
+  const int c = cellidx[j];
+  const double conc_b = models[c], conc_a = models[c + mld], fail_r = models[c + 2LL * mld];
+  const double m = log(modes[mode_off[j] + g]);
+  double e = __dmul_rn(conc_a, m);
+  if (sq) e = __dadd_rn(e, __dmul_rn(models[c + 11LL * mld], __dmul_rn(m, m)));
+  double mfp = 1.0 / (exp(__dadd_rn(e, conc_b)) + 1.0);
+  if (isnan(mfp)) mfp = 0.0;
+  const double sfp = pois_upper(counts[(long long)c * ld + g], exp(fail_r));
+  matw[i] = 1.0 - mfp * sfp;
+}
+
+hipError_t launch_vn_modes(const double* jp, long long jg, long long jk, int ngenes, int G, const double* mag,
+                           int expected, double* modes, hipStream_t st) {
+  if (ngenes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_vn_modes, dim3((ngenes + 255) / 256), dim3(256), 0, st, jp, jg, jk, ngenes, G, mag, expected,
+                     modes);
+  return hipGetLastError();
+}
+
+hipError_t launch_vn_matw(const int* counts, long long ld, int ngenes, const int* cellidx, int ncells,
+                          const double* models, int mld, int sq, const double* modes, const long long* mode_off,
+                          double* matw, hipStream_t st) {
+  const long long n = (long long)ngenes * ncells;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_vn_matw, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, counts, ld, ngenes, cellidx,
+                     ncells, models, mld, sq, modes, mode_off, matw);
+  return hipGetLastError();
+}
+
 hipError_t launch_winsorize(const double* m, int k, int n, int ntr, double* out, hipStream_t st) {
   int NP = 1;
   while (NP < n) NP <<= 1;

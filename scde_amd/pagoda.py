@@ -445,3 +445,51 @@ def plSemicompleteCor2(pl):
     n = np.zeros((npl, npl), np.int32, order="F")
     check(lib().scde_plSemicompleteCor2(npl, _p(off), _p(idx), _p(val), _p(r), _p(n)))
     return {"r": r, "n": n}
+
+
+def pagoda_varnorm_weights(models, counts, prior, batch=None, n_cores=1, n_randomizations=100,
+                           use_expected_value=True, ctx=None):
+    """pagoda.varnorm's posterior-mode consumer (R/functions.R:1401-1507), on the device:
+    scde.posteriors over all cells (and over each batch level's cells), the modes
+    ``jp %*% as.numeric(colnames(jp))`` (or the magnitude of each row's maximum with
+    ``use_expected_value=False``), and the weight matrix ``matw = 1 - mfp * sfp``
+    (mfp = scde.failure.probability at log(modes), sfp = ppois(count - 1, exp(fail.r),
+    lower.tail = FALSE)), plus the batch version ``bmatw``.  Batch levels with fewer than
+    2 cells join the largest level first (1404-1410).  Returns a dict: avmodes (genes),
+    modes (levels x genes with a batch, else None), matw, bmatw (genes x cells; bmatw None
+    without a batch)."""
+    import ctypes
+    from . import api
+    from ._lib import check, lib
+    from .models import model_matrix
+    ctx = ctx or api.default_context()
+    mat, _ = api._align_counts(models, counts)
+    N, C = mat.shape
+    mm, lt, sq = model_matrix(models)
+    px = np.ascontiguousarray(prior["x"], np.float64)
+    codes = None
+    nb = 0
+    if batch is not None:
+        b = np.asarray(batch)
+        levels = sorted(set(b.tolist()))
+        counts_per = {lv: int(np.sum(b == lv)) for lv in levels}
+        big = max(levels, key=lambda lv: counts_per[lv])
+        b = np.array([big if counts_per[x] < 2 else x for x in b.tolist()])
+        levels = sorted(set(b.tolist()))
+        if len(levels) > 1:
+            codes = np.ascontiguousarray([levels.index(x) for x in b.tolist()], np.int32)
+            nb = len(levels)
+    nm = 1 + nb if nb > 1 else 1
+    modes = np.zeros(nm * N)
+    matw = np.zeros((N, C), order="F")
+    bmatw = np.zeros((N, C), order="F") if nb > 1 else None
+    P = ctypes.c_void_p
+
+    def p(a):
+        return None if a is None else a.ctypes.data_as(P)
+    check(lib().scde_pagoda_varnorm_weights_host(ctx.handle, p(mat), N, N, C, p(mm), lt, sq, p(px), len(px),
+                                                 int(n_randomizations), int(n_cores), p(codes), nb,
+                                                 int(bool(use_expected_value)), p(modes), p(matw), p(bmatw)))
+    modes = modes.reshape(nm, N)
+    return {"avmodes": modes[0].copy(), "modes": modes[1:].copy() if nm > 1 else None, "matw": matw,
+            "bmatw": bmatw}

@@ -76,3 +76,34 @@ def test_host_glue_matches_oracle(oracle):
     np.testing.assert_array_equal(api.marginals(g["prior_x"]), oracle.marginals_from_prior_x(g["prior_x"]))
     dv = api.ratio_columns(g["prior_x"])
     assert api.expectation_column(dv, 0) == 400
+
+
+def test_r_shim_compiles_and_binds_exported_symbols():
+    """R/src/scde_hip_shim.c (the .Call shim, NAMESPACE:29 useDynLib(scde)) is valid C99 against
+    the C ABI header -- checked with declaration-only R API stubs (tests/rstub), as there is no R
+    here -- and every scde_* entry it calls is exported by libscde_hip.so.  It defines the
+    reference's ten .Call symbols (src/jpmatLogBoot.h:6-9, src/matSlideMult.h:6, src/bwpca.h:8,
+    src/pagoda.h:5-8) plus the fused-path ones R/R/scde_hip.R calls."""
+    import shutil
+    import subprocess
+    from scde_amd import _lib
+    src = os.path.join(ROOT, "R", "src", "scde_hip_shim.c")
+    gcc = shutil.which("gcc")
+    if gcc:
+        r = subprocess.run([gcc, "-fsyntax-only", "-Wall", "-Wextra", "-Wno-unused-parameter", "-Werror", "-std=c99",
+                            "-I", os.path.join(ROOT, "tests", "rstub"), "-I", os.path.join(ROOT, "include"), src],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+    txt = re.sub(r"/\*.*?\*/", "", open(src).read(), flags=re.S)
+    called = set(re.findall(r"\b(scde_[a-zA-Z0-9_]+)\s*\(", txt)) - {"scde_hip_expression_difference",
+                                                                      "scde_hip_posteriors",
+                                                                      "scde_hip_varnorm_weights"}
+    L = _lib.lib()
+    for n in called:
+        assert hasattr(L, n), n
+    defined = set(re.findall(r"^SEXP\s+([A-Za-z0-9_]+)\s*\(", txt, flags=re.M))
+    assert {"logBootPosterior", "logBootBatchPosterior", "jpmatLogBoot", "jpmatLogBatchBoot", "matSlideMult",
+            "baileyWPCA", "winsorizeMatrix", "matWCorr", "plSemicompleteCor2", "matCorr"} <= defined
+    rwrap = open(os.path.join(ROOT, "R", "R", "scde_hip.R")).read()
+    for sym in re.findall(r'\.Call\("([A-Za-z0-9_]+)"', rwrap):
+        assert sym in defined, sym

@@ -120,3 +120,46 @@ def test_plsemicompletecor2_matches_oracle():
     got, want = PG.plSemicompleteCor2(pl), OP.plSemicompleteCor2(pl)
     np.testing.assert_array_equal(got["n"], want["n"])
     np.testing.assert_allclose(got["r"], want["r"], rtol=1e-12, atol=1e-15)
+
+
+# ---- pagoda.varnorm's posterior-mode consumer (R/functions.R:1414-1507)
+def _varnorm_inputs(ngenes=70):
+    from conftest import golden
+    from oracle import oracle as O
+    g = golden("esmef500.npz")
+    models = {c: g["models"][:, j] for j, c in enumerate(O.MODEL_COLUMNS) if not np.all(np.isnan(g["models"][:, j]))}
+    return models, np.ascontiguousarray(g["counts"][:ngenes]), {"x": g["prior_x"], "y": g["prior_y"]}
+
+
+def test_oracle_varnorm_poisson_tail():
+    """sfp's upper tail P(X >= c) at the boundary cases R's ppois(c - 1, lambda, FALSE) has."""
+    from scipy.stats import poisson
+    lam = 0.1
+    assert poisson.sf(-1, lam) == 1.0  # count 0
+    assert poisson.sf(0, lam) == pytest.approx(1 - np.exp(-lam), rel=1e-14)
+    assert poisson.sf(2, lam) == pytest.approx(1 - np.exp(-lam) * (1 + lam + lam * lam / 2), rel=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("expected,batched", [(True, False), (False, False), (True, True)])
+def test_varnorm_weights_match_oracle(expected, batched):
+    from oracle import pagoda as OP
+    from scde_amd import api
+    from scde_amd import pagoda as PG
+    models, counts, prior = _varnorm_inputs()
+    C = counts.shape[1]
+    batch = np.array(["b%d" % (i % 3) for i in range(C)]) if batched else None
+    api.set_rand("glibc")
+    got = PG.pagoda_varnorm_weights(models, counts, prior, batch=batch, n_cores=2, n_randomizations=20,
+                                    use_expected_value=expected)
+    codes = np.array([i % 3 for i in range(C)]) if batched else None
+    want = OP.varnorm_weights(models, counts, prior["x"], batch_codes=codes, n_randomizations=20, n_cores=2,
+                              use_expected_value=expected)
+    # the joint posteriors' SURVEY 8(d) bar (1e-6 relative) carries into their expected values
+    # and through log(mode) into matw; the row-maximum modes are grid values, exact
+    rt = 1e-6 if expected else 0.0
+    np.testing.assert_allclose(got["avmodes"], want["modes"][0], rtol=rt)
+    np.testing.assert_allclose(got["matw"], want["matw"], rtol=1e-6 if expected else 1e-12, atol=1e-15)
+    if batched:
+        np.testing.assert_allclose(got["modes"], want["modes"][1:], rtol=rt)
+        np.testing.assert_allclose(got["bmatw"], want["bmatw"], rtol=1e-6, atol=1e-15)
