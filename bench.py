@@ -46,7 +46,9 @@ sys.path.insert(0, ROOT)
 NBOOT = 100
 LENGTH_OUT = 400
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
-FP64_VALU_PEAK_TF = 78.6  # FP64 vector spec = FP32 vector 157.3 TF (MI355X_MICROARCH.md) / 2; 67 TF measured (tools/micro)
+FP64_VALU_PEAK_TF = 78.6  # FP64 vector spec = FP32 vector 157.3 TF (MI355X_MICROARCH.md) / 2
+FP64_FMA_MEASURED_TF = 67.0  # v_fma_f64 rate measured on this part (tools/micro/f64_rates.hip)
+I8_MFMA_PEAK_TOPS = 5000.0  # int8 MFMA: 2x the BF16 rate per clock (MI355X_MICROARCH.md), BF16 ~2.5 PF dense
 METRIC = "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)"
 
 CONFIGS = {
@@ -114,6 +116,7 @@ def dominant_kernel_bytes(ngenes, cells_per_group):
 
 
 BOOT_STAGE = "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum_partials)"
+BOOTQ_STAGE = "fixed-point bootstrap (k_bootq)"
 
 
 def profiled_traffic(config: str):
@@ -138,9 +141,13 @@ def profiled_traffic(config: str):
         return None
     if any(v.get("traffic_bytes") is None for v in stage.values()):
         return None
-    return {"file": "profiles/" + cands[-1], "kernel": " + ".join(sorted(stage)),
-            "avg_ms": sum(v["avg_ms"] * v["calls"] for v in stage.values()) / n,
-            "traffic_bytes": sum(v["traffic_bytes"] * v["calls"] for v in stage.values()) / n}
+    out = {"file": "profiles/" + cands[-1], "kernel": " + ".join(sorted(stage)),
+           "avg_ms": sum(v["avg_ms"] * v["calls"] for v in stage.values()) / n,
+           "traffic_bytes": sum(v["traffic_bytes"] * v["calls"] for v in stage.values()) / n}
+    cyc = sum(v.get("SQ_WAVE_CYCLES", 0) * v["calls"] for v in stage.values())
+    if cyc > 0:  # share of the stage's wave cycles spent waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES)
+        out["wait_frac"] = sum(v.get("SQ_WAIT_ANY", 0) * v["calls"] for v in stage.values()) / cyc
+    return out
 
 
 def stage_kernel(name: str) -> bool:
@@ -150,7 +157,8 @@ def stage_kernel(name: str) -> bool:
 
 
 def stage_last(name: str) -> bool:
-    return name == "k_sum_partials"
+    """The kernel that ends one stage (one per bootstrap launch)."""
+    return name in ("k_sum_partials", "k_bootq")
 
 
 def _cpu_chunk(job):
@@ -575,31 +583,61 @@ def main():
     kt = ctx.kernel_times()
     ctx.set_profiling(False)
 
+    # arithmetic the bootstrap kernels issue in one step (one extra untimed step with the
+    # context's counters on): FP64 lane FMAs of k_boot2, int8 MACs of k_bootq
+    ctx.set_option("skip_stats", 1)
+    ctx.reset_stats()
+    run(dc.ptr)
+    ctx.synchronize()
+    step_fma, step_mac = ctx.stat("boot_f64_fma"), ctx.stat("boot_i8_mac")
+    ctx.set_option("skip_stats", 0)
+
     total_genes = NTOT * args.steps
     value = total_genes / dt
     boot_ms, boot_n = kt["boot"]
     boot_avg_s = (boot_ms / max(boot_n, 1)) / 1e3
+    boot_step_s = boot_ms / 1e3 / args.steps
     cpg = NC // 2 if de else NC
     # bootstrap launches of one step and their cells: (per group) + (all cells, per group) if batched
     launch_cells = ([cpg, cpg] if de else [NC]) + ([NC, NC] if batched else [])
     step_bytes = sum(dominant_kernel_bytes(NG, c) for c in launch_cells)
     per_launch_bytes = step_bytes / len(launch_cells)
-    achieved = step_bytes * args.steps / (boot_ms / 1e3) / 1e9 if boot_n else None
+    hbm_alg = step_bytes * args.steps / (boot_ms / 1e3) / 1e9 if boot_n else None
     prof = profiled_traffic(args.config)
     # reference-formulation FP64 adds per launch: B x C x G x N
     ref_adds = NBOOT * sum(launch_cells) / len(launch_cells) * G * NG
-    roof = {"bound": "hbm", "kernel": BOOT_STAGE,
-            "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": (achieved / HBM_PEAK_GBS) if achieved else None,
-            "traffic": prof["traffic_bytes"] if prof else None,
-            "traffic_source": (f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"
-                               if prof else None),
-            "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
-            "algorithmic_bytes_per_launch": per_launch_bytes,
-            "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None}
+    f64_tf = 2 * step_fma / boot_step_s / 1e12 if boot_n and step_fma else 0.0
+    i8_tops = 2 * step_mac / boot_step_s / 1e12 if boot_n and step_mac else 0.0
+    if step_mac > step_fma:
+        # fixed-point bootstrap (k_bootq): int8 MFMA ops issued over the stage time
+        roof = {"bound": "mfma", "kernel": BOOTQ_STAGE, "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS,
+                "unit": "TOPS (int8)", "frac": i8_tops / I8_MFMA_PEAK_TOPS,
+                "achieved_basis": "int8 MACs issued by k_bootq's v_mfma_i32_16x16x64_i8 (x2 ops) per step / "
+                                  "stage time per step (HIP events)"}
+    else:
+        # FP64 bootstrap (k_boot2): the FMAs its kept stretches issue, against the FP64 VALU peak
+        roof = {"bound": "fp64-valu", "kernel": BOOT_STAGE, "achieved": f64_tf, "peak": FP64_VALU_PEAK_TF,
+                "unit": "TFLOP/s", "frac": f64_tf / FP64_VALU_PEAK_TF,
+                "frac_of_measured_fma_rate": f64_tf / FP64_FMA_MEASURED_TF,
+                "achieved_basis": "k_boot2 lane FMAs issued (kept stretches x 64 x slab boots x entries, x2 flops) "
+                                  "per step / stage time per step (HIP events)"}
+    roof.update({
+        "traffic": prof["traffic_bytes"] if prof else None,
+        "traffic_source": (f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"
+                           if prof else None),
+        "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
+        # SURVEY.md §8(d)'s algorithmic bytes of the reference formulation over the stage time:
+        # the work avoided (sparse deltas, skipped stretches) counts as if it were read
+        "algorithmic_bytes_per_launch": per_launch_bytes,
+        "hbm_algorithmic_gbs": hbm_alg,
+        "hbm_algorithmic_frac": (hbm_alg / HBM_PEAK_GBS) if hbm_alg else None,
+        "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None,
+        "f64_fma_per_step": step_fma, "i8_mac_per_step": step_mac})
     if prof:
         # what the stage really moves: counter bytes per stage over the rocprof stage time
         roof["counter_bytes_frac"] = prof["traffic_bytes"] / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+        if prof.get("wait_frac") is not None:
+            roof["wait_frac"] = prof["wait_frac"]
     out = {
         "metric": (METRIC_BATCH if batched else METRIC) if de else "genes/sec for scde.posteriors with posterior modes "
                                                                    "(400-pt grid, 100 randomizations)",

@@ -118,12 +118,18 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
 /* Tuning and test options of a context (defaults are the product settings; nothing is read
  * from the environment on the compute path):
  *   "boot_skip"     1/0  grid-stretch skipping in the bootstrap (output unchanged either way)
+ *   "boot_q"        bootstrap kernel: 1 = fixed-point int8-MFMA k_bootq from boot_q_cells cells
+ *                   per call on (default), 2 = always where it applies, 0 = FP64 k_boot2 only
+ *   "boot_q_cells"  the cell count from which boot_q = 1 selects k_bootq (default 1000)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
  *   "ratio_window"  k_ratio_summary register window 4, 5, 7 or 8;  "ratio_block" 64, 128, 256
  *   "wpca_ms"       1/0  the multi-start npcs = 1 weighted-PCA kernel
- * Statistics: "skip_slabs", "skip_stretches", "skip_kept", "skip_redo" (with skip_stats). */
+ * Statistics: "skip_slabs", "skip_stretches", "skip_kept", "skip_redo", "degen", "tiles_<i>"
+ * (k_bootq slabs computing i tiles) (with skip_stats);
+ * "boot_f64_fma" (k_boot2: FP64 lane FMAs issued) and "boot_i8_mac" (k_bootq: int8 MACs issued
+ * by its MFMAs), also with skip_stats. */
 int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);
 int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
 int scde_ctx_reset_stats(scde_ctx* ctx);

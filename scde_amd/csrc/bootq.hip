@@ -396,6 +396,8 @@ __global__ __launch_bounds__(512) void k_bootq(BootQArgs a) {
       atomicAdd(&a.stats[2], NT);
       atomicAdd(&a.stats[3], rounds - 1);
       atomicAdd(&a.stats[4 + nk_s], 1);  // histogram of tiles per slab
+      atomicAdd(&a.stats[33], nk_s * (KP >> 6));  // 64-entry steps of the row MFMAs (14 each)
+      atomicAdd(&a.stats[34], KP >> 6);           // ... of the bound MFMAs (16 each)
     }
     // ---- 5. softmax terms, per-boot sums (tile order), jp
     const int nk = nk_s;

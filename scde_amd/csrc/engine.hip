@@ -189,6 +189,9 @@ struct scde_ctx {
   int opt_wpca_ms = 1;           // "wpca_ms": the multi-start npcs = 1 kernel (k_wpca_ms1)
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
+  // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
+  // stretches x 64 lanes x slab boots x entries) and int8 MACs of k_bootq (MFMAs x 16 x 16 x 64)
+  double st_boot_f64_fma = 0, st_boot_i8_mac = 0;
   static constexpr int kQMaxTilesHost = 28;
   double st_tile_hist[kQMaxTilesHost + 1] = {0};
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
@@ -513,6 +516,7 @@ int run_bootq(scde_ctx* cx, const PostSpec& s, UniqueSet& u, const TablesArgs& t
     cx->st_skip_stretches += h[4];
     cx->st_skip_redo += h[5];
     cx->st_degen += h[1];
+    cx->st_boot_i8_mac += ((double)h[35] * 14 + (double)h[36] * 16) * 16 * 16 * 64;
   }
   // exact fallback: T tables only when some gene was flagged (gate), then k_boot_exact
   if (!have_T) {
@@ -815,16 +819,21 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       }
       HCHK(launch_boot2(b2, st));
       if (stretch_skip && cx->opt_skip_stats) {  // diagnostics: kept stretches, redo slabs
-        std::vector<int> m((size_t)P * N), r((size_t)P * N);
+        std::vector<int> m((size_t)P * N), r((size_t)P * N), nz(N);
         HCHK(hipMemcpyAsync(m.data(), cx->smask.p, sizeof(int) * m.size(), hipMemcpyDeviceToHost, st));
         HCHK(hipMemcpyAsync(r.data(), cx->sredo.p, sizeof(int) * r.size(), hipMemcpyDeviceToHost, st));
+        HCHK(hipMemcpyAsync(nz.data(), cx->nnz.p, sizeof(int) * nz.size(), hipMemcpyDeviceToHost, st));
         HCHK(hipStreamSynchronize(st));
         const int nst = (G + 63) / 64;
         long long kept = 0, redo = 0;
-        for (size_t i = 0; i < m.size(); ++i) {
-          kept += __builtin_popcount((unsigned)m[i]);
+        double fma = 0;
+        for (size_t i = 0; i < m.size(); ++i) {  // i = g * P + p
+          const int k = __builtin_popcount((unsigned)m[i]);
+          kept += k;
           redo += r[i] != 0;
+          fma += (double)(k + (r[i] != 0 ? nst : 0)) * 64.0 * nb * nz[i / P];
         }
+        cx->st_boot_f64_fma += fma;
         cx->st_skip_slabs += (double)m.size();
         cx->st_skip_stretches += (double)(m.size() * nst);
         cx->st_skip_kept += (double)kept;
@@ -1082,6 +1091,8 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   if (n == "skip_slabs") *value = ctx->st_skip_slabs;
   else if (n == "skip_stretches") *value = ctx->st_skip_stretches;
   else if (n == "skip_kept") *value = ctx->st_skip_kept;
+  else if (n == "boot_f64_fma") *value = ctx->st_boot_f64_fma;
+  else if (n == "boot_i8_mac") *value = ctx->st_boot_i8_mac;
   else if (n == "skip_redo") *value = ctx->st_skip_redo;
   else if (n == "degen") *value = ctx->st_degen;
   else if (n.rfind("tiles_", 0) == 0 && atoi(n.c_str() + 6) >= 0 && atoi(n.c_str() + 6) <= 28)
@@ -1093,6 +1104,7 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
 int scde_ctx_reset_stats(scde_ctx* ctx) {
   if (!ctx) return fail(SCDE_EARG, "null argument");
   ctx->st_skip_slabs = ctx->st_skip_kept = ctx->st_skip_stretches = ctx->st_skip_redo = ctx->st_degen = 0;
+  ctx->st_boot_f64_fma = ctx->st_boot_i8_mac = 0;
   for (double& x : ctx->st_tile_hist) x = 0;
   return SCDE_OK;
 }

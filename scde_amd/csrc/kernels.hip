@@ -257,7 +257,18 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
       // log(e / s) as log e - log s (no division); e / s could round differently only
       // below DBL_MIN * s, where the reference's quotient is evaluated as written
       const double e = v[k];
-      r = (SCDE_KT_DIAG & 4) ? e - lsum : (e >= 0x1p-960) ? log_tab(e, lt) - lsum : log_tab(e / s, lt);
+      if (SCDE_KT_DIAG & 4) {
+        r = e - lsum;
+      } else {
+        // the quotient path only for waves that have a lane below 2^-960 (high counts at
+        // far grid points); a select would evaluate both logs and the division everywhere
+        const bool tiny = !(e >= 0x1p-960);
+        r = log_tab(tiny ? 1.0 : e, lt) - lsum;
+        if (__builtin_amdgcn_ballot_w64(tiny)) {
+          const double rq = log_tab(e / s, lt);
+          r = tiny ? rq : r;
+        }
+      }
       if (r > bv) {
         bv = r;
         bi = k;
