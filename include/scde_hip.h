@@ -118,9 +118,14 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
 /* Tuning and test options of a context (defaults are the product settings; nothing is read
  * from the environment on the compute path):
  *   "boot_skip"     1/0  grid-stretch skipping in the bootstrap (output unchanged either way)
- *   "boot_q"        bootstrap kernel: 1 = fixed-point int8-MFMA k_bootq from boot_q_cells cells
- *                   per call on (default), 2 = always where it applies, 0 = FP64 k_boot2 only
+ *   "boot_q"        fixed-point int8-MFMA bootstrap k_bootq: 0 = never (default), 1 = from
+ *                   boot_q_cells cells per call, 2 = always where it applies
  *   "boot_q_cells"  the cell count from which boot_q = 1 selects k_bootq (default 1000)
+ *   "boot_tiles"    1/0  the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles; default 1)
+ *   "boot_tiles_cells"  the cell count from which it is used (default 200; below: k_boot2's
+ *                   64-point stretch mask)
+ *   "tile_groups"   register groups of 4 tiles per k_boot_tiles wave, 1 or 2 (default 2; slabs
+ *                   needing more go to k_boot2 whole -- tests force that with 1)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)

@@ -40,29 +40,11 @@
 
 namespace scde {
 
-typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kQWaves = 8;        // waves per k_bootq block (one gene)
 constexpr int kQSlab = 32;        // boots per slab (two 16-boot MFMA tiles)
 constexpr int kQSlotsPerWave = 4; // computed tiles whose rows a wave holds: 8 x 4 >= 28 tiles
 constexpr int kQMaxTiles = 28;    // G <= 448
-
-__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
-
-// 4 x 4 byte transpose: p_i byte j = source j byte i.
-__device__ __forceinline__ void tr4(unsigned a, unsigned b, unsigned c, unsigned d, unsigned& p0, unsigned& p1,
-                                    unsigned& p2, unsigned& p3) {
-  const unsigned ab02 = __builtin_amdgcn_perm(b, a, 0x06020400u);
-  const unsigned ab13 = __builtin_amdgcn_perm(b, a, 0x07030501u);
-  const unsigned cd02 = __builtin_amdgcn_perm(d, c, 0x06020400u);
-  const unsigned cd13 = __builtin_amdgcn_perm(d, c, 0x07030501u);
-  p0 = __builtin_amdgcn_perm(cd02, ab02, 0x05040100u);
-  p2 = __builtin_amdgcn_perm(cd02, ab02, 0x07060302u);
-  p1 = __builtin_amdgcn_perm(cd13, ab13, 0x05040100u);
-  p3 = __builtin_amdgcn_perm(cd13, ab13, 0x07060302u);
-}
 
 constexpr int kZChunk = 64;  // cells per baseline-sum block
 

@@ -547,4 +547,24 @@ __device__ inline dd dd_add_d(dd a, double b) {
 }
 __device__ inline double dd_to_d(dd a) { return __dadd_rn(a.hi, a.lo); }
 
+// int8 matrix-core helpers (k_bootq rows and bounds, k_boot_tiles bounds)
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+// 4 x 4 byte transpose: p_i byte j = source j byte i.
+__device__ __forceinline__ void tr4(unsigned a, unsigned b, unsigned c, unsigned d, unsigned& p0, unsigned& p1,
+                                    unsigned& p2, unsigned& p3) {
+  const unsigned ab02 = __builtin_amdgcn_perm(b, a, 0x06020400u);
+  const unsigned ab13 = __builtin_amdgcn_perm(b, a, 0x07030501u);
+  const unsigned cd02 = __builtin_amdgcn_perm(d, c, 0x06020400u);
+  const unsigned cd13 = __builtin_amdgcn_perm(d, c, 0x07030501u);
+  p0 = __builtin_amdgcn_perm(cd02, ab02, 0x05040100u);
+  p2 = __builtin_amdgcn_perm(cd02, ab02, 0x07060302u);
+  p1 = __builtin_amdgcn_perm(cd13, ab13, 0x05040100u);
+  p3 = __builtin_amdgcn_perm(cd13, ab13, 0x07060302u);
+}
+
 }  // namespace scde

@@ -178,7 +178,7 @@ struct scde_ctx {
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, qflags;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
-  int opt_boot_q = 1;            // "boot_q": the fixed-point int8-MFMA bootstrap: 0 never, 1 from boot_q_cells, 2 always
+  int opt_boot_q = 0;            // "boot_q": the fixed-point int8-MFMA bootstrap: 0 never, 1 from boot_q_cells, 2 always
   int opt_boot_q_cells = 1000;   // "boot_q_cells": cells per call from which boot_q = 1 picks it
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 30 + 0.4 C); tests force redo slabs
@@ -187,6 +187,10 @@ struct scde_ctx {
   int opt_ratio_window = 4;      // "ratio_window": k_ratio_summary register window (4, 5, 7, 8)
   int opt_ratio_block = 128;     // "ratio_block": k_ratio_summary block size (64, 128, 256)
   int opt_wpca_ms = 1;           // "wpca_ms": the multi-start npcs = 1 kernel (k_wpca_ms1)
+  int opt_boot_tiles = 1;        // "boot_tiles": the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles)
+  int opt_boot_tiles_cells = 200;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
+                                   // rows are wide, most slabs need > 8 tiles, k_boot2's stretches win)
+  int opt_tile_groups = 2;       // "tile_groups": register groups of 4 tiles per k_boot_tiles wave (1 or 2)
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
@@ -640,6 +644,24 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     qpath = maxw <= 127 && ndraw < 65000 && bootq_lds_bytes(qstride) <= 130 * 1024 &&
             (ncols + 1) * (long long)GS < (1LL << 31);
   }
+  // FP64 path: boots per slab, draws (before the tables: the tile path needs the largest
+  // multiplicity to decide what the tables emit)
+  int nb = fast ? boot2_nb(s.nboot) : 16;
+  if (fast) {
+    const int v = cx->opt_boot_nb;  // tuning option: a multiple of 4 in [4, 32]
+    if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
+  }
+  const int Bp = (int)round_up(std::max(s.nboot, 1), nb);
+  if (fused && !qpath && s.nboot > 0) {
+    make_draws(s, Bp, draws, W, ndraw);
+    maxw = 0;
+    for (double w : W) maxw = std::max(maxw, (int)w);
+  }
+  // k_boot_tiles: G <= 448, nb <= 20, multiplicities <= 127 (int8), int32 digit sums
+  const bool tpath = fused && !qpath && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
+                     C >= cx->opt_boot_tiles_cells &&
+                     nb <= 20 && maxw <= 127 && C < 100000 && (ncols + 1) * (long long)GS < (1LL << 31);
+  const int Bt = (int)round_up(Bp, 32) + 32;  // byte multiplicity rows: the last slab reads 32 boots
   if (keep_T) HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
   HCHK(cx->maxi.ensure(sizeof(int) * std::max<long long>(1, ncols)));
   HCHK(cx->has_clamp.ensure(std::max<long long>(1, ncols)));
@@ -665,8 +687,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   ta.use_baseline = s.use_baseline ? 1 : 0;
   // k_boot2 grid-stretch skipping (G <= 448: at most 7 stretches of 64 points); the
   // tables kernel emits the per-column stretch maxima.  SCDE_BOOT_SKIP=0 disables it.
-  const bool stretch_skip = fused && !qpath && G <= 448 && cx->opt_boot_skip;
-  if (qpath) {
+  const bool stretch_skip = fused && !qpath && !tpath && G <= 448 && cx->opt_boot_skip;
+  if (qpath || tpath) {
     HCHK(cx->qflags.ensure(sizeof(int) * 40));
     HCHK(hipMemsetAsync(cx->qflags.p, 0, sizeof(int) * 40, st));
     HCHK(cx->ubound.ensure(sizeof(unsigned) * kQTiles * (size_t)(ncols + 1)));
@@ -734,13 +756,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   } else if (qpath) {
     RCHK(run_bootq(cx, s, u, ta, ncols, GS, draws, W, ndraw, Bq, qstride, keep_T));
   } else {
-    int nb = fast ? boot2_nb(s.nboot) : 16;
-    if (fast) {
-      const int v = cx->opt_boot_nb;  // tuning option: a multiple of 4 in [4, 32]
-      if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
-    }
-    const int Bp = (int)round_up(s.nboot, nb);
-    make_draws(s, Bp, draws, W, ndraw);
+    if (!fused) make_draws(s, Bp, draws, W, ndraw);
     RCHK(upload(cx, cx->Wt, W.data(), sizeof(double) * W.size()));
     RCHK(upload(cx, cx->draws, draws.data(), sizeof(int) * draws.size()));
     if (!fused) {
@@ -748,7 +764,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       HCHK(launch_base_cols(u.ucl.as<int>(), u.ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
                             s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
     }
-    const int stride = (int)round_up(C, 8) + 8;  // + one look-ahead batch (k_boot2)
+    // + one look-ahead batch (k_boot2); the tile path's bounds read whole 64-entry steps
+    const int stride = tpath ? qstride : (int)round_up(C, 8) + 8;
     HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * stride)));
     HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
     ev = cx->mark_begin(SLOT_OTHER);
@@ -760,7 +777,18 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     // the baseline columns: T (slow path) or the fused D buffer, which holds T there
     const double* Tbase = fused ? cx->E.as<double>() : cx->T.as<double>();
     HCHK(launch_ell(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->base_col.as<int>(), stride,
-                    (int)ncols, 8, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
+                    (int)ncols, tpath ? 64 : 8, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
+    if (tpath) {
+      // byte multiplicities [set][cell][boot] (baseline bound sums and the tile bounds)
+      std::vector<unsigned char> w8((size_t)nsets * C * Bt, 0);
+      for (int set = 0; set < nsets; ++set)
+        for (int c = 0; c < C; ++c)
+          for (int b = 0; b < Bp; ++b) w8[((size_t)set * C + c) * Bt + b] = (unsigned char)W[((size_t)set * C + c) * Bp + b];
+      RCHK(upload(cx, cx->w8, w8.data(), w8.size()));
+      HCHK(cx->zubound.ensure(sizeof(int) * (size_t)nsets * 4 * kQTiles * Bt));
+      HCHK(launch_zuq(cx->ubound.as<unsigned>(), cx->base_col.as<int>(), C, cx->w8.as<unsigned char>(), Bt, nsets,
+                      cx->zubound.as<int>(), st));
+    }
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
     HCHK(launch_baseline_z(Tbase, G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
                            cx->Z.as<double>(), st));
@@ -817,7 +845,31 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         b2.ubuf = cx->subuf.as<double>();
         b2.redo = cx->sredo.as<int>();
       }
-      HCHK(launch_boot2(b2, st));
+      if (tpath) {
+        HCHK(cx->sredo.ensure(sizeof(int) * ((size_t)P * N + 1)));
+        b2.redo = cx->sredo.as<int>();
+        TileBootArgs tb{};
+        tb.W8 = cx->w8.as<unsigned char>();
+        tb.Bq = Bt;
+        tb.UQ = cx->ubound.as<unsigned>();
+        tb.ZUq = cx->zubound.as<int>();
+        tb.nanflag = cx->qflags.as<int>();
+        tb.maxgroups = cx->opt_tile_groups;
+        tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
+        HCHK(launch_boot_tiles(b2, tb, st));
+        if (cx->opt_skip_stats) {
+          int h[8];
+          HCHK(hipMemcpyAsync(h, cx->qflags.p, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
+          HCHK(hipStreamSynchronize(st));
+          cx->st_skip_slabs += h[2];
+          cx->st_skip_kept += h[3];
+          cx->st_skip_stretches += h[4];
+          cx->st_skip_redo += h[5];
+          cx->st_boot_f64_fma += (double)h[6] * 64.0 * nb + (double)h[7] * nb * (double)round_up(G, 64);
+        }
+      } else {
+        HCHK(launch_boot2(b2, st));
+      }
       if (stretch_skip && cx->opt_skip_stats) {  // diagnostics: kept stretches, redo slabs
         std::vector<int> m((size_t)P * N), r((size_t)P * N), nz(N);
         HCHK(hipMemcpyAsync(m.data(), cx->smask.p, sizeof(int) * m.size(), hipMemcpyDeviceToHost, st));
@@ -1081,6 +1133,9 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "ratio_window") ctx->opt_ratio_window = (int)value;
   else if (n == "ratio_block") ctx->opt_ratio_block = (int)value;
   else if (n == "wpca_ms") ctx->opt_wpca_ms = value != 0;
+  else if (n == "boot_tiles") ctx->opt_boot_tiles = value != 0;
+  else if (n == "boot_tiles_cells") ctx->opt_boot_tiles_cells = (int)value;
+  else if (n == "tile_groups") ctx->opt_tile_groups = (int)value;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
 }

@@ -92,6 +92,7 @@ __host__ __device__ inline unsigned long long packq(long long d) {  // |d| < 2^5
 }
 __host__ __device__ inline long long unpackq(unsigned long long p) { return (long long)(p ^ kQBias) - (long long)kQBias; }
 __host__ __device__ inline unsigned packu(int u) { return ((unsigned)u + 0x80808080u) ^ 0x80808080u; }  // |u| < 2^31
+__host__ __device__ inline int unpacku(unsigned p) { return (int)((p ^ 0x80808080u) - 0x80808080u); }
 
 struct BootQArgs {
   const unsigned long long* DQ;  // [ncols + 1][GS] packed digits (TablesArgs::DQ)
@@ -170,6 +171,20 @@ struct Boot2Args {
   int* redo;     // [ngenes][P] slabs whose skipped stretches failed the post-check
   double slack;  // heuristic slack of the mask (NaN: the default 30 + 0.4 C)
 };
+
+// k_boot_tiles (with Boot2Args; needs G <= 448): multiplicities as bytes and the tables'
+// 16-point tile bounds for the exact integer tile bounds of each (gene, slab)
+struct TileBootArgs {
+  const unsigned char* W8;   // [nsets][ncells][Bq] draw multiplicities (<= 127)
+  int Bq;                    // a multiple of 32, >= the last slab's first boot + 32
+  const unsigned* UQ;        // [ncols + 1][kQTiles] packed tile maxima (units of 2^-8, rounded up)
+  const int* ZUq;            // [nsets][4][kQTiles][Bq] baseline tile-bound digit sums
+  const int* nanflag;        // tables saw a NaN: every slab goes to k_boot2
+  int maxgroups;             // register groups of 4 tiles (1 or 2)
+  int* stats;                // nullable: [0] slabs, [1] tiles computed, [2] tiles, [3] slabs left to k_boot2,
+                             // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left
+};
+hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 
 struct ExactArgs {
   const double* T;  // log tables; or fused D columns when base_col is set (T = D + D[base])

@@ -249,6 +249,10 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   unsigned long long* qout = (Q && phase) ? a.DQ + col * a.GS : nullptr;
   long long* vq = reinterpret_cast<long long*>(v);
   bool nanq = false;
+  // FP64 tile bounds for k_boot_tiles (UQ set, fused phases): per 16-point tile the column's
+  // maximum in units of 2^-8, rounded up; phase-2 columns store it minus their baseline
+  // column's value (exact integers, so base + delta >= the column's maximum)
+  const bool uqf = !Q && a.UQ && phase;
 #pragma unroll 1
   for (int j = 0; 64 * j < G; ++j) {
     const int k = lane + 64 * j;
@@ -283,7 +287,8 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         if (out) out[k] = r;
         if (dout) dout[k] = base ? r - base[k] : r;
       }
-      if (U) v[k] = r;  // the row of final values, for the stretch maxima below
+      if (U || uqf) v[k] = r;  // the row of final values, for the stretch / tile maxima below
+      if (uqf && r != r) nanq = true;
       if (qout) {
         long long q = 0;
         if (r != r)
@@ -314,6 +319,27 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
     m = o > m ? o : m;
     if ((lane & 1) == 0) {
       const int u = (t < nt) ? (int)(-((-m) >> (kQFrac - kQUFrac))) : 0;  // ceil(m / 2^28)
+      a.UQ[col * kQTiles + t] = packu(u);
+    }
+  }
+  if (uqf) {
+    if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
+    const int nt = (G + 15) / 16, t = lane >> 1;
+    double m = -INFINITY;
+    if (t < nt)
+      for (int i = 0; i < 8; ++i) {
+        const int k = 16 * t + 8 * (lane & 1) + i;
+        if (k < G) m = gt_max(m, v[k]);
+      }
+    m = gt_max(m, __shfl_xor(m, 1, 64));
+    if ((lane & 1) == 0) {
+      int u = 0;
+      if (t < nt) {
+        // r <= 0; below -2^21 the bound is raised to -2^21 (still an upper bound)
+        const double sc = fmax(m * 256.0, -0x1p29);
+        u = (int)ceil(sc);
+        if (bc_u >= 0) u -= unpacku(a.UQ[(long long)bc_u * kQTiles + t]);
+      }
       a.UQ[col * kQTiles + t] = packu(u);
     }
   }
@@ -545,7 +571,9 @@ __global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long l
     n += __popcll(m);
   }
   if (lane == 0) nnz[g] = n;
-  const int end = padto == 64 ? (n > 0 ? (n + 63) & ~63 : 64) : ((n + 7) & ~7) + 8;
+  // padto 64: k_bootq reads whole 64-entry steps; k_boot_tiles' FP64 loop also looks one
+  // 4-entry batch past its last batch, hence the extra 8
+  const int end = padto == 64 ? (n > 0 ? (n + 63) & ~63 : 64) + 8 : ((n + 7) & ~7) + 8;
   for (int p = n + lane; p < end && p < stride; p += 64) E[p] = make_int2(0, pad_col);
 }
 
@@ -832,6 +860,17 @@ __device__ __forceinline__ double red_op(double a, double b) {
   return MAX ? gt_max(a, b) : a + b;
 }
 
+// Sum over the 16 lanes of each row (16-lane group), the same bits on every lane of the row:
+// partners lane^1, lane^2 (quad_perm), lane^7 (row_half_mirror), lane^15 (row_mirror); each
+// step adds a pair of equal partial sums in both orders, and IEEE addition commutes.
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_d<kDppXor1>(v);
+  v += dpp_d<kDppXor2>(v);
+  v += dpp_d<kDppHalfMirror>(v);
+  v += dpp_d<kDppMirror>(v);
+  return v;
+}
+
 // Reduce-scatter of BC in {4, 8, 16} values over the wave, all on VALU.  Halving stages
 // pair lanes by bit 5, 4 (swaps: after the swap, a + b is the pair sum on every lane,
 // no selects), then bit 3 (lane ^ 15), bit 2 (lane ^ 7) with a keep/send select; the
@@ -968,6 +1007,15 @@ __device__ __forceinline__ void wave_max_partials(const double (&x)[NB], int I0,
   const float r = wave_max_scatter_f<BC>(t, lane);
   const int idx = (lane >> (6 - L2)) & (BC - 1);
   if ((lane & ((64 >> L2) - 1)) == 0) redf[wid * 32 + I0 + idx] = r;
+}
+
+// All NB boots' f32 maxima over one wave -> redf[slot * 32 + boot] (no barrier).
+template <int NB>
+__device__ __forceinline__ void wave_max_partials_all(const double (&x)[NB], float* redf, int lane, int slot) {
+#pragma unroll
+  for (int i0 = 0; i0 + 16 <= NB; i0 += 16) wave_max_partials<16, NB>(x, i0, redf, lane, slot);
+  if constexpr ((NB % 16) >= 8) wave_max_partials<8, NB>(x, NB - (NB % 16), redf, lane, slot);
+  if constexpr ((NB % 8) >= 4) wave_max_partials<4, NB>(x, NB - (NB % 8), redf, lane, slot);
 }
 
 // All NB boots' approximate maxima -> fin (as double).  redf: 16 x 32 floats.
@@ -1122,6 +1170,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
   static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
   constexpr int diag = SCDE_BOOT_DIAG;  // timing-only builds (tools/); 0 in production
   __shared__ double red[16 * 32];
+  __shared__ double tsum[64 * NB];  // [16-point tile][boot] partial sums (G <= 1024)
   __shared__ double fin[32];
   __shared__ double etab[64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
@@ -1321,7 +1370,23 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
     if (tid < NB) fin[tid] = acc[1];
     __syncthreads();
   } else {
-    block_sum_m<NB>(acc, live, red, fin, lane, wid, nw, wmask, lw);
+    // per-boot sums from 16-point tile partials added in tile order (row16_sum, the same
+    // form as k_boot_tiles): a slab's sums do not depend on which stretches or which
+    // kernel computed it (left-out tiles only ever hold terms the cut made zero)
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const double ps = row16_sum(acc[i]);
+      if ((lane & 15) == 0) tsum[(4 * wid + (lane >> 4)) * NB + i] = ps;
+    }
+    __syncthreads();
+    if (wsid == lw && lane < NB) {
+      const int nt = (G + 15) >> 4;
+      double r = 0.0;
+      for (int t = 0; t < nt; ++t)
+        if ((wmask >> (t >> 2)) & 1) r += tsum[t * NB + lane];
+      fin[lane] = r;
+    }
+    __syncthreads();
   }
   if (wsid == lw && lane < NB) fin[lane] = (b0 + lane < nboot) ? 1.0 / (fin[lane] * norm_mult) : 0.0;
   __syncthreads();
@@ -1329,6 +1394,319 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
 #pragma unroll
   for (int i = 0; i < NB; ++i) jpv = fma(acc[i], fin[i], jpv);
   if (live) part[(long long)p * part_stride + (long long)g * GS + tid] = jpv;
+}
+
+// ------------------------------------------------------------------ tile bootstrap
+// k_boot_tiles: k_boot2's FP64 bootstrap computed only where it matters, on 16-point grid
+// tiles chosen per (gene, boot slab) from exact integer bounds.  One wave per (gene, slab);
+// a block holds four consecutive (gene, slab) items, so a gene's slabs share the CU's
+// caches; the waves never synchronise with each other.
+//   1. bounds UB_bt = ZU_bt + sum_e W_be UQ_et for every boot and tile (UQ: the tables'
+//      per-tile column maxima in units of 2^-8, rounded up; ZU: the baseline cells' part),
+//      exact integers on the int8 matrix cores (4 balanced digits) -> LDS as f32 rounded up;
+//   2. the 4 tiles with the largest bound over the slab's live boots -> one register group
+//      (16 lanes per tile): rows Z_b + sum_e W_be D_e with k_boot2's arithmetic (scalar
+//      multiplicity operands, column look-ahead from asm), maxima m'_b (f32, as k_boot2);
+//   3. tiles not computed with UB_bt >= m'_b - 51 for some live boot: up to 4 more in a
+//      second register group; a slab needing more is left to k_boot2's redo launch;
+//   4. softmax terms, per-boot sums from 16-point tile partials in tile order (row16_sum),
+//      the jp partial row (zeros on the tiles not computed).
+// A tile left out has every row value <= UB_bt < m'_b - 51 <= m_b - 50, so all its terms
+// fall under the e^-50 cut; maxima, sums and jp rows are therefore bit for bit those of
+// k_boot2 with every stretch computed.
+constexpr int kTileMax = 28;  // G <= 448
+#ifndef SCDE_TILE_DIAG
+#define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only
+#endif
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int NB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_boot_tiles(
+    const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
+    const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
+    int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
+    long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8c, int Bq,
+    const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
+    int* __restrict__ redo, int* __restrict__ stats) {
+  static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
+  __shared__ float ubs[4][kTileMax * NB];  // [wave][tile][boot] bounds
+  __shared__ float fmx[4][2][32];          // [wave][group][boot] maxima
+  __shared__ double tsum[4][8][NB];        // [wave][tile slot][boot] partial sums
+  __shared__ double finv[4][32];
+  __shared__ double etab[64];
+  const int lane = threadIdx.x & 63;
+  const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
+  __syncthreads();
+  const int item = blockIdx.x * 4 + wsid;
+  if (item >= ngenes * P) return;
+  const int g = item / P, p = item - g * P, b0 = p * NB;
+  if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
+    if (lane == 0) redo[(long long)g * P + p] = 1;
+    return;
+  }
+  const int n = nnz[g];
+  const int NT = (G + 15) >> 4;
+  const int nlive = min(NB, nboot - b0);
+  const int r = lane & 15, h = lane >> 4;
+  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  const int set = wset ? wset[g] : 0;
+  float* ub = ubs[wsid];
+  // ---- 1. tile bounds (C layout of the 16x16x64 MFMA: tile 16 tg + r, boots 16 bt + 4 h + q);
+  // the A fragments are multiplicity bytes, cell-major, so each 16-lane row reads 16
+  // adjacent bytes
+  {
+    const unsigned char* __restrict__ W8 = W8c + (long long)set * ncells * Bq + b0;
+    const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
+    const int KP = (n + 63) & ~63;
+    for (int tg = 0; 16 * tg < NT; ++tg) {
+      const int t = 16 * tg + r;
+      i32x4 acc[2][4];
+#pragma unroll
+      for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+          acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + b0 + 16 * bt + 4 * h);
+      for (int e0 = 0; e0 < KP; e0 += 64) {
+        int cl[16], co[16];
+        const int4* E4 = reinterpret_cast<const int4*>(E + e0 + 16 * h);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int4 x = E4[q];
+          cl[2 * q] = x.x;
+          co[2 * q] = x.y;
+          cl[2 * q + 1] = x.z;
+          co[2 * q + 1] = x.w;
+        }
+        unsigned u[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) u[j] = UQ[(long long)co[j] * kQTiles + t];
+        i32x4 af[2];
+#pragma unroll
+        for (int bt = 0; bt < 2; ++bt) {
+          const unsigned char* wr = W8 + 16 * bt + r;
+          unsigned wd[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            wd[q] = (unsigned)wr[cl[4 * q] * Bq] | ((unsigned)wr[cl[4 * q + 1] * Bq] << 8) |
+                    ((unsigned)wr[cl[4 * q + 2] * Bq] << 16) | ((unsigned)wr[cl[4 * q + 3] * Bq] << 24);
+          af[bt] = i32x4{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+        }
+        unsigned pl[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+          const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
+          acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
+          acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
+        }
+      }
+      if (t < NT)
+#pragma unroll
+        for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int b = 16 * bt + 4 * h + q;
+            if (b < NB) {
+              const long long v =
+                  (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
+              const double x = (double)v * 0x1p-8;
+              float f = (float)x;
+              if ((double)f < x) f = nextafterf(f, INFINITY);
+              ub[t * NB + b] = f;
+            }
+          }
+    }
+  }
+#if SCDE_TILE_DIAG & 1
+  return;  // timing build: bounds only
+#endif
+  wave_sync();
+  // ---- 2. first group: the 4 tiles with the largest bound
+  float sc = -INFINITY;
+  if (lane < NT)
+    for (int b = 0; b < nlive; ++b) sc = fmaxf(sc, ub[lane * NB + b]);
+  int tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned done = 0;
+  const int n1 = min(4, NT);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (j < n1) {
+      float m = sc;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      const unsigned long long bl = __ballot(lane < NT && !((done >> lane) & 1) && sc == m);
+      const int t = __ffsll((long long)bl) - 1;
+      tl[j] = t;
+      done |= 1u << t;
+      if (lane == t) sc = -INFINITY;
+    }
+  }
+  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
+  const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
+  constexpr int EB = SCDE_BOOT_EB;
+  static_assert(EB == 4, "the asm look-ahead assumes 4-entry batches");
+  // rows of one register group, in k_boot2's exact arithmetic (see k_boot2 for the asm)
+  auto rows = [&](double (&acc)[NB], int koff, bool live) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) acc[i] = live ? Zs[(long long)(b0 + i) * GS + koff] : -INFINITY;
+    int cell[EB], cellb[EB];
+    double v[EB], vb[EB];
+    auto issue = [&](int e0, int (&c)[EB], double (&x)[EB]) {
+      const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
+#pragma unroll
+      for (int j = 0; j < EB / 2; ++j) {
+        const int4 t = E4[j];
+        c[2 * j] = t.x;
+        c[2 * j + 1] = t.z;
+        const double* p0 = D + (unsigned)(t.y * GS) + koff;
+        const double* p1 = D + (unsigned)(t.w * GS) + koff;
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j]) : "v"(p0));
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j + 1]) : "v"(p1));
+      }
+    };
+    auto ready = [&](double (&x)[EB]) {
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
+    };
+    auto accumulate = [&](const int (&c)[EB], const double (&x)[EB]) {
+#pragma unroll
+      for (int i0 = 0; i0 < NB; i0 += 2) {
+        double2 w[EB];
+#pragma unroll
+        for (int j = 0; j < EB; ++j)
+          w[j] = *reinterpret_cast<const double2*>(W + (unsigned)(__builtin_amdgcn_readfirstlane(c[j]) * Bp) + b0 + i0);
+#pragma unroll
+        for (int j = 0; j < EB; ++j) {
+          acc[i0] = fma(w[j].x, x[j], acc[i0]);
+          acc[i0 + 1] = fma(w[j].y, x[j], acc[i0 + 1]);
+        }
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));
+    issue(0, cell, v);
+    const int n4 = (n + EB - 1) & ~(EB - 1);
+    int e0 = 0;
+    for (; e0 + 2 * EB <= n4; e0 += 2 * EB) {
+      issue(e0 + EB, cellb, vb);
+      ready(v);
+      accumulate(cell, v);
+      issue(e0 + 2 * EB, cell, v);
+      ready(vb);
+      accumulate(cellb, vb);
+    }
+    if (e0 < n4) {
+      issue(e0 + EB, cellb, vb);
+      ready(v);
+      accumulate(cell, v);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+  };
+  double acc1[NB], acc2[NB];
+  const int k1 = 16 * tl[h] + r;
+  const bool live1 = h < n1 && k1 < G;
+  rows(acc1, k1, live1);
+  wave_max_partials_all<NB>(acc1, &fmx[0][0][0], lane, 2 * wsid);
+  wave_sync();
+  // ---- 3. tiles still needed against the exact maxima
+  bool need = false;
+  if (lane < NT && !((done >> lane) & 1))
+    for (int b = 0; b < nlive; ++b) need |= (double)ub[lane * NB + b] >= (double)fmx[wsid][0][b] - 51.0;
+  unsigned long long nm = __ballot(need);
+  const int cnt = __popcll(nm);
+  int ng = 1, n2 = 0;
+  if (cnt > 0) {
+    if (cnt > 4 || maxgroups < 2) {  // the whole slab goes to k_boot2's redo launch
+      if (lane == 0) {
+        redo[(long long)g * P + p] = 1;
+        if (stats) {
+          atomicAdd(&stats[3], 1);
+          atomicAdd(&stats[5], (n + 3) & ~3);
+        }
+      }
+      return;
+    }
+    n2 = cnt;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (j < n2) {
+        const int t = __ffsll((long long)nm) - 1;
+        nm &= nm - 1;
+        tl[4 + j] = t;
+        done |= 1u << t;
+      }
+    }
+    ng = 2;
+  }
+  const int k2 = 16 * tl[4 + h] + r;
+  const bool live2 = h < n2 && k2 < G;
+  if (ng == 2) {
+    rows(acc2, k2, live2);
+    wave_max_partials_all<NB>(acc2, &fmx[0][0][0], lane, 2 * wsid + 1);
+    wave_sync();
+    if (lane < NB) fmx[wsid][0][lane] = fmaxf(fmx[wsid][0][lane], fmx[wsid][1][lane]);
+    wave_sync();
+  }
+  if (lane < nlive && !(fabs((double)fmx[wsid][0][lane]) <= degen_thresh)) degen[g] = 1;
+  // ---- 4. softmax terms, tile partial sums, jp partial row
+  auto terms = [&](double (&acc)[NB], bool live, int slot0, int nt) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const double d = acc[i] - (double)fmx[wsid][0][i];
+      const bool nd = live && d >= kBootExpCut;
+      if (__builtin_amdgcn_ballot_w64(nd))
+        acc[i] = nd ? exp_tab(d, etab) : 0.0;
+      else
+        acc[i] = 0.0;
+      const double ps = row16_sum(acc[i]);
+      if (r == 0 && h < nt) tsum[wsid][slot0 + h][i] = ps;
+    }
+  };
+  terms(acc1, live1, 0, n1);
+  if (ng == 2) terms(acc2, live2, 4, n2);
+  wave_sync();
+  if (lane < NB) {
+    double S = 0.0;
+    for (unsigned m = done; m; m &= m - 1) {
+      const int t = __builtin_ffs((int)m) - 1;
+      int slot = 0;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        if (tl[s] == t && (s < n1 || (s >= 4 && s - 4 < n2))) slot = s;
+      S += tsum[wsid][slot][lane];
+    }
+    finv[wsid][lane] = (b0 + lane < nboot) ? 1.0 / (S * norm_mult) : 0.0;
+  }
+  wave_sync();
+  double* prow = part + (long long)p * part_stride + (long long)g * GS;
+  {
+    double jpv = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) jpv = fma(acc1[i], finv[wsid][i], jpv);
+    if (live1) prow[k1] = jpv;
+  }
+  if (ng == 2) {
+    double jpv = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) jpv = fma(acc2[i], finv[wsid][i], jpv);
+    if (live2) prow[k2] = jpv;
+  }
+  for (int t0 = 0; t0 < NT; t0 += 4) {
+    const int t = t0 + h, k = 16 * t + r;
+    if (t < NT && !((done >> t) & 1) && k < G) prow[k] = 0.0;
+  }
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], 1);
+    atomicAdd(&stats[1], __builtin_popcount(done));
+    atomicAdd(&stats[2], NT);
+    atomicAdd(&stats[4], ng * ((n + 3) & ~3));
+  }
 }
 
 // jp[g, k] = sum over slabs p (in order) of part[p][g][k]
@@ -2113,7 +2491,7 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
                       const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s) {
   if (ngenes <= 0) return hipSuccess;
-  if (padto == 64 ? stride < ((ncells + 63) & ~63) || stride < 64 : stride < ((ncells + 7) & ~7) + 8)
+  if (padto == 64 ? stride < ((ncells + 63) & ~63) + 8 || stride < 72 : stride < ((ncells + 7) & ~7) + 8)
     return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 4)), dim3(256), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
                      base_col, stride, pad_col, padto, ent, nnz);
@@ -2236,6 +2614,55 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (e != hipSuccess) return e;
   const long long n = (long long)a.ngenes * a.G;
   hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
+                     a.G, a.GS, a.out, a.out_g, a.out_k);
+  return hipGetLastError();
+}
+
+hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s) {
+  if (a.ngenes <= 0) return hipSuccess;
+  const int P = (a.nboot + a.nb - 1) / a.nb;
+  if (a.G > 16 * kTileMax || !a.redo || !tb.W8 || !tb.UQ || !tb.ZUq || !tb.nanflag ||
+      tb.Bq < (P - 1) * a.nb + 32 || tb.Bq % 32)
+    return hipErrorInvalidValue;
+  if ((long long)a.ncols_p1 * a.GS >= (1LL << 31) || (long long)a.ncells * a.Bp >= (1LL << 31))
+    return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.redo, 0, sizeof(int) * ((size_t)a.ngenes * P + 1), s);
+  if (e != hipSuccess) return e;
+  const long long items = (long long)a.ngenes * P;
+  const dim3 grid((unsigned)div_up(items, 4)), block(256);
+#define SCDE_BT(NBV)                                                                                             \
+  case NBV:                                                                                                       \
+    hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,       \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,       \
+                       a.part_stride, a.degen, a.ngenes, tb.W8, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
+                       a.redo, tb.stats);                                                                       \
+    break;
+  switch (a.nb) {
+    SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)
+    default: return hipErrorInvalidValue;
+  }
+#undef SCDE_BT
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // slabs the tile kernel left (more tiles than its registers hold, or NaN tables): k_boot2,
+  // whole slab, same sums
+  const int block2 = ((a.G + 63) / 64) * 64;
+  const int grid2 = (a.ngenes + 7) / 8 * 8 * P;
+#define SCDE_B2R(NBV)                                                                                             \
+  case NBV:                                                                                                        \
+    hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid2), dim3(block2), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
+                       a.part_stride, a.degen, a.ngenes, nullptr, nullptr, a.redo, 1);                          \
+    break;
+  switch (a.nb) {
+    SCDE_B2R(4) SCDE_B2R(8) SCDE_B2R(12) SCDE_B2R(16) SCDE_B2R(20)
+    default: return hipErrorInvalidValue;
+  }
+#undef SCDE_B2R
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const long long nn = (long long)a.ngenes * a.G;
+  hipLaunchKernelGGL(k_sum_partials, dim3(div_up(nn, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
                      a.G, a.GS, a.out, a.out_g, a.out_k);
   return hipGetLastError();
 }

@@ -4,12 +4,16 @@ The skipping is an optimisation that must not change results: a 64-point stretch
 left out of a boot slab when a rigorous upper bound of its row values stays more than 51
 below the exact row maximum (post-check), i.e. when every softmax term there falls under
 the e^-50 cut that zeroes it anyway; any slab that fails the check is recomputed whole.
-These tests run the same calls, for both bootstrap kernels (the fixed-point k_bootq with
-16-point tiles, and the FP64 k_boot2 with 64-point stretches; context option boot_q = 2 / 0),
-with skipping on (default), off (boot_skip = 0), and with a negative heuristic slack
-(skip_slack) that makes the mask drop tiles the post-check must reject, so the extra work
-really happens (its count is read back and must be > 0) -- and compare every run with the
-oracle at the SURVEY §8(d) bar, and the runs of one kernel with each other bit for bit.
+These tests run the same calls, for the bootstrap kernels (the fixed-point k_bootq with
+16-point tiles, boot_q = 2; the FP64 k_boot_tiles on bounded 16-point tiles, boot_q = 0; the
+FP64 k_boot2 with its 64-point stretch mask, boot_tiles = 0), with skipping on (default), off
+(boot_skip = 0), and forced onto the second-chance path so that the extra work really
+happens (its count is read back and must be > 0): a negative heuristic slack (skip_slack)
+that makes the masks drop tiles the post-check must reject, or k_boot_tiles limited to one
+register group (tile_groups = 1) so slabs needing more tiles go to k_boot2's redo launch --
+and compare every run with the oracle at the SURVEY §8(d) bar, and the runs of one
+arithmetic with each other bit for bit (the FP64 kernels share rows, maxima and
+tile-ordered sums).
 """
 import math
 
@@ -33,6 +37,9 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("boot_q", opts.get("boot_q", 2))
     ctx.set_option("boot_skip", opts.get("boot_skip", 1))
     ctx.set_option("skip_slack", opts.get("skip_slack", math.nan))
+    ctx.set_option("boot_tiles", opts.get("boot_tiles", 1))
+    ctx.set_option("tile_groups", opts.get("tile_groups", 2))
+    ctx.set_option("boot_tiles_cells", opts.get("boot_tiles_cells", 0))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -41,9 +48,12 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
                                              n_cores=ncores, return_posteriors=True)
         stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo")}
     finally:
-        ctx.set_option("boot_q", 1)
+        ctx.set_option("boot_q", 0)
         ctx.set_option("boot_skip", 1)
         ctx.set_option("skip_slack", math.nan)
+        ctx.set_option("boot_tiles", 1)
+        ctx.set_option("tile_groups", 2)
+        ctx.set_option("boot_tiles_cells", 200)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -62,7 +72,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "forced-redo": {"skip_slack": -45.0},
         "fp64": {"boot_q": 0},
         "fp64-noskip": {"boot_q": 0, "boot_skip": 0},
-        "fp64-forced-redo": {"boot_q": 0, "skip_slack": -45.0},
+        "fp64-forced-redo": {"boot_q": 0, "tile_groups": 1},
+        "fp64-stretch": {"boot_q": 0, "boot_tiles": 0},
+        "fp64-stretch-forced-redo": {"boot_q": 0, "boot_tiles": 0, "skip_slack": -45.0},
     }
     got = {}
     for name, opts in runs.items():
@@ -71,6 +83,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
             assert stats["skip_slabs"] == 0
         elif name == "noskip":
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] == stats["skip_stretches"], stats
+        elif name == "fp64-forced-redo":  # one register group: slabs needing > 4 tiles all go to k_boot2
+            assert stats["skip_redo"] > 0, stats
         else:
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
         if name.endswith("forced-redo"):
@@ -85,7 +99,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"], what=f"{name} Z")
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
-    for base, others in (("skip", ("noskip", "forced-redo")), ("fp64", ("fp64-noskip", "fp64-forced-redo"))):
+    for base, others in (("skip", ("noskip", "forced-redo")),
+                         ("fp64", ("fp64-noskip", "fp64-forced-redo", "fp64-stretch", "fp64-stretch-forced-redo"))):
         for name in others:
             for i in range(2):
                 np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got[base]["joint.posteriors"][i])

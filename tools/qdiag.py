@@ -49,12 +49,12 @@ def main():
             api.check(L.scde_posteriors_dev(ctx.handle, dc.ptr, NG, NG, P(cellidx), NC, P(mm), lt, sq, P(px), 401,
                                             100, 1, 0, NG, 1, 0, None, None, None, 0, P(jp), P(modes), None))
 
-    variants = [("q", {"boot_q": 2}), ("q-noskip", {"boot_q": 2, "boot_skip": 0}), ("fp64", {"boot_q": 0})]
+    variants = [("tiles", {}), ("stretch", {"boot_tiles": 0}), ("q", {"boot_q": 2}), ("noskip", {"boot_skip": 0})]
     if extra:
         variants = [("custom", {k: float(v) for k, v in extra.items()})]
     for name, opts in variants:
-        for k in ("boot_q", "boot_skip"):
-            ctx.set_option(k, 1)
+        for k, v in (("boot_q", 0), ("boot_skip", 1), ("boot_tiles", 1)):
+            ctx.set_option(k, v)
         for k, v in opts.items():
             ctx.set_option(k, v)
         run()
