@@ -115,8 +115,10 @@ def dominant_kernel_bytes(ngenes, cells_per_group):
     return ngenes * (cells_per_group * (4 + 8 * G) + 8 * G)
 
 
-BOOT_STAGE = "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum_partials)"
-BOOTQ_STAGE = "fixed-point bootstrap (k_bootq)"
+BOOT_STAGES = {0: "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum_partials)",
+               1: "bootstrap stage (k_boot_tiles + k_boot2 fallback launch + k_sum_partials)",
+               2: "fixed-point bootstrap (k_bootq)",
+               3: "bootstrap stage (general k_boot)"}
 
 
 def profiled_traffic(config: str):
@@ -590,6 +592,7 @@ def main():
     run(dc.ptr)
     ctx.synchronize()
     step_fma, step_mac = ctx.stat("boot_f64_fma"), ctx.stat("boot_i8_mac")
+    stage_name = BOOT_STAGES.get(int(ctx.stat("boot_path")), "bootstrap stage")
     ctx.set_option("skip_stats", 0)
 
     total_genes = NTOT * args.steps
@@ -610,17 +613,17 @@ def main():
     i8_tops = 2 * step_mac / boot_step_s / 1e12 if boot_n and step_mac else 0.0
     if step_mac > step_fma:
         # fixed-point bootstrap (k_bootq): int8 MFMA ops issued over the stage time
-        roof = {"bound": "mfma", "kernel": BOOTQ_STAGE, "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS,
+        roof = {"bound": "mfma", "kernel": stage_name, "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS,
                 "unit": "TOPS (int8)", "frac": i8_tops / I8_MFMA_PEAK_TOPS,
                 "achieved_basis": "int8 MACs issued by k_bootq's v_mfma_i32_16x16x64_i8 (x2 ops) per step / "
                                   "stage time per step (HIP events)"}
     else:
         # FP64 bootstrap (k_boot2): the FMAs its kept stretches issue, against the FP64 VALU peak
-        roof = {"bound": "fp64-valu", "kernel": BOOT_STAGE, "achieved": f64_tf, "peak": FP64_VALU_PEAK_TF,
+        roof = {"bound": "fp64-valu", "kernel": stage_name, "achieved": f64_tf, "peak": FP64_VALU_PEAK_TF,
                 "unit": "TFLOP/s", "frac": f64_tf / FP64_VALU_PEAK_TF,
                 "frac_of_measured_fma_rate": f64_tf / FP64_FMA_MEASURED_TF,
-                "achieved_basis": "k_boot2 lane FMAs issued (kept stretches x 64 x slab boots x entries, x2 flops) "
-                                  "per step / stage time per step (HIP events)"}
+                "achieved_basis": "lane FMAs the FP64 bootstrap kernels issue (computed grid points x slab boots x "
+                                  "entries, x2 flops) per step / stage time per step (HIP events)"}
     roof.update({
         "traffic": prof["traffic_bytes"] if prof else None,
         "traffic_source": (f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"

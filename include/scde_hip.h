@@ -134,7 +134,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  * Statistics: "skip_slabs", "skip_stretches", "skip_kept", "skip_redo", "degen", "tiles_<i>"
  * (k_bootq slabs computing i tiles) (with skip_stats);
  * "boot_f64_fma" (k_boot2: FP64 lane FMAs issued) and "boot_i8_mac" (k_bootq: int8 MACs issued
- * by its MFMAs), also with skip_stats. */
+ * by its MFMAs), also with skip_stats; "boot_path": the bootstrap kernel of the last posterior
+ * (0 k_boot2, 1 k_boot_tiles, 2 k_bootq, 3 the general k_boot). */
 int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);
 int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
 int scde_ctx_reset_stats(scde_ctx* ctx);

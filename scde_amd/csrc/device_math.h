@@ -344,8 +344,7 @@ struct LogTab {
   const double* lo;
 };
 
-__device__ __forceinline__ double log_tab(double x, const LogTab& t) {
-  if (!(x >= DBL_MIN && x < INFINITY)) return log_cold(x);
+__device__ __forceinline__ double log_tab_hot(double x, const LogTab& t) {  // x in [DBL_MIN, inf)
   int e;
   double m = frexp(x, &e);  // [0.5, 1)
   if (m < 0.75) {
@@ -364,6 +363,15 @@ __device__ __forceinline__ double log_tab(double x, const LogTab& t) {
   const double ed = (double)e;
   // e*ln2_hi is exact (ln2_hi has 11 trailing zero bits)
   return (fma(ed, 0.6931471805598903, t.hi[j]) + (fma(ed, 5.497923018708371e-14, t.lo[j]) + p));
+}
+
+// The hot path is branch-free; arguments outside [DBL_MIN, inf) (zero, subnormal, inf, NaN)
+// take the library log under a wave-uniform branch, only in waves that have such a lane.
+__device__ __forceinline__ double log_tab(double x, const LogTab& t) {
+  const bool cold = !(x >= DBL_MIN && x < INFINITY);
+  const double r0 = log_tab_hot(cold ? 1.0 : x, t);
+  if (__builtin_amdgcn_ballot_w64(cold)) return cold ? log_cold(x) : r0;
+  return r0;
 }
 
 // bd0's Taylor series (|x - np| < 0.1 (x + np)), out of line
@@ -512,18 +520,24 @@ __device__ __forceinline__ NbFast nb_fast(const NbConst& c) {
   return f;
 }
 
-// returns false when the lane must take the exact path
-__device__ __forceinline__ bool dnbinom_fast(const NbFast& f, double p, double q, double lp, double lq, double& out) {
-  if (!(p > 0.0 && p <= 1.0 && q > 0.0)) return false;
+// Evaluated for every lane without divergent branches; `bad` marks the lanes that must take
+// the exact path instead (their value here is meaningless).  The count-0 test is per column
+// (wave-uniform); the q < 0.1 branch runs only in waves that have such a lane.
+__device__ __forceinline__ double dnbinom_fast(const NbFast& f, double p, double q, double lp, double lq, bool& bad) {
   const double np = f.n * p, nq = f.n * q;
-  if (!(np > 0.0 && np < INFINITY && nq > 0.0 && nq < INFINITY)) return false;
+  bad = !(p > 0.0 && p <= 1.0 && q > 0.0 && np > 0.0 && np < INFINITY && nq > 0.0 && nq < INFINITY);
   double ans;
-  if (f.X == f.n)  // count 0: dbinom_raw's x == n branch
-    ans = (q < 0.1) ? -bd0_fast(f.n, np, -lp) - f.n * q : f.n * lp;
-  else
+  if (f.X == f.n) {  // count 0: dbinom_raw's x == n branch
+    const bool lowq = q < 0.1;
+    ans = f.n * lp;
+    if (__builtin_amdgcn_ballot_w64(lowq && !bad)) {
+      const double b = -bd0_fast(f.n, np, -lp) - f.n * q;
+      ans = lowq ? b : ans;
+    }
+  } else {
     ans = ((f.S - bd0_fast(f.X, np, f.lXn - lp)) - bd0_fast(f.nx, nq, f.lnxn - lq)) - f.hlf;
-  out = f.lp + ans;
-  return true;
+  }
+  return f.lp + ans;
 }
 
 // ---- double-double accumulation (emulates R's LDOUBLE rowSums / cumsum) ----

@@ -196,6 +196,7 @@ struct scde_ctx {
   // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
   // stretches x 64 lanes x slab boots x entries) and int8 MACs of k_bootq (MFMAs x 16 x 16 x 64)
   double st_boot_f64_fma = 0, st_boot_i8_mac = 0;
+  double st_boot_path = -1;  // the bootstrap kernel of the last posterior: 0 k_boot2, 1 k_boot_tiles, 2 k_bootq, 3 general
   static constexpr int kQMaxTilesHost = 28;
   double st_tile_hist[kQMaxTilesHost + 1] = {0};
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
@@ -754,6 +755,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     // logBootBatchPosterior with Nboot = 0 returns zeros (src/jpmatLogBoot.cpp:469-497)
     HCHK(hipMemsetAsync(s.jp, 0, sizeof(double) * (size_t)N * G, st));
   } else if (qpath) {
+    cx->st_boot_path = 2;
     RCHK(run_bootq(cx, s, u, ta, ncols, GS, draws, W, ndraw, Bq, qstride, keep_T));
   } else {
     if (!fused) make_draws(s, Bp, draws, W, ndraw);
@@ -845,6 +847,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         b2.ubuf = cx->subuf.as<double>();
         b2.redo = cx->sredo.as<int>();
       }
+      cx->st_boot_path = tpath ? 1 : 0;
       if (tpath) {
         HCHK(cx->sredo.ensure(sizeof(int) * ((size_t)P * N + 1)));
         b2.redo = cx->sredo.as<int>();
@@ -913,6 +916,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       ba.out_k = s.jp_k;
       ba.degen = cx->degen.as<int>();
       ba.ngenes = N;
+      cx->st_boot_path = 3;
       HCHK(launch_boot(ba, st));
     }
     cx->mark_end(SLOT_BOOT, ev);
@@ -1148,6 +1152,7 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "skip_kept") *value = ctx->st_skip_kept;
   else if (n == "boot_f64_fma") *value = ctx->st_boot_f64_fma;
   else if (n == "boot_i8_mac") *value = ctx->st_boot_i8_mac;
+  else if (n == "boot_path") *value = ctx->st_boot_path;
   else if (n == "skip_redo") *value = ctx->st_skip_redo;
   else if (n == "degen") *value = ctx->st_degen;
   else if (n.rfind("tiles_", 0) == 0 && atoi(n.c_str() + 6) >= 0 && atoi(n.c_str() + 6) <= 28)

@@ -185,18 +185,26 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
       const double mnext = last ? 0.0 : mu[k + 1];
       const bool over = (!last && x > muv && x < mnext) || (last && x > muv);
       double pr = P[k], qr = P[PS + k], lpr = P[2 * PS + k], lqr = P[3 * PS + k];
-      if (over) {
+      // wave-uniform branches around the rare lanes: the count's own grid point, and the
+      // exact dnbinom (out of line, the reference as written) where the fast form does not apply
+      if (__builtin_amdgcn_ballot_w64(over)) {
         const double t = th[k];
-        pr = t / (t + x);
-        qr = 1 - pr;
-        lpr = log_tab(pr, lt);
-        lqr = log_tab(qr, lt);
+        const double po = t / (t + x);
+        pr = over ? po : pr;
+        qr = over ? 1 - po : qr;
+        lpr = over ? log_tab(po, lt) : lpr;
+        lqr = over ? log_tab(1 - po, lt) : lqr;
       }
       double nb;
-      if (SCDE_KT_DIAG & 1)  // timing diagnostic: trivial dnbinom
+      if (SCDE_KT_DIAG & 1) {  // timing diagnostic: trivial dnbinom
         nb = lpr * x + lqr;
-      else if (!dnbinom_fast(nf, pr, qr, lpr, lqr, nb))
-        nb = dnbinom_log_cold(x, th[k], pr);  // out of line: the reference dnbinom as written
+      } else {
+        bool bad;
+        nb = dnbinom_fast(nf, pr, qr, lpr, lqr, bad);
+        if (__builtin_amdgcn_ballot_w64(bad)) {
+          if (bad) nb = dnbinom_log_cold(x, th[k], pr);
+        }
+      }
       nb += lcfpr[k];
       v[k] = nb;
       lmax = gt_max(lmax, nb);
