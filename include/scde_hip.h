@@ -126,6 +126,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   64-point stretch mask)
  *   "tile_groups"   register groups of 4 tiles per k_boot_tiles wave, 1 or 2 (default 2; slabs
  *                   needing more go to k_boot2 whole -- tests force that with 1)
+ *   "tile_order"    1/0  k_boot_tiles takes the genes in order of their count sums, so waves in
+ *                   flight share columns and tiles in L2 (default 1; results are the same)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)

@@ -180,4 +180,16 @@ hipError_t launch_bh_cz(const double* z, int n, double* cz, void* work, size_t* 
   return hipGetLastError();
 }
 
+// Gene order for the tile bootstrap: radix sort of (count sum, gene) pairs, ascending and
+// stable.  `work == nullptr` queries the temporary storage size.
+hipError_t launch_gene_order(const unsigned* key, const int* idx, int n, unsigned* key_out, int* order, void* work,
+                             size_t* work_bytes, hipStream_t s) {
+  if (!work) {
+    return hipcub::DeviceRadixSort::SortPairs(nullptr, *work_bytes, key, key_out, idx, order, n > 0 ? n : 1, 0, 32,
+                                              s);
+  }
+  if (n <= 0) return hipSuccess;
+  return hipcub::DeviceRadixSort::SortPairs(work, *work_bytes, key, key_out, idx, order, n, 0, 32, s);
+}
+
 }  // namespace scde

@@ -177,6 +177,8 @@ struct scde_ctx {
   Buf counts_in;
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, qflags;
+  // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
+  Buf gkey, gkey2, gidx, gorder, gwork;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_q = 0;            // "boot_q": the fixed-point int8-MFMA bootstrap: 0 never, 1 from boot_q_cells, 2 always
   int opt_boot_q_cells = 1000;   // "boot_q_cells": cells per call from which boot_q = 1 picks it
@@ -191,6 +193,7 @@ struct scde_ctx {
   int opt_boot_tiles_cells = 200;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
                                    // rows are wide, most slabs need > 8 tiles, k_boot2's stretches win)
   int opt_tile_groups = 2;       // "tile_groups": register groups of 4 tiles per k_boot_tiles wave (1 or 2)
+  int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
@@ -271,7 +274,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &qflags};
+                 &w8t,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
@@ -859,6 +862,20 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         tb.nanflag = cx->qflags.as<int>();
         tb.maxgroups = cx->opt_tile_groups;
         tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
+        if (cx->opt_tile_order && N > 1) {
+          HCHK(cx->gkey.ensure(sizeof(unsigned) * N));
+          HCHK(cx->gkey2.ensure(sizeof(unsigned) * N));
+          HCHK(cx->gidx.ensure(sizeof(int) * N));
+          HCHK(cx->gorder.ensure(sizeof(int) * N));
+          size_t wb = 0;
+          HCHK(launch_gene_order(nullptr, nullptr, N, nullptr, nullptr, nullptr, &wb, st));
+          HCHK(cx->gwork.ensure(std::max<size_t>(wb, 1)));
+          HCHK(launch_gene_key(cx->ent.as<int2>(), cx->nnz.as<int>(), stride, u.ucl.as<int>(), N,
+                               cx->gkey.as<unsigned>(), cx->gidx.as<int>(), st));
+          HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), N, cx->gkey2.as<unsigned>(),
+                                 cx->gorder.as<int>(), cx->gwork.p, &wb, st));
+          tb.order = cx->gorder.as<int>();
+        }
         HCHK(launch_boot_tiles(b2, tb, st));
         if (cx->opt_skip_stats) {
           int h[8];
@@ -1140,6 +1157,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "boot_tiles") ctx->opt_boot_tiles = value != 0;
   else if (n == "boot_tiles_cells") ctx->opt_boot_tiles_cells = (int)value;
   else if (n == "tile_groups") ctx->opt_tile_groups = (int)value;
+  else if (n == "tile_order") ctx->opt_tile_order = value != 0;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
 }

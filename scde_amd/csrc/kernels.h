@@ -183,8 +183,14 @@ struct TileBootArgs {
   int maxgroups;             // register groups of 4 tiles (1 or 2)
   int* stats;                // nullable: [0] slabs, [1] tiles computed, [2] tiles, [3] slabs left to k_boot2,
                              // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left
+  const int* order;          // nullable: genes in this order (launch_gene_order)
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
+// gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending
+hipError_t launch_gene_key(const int2* ent, const int* nnz, int ent_stride, const int* ucl, int ngenes, unsigned* key,
+                           int* idx, hipStream_t s);
+hipError_t launch_gene_order(const unsigned* key, const int* idx, int n, unsigned* key_out, int* order, void* work,
+                             size_t* work_bytes, hipStream_t s);
 
 struct ExactArgs {
   const double* T;  // log tables; or fused D columns when base_col is set (T = D + D[base])

@@ -1438,7 +1438,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8c, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
-    int* __restrict__ redo, int* __restrict__ stats) {
+    int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order) {
   static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
   __shared__ float ubs[4][kTileMax * NB];  // [wave][tile][boot] bounds
   __shared__ float fmx[4][2][32];          // [wave][group][boot] maxima
@@ -1451,7 +1451,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   __syncthreads();
   const int item = blockIdx.x * 4 + wsid;
   if (item >= ngenes * P) return;
-  const int g = item / P, p = item - g * P, b0 = p * NB;
+  // genes in `order` (by expression): waves in flight then share columns and tiles in L2
+  const int gi = item / P, p = item - gi * P, b0 = p * NB;
+  const int g = order ? order[gi] : gi;
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
     if (lane == 0) redo[(long long)g * P + p] = 1;
     return;
@@ -2626,6 +2628,33 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Per gene the sum of its counts over the call's cells (from the ELL entries: each entry's
+// column is a unique count), the key of the tile bootstrap's gene order.
+__global__ __launch_bounds__(256) void k_gene_key(const int2* __restrict__ ent, const int* __restrict__ nnz,
+                                                 int ent_stride, const int* __restrict__ ucl, int ngenes,
+                                                 unsigned* __restrict__ key, int* __restrict__ idx) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g >= ngenes) return;
+  const int2* E = ent + (long long)g * ent_stride;
+  const int n = nnz[g];
+  unsigned long long sum = 0;
+  for (int e = lane; e < n; e += 64) sum += (unsigned)max(ucl[E[e].y], 0);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if (lane == 0) {
+    key[g] = sum > 0xffffffffull ? 0xffffffffu : (unsigned)sum;
+    idx[g] = g;
+  }
+}
+
+hipError_t launch_gene_key(const int2* ent, const int* nnz, int ent_stride, const int* ucl, int ngenes, unsigned* key,
+                           int* idx, hipStream_t s) {
+  if (ngenes <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gene_key, dim3(div_up(ngenes, 4)), dim3(256), 0, s, ent, nnz, ent_stride, ucl, ngenes, key, idx);
+  return hipGetLastError();
+}
+
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const int P = (a.nboot + a.nb - 1) / a.nb;
@@ -2643,7 +2672,7 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
     hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,       \
                        a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,       \
                        a.part_stride, a.degen, a.ngenes, tb.W8, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
-                       a.redo, tb.stats);                                                                       \
+                       a.redo, tb.stats, tb.order);                                                             \
     break;
   switch (a.nb) {
     SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)

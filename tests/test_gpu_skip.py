@@ -40,6 +40,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("boot_tiles", opts.get("boot_tiles", 1))
     ctx.set_option("tile_groups", opts.get("tile_groups", 2))
     ctx.set_option("boot_tiles_cells", opts.get("boot_tiles_cells", 0))
+    ctx.set_option("tile_order", opts.get("tile_order", 1))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -54,6 +55,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("boot_tiles", 1)
         ctx.set_option("tile_groups", 2)
         ctx.set_option("boot_tiles_cells", 200)
+        ctx.set_option("tile_order", 1)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -73,6 +75,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "fp64": {"boot_q": 0},
         "fp64-noskip": {"boot_q": 0, "boot_skip": 0},
         "fp64-forced-redo": {"boot_q": 0, "tile_groups": 1},
+        "fp64-unordered": {"boot_q": 0, "tile_order": 0},
         "fp64-stretch": {"boot_q": 0, "boot_tiles": 0},
         "fp64-stretch-forced-redo": {"boot_q": 0, "boot_tiles": 0, "skip_slack": -45.0},
     }
@@ -100,7 +103,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("skip", ("noskip", "forced-redo")),
-                         ("fp64", ("fp64-noskip", "fp64-forced-redo", "fp64-stretch", "fp64-stretch-forced-redo"))):
+                         ("fp64", ("fp64-noskip", "fp64-forced-redo", "fp64-unordered", "fp64-stretch",
+                                  "fp64-stretch-forced-redo"))):
         for name in others:
             for i in range(2):
                 np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got[base]["joint.posteriors"][i])
