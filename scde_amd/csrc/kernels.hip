@@ -1426,13 +1426,21 @@ constexpr int kTileMax = 28;  // G <= 448
 #ifndef SCDE_TILE_DIAG
 #define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only
 #endif
+#ifndef SCDE_TILE_WPE
+// k_boot_tiles occupancy target (waves per SIMD): 128 VGPRs.  The row loop must not spill:
+// its look-ahead registers are written by asm loads the compiler believes complete at once,
+// so a spill or copy before the asm wait reads or reuses them early.  Builds at 5 and 6
+// waves per SIMD spilled there and faulted on the GPU; tests/test_kernel_resources.py
+// checks the loops of the shipped build for scratch traffic.
+#define SCDE_TILE_WPE 4
+#endif
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
 template <int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_boot_tiles(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_tiles(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
     const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
