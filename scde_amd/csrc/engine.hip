@@ -163,6 +163,10 @@ enum {
 struct scde_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // host-count entry points: the count upload runs on its own stream, in column chunks, so
+  // the first group's kernels start before the second group's columns have arrived
+  hipStream_t copy_stream = nullptr;
+  hipEvent_t up_ev[2] = {nullptr, nullptr};
   // workspace
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, pq, colc, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
       ubound, zubound, smask, subuf, sredo,
@@ -284,6 +288,9 @@ struct scde_ctx {
     }
     for (auto e : evpool) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    for (auto& e : up_ev)
+      if (e) (void)hipEventDestroy(e);
   }
 };
 
@@ -1570,9 +1577,45 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
   return ctx->sync();
 }
 
+// Host counts for de_run: copied in two column ranges on the context's copy stream.  A
+// pageable copy returns only once its data has left the host buffer, so the second range is
+// issued after the first group's kernels are queued: its transfer then overlaps them.
+struct HostUpload {
+  const int* counts;
+  int64_t ld;
+  int ngenes, cut, C;
+};
+static int upload_range(scde_ctx* ctx, const HostUpload& h, int k) {
+  const size_t row = sizeof(int) * (size_t)h.ngenes;
+  const int lo = k == 0 ? 0 : h.cut, hi = k == 0 ? h.cut : h.C;
+  if (hi > lo) {
+    char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
+    const int* src = h.counts + (size_t)h.ld * lo;
+    if (h.ld == h.ngenes)
+      HCHK(hipMemcpyAsync(dst, src, row * (hi - lo), hipMemcpyHostToDevice, ctx->copy_stream));
+    else
+      HCHK(hipMemcpy2DAsync(dst, row, src, sizeof(int) * (size_t)h.ld, row, hi - lo, hipMemcpyHostToDevice,
+                            ctx->copy_stream));
+  }
+  HCHK(hipEventRecord(ctx->up_ev[k], ctx->copy_stream));
+  HCHK(hipStreamWaitEvent(ctx->stream, ctx->up_ev[k], 0));
+  return SCDE_OK;
+}
+
+// up (nullable): the host-count entry's upload.  With it the groups run one after the other,
+// each once its columns are in HBM; without, both unique tables are built first (their host
+// syncs back to back), then the two posteriors.
+static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const scde_de_params* p,
+                  double* results, double* jp1, double* jp2, double* ratio, const HostUpload* up);
+
 int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes,
                                    const scde_de_params* p, double* results, double* jp1, double* jp2,
                                    double* ratio) {
+  return de_run(ctx, counts_dev, ld, ngenes, p, results, jp1, jp2, ratio, nullptr);
+}
+
+static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const scde_de_params* p,
+                  double* results, double* jp1, double* jp2, double* ratio, const HostUpload* up) {
   if (!ctx || !counts_dev || !p || !p->models || !p->groups || !p->prior_x || !p->prior_y)
     return fail(SCDE_EARG, "null argument");
   if (ngenes < 0 || p->ncells <= 0 || p->ngrid <= 1) return fail(SCDE_EARG, "bad dimensions");
@@ -1620,15 +1663,31 @@ int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t
     s.jp_g = G;  // gene-major rows for the ratio kernel
     s.jp_k = 1;
   }
-  // both groups' unique tables first (two host syncs, GPU otherwise idle), then the
-  // heavy per-group kernels back to back on the stream
-  {
+  if (up) {
+    // group by group, each after its columns have arrived (the first range ends with the
+    // last cell of the group whose cells end first)
+    int max0 = 0, max1 = 0;
+    for (int c : idx[0]) max0 = std::max(max0, c);
+    for (int c : idx[1]) max1 = std::max(max1, c);
+    const int first = max0 <= max1 ? 0 : 1;
+    for (int k = 0; k < 2; ++k) {
+      const int gi = k == 0 ? first : 1 - first;
+      RCHK(upload_range(ctx, *up, k));
+      ctx->us[gi].ready = false;
+      const PostSpec* sp[1] = {&specs[gi]};
+      UniqueSet* up[1] = {&ctx->us[gi]};
+      RCHK(build_unique_sets(ctx, sp, up, 1));
+      RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
+    }
+  } else {
+    // both groups' unique tables first (two host syncs, GPU otherwise idle), then the
+    // heavy per-group kernels back to back on the stream
     ctx->us[0].ready = ctx->us[1].ready = false;
     const PostSpec* sp[2] = {&specs[0], &specs[1]};
     UniqueSet* up[2] = {&ctx->us[0], &ctx->us[1]};
     RCHK(build_unique_sets(ctx, sp, up, 2));
+    for (int gi = 0; gi < 2; ++gi) RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
   }
-  for (int gi = 0; gi < 2; ++gi) RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
   // ratio posterior + summary
   const std::vector<double> diffv = ratio_diffv(p->prior_x, G);
   const int zi = expectation_index(diffv, p->expectation);
@@ -1888,10 +1947,35 @@ static int stage_counts(scde_ctx*& ctx, const int* counts, int64_t ld, int ngene
 int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes,
                                     const scde_de_params* p, double* results, double* jp1, double* jp2,
                                     double* ratio) {
-  if (!p) return fail(SCDE_EARG, "null argument");
-  const int* dev = nullptr;
-  RCHK(stage_counts(ctx, counts, ld, ngenes, p->ncells, &dev));
-  return scde_expression_difference_dev(ctx, dev, ngenes, ngenes, p, results, jp1, jp2, ratio);
+  if (!p || !p->groups) return fail(SCDE_EARG, "null argument");
+  if (!ctx) RCHK(default_ctx(&ctx));
+  if (!counts) return fail(SCDE_EARG, "null argument");
+  const int C = p->ncells;
+  if (ngenes < 0 || C <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
+  HCHK(hipSetDevice(ctx->device));
+  if (ngenes == 0) {
+    const int* dev = nullptr;
+    RCHK(stage_counts(ctx, counts, ld, ngenes, C, &dev));
+    return de_run(ctx, dev, ngenes, ngenes, p, results, jp1, jp2, ratio, nullptr);
+  }
+  // two column ranges: up to the last cell of the group whose cells end first, and the rest
+  int max0 = -1, max1 = -1;
+  for (int c = 0; c < C; ++c) {
+    if (p->groups[c] == 0) max0 = c;
+    if (p->groups[c] == 1) max1 = c;
+  }
+  if (max0 < 0 || max1 < 0) return fail(SCDE_EARG, "both groups need at least one cell");
+  const int cut = std::min(max0, max1) + 1;
+  if (!ctx->copy_stream) HCHK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+  for (auto& e : ctx->up_ev)
+    if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  const size_t row = sizeof(int) * (size_t)ngenes;
+  HCHK(ctx->counts_in.ensure(std::max<size_t>(1, row * C)));
+  // the previous call's kernels may still read counts_in: the copies wait for them
+  HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
+  HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
+  const HostUpload h{counts, ld, ngenes, cut, C};
+  return de_run(ctx, ctx->counts_in.as<int>(), ngenes, ngenes, p, results, jp1, jp2, ratio, &h);
 }
 
 int scde_expression_difference_batch_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes,
