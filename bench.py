@@ -121,13 +121,15 @@ BOOT_STAGES = {0: "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum
                3: "bootstrap stage (general k_boot)"}
 
 
-def profiled_traffic(config: str):
-    """HBM-side bytes per launch of the bootstrap stage from the newest committed rocprofv3
+def profiled_traffic(config: str, member=None, last=None):
+    """HBM-side bytes per stage of the measured kernels from the newest committed rocprofv3
     summary of this config (profiles/rNN_config<C>_summary.json, written by tools/profile.sh +
     tools/pmc_summary.py from separate --pmc passes of this same command; FETCH_SIZE x2 per
-    MI355X_MICROARCH.md).  The stage is what bench times as one bootstrap launch; bytes and
-    durations are summed over its kernels and divided by the number of stages (launches of
-    the stage's last kernel)."""
+    MI355X_MICROARCH.md).  `member(name)` picks the stage's kernels (default: the bootstrap
+    stage), `last(name)` the kernel that ends one stage (one launch per stage); bytes and
+    durations are summed over the stage's kernels and divided by the number of stages."""
+    member = member or stage_kernel
+    last = last or stage_last
     d = os.path.join(ROOT, "profiles")
     if not os.path.isdir(d):
         return None
@@ -137,8 +139,8 @@ def profiled_traffic(config: str):
         return None
     with open(os.path.join(d, cands[-1])) as f:
         ks = json.load(f)["kernels"]
-    stage = {k: v for k, v in ks.items() if stage_kernel(k)}
-    n = max((v.get("calls") or 0 for k, v in stage.items() if stage_last(k)), default=0)
+    stage = {k: v for k, v in ks.items() if member(k)}
+    n = max((v.get("calls") or 0 for k, v in stage.items() if last(k)), default=0)
     if not stage or not n:
         return None
     if any(v.get("traffic_bytes") is None for v in stage.values()):
@@ -150,6 +152,17 @@ def profiled_traffic(config: str):
     if cyc > 0:  # share of the stage's wave cycles spent waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES)
         out["wait_frac"] = sum(v.get("SQ_WAIT_ANY", 0) * v["calls"] for v in stage.values()) / cyc
     return out
+
+
+def add_profile_fields(roof: dict, prof):
+    """traffic / counter-bytes fraction / wait share from a profiled_traffic() record."""
+    if not prof:
+        return
+    roof["traffic"] = prof["traffic_bytes"]
+    roof["traffic_source"] = f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"
+    roof["counter_bytes_frac"] = prof["traffic_bytes"] / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+    if prof.get("wait_frac") is not None:
+        roof["wait_frac"] = prof["wait_frac"]
 
 
 def stage_kernel(name: str) -> bool:
@@ -255,6 +268,8 @@ def bench_prior(args, cfg, rank, world, device):
                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
                         "avg_launch_ms": bin_s * 1e3, "launches": bin_n, "algorithmic_bytes_per_launch": per_launch},
            "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
+    add_profile_fields(out["roofline"], profiled_traffic("prior", lambda k: k.startswith("k_prior_bin"),
+                                                         lambda k: k.startswith("k_prior_bin")))
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
     if rank == 0 and cpu_sample > 0:
         from oracle import prior as OP
@@ -339,6 +354,10 @@ def bench_wpca(args, cfg, rank, world, device):
                         "pass_bytes_note": "16 B x cells x genes per EM pass per start (the reference's reads); "
                                            "starts share their columns on chip, so HBM sees a fraction"},
            "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
+    # per step: the step's EM launches (one k_wpca_final<1> closes each step's npcs = 1 batch)
+    prof = profiled_traffic("5", lambda k: k.startswith("k_wpca_ms1") or k.startswith("k_wpca_em"),
+                            lambda k: k.startswith("k_wpca_final<1"))
+    add_profile_fields(res["roofline"], prof)
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
     if rank == 0 and cpu_sample > 0:
         from oracle import wpca as W
@@ -625,9 +644,7 @@ def main():
                 "achieved_basis": "lane FMAs the FP64 bootstrap kernels issue (computed grid points x slab boots x "
                                   "entries, x2 flops) per step / stage time per step (HIP events)"}
     roof.update({
-        "traffic": prof["traffic_bytes"] if prof else None,
-        "traffic_source": (f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"
-                           if prof else None),
+        "traffic": None,
         "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
         # SURVEY.md §8(d)'s algorithmic bytes of the reference formulation over the stage time:
         # the work avoided (sparse deltas, skipped stretches) counts as if it were read
@@ -636,11 +653,8 @@ def main():
         "hbm_algorithmic_frac": (hbm_alg / HBM_PEAK_GBS) if hbm_alg else None,
         "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None,
         "f64_fma_per_step": step_fma, "i8_mac_per_step": step_mac})
-    if prof:
-        # what the stage really moves: counter bytes per stage over the rocprof stage time
-        roof["counter_bytes_frac"] = prof["traffic_bytes"] / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
-        if prof.get("wait_frac") is not None:
-            roof["wait_frac"] = prof["wait_frac"]
+    # what the stage really moves: counter bytes per stage over the rocprof stage time
+    add_profile_fields(roof, prof)
     out = {
         "metric": (METRIC_BATCH if batched else METRIC) if de else "genes/sec for scde.posteriors with posterior modes "
                                                                    "(400-pt grid, 100 randomizations)",

@@ -182,7 +182,7 @@ struct scde_ctx {
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
-  Buf gkey, gkey2, gidx, gorder, gwork;
+  Buf gkey, gkey2, gidx, gorder, gwork, pmask;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_q = 0;            // "boot_q": the fixed-point int8-MFMA bootstrap: 0 never, 1 from boot_q_cells, 2 always
   int opt_boot_q_cells = 1000;   // "boot_q_cells": cells per call from which boot_q = 1 picks it
@@ -278,7 +278,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork};
+                 &w8t,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
@@ -869,6 +869,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         tb.nanflag = cx->qflags.as<int>();
         tb.maxgroups = cx->opt_tile_groups;
         tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
+        HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * N)));
+        tb.pmask = cx->pmask.as<unsigned>();
         if (cx->opt_tile_order && N > 1) {
           HCHK(cx->gkey.ensure(sizeof(unsigned) * N));
           HCHK(cx->gkey2.ensure(sizeof(unsigned) * N));

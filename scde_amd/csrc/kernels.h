@@ -184,6 +184,7 @@ struct TileBootArgs {
   int* stats;                // nullable: [0] slabs, [1] tiles computed, [2] tiles, [3] slabs left to k_boot2,
                              // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left
   const int* order;          // nullable: genes in this order (launch_gene_order)
+  unsigned* pmask;           // [ngenes][P] tiles each slab's partial row holds (k_sum_partials reads those)
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending

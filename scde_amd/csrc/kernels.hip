@@ -41,6 +41,47 @@ __device__ __forceinline__ double wave_sum(double v) {
 // arma-style max: NaN never wins (first-max semantics live in the argmax path)
 __device__ __forceinline__ double gt_max(double a, double b) { return (b > a) ? b : a; }
 
+// Whole-wave reductions on VALU only (no LDS round trips): within each 16-lane row by DPP
+// (lane^1, ^2 quad_perm; ^7 row_half_mirror; ^15 row_mirror), then across rows with gfx950's
+// v_permlane16_swap / v_permlane32_swap (each leaves the two halves' values side by side,
+// so one op combines them on every lane).  Every lane ends with the same bits.
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ void rows_swap16(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                   false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                   false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+__device__ __forceinline__ void rows_swap32(double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
+                                                   false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)__double2hiint(a), (unsigned)__double2hiint(b), false,
+                                                   false);
+  a = __hiloint2double((int)hi[0], (int)lo[0]);
+  b = __hiloint2double((int)hi[1], (int)lo[1]);
+}
+template <bool MAX>
+__device__ __forceinline__ double wave_allreduce(double v) {
+  auto op = [](double a, double b) { return MAX ? gt_max(a, b) : a + b; };
+  v = op(v, dpp64<0xB1>(v));   // quad_perm [1,0,3,2]: lane ^ 1
+  v = op(v, dpp64<0x4E>(v));   // quad_perm [2,3,0,1]: lane ^ 2
+  v = op(v, dpp64<0x141>(v));  // row_half_mirror
+  v = op(v, dpp64<0x140>(v));  // row_mirror
+  double w = v;
+  rows_swap16(v, w);
+  v = op(v, w);
+  w = v;
+  rows_swap32(v, w);
+  return op(v, w);
+}
+
 // ------------------------------------------------------------------ K0: cell prep
 // models: ncells x 12 column-major (R `mm`), columns per src/jpmatLogBoot.cpp:88-99
 __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ models, int ncells, int G, int GS,
@@ -224,9 +265,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
       lmax = gt_max(lmax, nb);
     }
   }
-  double maxp = lmax;
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) maxp = gt_max(maxp, __shfl_xor(maxp, m, 64));
+  double maxp = wave_allreduce<true>(lmax);
   if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
   double ls = 0.0;
 #pragma unroll 1
@@ -238,7 +277,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
     v[k] = e;
     ls += e;
   }
-  const double s = wave_sum(ls);
+  const double s = wave_allreduce<false>(ls);
   const double lsum = log_tab(s, lt);  // s >= 1 (the maximum term is exp(0))
   double bv = -INFINITY;
   int bi = 0x7fffffff;
@@ -556,33 +595,63 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
 // count is not the baseline and writes their (cell, column) pairs contiguously (mbcnt
 // prefix), keeping the cell order.  The row is padded with zero-column entries to a
 // multiple of 8 plus one more batch of 8 (the k_boot2 look-ahead).
+// ELL rows: per gene the (cell, column) pairs of the cells whose column is not the cell's
+// baseline, in cell order, then pad entries (cell 0, the zero column).  A block takes 64
+// genes: each 64-cell chunk of uci (genes fastest, as R lays out the count matrix) is read
+// coalesced into an LDS tile (stride 65 against bank conflicts), then each wave compacts 16
+// genes' rows from it with ballots.
 __global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
                                              int ncells, const long long* __restrict__ ucl_off,
                                              const int* __restrict__ base_col, int stride, int pad_col,
                                              int padto, int2* __restrict__ ent, int* __restrict__ nnz) {
-  const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= ngenes) return;
-  int2* E = ent + (long long)g * stride;
-  int n = 0;
+  __shared__ int tile[64][65];  // [cell][gene]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g0 = blockIdx.x * 64;
+  int n[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) n[i] = 0;
   for (int c0 = 0; c0 < ncells; c0 += 64) {
-    const int c = c0 + lane;
-    int col = -1;
-    bool keep = false;
-    if (c < ncells) {
-      col = (int)(ucl_off[c] + uci[(long long)g + ld_uci * c]);
-      keep = col != base_col[c];
+    __syncthreads();
+    for (int j = wid; j < 64; j += 4) {  // row j of the tile: cell c0 + j, lanes over genes
+      const int c = c0 + j, g = g0 + lane;
+      tile[j][lane] = (c < ncells && g < ngenes) ? uci[(long long)g + ld_uci * c] : 0;
     }
-    const unsigned long long m = __ballot(keep);
-    const int pos = n + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
-    if (keep) E[pos] = make_int2(c, col);
-    n += __popcll(m);
+    __syncthreads();
+    const int c = c0 + lane;
+    long long off = 0;
+    int bc = -1;
+    if (c < ncells) {
+      off = ucl_off[c];
+      bc = base_col[c];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int gl = wid * 16 + i, g = g0 + gl;
+      if (g >= ngenes) break;
+      int col = -1;
+      bool keep = false;
+      if (c < ncells) {
+        col = (int)(off + tile[lane][gl]);
+        keep = col != bc;
+      }
+      const unsigned long long m = __ballot(keep);
+      const int pos = n[i] + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+      if (keep) ent[(long long)g * stride + pos] = make_int2(c, col);
+      n[i] += __popcll(m);
+    }
   }
-  if (lane == 0) nnz[g] = n;
   // padto 64: k_bootq reads whole 64-entry steps; k_boot_tiles' FP64 loop also looks one
   // 4-entry batch past its last batch, hence the extra 8
-  const int end = padto == 64 ? (n > 0 ? (n + 63) & ~63 : 64) + 8 : ((n + 7) & ~7) + 8;
-  for (int p = n + lane; p < end && p < stride; p += 64) E[p] = make_int2(0, pad_col);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int g = g0 + wid * 16 + i;
+    if (g >= ngenes) break;
+    const int nn = n[i];
+    if (lane == 0) nnz[g] = nn;
+    const int end = padto == 64 ? (nn > 0 ? (nn + 63) & ~63 : 64) + 8 : ((nn + 7) & ~7) + 8;
+    int2* E = ent + (long long)g * stride;
+    for (int q = nn + lane; q < end && q < stride; q += 64) E[q] = make_int2(0, pad_col);
+  }
 }
 
 // D[col] = T[col] - T[baseline column of its cell] (or T[col] when the cell has no
@@ -613,17 +682,20 @@ __global__ __launch_bounds__(256) void k_delta(const double* __restrict__ T, con
 // One workgroup per (4 boots, 64-point tile of k, set): wave w takes the cells c = w
 // (mod 4), each lane one k with the 4 boots' partial sums (each baseline column read once
 // per 4 boots); the 4 waves' partials combine in a fixed order.  Bp is a multiple of 4.
-__global__ __launch_bounds__(256) void k_baseline_z(const double* __restrict__ T, int G, int GS,
-                                                    const int* __restrict__ base_col, int ncells,
-                                                    const double* __restrict__ Wt, int Bp,
-                                                    double* __restrict__ Z) {
-  __shared__ double part[4][4][64];  // [wave][boot][lane]
+// 16 waves per (set, 4 boots, 64 points), each over every 16th cell, partials added in wave
+// order: 4x the waves of a 4-wave block for the same latency-bound chains
+constexpr int kZWaves = 16;
+__global__ __launch_bounds__(64 * kZWaves) void k_baseline_z(const double* __restrict__ T, int G, int GS,
+                                                            const int* __restrict__ base_col, int ncells,
+                                                            const double* __restrict__ Wt, int Bp,
+                                                            double* __restrict__ Z) {
+  __shared__ double part[kZWaves][4][64];  // [wave][boot][lane]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int b0 = blockIdx.x * 4, k = blockIdx.y * 64 + lane, set = blockIdx.z;
   const double* W = Wt + (long long)set * ncells * Bp + b0;
   double z[4] = {0.0, 0.0, 0.0, 0.0};
   if (k < G) {
-    for (int c = wid; c < ncells; c += 4) {
+    for (int c = wid; c < ncells; c += kZWaves) {
       const int bc = base_col[c];
       if (bc < 0) continue;
       const double t = T[(long long)bc * GS + k];
@@ -635,9 +707,12 @@ __global__ __launch_bounds__(256) void k_baseline_z(const double* __restrict__ T
 #pragma unroll
   for (int r = 0; r < 4; ++r) part[wid][r][lane] = z[r];
   __syncthreads();
-  if (k < GS)
-    Z[((long long)set * Bp + b0 + wid) * GS + k] =
-        ((part[0][wid][lane] + part[1][wid][lane]) + part[2][wid][lane]) + part[3][wid][lane];
+  if (wid < 4 && k < GS) {
+    double s = part[0][wid][lane];
+#pragma unroll
+    for (int w = 1; w < kZWaves; ++w) s += part[w][wid][lane];
+    Z[((long long)set * Bp + b0 + wid) * GS + k] = s;
+  }
 }
 
 // ZU[set][b][j] = sum over baseline cells of W[set][c][b] * U[base_col[c]][j]: the
@@ -1446,7 +1521,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8c, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
-    int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order) {
+    int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
   static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
   __shared__ float ubs[4][kTileMax * NB];  // [wave][tile][boot] bounds
   __shared__ float fmx[4][2][32];          // [wave][group][boot] maxima
@@ -1463,7 +1538,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   const int gi = item / P, p = item - gi * P, b0 = p * NB;
   const int g = order ? order[gi] : gi;
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
-    if (lane == 0) redo[(long long)g * P + p] = 1;
+    if (lane == 0) {
+      redo[(long long)g * P + p] = 1;
+      pmask[(long long)g * P + p] = ~0u;  // k_boot2 writes the whole row
+    }
     return;
   }
   const int n = nnz[g];
@@ -1643,6 +1721,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     if (cnt > 4 || maxgroups < 2) {  // the whole slab goes to k_boot2's redo launch
       if (lane == 0) {
         redo[(long long)g * P + p] = 1;
+        pmask[(long long)g * P + p] = ~0u;
         if (stats) {
           atomicAdd(&stats[3], 1);
           atomicAdd(&stats[5], (n + 3) & ~3);
@@ -1715,10 +1794,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     for (int i = 0; i < NB; ++i) jpv = fma(acc2[i], finv[wsid][i], jpv);
     if (live2) prow[k2] = jpv;
   }
-  for (int t0 = 0; t0 < NT; t0 += 4) {
-    const int t = t0 + h, k = 16 * t + r;
-    if (t < NT && !((done >> t) & 1) && k < G) prow[k] = 0.0;
-  }
+  // tiles not computed stay unwritten: k_sum_partials reads only the tiles in pmask
+  if (lane == 0) pmask[(long long)g * P + p] = done;
   if (stats && lane == 0) {
     atomicAdd(&stats[0], 1);
     atomicAdd(&stats[1], __builtin_popcount(done));
@@ -1728,13 +1805,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
 }
 
 // jp[g, k] = sum over slabs p (in order) of part[p][g][k]
+// pmask (nullable, k_boot_tiles): per (gene, slab) the 16-point tiles written; the others
+// are zeros, read as +0.0, so the sums are those of full rows.
 __global__ void k_sum_partials(const double* __restrict__ part, long long part_stride, int P, int ngenes, int G,
-                               int GS, double* __restrict__ out, long long out_g, long long out_k) {
+                               int GS, double* __restrict__ out, long long out_g, long long out_k,
+                               const unsigned* __restrict__ pmask) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)ngenes * G) return;
   const int g = (int)(i / G), k = (int)(i % G);
-  double s = part[(long long)g * GS + k];
-  for (int p = 1; p < P; ++p) s += part[(long long)p * part_stride + (long long)g * GS + k];
+  const unsigned bit = 1u << (k >> 4);
+  double s = (!pmask || (pmask[(long long)g * P] & bit)) ? part[(long long)g * GS + k] : 0.0;
+  for (int p = 1; p < P; ++p)
+    s += (!pmask || (pmask[(long long)g * P + p] & bit)) ? part[(long long)p * part_stride + (long long)g * GS + k]
+                                                         : 0.0;
   out[(long long)g * out_g + (long long)k * out_k] = s;
 }
 
@@ -2511,7 +2594,7 @@ hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, 
   if (ngenes <= 0) return hipSuccess;
   if (padto == 64 ? stride < ((ncells + 63) & ~63) + 8 || stride < 72 : stride < ((ncells + 7) & ~7) + 8)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 4)), dim3(256), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
+  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 64)), dim3(256), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
                      base_col, stride, pad_col, padto, ent, nnz);
   return hipGetLastError();
 }
@@ -2525,7 +2608,7 @@ hipError_t launch_delta(const double* T, const long long* ucl_off, int ncells, l
 
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
                              int Bp, int nsets, double* Z, hipStream_t s) {
-  hipLaunchKernelGGL(k_baseline_z, dim3(Bp / 4, (GS + 63) / 64, nsets), dim3(256), 0, s, T, G, GS, base_col, ncells, Wt,
+  hipLaunchKernelGGL(k_baseline_z, dim3(Bp / 4, (GS + 63) / 64, nsets), dim3(64 * kZWaves), 0, s, T, G, GS, base_col, ncells, Wt,
                      Bp, Z);
   return hipGetLastError();
 }
@@ -2632,7 +2715,7 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (e != hipSuccess) return e;
   const long long n = (long long)a.ngenes * a.G;
   hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                     a.G, a.GS, a.out, a.out_g, a.out_k);
+                     a.G, a.GS, a.out, a.out_g, a.out_k, nullptr);
   return hipGetLastError();
 }
 
@@ -2666,7 +2749,7 @@ hipError_t launch_gene_key(const int2* ent, const int* nnz, int ent_stride, cons
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const int P = (a.nboot + a.nb - 1) / a.nb;
-  if (a.G > 16 * kTileMax || !a.redo || !tb.W8 || !tb.UQ || !tb.ZUq || !tb.nanflag ||
+  if (a.G > 16 * kTileMax || !a.redo || !tb.W8 || !tb.UQ || !tb.ZUq || !tb.nanflag || !tb.pmask ||
       tb.Bq < (P - 1) * a.nb + 32 || tb.Bq % 32)
     return hipErrorInvalidValue;
   if ((long long)a.ncols_p1 * a.GS >= (1LL << 31) || (long long)a.ncells * a.Bp >= (1LL << 31))
@@ -2680,7 +2763,7 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
     hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,       \
                        a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,       \
                        a.part_stride, a.degen, a.ngenes, tb.W8, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
-                       a.redo, tb.stats, tb.order);                                                             \
+                       a.redo, tb.stats, tb.order, tb.pmask);                                                   \
     break;
   switch (a.nb) {
     SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)
@@ -2708,7 +2791,7 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if (e != hipSuccess) return e;
   const long long nn = (long long)a.ngenes * a.G;
   hipLaunchKernelGGL(k_sum_partials, dim3(div_up(nn, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                     a.G, a.GS, a.out, a.out_g, a.out_k);
+                     a.G, a.GS, a.out, a.out_g, a.out_k, tb.pmask);
   return hipGetLastError();
 }
 

@@ -3,11 +3,11 @@
 #   GPU parity tests, rocprofv3 stats + PMC passes per profiled config (profiles/rNN_config<C>_*),
 #   then every bench config with its CPU baseline -> gpurun_out/fin/b_<cfg>.json.
 #   tools/round_measure.sh <round tag, e.g. r02> [bench configs...]
-#   PROF_CFGS (default "2 3 4") picks the profiled configs; SKIP_TESTS=1 skips the parity tests.
+#   PROF_CFGS (default: every config) picks the profiled configs; SKIP_TESTS=1 skips the parity tests.
 set -o pipefail
 TAG=${1:-r02}; shift || true
 CFGS=${@:-"3 2 4 2b prior 5"}
-PROF_CFGS=${PROF_CFGS:-"2 3 4"}
+PROF_CFGS=${PROF_CFGS:-"2 3 4 2b prior 5"}
 mkdir -p gpurun_out/fin
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/fin/gputests.log 2>&1 || { tail -20 gpurun_out/fin/gputests.log; exit 1; }
