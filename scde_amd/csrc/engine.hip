@@ -792,11 +792,24 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
                     (int)ncols, tpath ? 64 : 8, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
     if (tpath) {
       // byte multiplicities [set][cell][boot] (baseline bound sums and the tile bounds)
-      std::vector<unsigned char> w8((size_t)nsets * C * Bt, 0);
+      // and, for the tile bounds' A fragments, per slab the pairs (boot r, boot 16 + r) of its nb
+      // boots, so one 16-bit load serves both 16-boot MFMA tiles
+      const int P = (s.nboot + nb - 1) / nb;
+      std::vector<unsigned char> w8((size_t)nsets * C * Bt, 0), w8p((size_t)nsets * C * P * 32, 0);
       for (int set = 0; set < nsets; ++set)
-        for (int c = 0; c < C; ++c)
-          for (int b = 0; b < Bp; ++b) w8[((size_t)set * C + c) * Bt + b] = (unsigned char)W[((size_t)set * C + c) * Bp + b];
+        for (int c = 0; c < C; ++c) {
+          const double* wr = W.data() + ((size_t)set * C + c) * Bp;
+          for (int b = 0; b < Bp; ++b) w8[((size_t)set * C + c) * Bt + b] = (unsigned char)wr[b];
+          for (int p = 0; p < P; ++p)
+            for (int j = 0; j < 32 && j < nb; ++j) {
+              const int b = p * nb + j;
+              if (b >= Bp) continue;
+              const size_t slot = (j < 16) ? 2 * j : 2 * (j - 16) + 1;
+              w8p[(((size_t)set * C + c) * P + p) * 32 + slot] = (unsigned char)wr[b];
+            }
+        }
       RCHK(upload(cx, cx->w8, w8.data(), w8.size()));
+      RCHK(upload(cx, cx->w8t, w8p.data(), w8p.size()));
       HCHK(cx->zubound.ensure(sizeof(int) * (size_t)nsets * 4 * kQTiles * Bt));
       HCHK(launch_zuq(cx->ubound.as<unsigned>(), cx->base_col.as<int>(), C, cx->w8.as<unsigned char>(), Bt, nsets,
                       cx->zubound.as<int>(), st));
@@ -862,7 +875,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         HCHK(cx->sredo.ensure(sizeof(int) * ((size_t)P * N + 1)));
         b2.redo = cx->sredo.as<int>();
         TileBootArgs tb{};
-        tb.W8 = cx->w8.as<unsigned char>();
+        tb.W8p = cx->w8t.as<unsigned char>();
         tb.Bq = Bt;
         tb.UQ = cx->ubound.as<unsigned>();
         tb.ZUq = cx->zubound.as<int>();

@@ -175,8 +175,9 @@ struct Boot2Args {
 // k_boot_tiles (with Boot2Args; needs G <= 448): multiplicities as bytes and the tables'
 // 16-point tile bounds for the exact integer tile bounds of each (gene, slab)
 struct TileBootArgs {
-  const unsigned char* W8;   // [nsets][ncells][Bq] draw multiplicities (<= 127)
-  int Bq;                    // a multiple of 32, >= the last slab's first boot + 32
+  const unsigned char* W8p;  // [nsets][ncells][P][32] draw multiplicities (<= 127): per slab the pairs
+                             // (boot r, boot 16 + r) of its boots, r < 16 (0 past the slab's live boots)
+  int Bq;                    // ZUq's boot stride: a multiple of 32, >= the last slab's first boot + 32
   const unsigned* UQ;        // [ncols + 1][kQTiles] packed tile maxima (units of 2^-8, rounded up)
   const int* ZUq;            // [nsets][4][kQTiles][Bq] baseline tile-bound digit sums
   const int* nanflag;        // tables saw a NaN: every slab goes to k_boot2

@@ -1519,7 +1519,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
     const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
-    long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8c, int Bq,
+    long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8p, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
   static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
@@ -1555,7 +1555,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   // the A fragments are multiplicity bytes, cell-major, so each 16-lane row reads 16
   // adjacent bytes
   {
-    const unsigned char* __restrict__ W8 = W8c + (long long)set * ncells * Bq + b0;
+    // W8p: [set][cell][slab][32] multiplicity bytes, pairs (r, 16 + r) of the slab's boots
+    const unsigned pstride = 32u * (unsigned)P;
+    const unsigned char* __restrict__ W8 = W8p + (long long)set * ncells * pstride + 32 * p;
     const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
     const int KP = (n + 63) & ~63;
     for (int tg = 0; 16 * tg < NT; ++tg) {
@@ -1579,18 +1581,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
         }
         unsigned u[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) u[j] = UQ[(long long)co[j] * kQTiles + t];
+        for (int j = 0; j < 16; ++j) u[j] = UQ[(unsigned)(co[j] * kQTiles + t)];
         i32x4 af[2];
+        // the slab's multiplicity pairs (boots r and 16 + r of the slab, one 16-bit load per
+        // entry from 32-bit offsets off a wave-uniform base), split into the two boot tiles'
+        // A fragments by v_perm_b32; ncells x P x 32 and (ncols + 1) x 32 are < 2^31
+        unsigned lo4[4], hi4[4];
 #pragma unroll
-        for (int bt = 0; bt < 2; ++bt) {
-          const unsigned char* wr = W8 + 16 * bt + r;
-          unsigned wd[4];
+        for (int q = 0; q < 4; ++q) {
+          unsigned w2[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            wd[q] = (unsigned)wr[cl[4 * q] * Bq] | ((unsigned)wr[cl[4 * q + 1] * Bq] << 8) |
-                    ((unsigned)wr[cl[4 * q + 2] * Bq] << 16) | ((unsigned)wr[cl[4 * q + 3] * Bq] << 24);
-          af[bt] = i32x4{(int)wd[0], (int)wd[1], (int)wd[2], (int)wd[3]};
+          for (int i = 0; i < 4; ++i)
+            w2[i] = *reinterpret_cast<const unsigned short*>(W8 + (unsigned)(cl[4 * q + i] * pstride) + 2 * r);
+          const unsigned x01 = w2[0] | (w2[1] << 16), x23 = w2[2] | (w2[3] << 16);
+          lo4[q] = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
+          hi4[q] = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
         }
+        af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
+        af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
         unsigned pl[4][4];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -2749,10 +2757,11 @@ hipError_t launch_gene_key(const int2* ent, const int* nnz, int ent_stride, cons
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const int P = (a.nboot + a.nb - 1) / a.nb;
-  if (a.G > 16 * kTileMax || !a.redo || !tb.W8 || !tb.UQ || !tb.ZUq || !tb.nanflag || !tb.pmask ||
+  if (a.G > 16 * kTileMax || !a.redo || !tb.W8p || !tb.UQ || !tb.ZUq || !tb.nanflag || !tb.pmask ||
       tb.Bq < (P - 1) * a.nb + 32 || tb.Bq % 32)
     return hipErrorInvalidValue;
-  if ((long long)a.ncols_p1 * a.GS >= (1LL << 31) || (long long)a.ncells * a.Bp >= (1LL << 31))
+  if ((long long)a.ncols_p1 * a.GS >= (1LL << 31) || (long long)a.ncells * a.Bp >= (1LL << 31) ||
+      (long long)a.ncells * 32 * P >= (1LL << 31))
     return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(a.redo, 0, sizeof(int) * ((size_t)a.ngenes * P + 1), s);
   if (e != hipSuccess) return e;
@@ -2762,7 +2771,7 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   case NBV:                                                                                                       \
     hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,       \
                        a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,       \
-                       a.part_stride, a.degen, a.ngenes, tb.W8, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
+                       a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
                        a.redo, tb.stats, tb.order, tb.pmask);                                                   \
     break;
   switch (a.nb) {
