@@ -140,7 +140,7 @@ def profiled_traffic(config: str, member=None, last=None):
     with open(os.path.join(d, cands[-1])) as f:
         ks = json.load(f)["kernels"]
     stage = {k: v for k, v in ks.items() if member(k)}
-    n = max((v.get("calls") or 0 for k, v in stage.items() if last(k)), default=0)
+    n = max((v.get("calls") or 0 for k, v in ks.items() if last(k)), default=0)
     if not stage or not n:
         return None
     if any(v.get("traffic_bytes") is None for v in stage.values()):
@@ -268,8 +268,8 @@ def bench_prior(args, cfg, rank, world, device):
                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": None,
                         "avg_launch_ms": bin_s * 1e3, "launches": bin_n, "algorithmic_bytes_per_launch": per_launch},
            "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]}}
-    add_profile_fields(out["roofline"], profiled_traffic("prior", lambda k: k.startswith("k_prior_bin"),
-                                                         lambda k: k.startswith("k_prior_bin")))
+    add_profile_fields(out["roofline"], profiled_traffic("prior", lambda k: "k_prior_bin" in k,
+                                                         lambda k: "k_prior_bin" in k))
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
     if rank == 0 and cpu_sample > 0:
         from oracle import prior as OP

@@ -21,8 +21,9 @@ import pandas as pd
 
 
 def short_name(name: str) -> str:
-    """'void scde::k_boot2<20>(double const*, ...)' -> 'k_boot2<20>'."""
-    n = re.sub(r"^void ", "", name)
+    """'void scde::k_boot2<20>(double const*, ...)' -> 'k_boot2<20>';
+    'scde::(anonymous namespace)::k_prior_bin(int const*, ...)' -> 'k_prior_bin'."""
+    n = re.sub(r"^void ", "", name).replace("(anonymous namespace)::", "")
     n = n.split("(")[0]
     return n.replace("scde::", "")
 
