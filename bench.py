@@ -443,6 +443,9 @@ def main():
                     help="nccl (= RCCL, the real path) or gloo (CPU gather; rehearsal with ranks sharing one GPU)")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="oracle worker processes for the parallel CPU baseline (0 = skip; the GPU box's share is 16)")
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="readiness study, one process: time rank 0's shard of a strong split over this many "
+                         "ranks (no collective; not the metric)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
@@ -478,7 +481,7 @@ def main():
         # one data set of cfg genes, split by shard_range; global gene offsets keep the seeding
         NTOT = cfg["genes"]
         models, counts_all, groups = synthetic(cfg["seed"], NTOT, cfg["cells"], two_groups=de)
-        g0, g1 = shard_range(NTOT, world, rank)
+        g0, g1 = shard_range(NTOT, world, rank) if args.shard_of <= 1 else shard_range(NTOT, args.shard_of, 0)
         counts = np.asfortranarray(counts_all[g0:g1])
     else:
         NTOT = cfg["genes"] * world
@@ -674,6 +677,9 @@ def main():
                    "n_randomizations": NBOOT, "parallelism": f"gene-shard x{world} ({scaling})",
                    "timed_region": "host counts -> upload -> unique tables, posteriors, ratio, summary, BH -> "
                                    "host result table"},
+        **({"shard_of": args.shard_of,
+            "shard_note": "one process timing rank 0's shard of a strong split; value = all genes / that time "
+                          "(a projection, no collective, not the metric)"} if args.shard_of > 1 else {}),
         "device_resident_genes_per_s": NTOT * args.steps / dt_dev,
         "device_resident_ms_per_step": dt_dev / args.steps * 1e3,
         "roofline": roof,
