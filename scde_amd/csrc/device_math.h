@@ -336,7 +336,6 @@ __device__ __constant__ const double kLogCLo[97] = {
     -2.8811380259626426e-18};
 
 // cold paths kept out of line so they do not inflate the hot loops' register allocation
-__device__ __noinline__ double log_cold(double x) { return log(x); }
 
 struct LogTab {
   const double* inv;
@@ -344,9 +343,10 @@ struct LogTab {
   const double* lo;
 };
 
-__device__ __forceinline__ double log_tab_hot(double x, const LogTab& t) {  // x in [DBL_MIN, inf)
+__device__ __forceinline__ double log_tab_hot(double x, const LogTab& t, int eadj = 0) {  // x in [DBL_MIN, inf)
   int e;
   double m = frexp(x, &e);  // [0.5, 1)
+  e -= eadj;
   if (m < 0.75) {
     m *= 2.0;
     e -= 1;
@@ -365,13 +365,16 @@ __device__ __forceinline__ double log_tab_hot(double x, const LogTab& t) {  // x
   return (fma(ed, 0.6931471805598903, t.hi[j]) + (fma(ed, 5.497923018708371e-14, t.lo[j]) + p));
 }
 
-// The hot path is branch-free; arguments outside [DBL_MIN, inf) (zero, subnormal, inf, NaN)
-// take the library log under a wave-uniform branch, only in waves that have such a lane.
+// Branch-free and call-free over all inputs: a subnormal x is scaled by 2^64 first (exact)
+// and 64 comes off the exponent, so it takes the same table path as a normal x; zero, inf,
+// negative and NaN arguments are selected in (-inf, inf, NaN, NaN as the library log).
 __device__ __forceinline__ double log_tab(double x, const LogTab& t) {
-  const bool cold = !(x >= DBL_MIN && x < INFINITY);
-  const double r0 = log_tab_hot(cold ? 1.0 : x, t);
-  if (__builtin_amdgcn_ballot_w64(cold)) return cold ? log_cold(x) : r0;
-  return r0;
+  const bool sub = x > 0.0 && x < DBL_MIN;
+  const double xs = sub ? x * 0x1p64 : x;
+  const bool ok = xs >= DBL_MIN && xs < INFINITY;
+  const double r0 = log_tab_hot(ok ? xs : 1.0, t, sub ? 64 : 0);
+  const double rs = (x == 0.0) ? -INFINITY : (x == INFINITY) ? INFINITY : __builtin_nan("");
+  return ok ? r0 : rs;
 }
 
 // bd0's Taylor series (|x - np| < 0.1 (x + np)), out of line
@@ -538,6 +541,12 @@ __device__ __forceinline__ double dnbinom_fast(const NbFast& f, double p, double
     ans = ((f.S - bd0_fast(f.X, np, f.lXn - lp)) - bd0_fast(f.nx, nq, f.lnxn - lq)) - f.hlf;
   }
   return f.lp + ans;
+}
+
+// dnbinom_fast's value without its validity flag (the caller tests validity itself)
+__device__ __forceinline__ double dnbinom_fast(const NbFast& f, double p, double q, double lp, double lq) {
+  bool bad;
+  return dnbinom_fast(f, p, q, lp, lq, bad);
 }
 
 // ---- double-double accumulation (emulates R's LDOUBLE rowSums / cumsum) ----

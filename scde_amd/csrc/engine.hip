@@ -736,7 +736,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   }
   ev = cx->mark_begin(SLOT_TABLES);
   if (!s.localtheta && ncols > 0) {
-    HCHK(cx->colc.ensure(sizeof(double) * 8 * (size_t)ncols));
+    HCHK(cx->colc.ensure(sizeof(double) * (kColc * (size_t)ncols + 1)));  // + the slow-column flag
     HCHK(launch_col_consts(u.ucl.as<int>(), u.ucl_off.as<long long>(), ncols, C, cx->theta.as<double>(), GS,
                            cx->cellscal.as<double>(), cx->colc.as<double>(), st));
     ta.colc = cx->colc.as<double>();

@@ -7,6 +7,9 @@
 #ifndef SCDE_BOOT_ASMLD
 #define SCDE_BOOT_ASMLD 1  // k_boot2 column look-ahead issued from asm with explicit vmcnt waits
 #endif
+#ifndef SCDE_TABREG_WPE
+#define SCDE_TABREG_WPE 4  // k_tables_reg occupancy target (waves per SIMD)
+#endif
 #ifndef SCDE_TAB_WPE
 #define SCDE_TAB_WPE 4  // k_tables_cell occupancy target (waves per SIMD)
 #endif
@@ -29,6 +32,11 @@
 
 namespace scde {
 
+// k_col_consts record per column: [n or -1, n - x, stirlerr sum, 0.5 lf, log(size/(size+x)),
+// log X - log n, log(n - X) - log n, dpois_log(x, failure rate), log po, log(1 - po)] with
+// po = size / (size + x) (the count's own grid point), padded to 10 doubles
+constexpr int kColc = 10;
+
 struct TablesArgs {
   const int* ucl;            // flat unique counts, [ncols]
   const long long* ucl_off;  // [ncells + 1]
@@ -46,7 +54,7 @@ struct TablesArgs {
   unsigned char* has_clamp;  // [ncols]
   int const_theta;           // theta is the same at every grid point (no local theta fit)
   const double* pq;          // [ncells][4][GS] p, q, log p, log q (const_theta), nullable
-  const double* colc;        // [ncols][8] k_col_consts output (with pq), nullable
+  const double* colc;        // [ncols][kColc] k_col_consts output (with pq), nullable
   // Fused baseline-delta output (bootstrap path; the k_delta pass folded into the tables):
   //   phase 0: every column -> T (no D);
   //   phase 1: one wave per cell, its count-0 column -> D (and T if non-null); writes
@@ -78,6 +86,9 @@ struct TablesArgs {
   // nullable: the launch does nothing unless *gate != 0 (the exact fallback's T tables are
   // built only when some gene needs them)
   const int* gate;
+  // k_tables only: take just the columns k_tables_reg leaves (colc n < 0, flagged by
+  // k_col_consts in the int after colc's last column); the launch exits unless that flag is set
+  int slow_only;
 };
 
 // ---- fixed-point bootstrap constants (bootq.hip)

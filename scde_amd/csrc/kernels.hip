@@ -67,6 +67,14 @@ __device__ __forceinline__ void rows_swap32(double& a, double& b) {
   a = __hiloint2double((int)hi[0], (int)lo[0]);
   b = __hiloint2double((int)hi[1], (int)lo[1]);
 }
+// Maximum over each 16-lane row, on every lane of the row (same DPP partners as above).
+__device__ __forceinline__ int row16_max_i32(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false));
+  return v;
+}
 template <bool MAX>
 __device__ __forceinline__ double wave_allreduce(double v) {
   auto op = [](double a, double b) { return MAX ? gt_max(a, b) : a + b; };
@@ -149,12 +157,11 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
 // and the (theta, count)-only terms of dnbinom are computed once per column.
 // Per-column constants of the constant-theta fast path, one lane per column (k_tables
 // would otherwise evaluate them redundantly in all 64 lanes of the column's wave):
-// [n or -1, n - x, stirlerr sum, 0.5 lf, log(size/(size+x)), log X - log n,
-//  log(n - X) - log n, dpois_log(x, failure rate)].
+// the kColc record (kernels.h).
 __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl, const long long* __restrict__ ucl_off,
                                                     long long ncols, int ncells, const double* __restrict__ theta,
                                                     int GS, const double* __restrict__ cellscal,
-                                                    double* __restrict__ colc) {
+                                                    double* __restrict__ colc, int* __restrict__ slow) {
   const long long col = (long long)blockIdx.x * 256 + threadIdx.x;
   if (col >= ncols) return;
   int lo = 0, hi = ncells;
@@ -165,8 +172,9 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
   const double x = (double)ucl[col];
   const NbConst nc = nb_const(x, theta[(long long)lo * GS]);
   const NbFast f = nb_fast(nc);
-  double* o = colc + col * 8;
+  double* o = colc + col * kColc;
   o[0] = f.ok ? f.n : -1.0;
+  if (!f.ok) *slow = 1;  // k_tables_reg leaves this column to the gated k_tables pass
   o[1] = f.nx;
   o[2] = f.S;
   o[3] = f.hlf;
@@ -174,6 +182,9 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
   o[5] = f.lXn;
   o[6] = f.lnxn;
   o[7] = dpois_log(x, cellscal[2 * lo + 1]);
+  const double size = theta[(long long)lo * GS], po = size / (size + x);
+  o[8] = log(po);
+  o[9] = log(1 - po);
 }
 
 #ifndef SCDE_KT_DIAG
@@ -189,6 +200,7 @@ template <bool CT, bool Q>
 __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col, int c, int phase,
                                               const double* __restrict__ mu, const double* __restrict__ P,
                                               const double* __restrict__ lcfpr, const double* __restrict__ lcfp,
+                                              const double* __restrict__ cfpl, const unsigned* __restrict__ uqb,
                                               const double* __restrict__ th, const double* __restrict__ base,
                                               const long long* __restrict__ qbase, double* __restrict__ v,
                                               const double* etab, const LogTab& lt, int lane, int PS) {
@@ -200,7 +212,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   nf.ok = false;
   if (CT && P && a.colc) {
     // per-column constants from k_col_consts (wave-uniform scalar loads)
-    const double* cc = a.colc + col * 8;
+    const double* cc = a.colc + col * kColc;
     nf.n = cc[0];
     nf.nx = cc[1];
     nf.S = cc[2];
@@ -268,14 +280,28 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   double maxp = wave_allreduce<true>(lmax);
   if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
   double ls = 0.0;
+  if (cfpl) {
+    // the Poisson term exp(lcfp + fp - maxp) as cfp * exp(fp - maxp): cfp = exp(lcfp) per
+    // grid point staged with the cell, one exp per column (a few ulps from the quotient form)
+    const double d0 = fp - maxp;
+    const double E = d0 >= -746.0 ? exp_tab(d0, etab) : 0.0;
 #pragma unroll 1
-  for (int k = lane; k < G; k += 64) {
-    // both arguments are <= 0 (maxp bounds them); exp_tab below -746 would underflow anyway
-    const double d1 = v[k] - maxp, d2 = lcfp[k] + fp - maxp;
-    const double e = (SCDE_KT_DIAG & 2) ? (d1 + d2) * 1e-3 + 1.0
-                                        : (d1 >= -746.0 ? exp_tab(d1, etab) : 0.0) + (d2 >= -746.0 ? exp_tab(d2, etab) : 0.0);
-    v[k] = e;
-    ls += e;
+    for (int k = lane; k < G; k += 64) {
+      const double d1 = v[k] - maxp;
+      const double e = (SCDE_KT_DIAG & 2) ? d1 * 1e-3 + 1.0 : fma(cfpl[k], E, d1 >= -746.0 ? exp_tab(d1, etab) : 0.0);
+      v[k] = e;
+      ls += e;
+    }
+  } else {
+#pragma unroll 1
+    for (int k = lane; k < G; k += 64) {
+      // both arguments are <= 0 (maxp bounds them); exp_tab below -746 would underflow anyway
+      const double d1 = v[k] - maxp, d2 = lcfp[k] + fp - maxp;
+      const double e = (SCDE_KT_DIAG & 2) ? (d1 + d2) * 1e-3 + 1.0
+                                          : (d1 >= -746.0 ? exp_tab(d1, etab) : 0.0) + (d2 >= -746.0 ? exp_tab(d2, etab) : 0.0);
+      v[k] = e;
+      ls += e;
+    }
   }
   const double s = wave_allreduce<false>(ls);
   const double lsum = log_tab(s, lt);  // s >= 1 (the maximum term is exp(0))
@@ -334,7 +360,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         if (out) out[k] = r;
         if (dout) dout[k] = base ? r - base[k] : r;
       }
-      if (U || uqf) v[k] = r;  // the row of final values, for the stretch / tile maxima below
+      if (U) v[k] = r;  // the row of final values, for the stretch maxima below
       if (uqf && r != r) nanq = true;
       if (qout) {
         long long q = 0;
@@ -347,6 +373,20 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         const long long d = qbase ? q - qbase[k] : q;
         qout[k] = packq(d);
         vq[k] = d;
+      }
+    }
+    if (uqf) {
+      // this chunk's four 16-point tiles (one 16-lane row each): the maximum in units of
+      // 2^-8, rounded up, floored at -2^29 (lanes past the grid and NaN lanes hold the
+      // floor; ceil and the scaling are monotone, so this is ceil of the tile maximum)
+      int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
+      const int t = 4 * j + (lane >> 4);
+      if ((lane & 15) == 0) {
+        if (16 * t >= G)
+          u = 0;
+        else if (bc_u >= 0)
+          u -= unpacku(uqb ? uqb[t] : a.UQ[(long long)bc_u * kQTiles + t]);
+        a.UQ[col * kQTiles + t] = packu(u);
       }
     }
   }
@@ -371,24 +411,8 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   }
   if (uqf) {
     if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
-    const int nt = (G + 15) / 16, t = lane >> 1;
-    double m = -INFINITY;
-    if (t < nt)
-      for (int i = 0; i < 8; ++i) {
-        const int k = 16 * t + 8 * (lane & 1) + i;
-        if (k < G) m = gt_max(m, v[k]);
-      }
-    m = gt_max(m, __shfl_xor(m, 1, 64));
-    if ((lane & 1) == 0) {
-      int u = 0;
-      if (t < nt) {
-        // r <= 0; below -2^21 the bound is raised to -2^21 (still an upper bound)
-        const double sc = fmax(m * 256.0, -0x1p29);
-        u = (int)ceil(sc);
-        if (bc_u >= 0) u -= unpacku(a.UQ[(long long)bc_u * kQTiles + t]);
-      }
-      a.UQ[col * kQTiles + t] = packu(u);
-    }
+    const int t = 4 * ((G + 63) / 64) + lane;  // tiles past the chunks: 0
+    if (t < kQTiles) a.UQ[col * kQTiles + t] = 0u;
   }
   if (U) {
     // per-stretch maxima from the LDS row: lane l < 8 * stretches takes 8 points of
@@ -448,6 +472,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   __syncthreads();
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
   if (a.gate && *a.gate == 0) return;
+  if (a.slow_only && *reinterpret_cast<const int*>(a.colc + kColc * a.ncols) == 0) return;
   const int phase = a.phase;
   long long col;
   int c;
@@ -473,6 +498,30 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
     col = zc;
   } else {
     col = (long long)blockIdx.x * 4 + wid;
+    if (a.slow_only) {
+      // the columns k_tables_reg left (colc n < 0): 64 candidates per wave step, grid-stride
+      for (long long b0 = col * 64; b0 < a.ncols; b0 += (long long)gridDim.x * 4 * 64) {
+        const long long ci = b0 + lane;
+        unsigned long long m = __ballot(ci < a.ncols && !(a.colc[ci * kColc] > 0.0));
+        while (m) {
+          const long long cs = b0 + __ffsll((long long)m) - 1;
+          m &= m - 1;
+          int lo = 0, hi = a.ncells;
+          while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (a.ucl_off[mid] <= cs) lo = mid; else hi = mid;
+          }
+          if (phase == 2 && cs == a.zcol[lo]) continue;  // done in phase 1
+          const long long co = (long long)lo * a.GS;
+          const int bc = (phase == 2) ? a.base_col[lo] : -1;
+          const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
+          tables_column<CT, Q>(a, cs, lo, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
+                               a.lcfp + co, nullptr, nullptr, a.theta + co, base, nullptr,
+                               vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
+        }
+      }
+      return;
+    }
     if (phase == 2 && col == a.ncols) {  // the ELL pad column
       for (int k = lane; k < a.GS; k += 64) {
         if (a.D) a.D[col * a.GS + k] = 0.0;
@@ -495,7 +544,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const int bc = (phase == 2) ? a.base_col[c] : -1;
   const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
   tables_column<CT, Q>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
-                       a.lcfp + co, a.theta + co, base, nullptr, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
+                       a.lcfp + co, nullptr, nullptr, a.theta + co, base, nullptr, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
 }
 
 // Cell-staged form (phases 0 and 2, G <= kTabStagedG): one 8-wave block per task
@@ -508,8 +557,9 @@ constexpr int kTabStagedG = 448;
 constexpr int kTabWaves = 8;
 template <bool CT, bool Q>
 __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TAB_WPE))) void k_tables_cell(TablesArgs a) {
-  extern __shared__ double dyn[];  // vrow [8][G] | mu | P[4] | lcfpr | lcfp | th | base, each G
+  extern __shared__ double dyn[];  // vrow [8][G] | mu | P[4] | lcfpr | cfp | th | base, each G
   __shared__ double etab[64];
+  __shared__ unsigned suqb[kQTiles];  // the baseline column's tile bounds (phase 2)
   __shared__ double ltab[3][97];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int GS = a.GS, G = a.G;
@@ -538,10 +588,11 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   double* sbase = sth + G;
   const long long co = (long long)c * GS;
   const int bc = (phase == 2) ? a.base_col[c] : -1;
+  if (bc >= 0 && !Q && a.UQ && threadIdx.x < kQTiles) suqb[threadIdx.x] = a.UQ[(long long)bc * kQTiles + threadIdx.x];
   for (int k = threadIdx.x; k < G; k += 64 * kTabWaves) {
     smu[k] = a.mu[co + k];
     slr[k] = a.lcfpr[co + k];
-    slc[k] = a.lcfp[co + k];
+    slc[k] = exp(a.lcfp[co + k]);  // cfp, linear (tables_column's one-exp normalisation)
     sth[k] = a.theta[co + k];
     if (haveP) {
       const double* P = a.pq + 4 * co;
@@ -562,10 +613,316 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   const int zc = (phase == 2) ? a.zcol[c] : -1;
   for (int col = task.y + wid; col < task.z; col += kTabWaves) {
     if (col == zc) continue;  // done in phase 1
-    tables_column<CT, Q>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, slc, sth,
+    tables_column<CT, Q>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, nullptr, slc, (bc >= 0) ? suqb : nullptr, sth,
                          (bc >= 0 && !Q) ? sbase : nullptr,
                          (bc >= 0 && Q) ? reinterpret_cast<const long long*>(sbase) : nullptr, dyn + wid * G, etab,
                          lt, lane, G);
+  }
+}
+
+// Register-row form of the staged kernel for the constant-theta FP64 tables (the default
+// path): a column's 401 grid values stay in seven VGPR pairs through the three passes
+// (dnbinom + max, exp + sum, log + stores + tile maxima) instead of a per-wave LDS row, the
+// chunk loops are unrolled so the LDS reads of different chunks overlap, and the block's
+// LDS shrinks to the staged grid vectors (no row per wave: 3 -> 5 blocks per CU by LDS).
+// Lanes the fast dnbinom does not cover: q == 0 (grid point 0, mu = 0) in line; the rest
+// (p or q out of range, np or nq not a positive finite number) through the exact dnbinom
+// in a pass after the loop, only in waves that have such a lane.  Columns whose constants
+// rule out the fast form (colc n < 0) are left to the gated k_tables pass.
+#ifndef SCDE_KT_STAMP
+#define SCDE_KT_STAMP 0  // timing-only builds: per-phase cycle sums of k_tables_reg (scde_diag_kt_stamps)
+#endif
+#if SCDE_KT_STAMP
+__device__ unsigned long long g_kt_stamp[16];
+#define KT_STAMP(i)                                                                      \
+  do {                                                                                   \
+    const long long t_ = clock64();                                                      \
+    if (lane == 0) atomicAdd(&g_kt_stamp[i], (unsigned long long)(t_ - kt0_));           \
+    kt0_ = t_;                                                                           \
+  } while (0)
+#else
+#define KT_STAMP(i) \
+  do {              \
+  } while (0)
+#endif
+constexpr int kTabChunks = kTabStagedG / 64;
+constexpr int kTabRegWaves = 8;
+
+template <int CTRL>
+__device__ __forceinline__ float dpp32f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_maxf(float v) {
+  v = gt_maxf(v, dpp32f<0xB1>(v));
+  v = gt_maxf(v, dpp32f<0x4E>(v));
+  v = gt_maxf(v, dpp32f<0x141>(v));
+  v = gt_maxf(v, dpp32f<0x140>(v));
+  auto s16 = __builtin_amdgcn_permlane16_swap((unsigned)__float_as_int(v), (unsigned)__float_as_int(v), false, false);
+  v = gt_maxf(__int_as_float((int)s16[0]), __int_as_float((int)s16[1]));
+  auto s32 = __builtin_amdgcn_permlane32_swap((unsigned)__float_as_int(v), (unsigned)__float_as_int(v), false, false);
+  return gt_maxf(__int_as_float((int)s32[0]), __int_as_float((int)s32[1]));
+}
+
+// The staged rows have the fixed stride kTabStagedG (entries G.. are zero pads), so every
+// LDS read is lane * 8 plus an immediate offset: no per-chunk address registers (the
+// compiler would hoist ~8 per chunk out of the column loop and spill them).
+constexpr int kRS = kTabStagedG;
+enum { kRowMu = 0, kRowP = 1, kRowLcfpr = 5, kRowCfp = 6, kRowLcfp = 7, kRowBase = 8, kTabRegRows = 9 };
+
+// Per grid point k of a column, in log space relative to maxp: t1 = nb_k + log(1 - cfp_k)
+// - maxp (the NB term) and t2 = log cfp_k + fp - maxp (the Poisson term); the reference's
+// e_k = exp(t1) + exp(t2), s = sum e_k, T_k = log(e_k / s) (src/jpmatLogBoot.cpp:191-193).
+//   - the sum: exp(t1) only in chunks with a lane above t1 = -60 (smaller terms are below
+//     2^-86 of s >= 1 and do not reach its rounding); exp(t2) = cfp_k exp(fp - maxp);
+//   - T_k where one term exceeds the other by e^37.5 (log1p of the ratio < 5e-17):
+//     max(t1, t2) - log s, no exp or log per point;
+//   - T_k where neither dominates: log(exp(t1) + exp(t2)) - log s (table exp and log), only
+//     in chunks that have such a lane;
+//   - T_k where max(t1, t2) < -665 (e_k below 2^-960, subnormal ranges): the quotient
+//     log(e_k / s) as the reference forms it.
+__device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long col, int c, int phase,
+                                                  const double* __restrict__ sm, bool have_base,
+                                                  const unsigned* __restrict__ uqb, const double* etab,
+                                                  const LogTab& lt, int lane, double theta) {
+  const int G = a.G;
+#if SCDE_KT_STAMP
+  long long kt0_ = clock64();
+#endif
+  const double* cc = a.colc + col * kColc;
+  NbFast nf;
+  nf.n = cc[0];
+  if (!(nf.n > 0.0)) return;  // the gated k_tables pass takes this column
+  nf.nx = cc[1];
+  nf.S = cc[2];
+  nf.hlf = cc[3];
+  nf.lp = cc[4];
+  nf.lXn = cc[5];
+  nf.lnxn = cc[6];
+  const double fp = cc[7];
+  const double lpo = cc[8], lqo = cc[9];
+  nf.X = theta;
+  nf.ok = true;
+  const double x = (double)a.ucl[col];
+  const double maxcfp = a.cellscal[2 * c];
+  const double po = theta / (theta + x);  // the count's own grid point
+  const double* sl = sm + lane;
+  KT_STAMP(0);
+  double v[kTabChunks];
+  unsigned badm = 0;
+  double lmax = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < kTabChunks; ++j) {
+    v[j] = -INFINITY;
+    if (64 * j < G) {
+      const int k = lane + 64 * j;
+      const bool in = k < G;
+      const bool last = (k == G - 1);
+      double pr = sl[kRowP * kRS + 64 * j], qr = sl[(kRowP + 1) * kRS + 64 * j];
+      double lpr = sl[(kRowP + 2) * kRS + 64 * j], lqr = sl[(kRowP + 3) * kRS + 64 * j];
+      const double muv = sl[kRowMu * kRS + 64 * j], mnext = sl[kRowMu * kRS + 64 * j + 1];
+      const bool over = in && ((!last && x > muv && x < mnext) || (last && x > muv));
+      if (__builtin_amdgcn_ballot_w64(over)) {
+        pr = over ? po : pr;
+        qr = over ? 1 - po : qr;
+        lpr = over ? lpo : lpr;
+        lqr = over ? lqo : lqr;
+      }
+      // with n > 0 finite: np > 0 implies p > 0, nq > 0 implies q > 0, p <= 1 keeps np and
+      // nq finite -- the fast form's full validity condition
+      const double np = nf.n * pr, nq = nf.n * qr;
+      const bool bad = in && !(np > 0.0 && nq > 0.0 && pr <= 1.0);
+      double nb = (SCDE_KT_DIAG & 1) ? lpr * x + lqr : dnbinom_fast(nf, pr, qr, lpr, lqr);
+      badm |= bad ? (1u << j) : 0u;
+      nb += sl[kRowLcfpr * kRS + 64 * j];
+      v[j] = in ? nb : -INFINITY;
+      lmax = gt_max(lmax, bad ? -INFINITY : v[j]);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(badm != 0)) {
+    // q == 0 (prob 1: grid point 0, mu = 0) in line; other lanes through the exact dnbinom,
+    // one call site (rolled over chunks; the value goes back into its register by selects)
+    const double nbq0 = (nf.X == nf.n) ? nf.lp : -INFINITY;  // R dbinom_raw's q == 0 branch
+#pragma unroll 1
+    for (int j = 0; j < kTabChunks; ++j) {
+      const bool b = (badm >> j) & 1u;
+      if (!__builtin_amdgcn_ballot_w64(b)) continue;
+      double nv = 0.0;
+      if (b) {
+        const int k = lane + 64 * j;
+        const double muv = sm[kRowMu * kRS + k], mnext = sm[kRowMu * kRS + k + 1];
+        const bool last = (k == G - 1);
+        const bool over = (!last && x > muv && x < mnext) || (last && x > muv);
+        const double pr = over ? po : sm[kRowP * kRS + k];
+        const double qr = over ? 1 - po : sm[(kRowP + 1) * kRS + k];
+        if (qr == 0.0 && pr == 1.0)
+          nv = nbq0;
+        else
+          nv = dnbinom_log_cold(x, theta, pr);
+        nv += sm[kRowLcfpr * kRS + k];
+        lmax = gt_max(lmax, nv);
+      }
+#pragma unroll
+      for (int i = 0; i < kTabChunks; ++i) v[i] = (b && i == j) ? nv : v[i];
+    }
+  }
+  KT_STAMP(1);
+  double maxp = wave_allreduce<true>(lmax);
+  if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
+  KT_STAMP(2);
+  const double d0 = fp - maxp;
+  const double E = exp_tab(fmax(d0, -746.0), etab);  // exp(fp - maxp); 0 below -746 (and for NaN)
+  double ls = 0.0;
+#pragma unroll
+  for (int j = 0; j < kTabChunks; ++j) {
+    if (64 * j < G) {
+      const int k = lane + 64 * j;
+      const bool in = k < G;
+      v[j] -= maxp;  // t1
+      double e = sl[kRowCfp * kRS + 64 * j] * E;
+      if (!(SCDE_KT_DIAG & 2) && __builtin_amdgcn_ballot_w64(in && v[j] > -60.0)) e += exp_tab(fmax(v[j], -746.0), etab);
+      ls += in ? e : 0.0;
+    }
+  }
+  const double s = wave_allreduce<false>(ls);
+  const double lsum = log_tab(s, lt);  // s >= 1 (the maximum term is exp(0))
+  KT_STAMP(3);
+  const bool want_maxi = a.maxi != nullptr;
+  double bv = -INFINITY;
+  int bi = 0x7fffffff;
+  bool clamp = false, nanq = false;
+  KT_STAMP(4);
+  double* out = a.T ? a.T + col * a.GS : nullptr;
+  double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
+  const int bc_u = (phase == 2) ? a.base_col[c] : -1;
+  double* const U = a.U;
+  const double* ubase = (U && bc_u >= 0) ? U + (long long)bc_u * kStretchSlots : nullptr;
+  const bool uqf = a.UQ && phase;
+#pragma unroll
+  for (int j = 0; j < kTabChunks; ++j) {
+    if (64 * j < G) {
+      const int k = lane + 64 * j;
+      const bool in = k < G;
+      const double t1 = v[j], t2 = sl[kRowLcfp * kRS + 64 * j] + d0;
+      const double hi = gt_max(t2, t1), lo = (t1 > t2) ? t2 : t1;
+      const bool tiny = !(hi >= -665.0);
+      const bool mixed = !tiny && !(hi - lo > 37.5);
+      double r = hi - lsum;
+      if (__builtin_amdgcn_ballot_w64(in && (tiny || mixed))) {
+        const double e = fma(sl[kRowCfp * kRS + 64 * j], E, exp_tab(fmax(t1, -746.0), etab));
+        const double rm = (SCDE_KT_DIAG & 4) ? e - lsum : log_tab(tiny ? e / s : e, lt) - (tiny ? 0.0 : lsum);
+        r = (tiny || mixed) ? rm : r;
+      }
+      if (want_maxi && r > bv && in) {
+        bv = r;
+        bi = k;
+      }
+      if (r < a.minlogprob) {
+        r = a.minlogprob;
+        clamp = clamp || in;
+      }
+      if (in) {
+        if (SCDE_KT_DIAG & 8) {  // timing diagnostic: no stores
+          if (r == 12345.0) dout[k] = r;
+        } else {
+          if (out) out[k] = r;
+          if (dout) dout[k] = have_base ? r - sl[kRowBase * kRS + 64 * j] : r;
+        }
+      }
+      nanq = nanq || (in && r != r);
+      if (!in) r = -INFINITY;
+      if (uqf) {  // this chunk's four 16-point tile maxima (as tables_column)
+        int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
+        const int t = 4 * j + (lane >> 4);
+        if ((lane & 15) == 0) {
+          if (16 * t >= G)
+            u = 0;
+          else if (bc_u >= 0)
+            u -= unpacku(uqb ? uqb[t] : a.UQ[(long long)bc_u * kQTiles + t]);
+          a.UQ[col * kQTiles + t] = packu(u);
+        }
+      }
+      if (U) {  // the stretch maximum (64 points = this chunk), f32 widened as tables_column
+        const float mf = wave_maxf((float)r);
+        if (lane == 0) {
+          const double m = (double)mf + 0x1p-23 * fabs((double)mf);
+          U[col * kStretchSlots + j] = ubase ? m - ubase[j] : m;
+        }
+      }
+    }
+  }
+  KT_STAMP(5);
+  if (uqf) {
+    if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
+    const int t = 4 * ((G + 63) / 64) + lane;
+    if (t < kQTiles) a.UQ[col * kQTiles + t] = 0u;
+  }
+  if (dout)
+    for (int k = G + lane; k < a.GS; k += 64) dout[k] = 0.0;
+  if (want_maxi) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const double ov = __shfl_xor(bv, m, 64);
+      const int oi = __shfl_xor(bi, m, 64);
+      if (ov > bv || (ov == bv && oi < bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+    if (lane == 0) a.maxi[col] = (bi == 0x7fffffff) ? 0 : bi;
+  }
+  const unsigned long long anyc = __ballot(clamp);
+  if (lane == 0) a.has_clamp[col] = anyc ? 1 : 0;
+  KT_STAMP(6);
+#if SCDE_KT_STAMP
+  if (lane == 0) atomicAdd(&g_kt_stamp[7], 1ull);
+#endif
+}
+
+__global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TABREG_WPE))) void k_tables_reg(TablesArgs a) {
+  __shared__ double sm[kTabRegRows * kRS];  // mu | p | q | log p | log q | lcfpr | cfp | lcfp | base
+  __shared__ double etab[64];
+  __shared__ double ltab[3][97];
+  __shared__ unsigned suqb[kQTiles];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int GS = a.GS, G = a.G;
+  tables_tabs(etab, ltab);
+  if (a.gate && *a.gate == 0) return;
+  const int4 task = a.tasks[blockIdx.x];
+  const int c = task.x;
+  const int phase = a.phase;
+  if (c < 0) {  // the ELL pad column (phase 2)
+    if (wid == 0) {
+      for (int k = lane; k < GS; k += 64)
+        if (a.D) a.D[a.ncols * GS + k] = 0.0;
+      if (a.U && lane < kStretchSlots) a.U[a.ncols * kStretchSlots + lane] = 0.0;
+      if (a.UQ && lane < kQTiles) a.UQ[a.ncols * kQTiles + lane] = 0u;
+    }
+    return;
+  }
+  const long long co = (long long)c * GS;
+  const int bc = (phase == 2) ? a.base_col[c] : -1;
+  if (bc >= 0 && a.UQ && threadIdx.x < kQTiles) suqb[threadIdx.x] = a.UQ[(long long)bc * kQTiles + threadIdx.x];
+  const double* P = a.pq + 4 * co;
+  for (int k = threadIdx.x; k < kRS; k += 64 * kTabRegWaves) {
+    const bool in = k < G;
+    sm[kRowMu * kRS + k] = in ? a.mu[co + k] : 0.0;
+    sm[kRowP * kRS + k] = in ? P[k] : 0.0;
+    sm[(kRowP + 1) * kRS + k] = in ? P[GS + k] : 0.0;
+    sm[(kRowP + 2) * kRS + k] = in ? P[2 * GS + k] : 0.0;
+    sm[(kRowP + 3) * kRS + k] = in ? P[3 * GS + k] : 0.0;
+    sm[kRowLcfpr * kRS + k] = in ? a.lcfpr[co + k] : 0.0;
+    const double lc = in ? a.lcfp[co + k] : -INFINITY;
+    sm[kRowCfp * kRS + k] = exp(lc);
+    sm[kRowLcfp * kRS + k] = lc;
+    sm[kRowBase * kRS + k] = (in && bc >= 0) ? a.D[(long long)bc * GS + k] : 0.0;
+  }
+  __syncthreads();
+  const LogTab lt{ltab[0], ltab[1], ltab[2]};
+  const int zc = (phase == 2) ? a.zcol[c] : -1;
+  const double theta = a.theta[co];
+  for (int col = task.y + wid; col < task.z; col += kTabRegWaves) {
+    if (col == zc) continue;  // done in phase 1
+    tables_column_reg(a, col, c, phase, sm, bc >= 0, (bc >= 0) ? suqb : nullptr, etab, lt, lane, theta);
   }
 }
 
@@ -2542,11 +2899,25 @@ hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, con
   return hipGetLastError();
 }
 
+#if SCDE_KT_STAMP
+extern "C" int scde_diag_kt_stamps(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kt_stamp), sizeof(g_kt_stamp));
+  if (e == hipSuccess && reset) {
+    static const unsigned long long z[16] = {};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_kt_stamp), z, sizeof(z));
+  }
+  return (int)e;
+}
+#endif
+
 hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long ncols, int ncells,
                              const double* theta, int GS, const double* cellscal, double* colc, hipStream_t s) {
   if (ncols <= 0) return hipSuccess;
+  int* slow = reinterpret_cast<int*>(colc + kColc * ncols);  // colc holds kColc * ncols + 1 doubles
+  hipError_t e = hipMemsetAsync(slow, 0, sizeof(int), s);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_col_consts, dim3(div_up(ncols, 256)), dim3(256), 0, s, ucl, ucl_off, ncols, ncells, theta, GS,
-                     cellscal, colc);
+                     cellscal, colc, slow);
   return hipGetLastError();
 }
 
@@ -2554,6 +2925,19 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   if (a.ncols <= 0 && a.phase != 2) return hipSuccess;
   if (a.phase != 0 && ((!a.D && !a.DQ) || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
   if (a.DQ && (!a.UQ || !a.nanflag || a.G > kTabStagedG)) return hipErrorInvalidValue;
+  if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG && a.const_theta && !a.DQ && a.colc && a.pq &&
+      a.ncols > 0) {
+    // register-row kernel, then the columns it leaves (rare; the launch exits at once unless
+    // k_col_consts flagged one) by the column-per-wave kernel
+    hipLaunchKernelGGL(k_tables_reg, dim3(a.ntasks), dim3(64 * kTabRegWaves), 0, s, a);
+    TablesArgs b = a;
+    b.slow_only = 1;
+    const size_t shm = sizeof(double) * 4 * (size_t)a.GS;
+    if (shm > 64 * 1024) return hipErrorInvalidValue;
+    const long long nblk = std::min<long long>(1024, div_up(div_up(a.ncols, 64), 4));
+    hipLaunchKernelGGL((k_tables<true, false>), dim3(nblk), dim3(256), shm, s, b);
+    return hipGetLastError();
+  }
   if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG) {
     const size_t shm = sizeof(double) * (kTabWaves + 9) * (size_t)a.G;
     const dim3 grid(a.ntasks), block(64 * kTabWaves);
