@@ -724,7 +724,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   }
   // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
   if (G <= 448 && ncols > 0) {
-    constexpr long long kTaskCols = 64;
+    constexpr long long kTaskCols = kTabTaskCols;
     u.tasks_h.clear();
     for (int c = 0; c < C; ++c)
       for (long long b = ucl_off_h[c]; b < ucl_off_h[c + 1]; b += kTaskCols)

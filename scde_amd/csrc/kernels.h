@@ -8,7 +8,10 @@
 #define SCDE_BOOT_ASMLD 1  // k_boot2 column look-ahead issued from asm with explicit vmcnt waits
 #endif
 #ifndef SCDE_TABREG_WPE
-#define SCDE_TABREG_WPE 4  // k_tables_reg occupancy target (waves per SIMD)
+#define SCDE_TABREG_WPE 2  // k_tables_reg occupancy target (waves per SIMD; 4-wave blocks, two per CU)
+#endif
+#ifndef SCDE_TABREG_G401
+#define SCDE_TABREG_G401 1  // k_tables_reg specialised for the default 401-point grid
 #endif
 #ifndef SCDE_TAB_WPE
 #define SCDE_TAB_WPE 4  // k_tables_cell occupancy target (waves per SIMD)
@@ -36,6 +39,9 @@ namespace scde {
 // log X - log n, log(n - X) - log n, dpois_log(x, failure rate), log po, log(1 - po)] with
 // po = size / (size + x) (the count's own grid point), padded to 10 doubles
 constexpr int kColc = 10;
+// columns per task of the cell-staged tables kernels (k_tables_reg stages a task's column
+// constants in LDS: tasks must not exceed this)
+constexpr int kTabTaskCols = 64;
 
 struct TablesArgs {
   const int* ucl;            // flat unique counts, [ncols]

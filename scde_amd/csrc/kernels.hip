@@ -646,7 +646,10 @@ __device__ unsigned long long g_kt_stamp[16];
   } while (0)
 #endif
 constexpr int kTabChunks = kTabStagedG / 64;
-constexpr int kTabRegWaves = 8;
+#ifndef SCDE_TABREG_WAVES
+#define SCDE_TABREG_WAVES 4
+#endif
+constexpr int kTabRegWaves = SCDE_TABREG_WAVES;  // waves per k_tables_reg block (one task each)
 
 template <int CTRL>
 __device__ __forceinline__ float dpp32f(float x) {
@@ -680,15 +683,19 @@ enum { kRowMu = 0, kRowP = 1, kRowLcfpr = 5, kRowCfp = 6, kRowLcfp = 7, kRowBase
 //     in chunks that have such a lane;
 //   - T_k where max(t1, t2) < -665 (e_k below 2^-960, subnormal ranges): the quotient
 //     log(e_k / s) as the reference forms it.
+enum { kBoundNone = 0, kBoundTiles = 1, kBoundStretch = 2 };  // k_tables_reg's bound output
+// GC: the grid length as a compile-time constant (401, the default prior grid), so the
+// chunk masks fold away; 0 = a.G at run time
+template <int BM, int GC>
 __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long col, int c, int phase,
                                                   const double* __restrict__ sm, bool have_base,
                                                   const unsigned* __restrict__ uqb, const double* etab,
-                                                  const LogTab& lt, int lane, double theta) {
-  const int G = a.G;
+                                                  const LogTab& lt, int lane, double theta, const double* cc,
+                                                  double x, double maxcfp, int bc_u) {
+  const int G = GC ? GC : a.G;
 #if SCDE_KT_STAMP
   long long kt0_ = clock64();
 #endif
-  const double* cc = a.colc + col * kColc;
   NbFast nf;
   nf.n = cc[0];
   if (!(nf.n > 0.0)) return;  // the gated k_tables pass takes this column
@@ -702,9 +709,11 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
   const double lpo = cc[8], lqo = cc[9];
   nf.X = theta;
   nf.ok = true;
-  const double x = (double)a.ucl[col];
-  const double maxcfp = a.cellscal[2 * c];
   const double po = theta / (theta + x);  // the count's own grid point
+  if (SCDE_KT_DIAG & 32) {  // timing diagnostic: staging and constants only
+    if (po == 12345.0) a.has_clamp[col] = 1;
+    return;
+  }
   const double* sl = sm + lane;
   KT_STAMP(0);
   double v[kTabChunks];
@@ -766,6 +775,10 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
     }
   }
   KT_STAMP(1);
+  if (SCDE_KT_DIAG & 16) {  // timing diagnostic: loop 1 only
+    if (lmax == 12345.0) a.has_clamp[col] = 1;
+    return;
+  }
   double maxp = wave_allreduce<true>(lmax);
   if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
   KT_STAMP(2);
@@ -793,10 +806,8 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
   KT_STAMP(4);
   double* out = a.T ? a.T + col * a.GS : nullptr;
   double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
-  const int bc_u = (phase == 2) ? a.base_col[c] : -1;
-  double* const U = a.U;
-  const double* ubase = (U && bc_u >= 0) ? U + (long long)bc_u * kStretchSlots : nullptr;
-  const bool uqf = a.UQ && phase;
+  const double minlp = a.minlogprob;
+  unsigned uqv = 0;  // lane t < 32: tile t's bound (BM == kBoundTiles)
 #pragma unroll
   for (int j = 0; j < kTabChunks; ++j) {
     if (64 * j < G) {
@@ -816,48 +827,48 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
         bv = r;
         bi = k;
       }
-      if (r < a.minlogprob) {
-        r = a.minlogprob;
-        clamp = clamp || in;
-      }
-      if (in) {
-        if (SCDE_KT_DIAG & 8) {  // timing diagnostic: no stores
-          if (r == 12345.0) dout[k] = r;
-        } else {
-          if (out) out[k] = r;
-          if (dout) dout[k] = have_base ? r - sl[kRowBase * kRS + 64 * j] : r;
-        }
-      }
+      const bool cl = r < minlp;
+      r = cl ? minlp : r;
+      clamp = clamp || (cl && in);
       nanq = nanq || (in && r != r);
-      if (!in) r = -INFINITY;
-      if (uqf) {  // this chunk's four 16-point tile maxima (as tables_column)
-        int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
-        const int t = 4 * j + (lane >> 4);
-        if ((lane & 15) == 0) {
-          if (16 * t >= G)
-            u = 0;
-          else if (bc_u >= 0)
-            u -= unpacku(uqb ? uqb[t] : a.UQ[(long long)bc_u * kQTiles + t]);
-          a.UQ[col * kQTiles + t] = packu(u);
-        }
+      // unconditional stores: lanes past the grid write the pad zeros (k < GS always)
+      if (!(SCDE_KT_DIAG & 8)) {
+        if (out) out[k] = in ? r : 0.0;
+        if (dout) dout[k] = in ? (have_base ? r - sl[kRowBase * kRS + 64 * j] : r) : 0.0;
+      } else if (r == 12345.0) {
+        dout[k] = r;
       }
-      if (U) {  // the stretch maximum (64 points = this chunk), f32 widened as tables_column
+      r = in ? r : -INFINITY;
+      if (BM == kBoundTiles) {
+        // this chunk's four 16-point tile maxima (one row each, rounded up to 2^-8, floor
+        // -2^29); lanes 4j..4j+3 collect them from rows 0..3 (lane 16 r)
+        const int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
+        const int g = __builtin_amdgcn_ds_bpermute(((lane - 4 * j) & 3) << 6, u);
+        uqv = ((lane >> 2) == j) ? (unsigned)g : uqv;
+      }
+      if (BM == kBoundStretch) {  // the stretch maximum (64 points = this chunk), f32 widened
         const float mf = wave_maxf((float)r);
         if (lane == 0) {
           const double m = (double)mf + 0x1p-23 * fabs((double)mf);
-          U[col * kStretchSlots + j] = ubase ? m - ubase[j] : m;
+          a.U[col * kStretchSlots + j] = (bc_u >= 0) ? m - a.U[(long long)bc_u * kStretchSlots + j] : m;
         }
       }
     }
   }
   KT_STAMP(5);
-  if (uqf) {
+  if (BM == kBoundTiles) {
     if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
-    const int t = 4 * ((G + 63) / 64) + lane;
-    if (t < kQTiles) a.UQ[col * kQTiles + t] = 0u;
+    if (lane < kQTiles) {
+      int u = (int)uqv;
+      if (16 * lane >= G)
+        u = 0;
+      else if (bc_u >= 0)
+        u -= unpacku(uqb[lane]);
+      a.UQ[col * kQTiles + lane] = packu(u);
+    }
   }
   if (dout)
-    for (int k = G + lane; k < a.GS; k += 64) dout[k] = 0.0;
+    for (int k = 64 * ((G + 63) / 64) + lane; k < a.GS; k += 64) dout[k] = 0.0;
   if (want_maxi) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
@@ -878,18 +889,27 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 #endif
 }
 
+template <int BM, int GC>
 __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TABREG_WPE))) void k_tables_reg(TablesArgs a) {
   __shared__ double sm[kTabRegRows * kRS];  // mu | p | q | log p | log q | lcfpr | cfp | lcfp | base
   __shared__ double etab[64];
   __shared__ double ltab[3][97];
   __shared__ unsigned suqb[kQTiles];
+  __shared__ double scc[kTabTaskCols * kColc];  // the task's column constants and counts
+  __shared__ int sx[kTabTaskCols];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int GS = a.GS, G = a.G;
+  const int GS = a.GS, G = GC ? GC : a.G;
   tables_tabs(etab, ltab);
   if (a.gate && *a.gate == 0) return;
   const int4 task = a.tasks[blockIdx.x];
   const int c = task.x;
   const int phase = a.phase;
+  if (c >= 0) {
+    // one latency per task for every column's constants (not one per column and wave)
+    const int ncc = (task.z - task.y) * kColc;
+    for (int t = threadIdx.x; t < ncc; t += 64 * kTabRegWaves) scc[t] = a.colc[(long long)task.y * kColc + t];
+    if (threadIdx.x < task.z - task.y) sx[threadIdx.x] = a.ucl[task.y + threadIdx.x];
+  }
   if (c < 0) {  // the ELL pad column (phase 2)
     if (wid == 0) {
       for (int k = lane; k < GS; k += 64)
@@ -920,9 +940,12 @@ __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
   const int zc = (phase == 2) ? a.zcol[c] : -1;
   const double theta = a.theta[co];
+  const double maxcfp = a.cellscal[2 * c];
   for (int col = task.y + wid; col < task.z; col += kTabRegWaves) {
     if (col == zc) continue;  // done in phase 1
-    tables_column_reg(a, col, c, phase, sm, bc >= 0, (bc >= 0) ? suqb : nullptr, etab, lt, lane, theta);
+    const int i = col - task.y;
+    tables_column_reg<BM, GC>(a, col, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta,
+                      scc + i * kColc, (double)sx[i], maxcfp, bc);
   }
 }
 
@@ -2929,7 +2952,23 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
       a.ncols > 0) {
     // register-row kernel, then the columns it leaves (rare; the launch exits at once unless
     // k_col_consts flagged one) by the column-per-wave kernel
-    hipLaunchKernelGGL(k_tables_reg, dim3(a.ntasks), dim3(64 * kTabRegWaves), 0, s, a);
+    const dim3 grid(a.ntasks), block(64 * kTabRegWaves);
+    const int bm = (a.UQ && a.phase == 2) ? kBoundTiles : (a.U && a.phase == 2) ? kBoundStretch : kBoundNone;
+    if (SCDE_TABREG_G401 && a.G == 401) {
+      if (bm == kBoundTiles)
+        hipLaunchKernelGGL((k_tables_reg<kBoundTiles, 401>), grid, block, 0, s, a);
+      else if (bm == kBoundStretch)
+        hipLaunchKernelGGL((k_tables_reg<kBoundStretch, 401>), grid, block, 0, s, a);
+      else
+        hipLaunchKernelGGL((k_tables_reg<kBoundNone, 401>), grid, block, 0, s, a);
+    } else {
+      if (bm == kBoundTiles)
+        hipLaunchKernelGGL((k_tables_reg<kBoundTiles, 0>), grid, block, 0, s, a);
+      else if (bm == kBoundStretch)
+        hipLaunchKernelGGL((k_tables_reg<kBoundStretch, 0>), grid, block, 0, s, a);
+      else
+        hipLaunchKernelGGL((k_tables_reg<kBoundNone, 0>), grid, block, 0, s, a);
+    }
     TablesArgs b = a;
     b.slow_only = 1;
     const size_t shm = sizeof(double) * 4 * (size_t)a.GS;

@@ -69,3 +69,13 @@ def test_lookahead_loops_do_not_touch_scratch(isa, kernel):
         for a, b in spans:
             bad = [ln.strip() for ln in lines[a:b + 1] if "scratch_" in ln or "buffer_store" in ln]
             assert not bad, f"{sym}: scratch access inside a loop: {bad[:3]}"
+
+
+def test_tables_register_row_does_not_spill(isa):
+    """k_tables_reg keeps a column's 401 grid values in VGPRs; builds that spilled them (or
+    the hoisted polynomial constants) to scratch ran 15-40 % slower."""
+    bodies = _bodies(isa, "k_tables_reg")
+    assert len(bodies) == 6, [s for s, _ in bodies]
+    for sym, body in bodies:
+        bad = [ln.strip() for ln in body.split("\n") if "scratch_" in ln]
+        assert not bad, f"{sym}: scratch access: {bad[:3]}"
