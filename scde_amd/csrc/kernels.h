@@ -41,7 +41,10 @@ namespace scde {
 constexpr int kColc = 10;
 // columns per task of the cell-staged tables kernels (k_tables_reg stages a task's column
 // constants in LDS: tasks must not exceed this)
-constexpr int kTabTaskCols = 64;
+#ifndef SCDE_TAB_TASK_COLS
+#define SCDE_TAB_TASK_COLS 64
+#endif
+constexpr int kTabTaskCols = SCDE_TAB_TASK_COLS;
 
 struct TablesArgs {
   const int* ucl;            // flat unique counts, [ncols]

@@ -980,19 +980,22 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
 // genes: each 64-cell chunk of uci (genes fastest, as R lays out the count matrix) is read
 // coalesced into an LDS tile (stride 65 against bank conflicts), then each wave compacts 16
 // genes' rows from it with ballots.
-__global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
+// 16 waves per 64-gene block (4 genes each): the grid has only ngenes / 64 blocks
+constexpr int kEllWaves = 16;
+__global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
                                              int ncells, const long long* __restrict__ ucl_off,
                                              const int* __restrict__ base_col, int stride, int pad_col,
                                              int padto, int2* __restrict__ ent, int* __restrict__ nnz) {
   __shared__ int tile[64][65];  // [cell][gene]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g0 = blockIdx.x * 64;
-  int n[16];
+  constexpr int GPW = 64 / kEllWaves;  // genes per wave
+  int n[GPW];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) n[i] = 0;
+  for (int i = 0; i < GPW; ++i) n[i] = 0;
   for (int c0 = 0; c0 < ncells; c0 += 64) {
     __syncthreads();
-    for (int j = wid; j < 64; j += 4) {  // row j of the tile: cell c0 + j, lanes over genes
+    for (int j = wid; j < 64; j += kEllWaves) {  // row j of the tile: cell c0 + j, lanes over genes
       const int c = c0 + j, g = g0 + lane;
       tile[j][lane] = (c < ncells && g < ngenes) ? uci[(long long)g + ld_uci * c] : 0;
     }
@@ -1005,8 +1008,8 @@ __global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long l
       bc = base_col[c];
     }
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int gl = wid * 16 + i, g = g0 + gl;
+    for (int i = 0; i < GPW; ++i) {
+      const int gl = wid * GPW + i, g = g0 + gl;
       if (g >= ngenes) break;
       int col = -1;
       bool keep = false;
@@ -1023,8 +1026,8 @@ __global__ __launch_bounds__(256) void k_ell(const int* __restrict__ uci, long l
   // padto 64: k_bootq reads whole 64-entry steps; k_boot_tiles' FP64 loop also looks one
   // 4-entry batch past its last batch, hence the extra 8
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int g = g0 + wid * 16 + i;
+  for (int i = 0; i < GPW; ++i) {
+    const int g = g0 + wid * GPW + i;
     if (g >= ngenes) break;
     const int nn = n[i];
     if (lane == 0) nnz[g] = nn;
@@ -3025,7 +3028,7 @@ hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, 
   if (ngenes <= 0) return hipSuccess;
   if (padto == 64 ? stride < ((ncells + 63) & ~63) + 8 || stride < 72 : stride < ((ncells + 7) & ~7) + 8)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 64)), dim3(256), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
+  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 64)), dim3(64 * kEllWaves), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
                      base_col, stride, pad_col, padto, ent, nnz);
   return hipGetLastError();
 }
