@@ -2368,10 +2368,22 @@ __global__ void k_cell_minmax(const int* __restrict__ counts, long long ld, long
   const int c = blockIdx.x;
   const int* col = counts + (long long)cellidx[c] * ld + g0;
   int mx = 0, mn = 0x7fffffff;
-  for (int g = threadIdx.x; g < ngenes; g += blockDim.x) {
-    const int x = col[g];
-    mx = max(mx, x);
-    mn = min(mn, x);
+  // 16-byte loads over the aligned middle of the column (one count matrix pass, HBM-bound)
+  const int head = (int)min<long long>(ngenes, (4 - (((uintptr_t)col >> 2) & 3)) & 3);
+  const int nv = (ngenes - head) >> 2;
+  const int4* col4 = reinterpret_cast<const int4*>(col + head);
+  for (int i = threadIdx.x; i < nv; i += blockDim.x) {
+    const int4 x = col4[i];
+    mx = max(mx, max(max(x.x, x.y), max(x.z, x.w)));
+    mn = min(mn, min(min(x.x, x.y), min(x.z, x.w)));
+  }
+  for (int g = threadIdx.x; g < head; g += blockDim.x) {
+    mx = max(mx, col[g]);
+    mn = min(mn, col[g]);
+  }
+  for (int g = head + 4 * nv + threadIdx.x; g < ngenes; g += blockDim.x) {
+    mx = max(mx, col[g]);
+    mn = min(mn, col[g]);
   }
   for (int m = 32; m >= 1; m >>= 1) {
     mx = max(mx, __shfl_xor(mx, m, 64));
