@@ -5,12 +5,12 @@
  * kernel behind bwpca() / pagoda.pathway.wPCA().  Imported only by tests/ and
  * bench.py's cpu_baseline leg, never by the product (scde_amd/).
  *
- *   o_baileyWPCA          src/bwpca.cpp:59-182   (baileyWPCA: smoothing coefficients,
+ *   o_baileyWPCA          src/bwpca.cpp:59-171   (baileyWPCA: smoothing coefficients,
  *                                                 variance explained, scoreweights,
  *                                                 internal shuffles)
- *   wpca_round            src/bwpca.cpp:186-322  (baileyWPCAround: random orthonormal
+ *   wpca_round            src/bwpca.cpp:173-322  (baileyWPCAround: random orthonormal
  *                                                 starts, EM iterations, best model)
- *   o_shuffle_perms       src/bwpca.cpp:41-57    (set_random_matrices: libstdc++
+ *   o_shuffle_perms       src/bwpca.cpp:40-57    (set_random_matrices: libstdc++
  *                                                 std::random_shuffle over rand())
  *   o_r_set_seed/o_r_unif_rand/o_r_sample        R's RNG.c Mersenne-Twister, set.seed()
  *                                                 scrambling, unif_rand() fixup, and
@@ -25,7 +25,7 @@
  *   by rounding only.
  *
  * The random start: the reference calls arma::randu<arma::mat>(d, npcs) after
- * arma_rng::set_seed(seed + nstart) (bwpca.cpp:197-198).  Under RcppArmadillo that
+ * arma_rng::set_seed(seed + nstart) (bwpca.cpp:184-185).  Under RcppArmadillo that
  * draws from R's unif_rand() stream (set_seed is a no-op there), so the starts are the
  * caller's R RNG stream; this restatement takes them as an input array of uniforms in
  * draw order, exactly what the R-side shim passes.
@@ -128,7 +128,7 @@ void o_r_sample(uint32_t* st, int n, int k, int* out) {
     free(x);
 }
 
-/* set_random_matrices (bwpca.cpp:41-57): ind = 0..n-1 once per call; per column
+/* set_random_matrices (bwpca.cpp:40-57): ind = 0..n-1 once per call; per column
  * std::random_shuffle(ind) (libstdc++: for i in 1..n-1, j = rand() % (i+1), swap),
  * continuing from the previous column's order.  perms: nshuffles x d x n. */
 void o_shuffle_perms(unsigned int seed, int nshuffles, int d, int n, int* perms) {
@@ -347,7 +347,7 @@ static int o_smooth_coef(int smooth, double* sc) {
 }
 
 /* ------------------------------------------------------------------ */
-/* baileyWPCAround (src/bwpca.cpp:186-322)                              */
+/* baileyWPCAround (src/bwpca.cpp:173-322)                              */
 /* ------------------------------------------------------------------ */
 /* starts: nstarts x (d x K) uniforms, consumed in order.  Outputs bestcoef (n x K),
  * besteigenv (d x K).  it_out (optional): iterations run per start. */
@@ -376,7 +376,7 @@ static void wpca_round(const double* m, const double* mw, int n, int d, int nsta
         while (ii < maxiter) {
             int j, g, k, kx;
             double npres;
-            /* coefficients: per observation, weighted least squares (bwpca.cpp:221-238) */
+            /* coefficients: per observation, weighted least squares (bwpca.cpp:205-221) */
             for (j = 0; j < n; j++) {
                 double A[64], b[8];
                 for (k = 0; k < K; k++) {
@@ -393,7 +393,7 @@ static void wpca_round(const double* m, const double* mw, int n, int d, int nsta
                 o_solve_small(A, b, K);
                 for (k = 0; k < K; k++) coef[j + (long)k * n] = b[k];
             }
-            /* eigenvectors (bwpca.cpp:243-267) */
+            /* eigenvectors (bwpca.cpp:226-250) */
             memcpy(dat, m, sizeof(double) * nd);
             for (k = 0; k < K; k++) {
                 for (g = 0; g < d; g++) {
@@ -425,7 +425,7 @@ static void wpca_round(const double* m, const double* mw, int n, int d, int nsta
                     for (g = 0; g < d; g++)
                         for (j = 0; j < n; j++) dat[j + (long)g * n] -= coef[j + (long)k * n] * E[g + k * d];
             }
-            /* renormalise and re-orthogonalise (bwpca.cpp:270-277) */
+            /* renormalise and re-orthogonalise (bwpca.cpp:253-261) */
             {
                 const double nr = sqrt(o_dot(E, E, d));
                 for (g = 0; g < d; g++) E[g] /= nr;
@@ -439,7 +439,7 @@ static void wpca_round(const double* m, const double* mw, int n, int d, int nsta
                 nr = sqrt(o_dot(E + k * d, E + k * d, d));
                 for (g = 0; g < d; g++) E[g + k * d] /= nr;
             }
-            /* model fit (bwpca.cpp:283-294) */
+            /* model fit (bwpca.cpp:266-277) */
             for (g = 0; g < d; g++)
                 for (j = 0; j < n; j++) {
                     double mo = 0, dl;
@@ -484,7 +484,7 @@ static void wpca_round(const double* m, const double* mw, int n, int d, int nsta
 }
 
 /* ------------------------------------------------------------------ */
-/* baileyWPCA (src/bwpca.cpp:59-182)                                    */
+/* baileyWPCA (src/bwpca.cpp:59-171)                                    */
 /* ------------------------------------------------------------------ */
 /* m, mw: n x d.  starts: (1 + nshuffles) x nstarts x (d x K') uniforms, K' = min(npcs, d).
  * perms: nshuffles x d x n (see o_shuffle_perms) or NULL when nshuffles == 0.
