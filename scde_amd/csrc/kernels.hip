@@ -1623,16 +1623,18 @@ constexpr double kBootExpCut = -50.0;  // k_boot2 softmax terms below e^-50 are 
 // of a gene are placed 8 blocks apart (same XCD under round-robin dispatch) so they
 // share the gene's columns in L2; each writes a partial jp row, summed in slab order
 // by k_sum_partials.
+// One (gene g, slab p) per block; k_boot2 maps the grid onto items, k_boot2_list walks the
+// compacted item list k_boot_tiles leaves behind.
 template <int NB>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ? SCDE_BOOT_WPE : 1))) void k_boot2(const double* __restrict__ D, const int2* __restrict__ ent,
-                                                const int* __restrict__ nnz, int ent_stride,
-                                                const double* __restrict__ Wt, int Bp, int ncells,
-                                                const int* __restrict__ wset, const double* __restrict__ Z, int G,
-                                                int GS, int P, int nboot, double norm_mult, double degen_thresh,
-                                                double* __restrict__ part, long long part_stride,
-                                                int* __restrict__ degen, int ngenes,
-                                                const int* __restrict__ smask, const double* __restrict__ sub,
-                                                int* __restrict__ redo, int redo_pass) {
+__device__ __forceinline__ void boot2_slab(const double* __restrict__ D, const int2* __restrict__ ent,
+                                           const int* __restrict__ nnz, int ent_stride,
+                                           const double* __restrict__ Wt, int Bp, int ncells,
+                                           const int* __restrict__ wset, const double* __restrict__ Z, int G,
+                                           int GS, int P, int nboot, double norm_mult, double degen_thresh,
+                                           double* __restrict__ part, long long part_stride,
+                                           int* __restrict__ degen, int ngenes,
+                                           const int* __restrict__ smask, const double* __restrict__ sub,
+                                           int* __restrict__ redo, int redo_pass, int g, int p) {
   static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
   constexpr int diag = SCDE_BOOT_DIAG;  // timing-only builds (tools/); 0 in production
   __shared__ double red[16 * 32];
@@ -1641,10 +1643,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
   __shared__ double etab[64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
   const bool live = tid < G;
-  const int within = blockIdx.x % (8 * P);
-  const int p = within >> 3;
-  const int g = (blockIdx.x / (8 * P)) * 8 + (within & 7);
-  if (g >= ngenes) return;
   const int b0 = p * NB;
   const int n = nnz[g];
   const int2* __restrict__ E = ent + (long long)g * ent_stride;
@@ -1862,6 +1860,42 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
   if (live) part[(long long)p * part_stride + (long long)g * GS + tid] = jpv;
 }
 
+template <int NB>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ? SCDE_BOOT_WPE : 1))) void k_boot2(
+    const double* __restrict__ D, const int2* __restrict__ ent,
+    const int* __restrict__ nnz, int ent_stride,
+    const double* __restrict__ Wt, int Bp, int ncells,
+    const int* __restrict__ wset, const double* __restrict__ Z, int G,
+    int GS, int P, int nboot, double norm_mult, double degen_thresh,
+    double* __restrict__ part, long long part_stride,
+    int* __restrict__ degen, int ngenes,
+    const int* __restrict__ smask, const double* __restrict__ sub,
+    int* __restrict__ redo, int redo_pass) {
+  const int within = blockIdx.x % (8 * P);
+  const int p = within >> 3;
+  const int g = (blockIdx.x / (8 * P)) * 8 + (within & 7);
+  if (g >= ngenes) return;
+  boot2_slab<NB>(D, ent, nnz, ent_stride, Wt, Bp, ncells, wset, Z, G, GS, P, nboot, norm_mult, degen_thresh, part, part_stride, degen, ngenes, smask, sub, redo, redo_pass, g, p);
+}
+
+// k_boot_tiles' fallback: the (gene, slab) items it could not finish, appended to
+// list[0 .. list[nitems]) (whole slabs, no skipping).  A small grid walks the list, so the
+// usual empty fallback costs one short launch, not a block per slab.
+template <int NB>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ? SCDE_BOOT_WPE : 1))) void k_boot2_list(
+    const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
+    const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
+    int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
+    long long part_stride, int* __restrict__ degen, int ngenes, const int* __restrict__ list, long long nitems) {
+  const int cnt = __builtin_amdgcn_readfirstlane(list[nitems]);
+  for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
+    const int item = __builtin_amdgcn_readfirstlane(list[it]);
+    const int g = item / P, p = item - g * P;
+    boot2_slab<NB>(D, ent, nnz, ent_stride, Wt, Bp, ncells, wset, Z, G, GS, P, nboot, norm_mult, degen_thresh, part, part_stride, degen, ngenes, nullptr, nullptr, nullptr, 0, g, p);
+    __syncthreads();  // the next item reuses the block's LDS
+  }
+}
+
 // ------------------------------------------------------------------ tile bootstrap
 // k_boot_tiles: k_boot2's FP64 bootstrap computed only where it matters, on 16-point grid
 // tiles chosen per (gene, boot slab) from exact integer bounds.  One wave per (gene, slab);
@@ -1922,7 +1956,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   const int g = order ? order[gi] : gi;
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
     if (lane == 0) {
-      redo[(long long)g * P + p] = 1;
+      redo[atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;  // k_boot2_list's item list
       pmask[(long long)g * P + p] = ~0u;  // k_boot2 writes the whole row
     }
     return;
@@ -2111,7 +2145,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   if (cnt > 0) {
     if (cnt > 4 || maxgroups < 2) {  // the whole slab goes to k_boot2's redo launch
       if (lane == 0) {
-        redo[(long long)g * P + p] = 1;
+        redo[atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
         pmask[(long long)g * P + p] = ~0u;
         if (stats) {
           atomicAdd(&stats[3], 1);
@@ -3221,13 +3255,14 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if (e != hipSuccess) return e;
   // slabs the tile kernel left (more tiles than its registers hold, or NaN tables): k_boot2,
   // whole slab, same sums
+  // (the list: redo[0 .. redo[items]), appended by k_boot_tiles; a grid of 512 blocks walks it)
   const int block2 = ((a.G + 63) / 64) * 64;
-  const int grid2 = (a.ngenes + 7) / 8 * 8 * P;
+  const int grid2 = (int)std::min<long long>(items, 512);
 #define SCDE_B2R(NBV)                                                                                             \
   case NBV:                                                                                                        \
-    hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid2), dim3(block2), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
-                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
-                       a.part_stride, a.degen, a.ngenes, nullptr, nullptr, a.redo, 1);                          \
+    hipLaunchKernelGGL(k_boot2_list<NBV>, dim3(grid2), dim3(block2), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, \
+                       a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,   \
+                       a.part_stride, a.degen, a.ngenes, a.redo, items);                                        \
     break;
   switch (a.nb) {
     SCDE_B2R(4) SCDE_B2R(8) SCDE_B2R(12) SCDE_B2R(16) SCDE_B2R(20)
