@@ -1881,8 +1881,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
 // k_boot_tiles' fallback: the (gene, slab) items it could not finish, appended to
 // list[0 .. list[nitems]) (whole slabs, no skipping).  A small grid walks the list, so the
 // usual empty fallback costs one short launch, not a block per slab.
+// (a rare path: no occupancy target, so the item loop never spills around the asm look-ahead;
+// the tile path has G <= 448, blocks of at most 448 threads)
 template <int NB>
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ? SCDE_BOOT_WPE : 1))) void k_boot2_list(
+__global__ __launch_bounds__(512) void k_boot2_list(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
     const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,

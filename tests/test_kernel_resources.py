@@ -3,8 +3,8 @@ waited with an explicit vmcnt) is only correct while the compiler keeps the load
 in place between the asm load and its wait: a spill or register copy in between reads the
 register before the data lands, or reuses it while the load is still in flight.  Builds that
 spill inside those loops have faulted on the GPU.  This test compiles
-kernels.hip for gfx950 (device only, as the library is built) and checks that no loop of the
-two kernels touches scratch memory.
+kernels.hip for gfx950 (device only, as the library is built) and checks that no loop of those
+kernels (and of k_boot2_list, whose item loop holds k_boot2's body) touches scratch memory.
 """
 import os
 import re
@@ -59,7 +59,7 @@ def _loop_spans(body):
     return lines, spans
 
 
-@pytest.mark.parametrize("kernel", ["k_boot2ILi20E", "k_boot_tilesILi20E"])
+@pytest.mark.parametrize("kernel", ["k_boot2ILi20E", "k_boot_tilesILi20E", "k_boot2_listILi20E"])
 def test_lookahead_loops_do_not_touch_scratch(isa, kernel):
     bodies = _bodies(isa, kernel)
     assert bodies, f"{kernel} not found in the ISA"
