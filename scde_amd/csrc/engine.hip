@@ -167,6 +167,7 @@ struct scde_ctx {
   // the first group's kernels start before the second group's columns have arrived
   hipStream_t copy_stream = nullptr;
   hipEvent_t up_ev[2] = {nullptr, nullptr};
+  hipEvent_t uq_ev = nullptr;  // the second group's unique sets (built on copy_stream) are ready
   // workspace
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, pq, colc, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
       ubound, zubound, smask, subuf, sredo,
@@ -289,6 +290,7 @@ struct scde_ctx {
     for (auto e : evpool) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (uq_ev) (void)hipEventDestroy(uq_ev);
     for (auto& e : up_ev)
       if (e) (void)hipEventDestroy(e);
   }
@@ -1691,7 +1693,21 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       ctx->us[gi].ready = false;
       const PostSpec* sp[1] = {&specs[gi]};
       UniqueSet* up[1] = {&ctx->us[gi]};
-      RCHK(build_unique_sets(ctx, sp, up, 1));
+      if (k == 0) {
+        RCHK(build_unique_sets(ctx, sp, up, 1));
+      } else {
+        // the second group's unique sets on the copy stream, behind its own upload: their two
+        // host syncs then wait for its small kernels, not for the first group's posterior
+        // still running on the main stream, and its tables queue before that posterior ends
+        if (!ctx->uq_ev) HCHK(hipEventCreateWithFlags(&ctx->uq_ev, hipEventDisableTiming));
+        const hipStream_t main = ctx->stream;
+        ctx->stream = ctx->copy_stream;
+        const int rc = build_unique_sets(ctx, sp, up, 1);
+        ctx->stream = main;
+        RCHK(rc);
+        HCHK(hipEventRecord(ctx->uq_ev, ctx->copy_stream));
+        HCHK(hipStreamWaitEvent(ctx->stream, ctx->uq_ev, 0));
+      }
       RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
     }
   } else {

@@ -93,3 +93,43 @@ def test_config5_ms1_kernel_3000_cells():
     np.testing.assert_allclose(got["var"], ref["var"], rtol=1e-8)
     assert got["totvar"] == pytest.approx(ref["totvar"], rel=1e-12)
     np.testing.assert_allclose(got["randvar"], ref["randvar"], rtol=1e-8)
+
+
+def test_config3_host_pipeline_equals_device_resident(api):
+    """Full config 3 (20,000 x 1,000: an 80 MB matrix, above the 48 MB pipelining threshold):
+    scde_expression_difference_host uploads the counts in two column ranges and builds the
+    second group's unique sets on its copy stream beside the first group's posterior
+    (engine.hip de_run); the table must equal, bit for bit, the device-resident entry on the
+    same counts (one stream, no pipelining)."""
+    import ctypes
+    import bench
+    from scde_amd._lib import DEParams, check, lib
+    from scde_amd.models import model_matrix
+    from scde_amd.prior import expression_prior
+    cfg = bench.CONFIGS["3"]
+    models, counts, groups = bench.synthetic(cfg["seed"], cfg["genes"], cfg["cells"], two_groups=True)
+    prior = expression_prior(models, counts, length_out=bench.LENGTH_OUT)
+    mat = np.asfortranarray(counts, dtype=np.int32)
+    N, C = mat.shape
+    assert mat.nbytes >= 48 << 20
+    codes = np.ascontiguousarray(np.asarray(groups), np.int32)
+    mm, lt, sq = model_matrix(models)
+    px = np.ascontiguousarray(prior["x"], np.float64)
+    py = np.ascontiguousarray(prior["y"], np.float64)
+    ctx = api.default_context()
+    params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, len(px), 100, 1,
+                      0, N, 0.0, api.get_rand_kind(), 1)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    host = np.zeros((N, 6), order="F")
+    for _ in range(2):  # the second call reuses the context's buffers and streams
+        check(lib().scde_expression_difference_host(ctx.handle, vp(mat), N, N, ctypes.byref(params), vp(host), None,
+                                                    None, None))
+    dc = api.DeviceCounts(ctx, mat)
+    try:
+        dev = np.zeros((N, 6), order="F")
+        check(lib().scde_expression_difference_dev(ctx.handle, dc.ptr, N, N, ctypes.byref(params), vp(dev), None,
+                                                   None, None))
+    finally:
+        dc.free()
+    assert np.isfinite(host[:, :4]).all()
+    np.testing.assert_array_equal(host, dev)
