@@ -168,6 +168,13 @@ struct scde_ctx {
   hipStream_t copy_stream = nullptr;
   hipEvent_t up_ev[2] = {nullptr, nullptr};
   hipEvent_t uq_ev = nullptr;  // the second group's unique sets (built on copy_stream) are ready
+  // Pinned staging arena for the small per-call transfers (cell lists, offsets, draws,
+  // multiplicities, tasks; the unique builder's size read-backs).  A pageable copy is staged
+  // by the runtime and costs 20-40 us of host latency each; from pinned memory it is a plain
+  // asynchronous DMA.  Bump-allocated; when full, the device is synchronised (every staged
+  // copy has landed) and allocation restarts at 0.
+  char* pin = nullptr;
+  size_t pin_off = 0;
   // workspace
   Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, pq, colc, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
       ubound, zubound, smask, subuf, sredo,
@@ -213,6 +220,7 @@ struct scde_ctx {
     Buf cellidx, cmax, cmin, woff, bits, rank, nuniq, ucl, ucl_off, uci;
     std::vector<int> cmax_h, cmin_h, nuniq_h;
     std::vector<long long> woff_h, ucl_off_h;
+    const int* pin_in = nullptr;  // pinned landing area of the phase's device -> host copy
     std::vector<int4> tasks_h;  // cell-staged tables tasks (k_tables_cell)
     Buf tasks;
     bool ready = false;
@@ -291,6 +299,7 @@ struct scde_ctx {
     if (stream) (void)hipStreamDestroy(stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (uq_ev) (void)hipEventDestroy(uq_ev);
+    if (pin) (void)hipHostFree(pin);
     for (auto& e : up_ev)
       if (e) (void)hipEventDestroy(e);
   }
@@ -335,9 +344,39 @@ struct PostSpec {
   int rand_kind = 0;
 };
 
+constexpr size_t kPinCap = size_t(16) << 20;  // the arena
+constexpr size_t kPinMax = size_t(2) << 20;   // larger transfers go direct
+
+// `bytes` of the context's pinned arena (nullptr: too large, or the pinned allocation failed)
+char* pin_alloc(scde_ctx* cx, size_t bytes) {
+  if (bytes > kPinMax) return nullptr;
+  if (!cx->pin) {
+    if (hipHostMalloc(reinterpret_cast<void**>(&cx->pin), kPinCap, hipHostMallocDefault) != hipSuccess) {
+      cx->pin = nullptr;
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    cx->pin_off = 0;
+  }
+  size_t off = (cx->pin_off + 255) & ~size_t(255);
+  if (off + bytes > kPinCap) {
+    // reuse from the start: every copy staged so far (on any of the context's streams) must
+    // have landed first
+    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+    off = 0;
+  }
+  cx->pin_off = off + bytes;
+  return cx->pin + off;
+}
+
 int upload(scde_ctx* cx, Buf& b, const void* src, size_t bytes) {
   HCHK(b.ensure(bytes));
-  if (bytes) HCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, cx->stream));
+  if (!bytes) return SCDE_OK;
+  if (char* h = pin_alloc(cx, bytes)) {
+    std::memcpy(h, src, bytes);
+    src = h;
+  }
+  HCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, cx->stream));
   return SCDE_OK;
 }
 
@@ -358,14 +397,20 @@ int unique_phase1(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   HCHK(launch_cell_minmax(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.cmax.as<int>(), u.cmin.as<int>(), st));
   u.cmax_h.assign(C, 0);
   u.cmin_h.assign(C, 0);
-  HCHK(hipMemcpyAsync(u.cmax_h.data(), u.cmax.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
-  HCHK(hipMemcpyAsync(u.cmin_h.data(), u.cmin.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  int* h = reinterpret_cast<int*>(pin_alloc(cx, sizeof(int) * 2 * (size_t)C));
+  u.pin_in = h;
+  HCHK(hipMemcpyAsync(h ? h : u.cmax_h.data(), u.cmax.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  HCHK(hipMemcpyAsync(h ? h + C : u.cmin_h.data(), u.cmin.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
   return SCDE_OK;
 }
 
 int unique_phase2(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, N = s.ngenes;
   hipStream_t st = cx->stream;
+  if (u.pin_in) {  // landed (the caller synchronised)
+    std::copy(u.pin_in, u.pin_in + C, u.cmax_h.begin());
+    std::copy(u.pin_in + C, u.pin_in + 2 * (size_t)C, u.cmin_h.begin());
+  }
   u.woff_h.assign(C + 1, 0);
   for (int c = 0; c < C; ++c) {
     if (N > 0 && u.cmin_h[c] < 0) return fail(SCDE_EARG, "negative count in cell %d", c);
@@ -381,13 +426,16 @@ int unique_phase2(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   HCHK(launch_rank(u.bits.as<unsigned long long>(), u.woff.as<long long>(), C, u.rank.as<int>(),
                    u.nuniq.as<int>(), st));
   u.nuniq_h.assign(C, 0);
-  HCHK(hipMemcpyAsync(u.nuniq_h.data(), u.nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  int* h = reinterpret_cast<int*>(pin_alloc(cx, sizeof(int) * (size_t)C));
+  u.pin_in = h;
+  HCHK(hipMemcpyAsync(h ? h : u.nuniq_h.data(), u.nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
   return SCDE_OK;
 }
 
 int unique_phase3(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, N = s.ngenes;
   hipStream_t st = cx->stream;
+  if (u.pin_in) std::copy(u.pin_in, u.pin_in + C, u.nuniq_h.begin());
   u.ucl_off_h.assign(C + 1, 0);
   for (int c = 0; c < C; ++c) u.ucl_off_h[c + 1] = u.ucl_off_h[c] + u.nuniq_h[c];
   RCHK(upload(cx, u.ucl_off, u.ucl_off_h.data(), sizeof(long long) * (C + 1)));
