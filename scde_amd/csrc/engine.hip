@@ -922,7 +922,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       }
       cx->st_boot_path = tpath ? 1 : 0;
       if (tpath) {
-        HCHK(cx->sredo.ensure(sizeof(int) * ((size_t)P * N + 1)));
+        HCHK(cx->sredo.ensure(sizeof(int) * (2 * (size_t)P * N + 1)));  // flags, list length, list
         b2.redo = cx->sredo.as<int>();
         TileBootArgs tb{};
         tb.W8p = cx->w8t.as<unsigned char>();

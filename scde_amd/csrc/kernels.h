@@ -188,7 +188,8 @@ struct Boot2Args {
   const double* ZU;
   int* mask;     // [ngenes][P] needed-stretch bits (k_stretch_mask output)
   double* ubuf;  // [ngenes][P][8][nb] stretch upper bounds (k_stretch_mask output)
-  int* redo;     // [ngenes][P] slabs whose skipped stretches failed the post-check
+  int* redo;     // [ngenes][P] slabs whose skipped stretches failed the post-check (tile path:
+                 // fallback flags, then the fallback list length and [ngenes * P] list)
   double slack;  // heuristic slack of the mask (NaN: the default 30 + 0.4 C)
 };
 

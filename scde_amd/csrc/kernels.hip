@@ -1879,8 +1879,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(NB <= 20 ?
 }
 
 // k_boot_tiles' fallback: the (gene, slab) items it could not finish, appended to
-// list[0 .. list[nitems]) (whole slabs, no skipping).  A small grid walks the list, so the
-// usual empty fallback costs one short launch, not a block per slab.
+// list[0 .. *count) (whole slabs, no skipping).  A small grid walks the list, so the usual
+// empty fallback costs one short launch, not a block per slab.
 // (a rare path: no occupancy target, so the item loop never spills around the asm look-ahead;
 // the tile path has G <= 448, blocks of at most 448 threads)
 template <int NB>
@@ -1888,8 +1888,9 @@ __global__ __launch_bounds__(512) void k_boot2_list(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
     const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
-    long long part_stride, int* __restrict__ degen, int ngenes, const int* __restrict__ list, long long nitems) {
-  const int cnt = __builtin_amdgcn_readfirstlane(list[nitems]);
+    long long part_stride, int* __restrict__ degen, int ngenes, const int* __restrict__ count,
+    const int* __restrict__ list) {
+  const int cnt = __builtin_amdgcn_readfirstlane(*count);
   for (int it = blockIdx.x; it < cnt; it += gridDim.x) {
     const int item = __builtin_amdgcn_readfirstlane(list[it]);
     const int g = item / P, p = item - g * P;
@@ -1958,7 +1959,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   const int g = order ? order[gi] : gi;
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
     if (lane == 0) {
-      redo[atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;  // k_boot2_list's item list
+      redo[(long long)g * P + p] = 1;  // flag (k_boot2's full-grid redo launch) and list entry (k_boot2_list)
+      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
       pmask[(long long)g * P + p] = ~0u;  // k_boot2 writes the whole row
     }
     return;
@@ -2147,7 +2149,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   if (cnt > 0) {
     if (cnt > 4 || maxgroups < 2) {  // the whole slab goes to k_boot2's redo launch
       if (lane == 0) {
-        redo[atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
+        redo[(long long)g * P + p] = 1;
+        redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
         pmask[(long long)g * P + p] = ~0u;
         if (stats) {
           atomicAdd(&stats[3], 1);
@@ -3237,6 +3240,7 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if ((long long)a.ncols_p1 * a.GS >= (1LL << 31) || (long long)a.ncells * a.Bp >= (1LL << 31) ||
       (long long)a.ncells * 32 * P >= (1LL << 31))
     return hipErrorInvalidValue;
+  // redo: [items] fallback flags, [1] the fallback list's length, [items] the list
   hipError_t e = hipMemsetAsync(a.redo, 0, sizeof(int) * ((size_t)a.ngenes * P + 1), s);
   if (e != hipSuccess) return e;
   const long long items = (long long)a.ngenes * P;
@@ -3257,20 +3261,39 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if (e != hipSuccess) return e;
   // slabs the tile kernel left (more tiles than its registers hold, or NaN tables): k_boot2,
   // whole slab, same sums
-  // (the list: redo[0 .. redo[items]), appended by k_boot_tiles; a grid of 512 blocks walks it)
+  // From kListCells cells per call the fallback is rare (config 3: no slab) and a 512-block
+  // k_boot2_list walks the compacted list (one short launch instead of one early-exit block
+  // per slab).  Below it a fifth of the slabs can fall back (~100 cells per call), and the
+  // full-grid k_boot2 with its occupancy target takes the flagged slabs faster.
+  constexpr int kListCells = 400;
   const int block2 = ((a.G + 63) / 64) * 64;
-  const int grid2 = (int)std::min<long long>(items, 512);
-#define SCDE_B2R(NBV)                                                                                             \
+  if (a.ncells >= kListCells) {
+    const int grid2 = (int)std::min<long long>(items, 512);
+#define SCDE_B2L(NBV)                                                                                             \
   case NBV:                                                                                                        \
     hipLaunchKernelGGL(k_boot2_list<NBV>, dim3(grid2), dim3(block2), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, \
                        a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,   \
-                       a.part_stride, a.degen, a.ngenes, a.redo, items);                                        \
+                       a.part_stride, a.degen, a.ngenes, a.redo + items, a.redo + items + 1);                   \
     break;
-  switch (a.nb) {
-    SCDE_B2R(4) SCDE_B2R(8) SCDE_B2R(12) SCDE_B2R(16) SCDE_B2R(20)
-    default: return hipErrorInvalidValue;
-  }
+    switch (a.nb) {
+      SCDE_B2L(4) SCDE_B2L(8) SCDE_B2L(12) SCDE_B2L(16) SCDE_B2L(20)
+      default: return hipErrorInvalidValue;
+    }
+#undef SCDE_B2L
+  } else {
+    const int grid2 = (a.ngenes + 7) / 8 * 8 * P;
+#define SCDE_B2R(NBV)                                                                                             \
+  case NBV:                                                                                                        \
+    hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid2), dim3(block2), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
+                       a.part_stride, a.degen, a.ngenes, nullptr, nullptr, a.redo, 1);                          \
+    break;
+    switch (a.nb) {
+      SCDE_B2R(4) SCDE_B2R(8) SCDE_B2R(12) SCDE_B2R(16) SCDE_B2R(20)
+      default: return hipErrorInvalidValue;
+    }
 #undef SCDE_B2R
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   const long long nn = (long long)a.ngenes * a.G;
