@@ -705,23 +705,19 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     qpath = maxw <= 127 && ndraw < 65000 && bootq_lds_bytes(qstride) <= 130 * 1024 &&
             (ncols + 1) * (long long)GS < (1LL << 31);
   }
-  // FP64 path: boots per slab, draws (before the tables: the tile path needs the largest
-  // multiplicity to decide what the tables emit)
+  // FP64 path: boots per slab; the draws come after the tables launch (the host's RNG work
+  // then overlaps the tables kernel instead of leaving the GPU idle in front of it)
   int nb = fast ? boot2_nb(s.nboot) : 16;
   if (fast) {
     const int v = cx->opt_boot_nb;  // tuning option: a multiple of 4 in [4, 32]
     if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
   }
   const int Bp = (int)round_up(std::max(s.nboot, 1), nb);
-  if (fused && !qpath && s.nboot > 0) {
-    make_draws(s, Bp, draws, W, ndraw);
-    maxw = 0;
-    for (double w : W) maxw = std::max(maxw, (int)w);
-  }
-  // k_boot_tiles: G <= 448, nb <= 20, multiplicities <= 127 (int8), int32 digit sums
-  const bool tpath = fused && !qpath && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
-                     C >= cx->opt_boot_tiles_cells &&
-                     nb <= 20 && maxw <= 127 && C < 100000 && (ncols + 1) * (long long)GS < (1LL << 31);
+  // k_boot_tiles: G <= 448, nb <= 20, multiplicities <= 127 (int8), int32 digit sums.  The
+  // tables are set up for it before the draws exist; should a multiplicity exceed 127 (a
+  // cell drawn 128 times in one boot), plain k_boot2 runs on the same D columns instead.
+  bool tpath = fused && !qpath && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
+               C >= cx->opt_boot_tiles_cells && nb <= 20 && C < 100000 && (ncols + 1) * (long long)GS < (1LL << 31);
   const int Bt = (int)round_up(Bp, 32) + 32;  // byte multiplicity rows: the last slab reads 32 boots
   if (keep_T) HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
   HCHK(cx->maxi.ensure(sizeof(int) * std::max<long long>(1, ncols)));
@@ -800,6 +796,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     HCHK(launch_tables(ta, st));
   }
   cx->mark_end(SLOT_TABLES, ev);
+  if (fused && !qpath && s.nboot > 0) {
+    make_draws(s, Bp, draws, W, ndraw);
+    maxw = 0;
+    for (double w : W) maxw = std::max(maxw, (int)w);
+    tpath = tpath && maxw <= 127;
+  }
   // ---- joint posterior
   if (!s.batch_call && s.ensemble) {
     HCHK(cx->E.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
