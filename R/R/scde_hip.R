@@ -4,8 +4,10 @@
 # (R/functions.R:566, 304) already run on the GPU through the layer-1 .Call symbols.  These
 # functions keep exactly those signatures but hand the whole call to the device in one .Call:
 # unique-count tables, both groups' posteriors, the ratio posterior, the summary and BH run
-# in HBM (scde_expression_difference_host).  Arguments the fused path does not cover (batch
-# correction) go to the reference implementation, which is saved as .scde.ref.* first.
+# in HBM (scde_expression_difference_host; the batch-corrected branch, R/functions.R:321-399, through
+# scde_expression_difference_batch_host).  Arguments the fused path does not cover (batch.models of
+# another model type than models, scde.posteriors with a batch) go to the reference implementation,
+# saved as .scde.ref.* first, which runs over the layer-1 .Call symbols of the same library.
 
 .scde.model.matrix <- function(models) {
     # R/functions.R:601-604 (mm), with the flags R/functions.R:595-598 derives
@@ -22,10 +24,6 @@ if (!exists(".scde.ref.posteriors")) .scde.ref.posteriors <- scde.posteriors
 scde.expression.difference <- function(models, counts, prior, groups = NULL, batch = NULL, n.randomizations = 150,
                                        n.cores = 10, batch.models = models, return.posteriors = FALSE,
                                        expectation = 0, verbose = 0) {
-    if (!is.null(batch) && length(unique(batch)) > 1) {
-        return(.scde.ref.expression.difference(models, counts, prior, groups, batch, n.randomizations, n.cores,
-                                               batch.models, return.posteriors, expectation, verbose))
-    }
     if (!all(rownames(models) %in% colnames(counts))) {
         stop("ERROR: provided count data does not cover all of the cells specified in the model matrix")
     }
@@ -39,25 +37,71 @@ scde.expression.difference <- function(models, counts, prior, groups = NULL, bat
         stop(paste("ERROR: wrong number of levels in the grouping factor (", paste(levels(groups), collapse = " "),
                    "), but must be two.", sep = ""))
     }
+    # the reference splits the model rows by position, tapply(seq_len(nrow(models)), groups, ...)
+    # (R/functions.R:355, 372): the codes go by position too, never by name
+    if (length(groups) != nrow(models)) stop("arguments must have same length")
+    gcodes <- as.integer(groups)
+    correct.batch <- !is.null(batch) && length(levels(batch)) > 1  # R/functions.R:321-330
     storage.mode(counts) <- "integer"
     m <- .scde.model.matrix(models)
     m$mm[, 5] <- pmax(m$mm[, 5], 1e-10)  # R/functions.R:579-583
-    x <- .Call("scde_hip_expression_difference", m$mm, counts, prior$x, prior$y,
-               as.integer(groups[rownames(models)]), n.randomizations, n.cores, m$localtheta, m$squarelogit,
-               expectation, return.posteriors, PACKAGE = "scde")
-    res <- as.data.frame(x$results)
-    colnames(res) <- c("lb", "mle", "ub", "ce", "Z", "cZ")
-    rownames(res) <- rownames(counts)
-    if (!return.posteriors) return(res)
     marginals <- log(pmax(10^prior$x - 1, 0))
-    jp <- lapply(list(x$jp1, x$jp2), function(j) {
+    rv <- seq(prior$x[1] - prior$x[length(prior$x)], prior$x[length(prior$x)] - prior$x[1],
+              length = length(prior$x) * 2 - 1)
+    name.jp <- function(j) {
         rownames(j) <- rownames(counts)
         colnames(j) <- as.character(exp(marginals))
         j
-    })
+    }
+    name.tab <- function(t) {
+        res <- as.data.frame(t)
+        colnames(res) <- c("lb", "mle", "ub", "ce", "Z", "cZ")
+        rownames(res) <- rownames(counts)
+        res
+    }
+    if (correct.batch) {
+        batch <- as.factor(batch)
+        if (length(batch) != nrow(models)) stop("arguments must have same length")
+        bm <- .scde.model.matrix(batch.models)
+        if (bm$localtheta != m$localtheta || bm$squarelogit != m$squarelogit || nrow(bm$mm) != nrow(m$mm)) {
+            # batch.models of another model type: the reference glue over the layer-1 symbols
+            return(.scde.ref.expression.difference(models, counts, prior, groups, batch, n.randomizations, n.cores,
+                                                   batch.models, return.posteriors, expectation, verbose))
+        }
+        bgti <- table(groups, batch)  # R/functions.R:336-349
+        bgti.ft <- fisher.test(bgti)
+        if (verbose) {
+            cat("controlling for batch effects. interaction:\n")
+            print(bgti)
+        }
+        if (bgti.ft$p.value < 1e-3) {
+            cat("WARNING: strong interaction between groups and batches! Correction may be ineffective:\n")
+            print(bgti.ft)
+        }
+        bm$mm[, 5] <- pmax(bm$mm[, 5], 1e-10)
+        x <- .Call("scde_hip_expression_difference_batch", m$mm, bm$mm, counts, prior$x, prior$y, gcodes,
+                   as.integer(batch), length(levels(batch)), n.randomizations, n.cores, m$localtheta, m$squarelogit,
+                   expectation, return.posteriors, PACKAGE = "scde")
+        out <- list(batch.adjusted = name.tab(x$batch.adjusted), results = name.tab(x$results),
+                    batch.effect = name.tab(x$batch.effect))
+        if (!return.posteriors) return(out)
+        ratio <- x$ratio
+        dimnames(ratio) <- list(rownames(counts), as.character(rv))
+        rv2 <- as.numeric(colnames(ratio))  # the second level's prior x (R/functions.R:391)
+        rv2 <- seq(rv2[1] - rv2[length(rv2)], rv2[length(rv2)] - rv2[1], length = length(rv2) * 2 - 1)
+        aratio <- x$adj.ratio
+        dimnames(aratio) <- list(rownames(counts), as.character(rv2))
+        jp <- lapply(list(x$jp1, x$jp2), name.jp)
+        names(jp) <- levels(groups)
+        return(c(out, list(difference.posterior = ratio, batch.adjusted.difference.posterior = aratio,
+                           joint.posteriors = jp)))
+    }
+    x <- .Call("scde_hip_expression_difference", m$mm, counts, prior$x, prior$y, gcodes, n.randomizations, n.cores,
+               m$localtheta, m$squarelogit, expectation, return.posteriors, PACKAGE = "scde")
+    res <- name.tab(x$results)
+    if (!return.posteriors) return(res)
+    jp <- lapply(list(x$jp1, x$jp2), name.jp)
     names(jp) <- levels(groups)
-    rv <- seq(prior$x[1] - prior$x[length(prior$x)], prior$x[length(prior$x)] - prior$x[1],
-              length = length(prior$x) * 2 - 1)
     ratio <- x$ratio
     rownames(ratio) <- rownames(counts)
     colnames(ratio) <- as.character(rv)

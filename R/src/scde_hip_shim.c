@@ -12,7 +12,8 @@
  *   baileyWPCA             src/bwpca.cpp:59         (decl src/bwpca.h:8)
  *   winsorizeMatrix, matWCorr, plSemicompleteCor2, matCorr  src/pagoda.cpp (decl src/pagoda.h:5-8)
  * Layer 2 (the fused device path behind R/scde_hip.R's wrappers):
- *   scde_hip_expression_difference, scde_hip_posteriors, scde_hip_varnorm_weights
+ *   scde_hip_expression_difference, scde_hip_expression_difference_batch, scde_hip_posteriors,
+ *   scde_hip_varnorm_weights
  *
  * Build: src/Makevars adds -I$(SCDE_HIP_HOME)/include and -lscde_hip.
  * Errors from the library become Rf_error; there is no CPU fallback.
@@ -151,7 +152,10 @@ SEXP jpmatLogBatchBoot(SEXP Matll, SEXP Comp, SEXP Nboot, SEXP Seed) {
   for (int k = 0; k < nt; k++)
     for (int j = 0; j < off[k + 1] - off[k]; j++) mats[off[k] + j] = REAL(VECTOR_ELT(VECTOR_ELT(Matll, k), j));
   SEXP comp = PROTECT(Rf_coerceVector(Comp, INTSXP));
-  SEXP m0 = off[1] > 0 ? VECTOR_ELT(VECTOR_ELT(Matll, 0), 0) : VECTOR_ELT(VECTOR_ELT(Matll, nt - 1), 0);
+  /* the output shape comes from the first non-empty sublist (tot > 0: one exists) */
+  int k0 = 0;
+  while (off[k0 + 1] == off[k0]) k0++;
+  SEXP m0 = VECTOR_ELT(VECTOR_ELT(Matll, k0), 0);
   SEXP out = PROTECT(Rf_allocMatrix(REALSXP, Rf_nrows(m0), Rf_ncols(m0)));
   chk(scde_jpmatLogBatchBoot(mats, off, INTEGER(comp), nt, Rf_nrows(m0), Rf_ncols(m0), as_int(Nboot),
                              as_int(Seed), REAL(out)));
@@ -292,6 +296,55 @@ SEXP scde_hip_expression_difference(SEXP Models, SEXP Counts, SEXP PriorX, SEXP 
   SEXP out = PROTECT(Rf_mkNamed(VECSXP, nm));
   SET_VECTOR_ELT(out, 0, res); SET_VECTOR_ELT(out, 1, jp1); SET_VECTOR_ELT(out, 2, jp2); SET_VECTOR_ELT(out, 3, ratio);
   UNPROTECT(10);
+  return out;
+}
+
+/* Batch-corrected scde.expression.difference (R/functions.R:321-399) in one call.  Groups and
+ * Batch are factor codes by model row (1-based, NA allowed: such cells join no group / no batch
+ * level, as tapply and table drop them); NBatch = nlevels(batch).  Returns the three N x 6
+ * summaries (batch.adjusted, results, batch.effect) and, with ReturnPosteriors, the group
+ * difference posterior (N x 2G-1), the batch-adjusted one (N x 4G-3) and both joint posteriors. */
+SEXP scde_hip_expression_difference_batch(SEXP Models, SEXP BatchModels, SEXP Counts, SEXP PriorX, SEXP PriorY,
+                                          SEXP Groups, SEXP Batch, SEXP NBatch, SEXP Nboot, SEXP NCores,
+                                          SEXP LocalTheta, SEXP SquareLogitConc, SEXP Expectation,
+                                          SEXP ReturnPosteriors) {
+  SEXP mm = PROTECT(Rf_coerceVector(Models, REALSXP)), bmm = PROTECT(Rf_coerceVector(BatchModels, REALSXP));
+  SEXP px = PROTECT(Rf_coerceVector(PriorX, REALSXP)), py = PROTECT(Rf_coerceVector(PriorY, REALSXP));
+  SEXP gr = PROTECT(Rf_coerceVector(Groups, INTSXP)), bt = PROTECT(Rf_coerceVector(Batch, INTSXP));
+  SEXP ci = PROTECT(Rf_coerceVector(Counts, INTSXP));
+  const int ngenes = Rf_nrows(Counts), ncells = Rf_ncols(Counts), G = XLENGTH(px), nb = as_int(NBatch);
+  if (XLENGTH(gr) != ncells || XLENGTH(bt) != ncells) Rf_error("scde_hip: groups/batch length differs from the cell count");
+  if (Rf_nrows(mm) != ncells || Rf_nrows(bmm) != ncells) Rf_error("scde_hip: model rows differ from the cell count");
+  int *codes = (int *) R_alloc(ncells, sizeof(int)), *bcodes = (int *) R_alloc(ncells, sizeof(int));
+  for (int c = 0; c < ncells; c++) {
+    codes[c] = INTEGER(gr)[c] == NA_INTEGER ? -1 : INTEGER(gr)[c] - 1;
+    bcodes[c] = INTEGER(bt)[c] == NA_INTEGER ? -1 : INTEGER(bt)[c] - 1;
+  }
+  scde_de_params p;
+  memset(&p, 0, sizeof(p));
+  p.ncells = ncells; p.models = REAL(mm); p.local_theta = as_int(LocalTheta); p.square_logit_conc = as_int(SquareLogitConc);
+  p.groups = codes; p.prior_x = REAL(px); p.prior_y = REAL(py); p.ngrid = G; p.nboot = as_int(Nboot);
+  p.n_cores = as_int(NCores); p.gene_offset = 0; p.ngenes_total = ngenes; p.expectation = Rf_asReal(Expectation);
+  p.rand_kind = scde_get_rand_kind(); p.compute_cz = 1;
+  const int rp = as_int(ReturnPosteriors), m = 2 * G - 1;
+  double *res = (double *) R_alloc((size_t) 18 * ngenes > 0 ? (size_t) 18 * ngenes : 1, sizeof(double));
+  SEXP jp1 = PROTECT(rp ? Rf_allocMatrix(REALSXP, ngenes, G) : R_NilValue);
+  SEXP jp2 = PROTECT(rp ? Rf_allocMatrix(REALSXP, ngenes, G) : R_NilValue);
+  SEXP ratio = PROTECT(rp ? Rf_allocMatrix(REALSXP, ngenes, m) : R_NilValue);
+  SEXP aratio = PROTECT(rp ? Rf_allocMatrix(REALSXP, ngenes, 2 * m - 1) : R_NilValue);
+  chk(scde_expression_difference_batch_host(NULL, INTEGER(ci), ngenes, ngenes, &p, REAL(bmm), bcodes, nb, res,
+                                            rp ? REAL(jp1) : NULL, rp ? REAL(jp2) : NULL, rp ? REAL(ratio) : NULL,
+                                            rp ? REAL(aratio) : NULL, NULL));
+  SEXP tabs[3];
+  for (int t = 0; t < 3; t++) {
+    tabs[t] = PROTECT(Rf_allocMatrix(REALSXP, ngenes, 6));
+    memcpy(REAL(tabs[t]), res + (size_t) t * 6 * ngenes, sizeof(double) * 6 * (size_t) ngenes);
+  }
+  const char *nm[] = {"batch.adjusted", "results", "batch.effect", "jp1", "jp2", "ratio", "adj.ratio", ""};
+  SEXP out = PROTECT(Rf_mkNamed(VECSXP, nm));
+  for (int t = 0; t < 3; t++) SET_VECTOR_ELT(out, t, tabs[t]);
+  SET_VECTOR_ELT(out, 3, jp1); SET_VECTOR_ELT(out, 4, jp2); SET_VECTOR_ELT(out, 5, ratio); SET_VECTOR_ELT(out, 6, aratio);
+  UNPROTECT(15);
   return out;
 }
 

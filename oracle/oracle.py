@@ -276,7 +276,8 @@ def scde_posteriors(models, counts, prior_x, n_randomizations=100, batch=None, c
         postflag = 1
     ens = 1 if ensemble_posterior else 0
     if batch is not None:
-        levels = sorted(set(batch))
+        # None is an NA batch label: tapply (R/functions.R:570) leaves such cells out of BatchIL
+        levels = sorted(set(b for b in batch if b is not None))
         batchil = [np.array([i for i in range(C) if batch[i] == lv], np.int32) for lv in levels]
 
     def call(ii, seed):
@@ -375,7 +376,7 @@ def scde_expression_difference_batch(models, counts, prior_x, prior_y, groups, b
     and its summary over the 1601 columns (batch.adjusted)."""
     groups = np.asarray(groups)
     batch = list(batch)
-    levels = sorted(set(batch))
+    levels = sorted(set(b for b in batch if b is not None))  # None: NA (no level; table() drops it)
     bm = models if batch_models is None else batch_models
     cnt = np.asarray(counts)
     diffv = ratio_grid(prior_x)

@@ -431,9 +431,11 @@ def scde_expression_difference(models, counts, prior, groups=None, batch=None, n
     px = np.ascontiguousarray(prior["x"], np.float64)
     py = np.ascontiguousarray(prior["y"], np.float64)
     G = len(px)
-    correct_batch = batch is not None and len(set(np.asarray(batch).tolist())) > 1
+    correct_batch = batch is not None and len(set(b for b in np.asarray(batch, dtype=object).tolist()
+                                                  if b is not None)) > 1
     if correct_batch:
-        return _expression_difference_batch(models, mat, genes, prior, codes, np.asarray(batch), n_randomizations,
+        return _expression_difference_batch(models, mat, genes, prior, codes, np.asarray(batch, dtype=object),
+                                            n_randomizations,
                                             n_cores, batch_models if batch_models is not None else models,
                                             return_posteriors, expectation, ctx)
     params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, G,
@@ -458,8 +460,9 @@ def _expression_difference_batch(models, mat, genes, prior, codes, batch, nrand,
     group's batch composition, the group posteriors, the three ratio posteriors and their
     summaries with BH, all in HBM."""
     N, C = mat.shape
-    levels = sorted(set(batch.tolist()))
-    bcodes = np.ascontiguousarray([levels.index(b) for b in batch.tolist()], np.int32)
+    # None is an NA batch label: the cell joins no level (code -1), as tapply/table drop it
+    levels = sorted(set(b for b in batch.tolist() if b is not None))
+    bcodes = np.ascontiguousarray([-1 if b is None else levels.index(b) for b in batch.tolist()], np.int32)
     mm, lt, sq = model_matrix(models)
     bmm, blt, bsq = model_matrix(batch_models)
     if (blt, bsq) != (lt, sq):

@@ -1845,20 +1845,22 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
   for (int c = 0; c < C; ++c)
     if (p->groups[c] == 0 || p->groups[c] == 1) idx[p->groups[c]].push_back(c);
   if (idx[0].empty() || idx[1].empty()) return fail(SCDE_EARG, "both groups need at least one cell");
-  // BatchIL (0-based cell indices per batch level) and table(batch[ii]) per group
+  // BatchIL (0-based cell indices per batch level) and table(batch[ii]) per group; code -1 is
+  // an NA batch: tapply (R/functions.R:570) and table leave such cells out of every level
   std::vector<int> bvals;
   std::vector<int64_t> boff(nbatch + 1, 0);
+  for (int c = 0; c < C; ++c)
+    if (batch_codes[c] < -1 || batch_codes[c] >= nbatch) return fail(SCDE_EARG, "batch code out of range");
   for (int k = 0; k < nbatch; ++k) {
-    for (int c = 0; c < C; ++c) {
-      if (batch_codes[c] < 0 || batch_codes[c] >= nbatch) return fail(SCDE_EARG, "batch code out of range");
+    for (int c = 0; c < C; ++c)
       if (batch_codes[c] == k) bvals.push_back(c);
-    }
     boff[k + 1] = (int64_t)bvals.size();
   }
   std::vector<int> comp[2];
   for (int gi = 0; gi < 2; ++gi) {
     comp[gi].assign(nbatch, 0);
-    for (int c : idx[gi]) comp[gi][batch_codes[c]]++;
+    for (int c : idx[gi])
+      if (batch_codes[c] >= 0) comp[gi][batch_codes[c]]++;
   }
   const std::vector<double> mag = marginals(p->prior_x, G);
   std::vector<int> seeds, wset;

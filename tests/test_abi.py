@@ -95,15 +95,19 @@ def test_r_shim_compiles_and_binds_exported_symbols():
                            capture_output=True, text=True)
         assert r.returncode == 0, r.stderr
     txt = re.sub(r"/\*.*?\*/", "", open(src).read(), flags=re.S)
-    called = set(re.findall(r"\b(scde_[a-zA-Z0-9_]+)\s*\(", txt)) - {"scde_hip_expression_difference",
-                                                                      "scde_hip_posteriors",
-                                                                      "scde_hip_varnorm_weights"}
+    defined = set(re.findall(r"^SEXP\s+([A-Za-z0-9_]+)\s*\(", txt, flags=re.M))
+    called = set(re.findall(r"\b(scde_[a-zA-Z0-9_]+)\s*\(", txt)) - defined
     L = _lib.lib()
     for n in called:
         assert hasattr(L, n), n
-    defined = set(re.findall(r"^SEXP\s+([A-Za-z0-9_]+)\s*\(", txt, flags=re.M))
+    assert "scde_expression_difference_batch_host" in called  # the fused batch branch
+    assert {"scde_hip_expression_difference", "scde_hip_expression_difference_batch", "scde_hip_posteriors",
+            "scde_hip_varnorm_weights"} <= defined
     assert {"logBootPosterior", "logBootBatchPosterior", "jpmatLogBoot", "jpmatLogBatchBoot", "matSlideMult",
             "baileyWPCA", "winsorizeMatrix", "matWCorr", "plSemicompleteCor2", "matCorr"} <= defined
     rwrap = open(os.path.join(ROOT, "R", "R", "scde_hip.R")).read()
     for sym in re.findall(r'\.Call\("([A-Za-z0-9_]+)"', rwrap):
         assert sym in defined, sym
+    assert '.Call("scde_hip_expression_difference_batch"' in rwrap
+    # group codes by position, as the reference's tapply(seq_len(nrow(models)), groups, ...)
+    assert "groups[rownames(models)]" not in rwrap and "as.integer(groups)" in rwrap

@@ -1,0 +1,122 @@
+"""GPU parity at the BASELINE shapes, beyond the 64-gene slices of test_gpu_configs.py:
+
+* config 3 WHOLE: the bench's own 20,000 x 1,000 data set (500/500 cells), B = 100, n.cores = 16
+  seeding, through scde_expression_difference_host (two-range pipelined upload, device gene
+  ordering, compacted fallback list, device BH over all genes), against the oracle's table for
+  every gene (tests/golden/config3_full.npz, tools/make_config3_fixture.py): lb/mle/ub/ce exact,
+  Z and the global-BH cZ (R/functions.R:5051, 3527-3531) within conftest's tolerances; the joint
+  and ratio posteriors of a 48-gene window straddling the first n.cores chunk boundary (gene
+  1,250) against the live oracle;
+* config 4: a 1,000-gene x 2,000-cell slice, B = 100, postflag 1 (modes exact), oracle run in
+  worker processes (mclapply-style contiguous chunks of the n.cores = 1 call: one draw list);
+* config 2b: a 256-gene slice of the batch-corrected bench set, B = 100, all three tables and
+  every posterior.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_posterior_close, assert_z_close
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def api():
+    from scde_amd import api as A
+    A.set_rand("glibc")
+    return A
+
+
+def _posteriors_chunk(job):
+    models, sub, px, nboot, lo, ntot = job
+    from oracle import oracle as O
+    O.set_rng(0)
+    r = O.scde_posteriors(models, np.ascontiguousarray(sub), px, n_randomizations=nboot,
+                          return_individual_posterior_modes=True, n_cores=1, gene_offset=lo, ngenes_total=ntot)
+    return lo, r["jp"], r["modes"]
+
+
+def _workers():
+    # the GPU box's CPU share is 16 (os.cpu_count() shows the whole machine)
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def test_config3_whole_table_vs_oracle(api, oracle):
+    import bench
+    g = np.load(os.path.join(ROOT, "tests", "golden", "config3_full.npz"), allow_pickle=False)
+    seed, ngenes, ncells, nboot, ncores = (int(v) for v in g["meta"])
+    cfg = bench.CONFIGS["3"]
+    assert (seed, ngenes, ncells) == (cfg["seed"], cfg["genes"], cfg["cells"])
+    models, counts, groups = bench.synthetic(seed, ngenes, ncells, two_groups=True)
+    prior = {"x": g["prior_x"], "y": g["prior_y"]}
+    api.set_rand("glibc")
+    got = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=nboot,
+                                         n_cores=ncores, return_posteriors=True)
+    res, want = got["results"], g["results"]
+    for j, k in enumerate(("lb", "mle", "ub", "ce")):
+        np.testing.assert_array_equal(res[k].to_numpy(), want[:, j], err_msg=k)
+    assert_z_close(res["Z"].to_numpy(), want[:, 4], what="Z")
+    assert_z_close(res["cZ"].to_numpy(), want[:, 5], what="cZ")
+    # posteriors of a window across the first chunk boundary (two draw lists), live oracle
+    lo, hi = 1226, 1274
+    ref = oracle.scde_expression_difference(models, np.ascontiguousarray(counts[lo:hi]), prior["x"], prior["y"],
+                                            groups, n_randomizations=nboot, n_cores=ncores, gene_offset=lo,
+                                            ngenes_total=ngenes, return_posteriors=True)
+    for i in range(2):
+        assert_posterior_close(got["joint.posteriors"][i][lo:hi], ref["joint.posteriors"][i], what=f"jp{i}")
+    assert_posterior_close(got["difference.posterior"].values[lo:hi], ref["difference.posterior"], what="ratio")
+
+
+def test_config4_1000_gene_slice_modes(api):
+    import multiprocessing as mp
+
+    import bench
+    from scde_amd.prior import expression_prior
+    cfg = bench.CONFIGS["4"]
+    models, counts, _ = bench.synthetic(cfg["seed"], cfg["genes"], cfg["cells"], two_groups=False)
+    prior = expression_prior(models, counts, length_out=bench.LENGTH_OUT)
+    n = 1000
+    sub = np.asfortranarray(counts[:n])
+    api.set_rand("glibc")
+    got = api.scde_posteriors(models, sub, prior, n_randomizations=100, return_individual_posterior_modes=True,
+                              n_cores=1)
+    px = np.asarray(prior["x"])
+    w = _workers()
+    bounds = np.linspace(0, n, w + 1).astype(int)
+    jobs = [(models, sub[bounds[i]:bounds[i + 1]], px, 100, int(bounds[i]), n) for i in range(w)
+            if bounds[i + 1] > bounds[i]]
+    with mp.get_context("spawn").Pool(len(jobs)) as pool:
+        parts = pool.map(_posteriors_chunk, jobs)
+    jp = np.vstack([p[1] for p in parts])
+    modes = np.vstack([p[2] for p in parts])
+    assert_posterior_close(got["jp"], jp, what="jp")
+    np.testing.assert_array_equal(got["modes"], modes)
+
+
+def test_config2b_slice_b100(api, oracle):
+    import bench
+    from scde_amd.prior import expression_prior
+    cfg = bench.CONFIGS["2b"]
+    models, counts, groups = bench.synthetic(cfg["seed"], cfg["genes"], cfg["cells"], two_groups=True)
+    batch = bench.synthetic_batch(cfg["seed"], cfg["cells"], cfg["nbatch"])
+    prior = expression_prior(models, counts, length_out=bench.LENGTH_OUT)
+    sub = np.asfortranarray(counts[:256])
+    api.set_rand("glibc")
+    out = api.scde_expression_difference(models, sub, prior, groups=list(groups), batch=batch, n_randomizations=100,
+                                         n_cores=1, return_posteriors=True)
+    ref = oracle.scde_expression_difference_batch(models, sub, prior["x"], prior["y"], groups, list(batch),
+                                                  n_randomizations=100, n_cores=1, return_posteriors=True)
+    for i in range(2):
+        assert_posterior_close(out["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"jp{i}")
+    assert_posterior_close(out["difference.posterior"].values, ref["difference.posterior"], what="ratio")
+    assert_posterior_close(out["batch.adjusted.difference.posterior"].values,
+                           ref["batch.adjusted.difference.posterior"], what="batch-adjusted ratio")
+    for table in ("batch.effect", "results", "batch.adjusted"):
+        got, want = out[table], ref[table]
+        for k in ("lb", "mle", "ub", "ce"):
+            np.testing.assert_array_equal(got[k].to_numpy(), want[k], err_msg=f"{table}.{k}")
+        assert_z_close(got["Z"].to_numpy(), want["Z"], what=f"{table}.Z")
+        assert_z_close(got["cZ"].to_numpy(), want["cZ"], what=f"{table}.cZ")

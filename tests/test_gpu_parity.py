@@ -284,17 +284,21 @@ def test_negative_counts_rejected(api):
         api.scde_posteriors(models, -np.ones((3, 4), np.int32), {"x": g["prior_x"], "y": g["prior_y"]}, n_cores=1)
 
 
-@pytest.mark.parametrize("ncores,nlev", [(1, 2), (3, 2), (2, 3)])
+@pytest.mark.parametrize("ncores,nlev", [(1, 2), (3, 2), (2, 3), (2, "na")])
 def test_batch_corrected_difference(api, oracle, ncores, nlev):
     """Batch branch (R/functions.R:321-399) end to end against the oracle's restatement:
     batch.effect, results and batch.adjusted tables (lb/mle/ub/ce exact, Z/cZ per spec) and
-    every posterior (jp, batch ratio, ratio, 1601-column batch-adjusted ratio) within 1e-6."""
+    every posterior (jp, batch ratio, ratio, 1601-column batch-adjusted ratio) within 1e-6.
+    "na": two levels with every seventh cell's batch NA (tapply and table drop such cells:
+    never drawn in the batch posteriors, absent from the compositions)."""
     g = golden("esmef500.npz")
     models, counts, groups = _frame_inputs(g)
     counts = counts.iloc[:120]
     prior = {"x": g["prior_x"], "y": g["prior_y"]}
     if nlev == 2:
         batch = np.array(["b1" if (i * 5) % 3 else "b2" for i in range(40)])
+    elif nlev == "na":
+        batch = np.array([None if i % 7 == 3 else ("b1" if (i * 5) % 3 else "b2") for i in range(40)], dtype=object)
     else:
         batch = np.array([("b1", "b2", "b3")[(i * 7 + i // 5) % 3] for i in range(40)])
     out = api.scde_expression_difference(models, counts, prior, groups=groups, batch=batch, n_randomizations=10,

@@ -1,12 +1,15 @@
 """CPU tests: the oracle (oracle/) against the reference's own known answers and
 against independent references for the third-party arithmetic it restates."""
 import ctypes
+import os
 
 import mpmath
 import numpy as np
 import pytest
 
 from conftest import golden
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # vignettes/diffexp.md:113-119 (scde.expression.difference, n.randomizations=100, n.cores=1)
 VIGNETTE_TOP6 = {
@@ -143,3 +146,33 @@ def test_oracle_reproduces_golden_small(oracle):
     np.testing.assert_array_equal(r["joint.posteriors"][1], g["jp2"][:60])
     for k in ("lb", "mle", "ub", "ce", "Z"):
         np.testing.assert_array_equal(r["results"][k], g[k][:60])
+
+
+def test_config3_fixture_matches_live_oracle(oracle):
+    """tests/golden/config3_full.npz (tools/make_config3_fixture.py: the oracle over all 20,000
+    genes of the bench's config-3 set in 16 n.cores chunks, cZ by BH over every gene) holds what
+    the oracle computes: its prior is the numpy restatement's for these counts, and a window
+    across the first chunk boundary (genes 1,240-1,259: two draw lists) recomputed live gives
+    the stored lb/mle/ub/ce/Z bit for bit; cZ is the BH of the stored Z column."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    from oracle.prior import expression_prior
+    g = np.load(os.path.join(ROOT, "tests", "golden", "config3_full.npz"), allow_pickle=False)
+    seed, ngenes, ncells, nboot, ncores = (int(v) for v in g["meta"])
+    models, counts, groups = bench.synthetic(seed, ngenes, ncells, two_groups=True)
+    prior = expression_prior(models, counts, bench.LENGTH_OUT)
+    np.testing.assert_array_equal(prior["x"], g["prior_x"])
+    np.testing.assert_array_equal(prior["y"], g["prior_y"])
+    lo, hi = 1240, 1260
+    oracle.set_rng(0)
+    r = oracle.scde_expression_difference(models, np.ascontiguousarray(counts[lo:hi]), g["prior_x"], g["prior_y"],
+                                          groups, n_randomizations=nboot, n_cores=ncores, gene_offset=lo,
+                                          ngenes_total=ngenes)
+    want = g["results"][lo:hi]
+    for j, k in enumerate(("lb", "mle", "ub", "ce", "Z")):
+        np.testing.assert_array_equal(r[k], want[:, j], err_msg=k)
+    z = np.ascontiguousarray(g["results"][:, 4])
+    cz = np.zeros(ngenes)
+    oracle.lib().o_bh_cz(oracle._p(z), ngenes, oracle._p(cz))
+    np.testing.assert_array_equal(cz, g["results"][:, 5])
