@@ -21,6 +21,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdint>
+#include <utility>
 
 #include "device_math.h"
 #include "kernels.h"
@@ -1934,6 +1935,31 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef SCDE_TILE_DPPW
+// k_boot_tiles' multiplicity operand: 1 = a vector load per entry (each 16-lane row holds the
+// slab's multiplicity pairs, lane j boots 2j and 2j + 1) broadcast to the row by DPP64
+// row_newbcast:j on the FMA itself; 0 = scalar loads (the FMA's SGPR operand).  Same value,
+// same fma, same bits either way.
+#define SCDE_TILE_DPPW 1
+#endif
+typedef double d2_t __attribute__((ext_vector_type(2)));
+
+// acc += (w on lane J of this lane's 16-lane row) * x, one v_fmac_f64 with a DPP64 source.
+// w must come from a load, never from a VALU write in the two preceding instructions (the
+// DPP read hazard; tests/test_kernel_resources.py checks the shipped ISA).
+template <int J>
+__device__ __forceinline__ void fmac_bcast(double& acc, double w, double x) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(w), "v"(x),
+               "n"(J));
+}
+
+// one entry into NB accumulators: boots 2j, 2j + 1 of the slab from lane j of wv
+template <int NB, int... J>
+__device__ __forceinline__ void fmac_entry(double (&acc)[NB], const d2_t& wv, double x,
+                                           std::integer_sequence<int, J...>) {
+  ((fmac_bcast<J>(acc[2 * J], wv.x, x), fmac_bcast<J>(acc[2 * J + 1], wv.y, x)), ...);
+}
+
 template <int NB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_tiles(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
@@ -2077,6 +2103,82 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   constexpr int EB = SCDE_BOOT_EB;
   static_assert(EB == 4, "the asm look-ahead assumes 4-entry batches");
   // rows of one register group, in k_boot2's exact arithmetic (see k_boot2 for the asm)
+#if SCDE_TILE_DPPW
+  // Column and multiplicity loads both from asm (saddr form: the entry's column / cell row base
+  // in SGPRs, the lane's offset in a loop-invariant VGPR), waited with one explicit vmcnt: per
+  // batch 2 x EB loads, so vmcnt(2 EB) leaves only the next batch in flight.
+  const unsigned woff = (unsigned)(b0 + 2 * min(r, NB / 2 - 1)) * 8u;
+  auto rows = [&](double (&acc)[NB], int koff, bool live) {
+#pragma unroll
+    for (int i = 0; i < NB; ++i) acc[i] = live ? Zs[(long long)(b0 + i) * GS + koff] : -INFINITY;
+    const unsigned doff = (unsigned)koff * 8u;
+    double v[EB], vb[EB];
+    d2_t w[EB], wb[EB];
+    // the ELL entries (scalar loads, the only ones in the loop) are fetched one batch ahead of
+    // the batch whose loads they address, so their latency hides behind a batch of FMAs
+    auto fetch = [&](int e0, int4 (&t)[EB / 2]) {
+      const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
+#pragma unroll
+      for (int j = 0; j < EB / 2; ++j) t[j] = E4[j];
+    };
+    auto issue = [&](const int4 (&t4)[EB / 2], double (&x)[EB], d2_t (&wv)[EB]) {
+#pragma unroll
+      for (int j = 0; j < EB / 2; ++j) {
+        int4 t = t4[j];
+        // pins the address arithmetic (and the wait for the fetch) here, after the previous
+        // batch's FMAs, instead of where the compiler would hoist it
+        asm volatile("" : "+s"(t.x), "+s"(t.y), "+s"(t.z), "+s"(t.w));
+        // 32-bit offsets: (ncols + 1) x GS and ncells x Bp are < 2^31 (checked by the launcher)
+        const double* d0 = D + (unsigned)(t.y * GS);
+        const double* d1 = D + (unsigned)(t.w * GS);
+        const double* w0 = W + (unsigned)(t.x * Bp);
+        const double* w1 = W + (unsigned)(t.z * Bp);
+        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(x[2 * j]) : "v"(doff), "s"(d0));
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[2 * j]) : "v"(woff), "s"(w0));
+        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(x[2 * j + 1]) : "v"(doff), "s"(d1));
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[2 * j + 1]) : "v"(woff), "s"(w1));
+      }
+    };
+    static_assert(EB == 4, "the vmcnt below counts 2 x 4 loads per batch");
+    auto ready = [&](double (&x)[EB], d2_t (&wv)[EB]) {  // all but the next batch's 8 loads have landed
+      asm volatile("s_waitcnt vmcnt(8)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(wv[0]), "+v"(wv[1]),
+                   "+v"(wv[2]), "+v"(wv[3]));
+    };
+    auto accumulate = [&](const double (&x)[EB], const d2_t (&wv)[EB]) {
+#pragma unroll
+      for (int j = 0; j < EB; ++j) fmac_entry<NB>(acc, wv[j], x[j], std::make_integer_sequence<int, NB / 2>{});
+    };
+#pragma unroll
+    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));
+    // rows are padded to a multiple of 64 entries plus 8 zero-column entries: every fetch and
+    // look-ahead batch below stays inside the row
+    int4 ta[EB / 2], tb[EB / 2];
+    fetch(0, ta);
+    issue(ta, v, w);
+    fetch(EB, tb);
+    const int n4 = (n + EB - 1) & ~(EB - 1);
+    int e0 = 0;
+    for (; e0 + 2 * EB <= n4; e0 += 2 * EB) {
+      issue(tb, vb, wb);
+      fetch(e0 + 2 * EB, ta);
+      ready(v, w);
+      accumulate(v, w);
+      issue(ta, v, w);
+      fetch(e0 + 3 * EB, tb);
+      ready(vb, wb);
+      accumulate(vb, wb);
+    }
+    if (e0 < n4) {
+      issue(tb, vb, wb);
+      ready(v, w);
+      accumulate(v, w);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]), "+v"(wb[0]),
+                   "+v"(wb[1]), "+v"(wb[2]), "+v"(wb[3]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(w[0]), "+v"(w[1]),
+                 "+v"(w[2]), "+v"(w[3]));
+  };
+#else
   auto rows = [&](double (&acc)[NB], int koff, bool live) {
 #pragma unroll
     for (int i = 0; i < NB; ++i) acc[i] = live ? Zs[(long long)(b0 + i) * GS + koff] : -INFINITY;
@@ -2133,6 +2235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
   };
+#endif
   double acc1[NB], acc2[NB];
   const int k1 = 16 * tl[h] + r;
   const bool live1 = h < n1 && k1 < G;
