@@ -48,7 +48,6 @@ LENGTH_OUT = 400
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 FP64_VALU_PEAK_TF = 78.6  # FP64 vector spec = FP32 vector 157.3 TF (MI355X_MICROARCH.md) / 2
 FP64_FMA_MEASURED_TF = 67.0  # v_fma_f64 rate measured on this part (tools/micro/f64_rates.hip)
-I8_MFMA_PEAK_TOPS = 5000.0  # int8 MFMA: 2x the BF16 rate per clock (MI355X_MICROARCH.md), BF16 ~2.5 PF dense
 METRIC = "genes/sec for scde.expression.difference (400-pt grid, 100 randomizations)"
 
 CONFIGS = {
@@ -117,7 +116,6 @@ def dominant_kernel_bytes(ngenes, cells_per_group):
 
 BOOT_STAGES = {0: "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum_partials)",
                1: "bootstrap stage (k_boot_tiles + k_boot2_list fallback + k_sum_partials)",
-               2: "fixed-point bootstrap (k_bootq)",
                3: "bootstrap stage (general k_boot)"}
 
 
@@ -154,13 +152,20 @@ def profiled_traffic(config: str, member=None, last=None):
     return out
 
 
-def add_profile_fields(roof: dict, prof):
-    """traffic / counter-bytes fraction / wait share from a profiled_traffic() record."""
+def add_profile_fields(roof: dict, prof, stage_s=None):
+    """traffic / counter-bytes fraction / wait share from a profiled_traffic() record.  Every
+    fraction in a roofline is on ONE time base: the stage's live HIP-event time in this run
+    (stage_s, seconds per stage) when given, else the profile's own rocprof time (stated in
+    `time_base`); the rocprof average stays beside it as a cross-check."""
     if not prof:
         return
     roof["traffic"] = prof["traffic_bytes"]
     roof["traffic_source"] = f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"
-    roof["counter_bytes_frac"] = prof["traffic_bytes"] / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+    roof["rocprof_stage_ms"] = prof["avg_ms"]
+    t = stage_s if stage_s else prof["avg_ms"] / 1e3
+    roof["counter_bytes_frac"] = prof["traffic_bytes"] / t / 1e9 / HBM_PEAK_GBS
+    roof["time_base"] = ("HIP events around the stage in this run" if stage_s else
+                         "rocprofv3 kernel durations of the committed profile")
     if prof.get("wait_frac") is not None:
         roof["wait_frac"] = prof["wait_frac"]
 
@@ -173,7 +178,7 @@ def stage_kernel(name: str) -> bool:
 
 def stage_last(name: str) -> bool:
     """The kernel that ends one stage (one per bootstrap launch)."""
-    return name in ("k_sum_partials", "k_bootq")
+    return name == "k_sum_partials"
 
 
 def _cpu_chunk(job):
@@ -608,12 +613,12 @@ def main():
     ctx.set_profiling(False)
 
     # arithmetic the bootstrap kernels issue in one step (one extra untimed step with the
-    # context's counters on): FP64 lane FMAs of k_boot2, int8 MACs of k_bootq
+    # context's counters on): FP64 lane FMAs of k_boot_tiles / k_boot2
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     run(dc.ptr)
     ctx.synchronize()
-    step_fma, step_mac = ctx.stat("boot_f64_fma"), ctx.stat("boot_i8_mac")
+    step_fma = ctx.stat("boot_f64_fma")
     stage_name = BOOT_STAGES.get(int(ctx.stat("boot_path")), "bootstrap stage")
     ctx.set_option("skip_stats", 0)
 
@@ -632,20 +637,12 @@ def main():
     # reference-formulation FP64 adds per launch: B x C x G x N
     ref_adds = NBOOT * sum(launch_cells) / len(launch_cells) * G * NG
     f64_tf = 2 * step_fma / boot_step_s / 1e12 if boot_n and step_fma else 0.0
-    i8_tops = 2 * step_mac / boot_step_s / 1e12 if boot_n and step_mac else 0.0
-    if step_mac > step_fma:
-        # fixed-point bootstrap (k_bootq): int8 MFMA ops issued over the stage time
-        roof = {"bound": "mfma", "kernel": stage_name, "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS,
-                "unit": "TOPS (int8)", "frac": i8_tops / I8_MFMA_PEAK_TOPS,
-                "achieved_basis": "int8 MACs issued by k_bootq's v_mfma_i32_16x16x64_i8 (x2 ops) per step / "
-                                  "stage time per step (HIP events)"}
-    else:
-        # FP64 bootstrap (k_boot2): the FMAs its kept stretches issue, against the FP64 VALU peak
-        roof = {"bound": "fp64-valu", "kernel": stage_name, "achieved": f64_tf, "peak": FP64_VALU_PEAK_TF,
-                "unit": "TFLOP/s", "frac": f64_tf / FP64_VALU_PEAK_TF,
-                "frac_of_measured_fma_rate": f64_tf / FP64_FMA_MEASURED_TF,
-                "achieved_basis": "lane FMAs the FP64 bootstrap kernels issue (computed grid points x slab boots x "
-                                  "entries, x2 flops) per step / stage time per step (HIP events)"}
+    # FP64 bootstrap: the FMAs its computed tiles / kept stretches issue, against the FP64 VALU peak
+    roof = {"bound": "fp64-valu", "kernel": stage_name, "achieved": f64_tf, "peak": FP64_VALU_PEAK_TF,
+            "unit": "TFLOP/s", "frac": f64_tf / FP64_VALU_PEAK_TF,
+            "frac_of_measured_fma_rate": f64_tf / FP64_FMA_MEASURED_TF,
+            "achieved_basis": "lane FMAs the FP64 bootstrap kernels issue (computed grid points x slab boots x "
+                              "entries, x2 flops) per step / stage time per step (HIP events)"}
     roof.update({
         "traffic": None,
         "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
@@ -655,9 +652,12 @@ def main():
         "hbm_algorithmic_gbs": hbm_alg,
         "hbm_algorithmic_frac": (hbm_alg / HBM_PEAK_GBS) if hbm_alg else None,
         "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None,
-        "f64_fma_per_step": step_fma, "i8_mac_per_step": step_mac})
-    # what the stage really moves: counter bytes per stage over the rocprof stage time
-    add_profile_fields(roof, prof)
+        "f64_fma_per_step": step_fma})
+    # what the stage really moves: counter bytes per stage (committed profile of this config at
+    # N = 1), over this run's stage time; a shard's stage moves other bytes, so --shard-of lines
+    # carry no traffic
+    if args.shard_of <= 1 and world == 1:
+        add_profile_fields(roof, prof, boot_avg_s if boot_n else None)
     out = {
         "metric": (METRIC_BATCH if batched else METRIC) if de else "genes/sec for scde.posteriors with posterior modes "
                                                                    "(400-pt grid, 100 randomizations)",

@@ -118,14 +118,14 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
 /* Tuning and test options of a context (defaults are the product settings; nothing is read
  * from the environment on the compute path):
  *   "boot_skip"     1/0  grid-stretch skipping in the bootstrap (output unchanged either way)
- *   "boot_q"        fixed-point int8-MFMA bootstrap k_bootq: 0 = never (default), 1 = from
- *                   boot_q_cells cells per call, 2 = always where it applies
- *   "boot_q_cells"  the cell count from which boot_q = 1 selects k_bootq (default 1000)
  *   "boot_tiles"    1/0  the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles; default 1)
  *   "boot_tiles_cells"  the cell count from which it is used (default 200; below: k_boot2's
  *                   64-point stretch mask)
  *   "tile_groups"   register groups of 4 tiles per k_boot_tiles wave, 1 or 2 (default 2; slabs
  *                   needing more go to k_boot2 whole -- tests force that with 1)
+ *   "tile_max_mult" the largest draw multiplicity the tile path takes (default 127, the int8 bound
+ *                   operand; a call with a larger one runs plain k_boot2 on the same columns --
+ *                   tests force that fallback with a small value)
  *   "tile_order"    1/0  k_boot_tiles takes the genes in order of their count sums, so waves in
  *                   flight share columns and tiles in L2 (default 1; results are the same)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
@@ -134,10 +134,9 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "ratio_window"  k_ratio_summary register window 4, 5, 7 or 8;  "ratio_block" 64, 128, 256
  *   "wpca_ms"       1/0  the multi-start npcs = 1 weighted-PCA kernel
  * Statistics: "skip_slabs", "skip_stretches", "skip_kept", "skip_redo", "degen", "tiles_<i>"
- * (k_bootq slabs computing i tiles) (with skip_stats);
- * "boot_f64_fma" (k_boot2: FP64 lane FMAs issued) and "boot_i8_mac" (k_bootq: int8 MACs issued
- * by its MFMAs), also with skip_stats; "boot_path": the bootstrap kernel of the last posterior
- * (0 k_boot2, 1 k_boot_tiles, 2 k_bootq, 3 the general k_boot). */
+ * (k_boot_tiles slabs computing i tiles) (with skip_stats); "boot_f64_fma" (FP64 lane FMAs the
+ * bootstrap kernels issued), also with skip_stats; "boot_path": the bootstrap kernel of the last
+ * posterior (0 k_boot2, 1 k_boot_tiles, 3 the general k_boot). */
 int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);
 int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
 int scde_ctx_reset_stats(scde_ctx* ctx);

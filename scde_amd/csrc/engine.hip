@@ -192,8 +192,6 @@ struct scde_ctx {
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
   Buf gkey, gkey2, gidx, gorder, gwork, pmask;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
-  int opt_boot_q = 0;            // "boot_q": the fixed-point int8-MFMA bootstrap: 0 never, 1 from boot_q_cells, 2 always
-  int opt_boot_q_cells = 1000;   // "boot_q_cells": cells per call from which boot_q = 1 picks it
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 30 + 0.4 C); tests force redo slabs
   int opt_boot_nb = 0;           // "boot_nb": boots per slab (0 = automatic; a multiple of 4 in [4, 32])
@@ -205,13 +203,15 @@ struct scde_ctx {
   int opt_boot_tiles_cells = 200;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
                                    // rows are wide, most slabs need > 8 tiles, k_boot2's stretches win)
   int opt_tile_groups = 2;       // "tile_groups": register groups of 4 tiles per k_boot_tiles wave (1 or 2)
+  int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
+                                 // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
-  // stretches x 64 lanes x slab boots x entries) and int8 MACs of k_bootq (MFMAs x 16 x 16 x 64)
-  double st_boot_f64_fma = 0, st_boot_i8_mac = 0;
-  double st_boot_path = -1;  // the bootstrap kernel of the last posterior: 0 k_boot2, 1 k_boot_tiles, 2 k_bootq, 3 general
+  // stretches x 64 lanes x slab boots x entries)
+  double st_boot_f64_fma = 0;
+  double st_boot_path = -1;  // the bootstrap kernel of the last posterior: 0 k_boot2, 1 k_boot_tiles, 3 general
   static constexpr int kQMaxTilesHost = 28;
   double st_tile_hist[kQMaxTilesHost + 1] = {0};
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
@@ -502,123 +502,6 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
   }
 }
 
-// The fixed-point bootstrap (bootq.hip) after the tables kernel has written the digit
-// columns DQ (cx->E) and tile bounds UQ (cx->ubound): ELL rows padded to 64 entries, the
-// baseline digit sums, k_bootq; then the exact FP64 path for genes it flags (T tables built
-// by a gated launch that does nothing when no gene is flagged).
-int run_bootq(scde_ctx* cx, const PostSpec& s, UniqueSet& u, const TablesArgs& ta, long long ncols, int GS,
-              const std::vector<int>& draws, const std::vector<double>& W, int ndraw, int Bq, int stride,
-              bool have_T) {
-  const int C = s.ncells, G = s.G, N = s.ngenes, nsets = (int)s.seeds.size();
-  hipStream_t st = cx->stream;
-  // multiplicities as bytes: [set][cell][boot] (baseline sums) and [set][boot][cell] (k_bootq)
-  std::vector<unsigned char> w8((size_t)nsets * C * Bq), w8t((size_t)nsets * C * Bq);
-  for (int set = 0; set < nsets; ++set)
-    for (int c = 0; c < C; ++c)
-      for (int b = 0; b < Bq; ++b) {
-        const unsigned char v = (unsigned char)W[((size_t)set * C + c) * Bq + b];
-        w8[((size_t)set * C + c) * Bq + b] = v;
-        w8t[((size_t)set * Bq + b) * C + c] = v;
-      }
-  RCHK(upload(cx, cx->w8, w8.data(), w8.size()));
-  RCHK(upload(cx, cx->w8t, w8t.data(), w8t.size()));
-  RCHK(upload(cx, cx->draws, draws.data(), sizeof(int) * draws.size()));
-  HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * stride)));
-  HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
-  HCHK(cx->Z.ensure(sizeof(int) * (size_t)nsets * 7 * GS * Bq));
-  HCHK(cx->zubound.ensure(sizeof(int) * (size_t)nsets * 4 * kQTiles * Bq));
-  const unsigned long long* DQ = reinterpret_cast<const unsigned long long*>(cx->E.p);
-  hipEvent_t ev = cx->mark_begin(SLOT_OTHER);
-  HCHK(launch_ell(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->base_col.as<int>(), stride, (int)ncols,
-                  64, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
-  HCHK(launch_zq(DQ, G, GS, cx->base_col.as<int>(), C, cx->w8.as<unsigned char>(), Bq, nsets, cx->Z.as<int>(), st));
-  HCHK(launch_zuq(cx->ubound.as<unsigned>(), cx->base_col.as<int>(), C, cx->w8.as<unsigned char>(), Bq, nsets,
-                  cx->zubound.as<int>(), st));
-  cx->mark_end(SLOT_OTHER, ev);
-  if (nsets > 1) {
-    if ((int)s.wset.size() != N) return fail(SCDE_EINTERNAL, "wset size mismatch");
-    RCHK(upload(cx, cx->wset, s.wset.data(), sizeof(int) * N));
-  }
-  HCHK(cx->degen.ensure(sizeof(int) * std::max(1, N)));
-  HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, N), st));
-  const int* wset_d = nsets > 1 ? cx->wset.as<int>() : nullptr;
-  int* qf = cx->qflags.as<int>();
-  BootQArgs qa{};
-  qa.DQ = DQ;
-  qa.UQ = cx->ubound.as<unsigned>();
-  qa.ent = cx->ent.as<int2>();
-  qa.nnz = cx->nnz.as<int>();
-  qa.ent_stride = stride;
-  qa.W8T = cx->w8t.as<unsigned char>();
-  qa.Bp = Bq;
-  qa.ncells = C;
-  qa.wset = wset_d;
-  qa.Zq = cx->Z.as<int>();
-  qa.ZUq = cx->zubound.as<int>();
-  qa.G = G;
-  qa.GS = GS;
-  qa.nboot = s.nboot;
-  qa.norm_mult = (double)s.nboot;
-  qa.slack = !cx->opt_boot_skip ? INFINITY : std::isnan(cx->opt_skip_slack) ? 30.0 + 0.4 * C : cx->opt_skip_slack;
-  qa.out = s.jp;
-  qa.out_g = s.jp_g;
-  qa.out_k = s.jp_k;
-  qa.degen = cx->degen.as<int>();
-  qa.ndegen = qf + 1;
-  qa.nanflag = qf;
-  qa.ngenes = N;
-  qa.stats = cx->opt_skip_stats ? qf + 2 : nullptr;
-  ev = cx->mark_begin(SLOT_BOOT);
-  HCHK(launch_bootq(qa, st));
-  cx->mark_end(SLOT_BOOT, ev);
-  if (cx->opt_skip_stats) {
-    int h[40];
-    HCHK(hipMemcpyAsync(h, qf, sizeof(int) * 40, hipMemcpyDeviceToHost, st));
-    HCHK(hipStreamSynchronize(st));
-    for (int i = 0; i <= scde_ctx::kQMaxTilesHost; ++i) cx->st_tile_hist[i] += h[6 + i];
-    cx->st_skip_slabs += h[2];
-    cx->st_skip_kept += h[3];
-    cx->st_skip_stretches += h[4];
-    cx->st_skip_redo += h[5];
-    cx->st_degen += h[1];
-    cx->st_boot_i8_mac += ((double)h[35] * 14 + (double)h[36] * 16) * 16 * 16 * 64;
-  }
-  // exact fallback: T tables only when some gene was flagged (gate), then k_boot_exact
-  if (!have_T) {
-    HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
-    TablesArgs tt = ta;
-    tt.phase = 0;
-    tt.T = cx->T.as<double>();
-    tt.maxi = nullptr;
-    tt.D = nullptr;
-    tt.DQ = nullptr;
-    tt.UQ = nullptr;
-    tt.U = nullptr;
-    tt.gate = qf + 1;
-    HCHK(launch_tables(tt, st));
-  }
-  ExactArgs xa{};
-  xa.T = cx->T.as<double>();
-  xa.base_col = nullptr;
-  xa.G = G;
-  xa.GS = GS;
-  xa.draws = cx->draws.as<int>();
-  xa.ndraw = ndraw;
-  xa.nboot = s.nboot;
-  xa.wset = wset_d;
-  xa.ucl_off = u.ucl_off.as<long long>();
-  xa.uci = u.uci.as<int>();
-  xa.ld_uci = N;
-  xa.norm_mult = (double)s.nboot;
-  xa.degen = cx->degen.as<int>();
-  xa.out = s.jp;
-  xa.out_g = s.jp_g;
-  xa.out_k = s.jp_k;
-  xa.ngenes = N;
-  HCHK(launch_boot_exact(xa, st));
-  return SCDE_OK;
-}
-
 int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
   // column stride: >= the k_boot2 block (lanes never read past a column); 512 keeps
@@ -688,23 +571,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const bool fused = boot_path && fast;
   const bool want_post = s.batch_call ? (s.postflag == 2) : (s.postflag == 2 || s.postflag == 3);
   const bool keep_T = !fused || (want_post && s.post);
-  // Fixed-point bootstrap on the int8 matrix cores (bootq.hip): G <= 448, multiplicities
-  // <= 127, draws per boot < 65,000 (int32 digit sums), the gene's entries in LDS.
   std::vector<int> draws;
   std::vector<double> W;
   int ndraw = 0, maxw = 0;
   const int nsets = (int)s.seeds.size();
-  const int Bq = (int)round_up(std::max(s.nboot, 1), 32);
+  // tile path ELL rows: a multiple of 64 entries (the bound MFMAs' K steps) plus 64
   const int qstride = (int)round_up(std::max(C, 1), 64) + 64;
-  bool qpath = false;
-  // boot_q: 1 = where it is the faster kernel (measured: from ~1,000 cells per call), 2 = always
-  const bool qwant = cx->opt_boot_q == 2 || (cx->opt_boot_q == 1 && C >= cx->opt_boot_q_cells);
-  if (fused && G <= 448 && qwant) {
-    make_draws(s, Bq, draws, W, ndraw);
-    for (double w : W) maxw = std::max(maxw, (int)w);
-    qpath = maxw <= 127 && ndraw < 65000 && bootq_lds_bytes(qstride) <= 130 * 1024 &&
-            (ncols + 1) * (long long)GS < (1LL << 31);
-  }
   // FP64 path: boots per slab; the draws come after the tables launch (the host's RNG work
   // then overlaps the tables kernel instead of leaving the GPU idle in front of it)
   int nb = fast ? boot2_nb(s.nboot) : 16;
@@ -716,7 +588,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   // k_boot_tiles: G <= 448, nb <= 20, multiplicities <= 127 (int8), int32 digit sums.  The
   // tables are set up for it before the draws exist; should a multiplicity exceed 127 (a
   // cell drawn 128 times in one boot), plain k_boot2 runs on the same D columns instead.
-  bool tpath = fused && !qpath && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
+  bool tpath = fused && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
                C >= cx->opt_boot_tiles_cells && nb <= 20 && C < 100000 && (ncols + 1) * (long long)GS < (1LL << 31);
   const int Bt = (int)round_up(Bp, 32) + 32;  // byte multiplicity rows: the last slab reads 32 boots
   if (keep_T) HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
@@ -744,8 +616,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   ta.use_baseline = s.use_baseline ? 1 : 0;
   // k_boot2 grid-stretch skipping (G <= 448: at most 7 stretches of 64 points); the
   // tables kernel emits the per-column stretch maxima.  SCDE_BOOT_SKIP=0 disables it.
-  const bool stretch_skip = fused && !qpath && !tpath && G <= 448 && cx->opt_boot_skip;
-  if (qpath || tpath) {
+  const bool stretch_skip = fused && !tpath && G <= 448 && cx->opt_boot_skip;
+  if (tpath) {
     HCHK(cx->qflags.ensure(sizeof(int) * 40));
     HCHK(hipMemsetAsync(cx->qflags.p, 0, sizeof(int) * 40, st));
     HCHK(cx->ubound.ensure(sizeof(unsigned) * kQTiles * (size_t)(ncols + 1)));
@@ -756,11 +628,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
     HCHK(cx->base_col.ensure(sizeof(int) * std::max(1, C)));
     HCHK(cx->zcol.ensure(sizeof(int) * std::max(1, C)));
-    if (qpath) {
-      ta.DQ = reinterpret_cast<unsigned long long*>(cx->E.p);
-    } else {
-      ta.D = cx->E.as<double>();
-    }
+    ta.D = cx->E.as<double>();
     ta.zcol = cx->zcol.as<int>();
     ta.base_col = cx->base_col.as<int>();
     if (stretch_skip) {
@@ -796,11 +664,11 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     HCHK(launch_tables(ta, st));
   }
   cx->mark_end(SLOT_TABLES, ev);
-  if (fused && !qpath && s.nboot > 0) {
+  if (fused && s.nboot > 0) {
     make_draws(s, Bp, draws, W, ndraw);
     maxw = 0;
     for (double w : W) maxw = std::max(maxw, (int)w);
-    tpath = tpath && maxw <= 127;
+    tpath = tpath && maxw <= std::min(127, cx->opt_tile_max_mult);
   }
   // ---- joint posterior
   if (!s.batch_call && s.ensemble) {
@@ -816,9 +684,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   } else if (s.nboot == 0) {
     // logBootBatchPosterior with Nboot = 0 returns zeros (src/jpmatLogBoot.cpp:469-497)
     HCHK(hipMemsetAsync(s.jp, 0, sizeof(double) * (size_t)N * G, st));
-  } else if (qpath) {
-    cx->st_boot_path = 2;
-    RCHK(run_bootq(cx, s, u, ta, ncols, GS, draws, W, ndraw, Bq, qstride, keep_T));
   } else {
     if (!fused) make_draws(s, Bp, draws, W, ndraw);
     RCHK(upload(cx, cx->Wt, W.data(), sizeof(double) * W.size()));
@@ -952,9 +817,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         }
         HCHK(launch_boot_tiles(b2, tb, st));
         if (cx->opt_skip_stats) {
-          int h[8];
-          HCHK(hipMemcpyAsync(h, cx->qflags.p, sizeof(int) * 8, hipMemcpyDeviceToHost, st));
+          int h[40];
+          HCHK(hipMemcpyAsync(h, cx->qflags.p, sizeof(int) * 40, hipMemcpyDeviceToHost, st));
           HCHK(hipStreamSynchronize(st));
+          for (int i = 0; i <= scde_ctx::kQMaxTilesHost; ++i) cx->st_tile_hist[i] += h[8 + i];
           cx->st_skip_slabs += h[2];
           cx->st_skip_kept += h[3];
           cx->st_skip_stretches += h[4];
@@ -1220,8 +1086,6 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   if (!ctx || !name) return fail(SCDE_EARG, "null argument");
   const std::string n(name);
   if (n == "boot_skip") ctx->opt_boot_skip = value != 0;
-  else if (n == "boot_q") ctx->opt_boot_q = (int)value;
-  else if (n == "boot_q_cells") ctx->opt_boot_q_cells = (int)value;
   else if (n == "skip_slack") ctx->opt_skip_slack = value;
   else if (n == "boot_nb") ctx->opt_boot_nb = (int)value;
   else if (n == "skip_stats") ctx->opt_skip_stats = value != 0;
@@ -1231,6 +1095,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "boot_tiles") ctx->opt_boot_tiles = value != 0;
   else if (n == "boot_tiles_cells") ctx->opt_boot_tiles_cells = (int)value;
   else if (n == "tile_groups") ctx->opt_tile_groups = (int)value;
+  else if (n == "tile_max_mult") ctx->opt_tile_max_mult = (int)value;
   else if (n == "tile_order") ctx->opt_tile_order = value != 0;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
@@ -1243,7 +1108,6 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "skip_stretches") *value = ctx->st_skip_stretches;
   else if (n == "skip_kept") *value = ctx->st_skip_kept;
   else if (n == "boot_f64_fma") *value = ctx->st_boot_f64_fma;
-  else if (n == "boot_i8_mac") *value = ctx->st_boot_i8_mac;
   else if (n == "boot_path") *value = ctx->st_boot_path;
   else if (n == "skip_redo") *value = ctx->st_skip_redo;
   else if (n == "degen") *value = ctx->st_degen;
@@ -1256,7 +1120,7 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
 int scde_ctx_reset_stats(scde_ctx* ctx) {
   if (!ctx) return fail(SCDE_EARG, "null argument");
   ctx->st_skip_slabs = ctx->st_skip_kept = ctx->st_skip_stretches = ctx->st_skip_redo = ctx->st_degen = 0;
-  ctx->st_boot_f64_fma = ctx->st_boot_i8_mac = 0;
+  ctx->st_boot_f64_fma = 0;
   for (double& x : ctx->st_tile_hist) x = 0;
   return SCDE_OK;
 }

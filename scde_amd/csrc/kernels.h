@@ -84,12 +84,9 @@ struct TablesArgs {
   // stretch j, max_j T (phase 1) or max_j T - max_j T[baseline column] (phase 2; the
   // maximum itself where the cell has no baseline); 0 for the pad column.  [ncols + 1][8]
   double* U;
-  // Fixed-point bootstrap (k_bootq, bootq.hip) instead of D / U: each value r becomes
-  // q = round(r * 2^kQFrac) clamped to [-2^kQSatLog2, 0] (r <= 0 always; NaN -> 0 and
-  // *nanflag = 1); phase-1 columns store q, phase-2 columns q - q[base column] (exact), as
-  // seven balanced base-256 digits packed in a u64 (packq); UQ holds per 16-point tile the
-  // column's maximum rounded up to 2^-8 as four packed digits.  Pad lanes and column ncols: 0.
-  unsigned long long* DQ;  // [ncols + 1][GS]
+  // k_boot_tiles' tile bounds (phase 2; nullable): per 16-point tile the column's maximum in
+  // units of 2^-8, rounded up, as four balanced base-256 digits (packu); phase-2 columns
+  // store it minus their baseline column's value.  Pad column: 0.  A NaN sets *nanflag.
   unsigned* UQ;            // [ncols + 1][kQTiles]
   int* nanflag;
   // nullable: the launch does nothing unless *gate != 0 (the exact fallback's T tables are
@@ -100,50 +97,13 @@ struct TablesArgs {
   int slow_only;
 };
 
-// ---- fixed-point bootstrap constants (bootq.hip)
-constexpr int kQFrac = 36;                 // fractional bits of the fixed-point log posteriors
-constexpr int kQSatLog2 = 54;              // |q| <= 2^54: values below -2^18 saturate
-constexpr double kQSat = 262144.0;         // 2^(kQSatLog2 - kQFrac)
-constexpr int kQTiles = 32;                // 16-point grid tiles per column (G <= 448 uses <= 28)
-constexpr int kQUFrac = 8;                 // fractional bits of the tile bounds
-constexpr unsigned long long kQBias = 0x0080808080808080ull;
-__host__ __device__ inline unsigned long long packq(long long d) {  // |d| < 2^55: 7 balanced digits
-  return ((unsigned long long)d + kQBias) ^ kQBias;
-}
-__host__ __device__ inline long long unpackq(unsigned long long p) { return (long long)(p ^ kQBias) - (long long)kQBias; }
+// ---- k_boot_tiles' integer tile bounds
+constexpr int kQTiles = 32;  // 16-point grid tiles per column (G <= 448 uses <= 28)
 __host__ __device__ inline unsigned packu(int u) { return ((unsigned)u + 0x80808080u) ^ 0x80808080u; }  // |u| < 2^31
 __host__ __device__ inline int unpacku(unsigned p) { return (int)((p ^ 0x80808080u) - 0x80808080u); }
-
-struct BootQArgs {
-  const unsigned long long* DQ;  // [ncols + 1][GS] packed digits (TablesArgs::DQ)
-  const unsigned* UQ;            // [ncols + 1][kQTiles]
-  const int2* ent;               // [ngenes][ent_stride] (cell, column), rows padded to a multiple of 64
-  const int* nnz;
-  int ent_stride;
-  const unsigned char* W8T;  // [nsets][Bp][ncells] draw multiplicities (<= 127)
-  int Bp, ncells;
-  const int* wset;
-  const int* Zq;   // [nsets][7][GS][Bp] baseline digit sums
-  const int* ZUq;  // [nsets][4][kQTiles][Bp] baseline tile-bound digit sums
-  int G, GS, nboot;
-  double norm_mult;
-  double slack;  // NaN: 30 + 0.4 C
-  double* out;
-  long long out_g, out_k;
-  int* degen;     // [ngenes]
-  int* ndegen;    // genes flagged (gates the exact fallback)
-  const int* nanflag;
-  int ngenes;
-  int* stats;     // nullable: [0] slabs, [1] tiles kept, [2] tiles (slabs x NT), [3] post-check rounds,
-                  // [4 + n] slabs computing n tiles (n <= 28)
-};
-hipError_t launch_zq(const unsigned long long* DQ, int G, int GS, const int* base_col, int ncells,
-                     const unsigned char* W8, int Bp, int nsets, int* Zq, hipStream_t s);
+// ZUq[set][l][t][Bp]: the baseline cells' part of the tile bounds (four digits l)
 hipError_t launch_zuq(const unsigned* UQ, const int* base_col, int ncells, const unsigned char* W8, int Bp, int nsets,
                       int* ZUq, hipStream_t s);
-hipError_t launch_bootq(const BootQArgs& a, hipStream_t s);
-size_t bootq_lds_bytes(int ent_stride);
-
 
 struct BootArgs {
   const double* T;  // [ncols][GS]
@@ -204,7 +164,8 @@ struct TileBootArgs {
   const int* nanflag;        // tables saw a NaN: every slab goes to k_boot2
   int maxgroups;             // register groups of 4 tiles (1 or 2)
   int* stats;                // nullable: [0] slabs, [1] tiles computed, [2] tiles, [3] slabs left to k_boot2,
-                             // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left
+                             // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left,
+                             // [6 + i] slabs that computed i tiles (i <= 28)
   const int* order;          // nullable: genes in this order (launch_gene_order)
   unsigned* pmask;           // [ngenes][P] tiles each slab's partial row holds (k_sum_partials reads those)
 };
@@ -274,7 +235,7 @@ hipError_t launch_stretch_zu(const double* U, const int* base_col, int ncells, c
 hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells, const unsigned char* has_clamp,
                             int use_baseline, int* base_col, hipStream_t s);
 // padto 8: rows padded to a multiple of 8 plus one batch of 8 (k_boot2's look-ahead); 64: to a
-// multiple of 64 (k_bootq's MFMA K steps)
+// multiple of 64 plus 8 (k_boot_tiles' bound MFMAs take 64-entry steps)
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
                       const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s);
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,

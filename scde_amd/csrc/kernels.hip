@@ -197,13 +197,13 @@ __device__ __forceinline__ float gt_maxf(float a, float b) { return (b > a) ? b 
 // One (cell, unique count) column, one wavefront, lanes over grid points.  The per-cell
 // grid vectors (mu, pq, lcfpr, lcfp, theta) and the baseline column come in as pointers:
 // global memory (k_tables) or an LDS copy staged once per cell (k_tables_cell).
-template <bool CT, bool Q>
+template <bool CT>
 __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col, int c, int phase,
                                               const double* __restrict__ mu, const double* __restrict__ P,
                                               const double* __restrict__ lcfpr, const double* __restrict__ lcfp,
                                               const double* __restrict__ cfpl, const unsigned* __restrict__ uqb,
                                               const double* __restrict__ th, const double* __restrict__ base,
-                                              const long long* __restrict__ qbase, double* __restrict__ v,
+                                              double* __restrict__ v,
                                               const double* etab, const LogTab& lt, int lane, int PS) {
   const int G = a.G;
   const double x = (double)a.ucl[col];
@@ -311,22 +311,18 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   bool clamp = false;
   double* out = a.T ? a.T + col * a.GS : nullptr;
   // fused delta (phase 2): D = T - T[baseline column of the cell], as k_delta computes it
-  double* dout = (!Q && phase && a.D) ? a.D + col * a.GS : nullptr;
+  double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
   const int bc_u = (phase == 2) ? a.base_col[c] : -1;
   // per 64-point stretch j (grid points 64j .. 64j+63, one k_boot2 wave each): the
   // column's maximum, for k_boot2's stretch bounds (U: raw maxima for phase-1 columns,
   // maxima minus the cell's baseline-column maxima for phase-2 columns)
-  double* const U = Q ? nullptr : a.U;
+  double* const U = a.U;
   const double* ubase = (U && bc_u >= 0) ? U + (long long)bc_u * kStretchSlots : nullptr;
-  // fixed-point output (k_bootq): q, or q - q[base] in phase 2; the row of final digits'
-  // values (int64) for the tile bounds
-  unsigned long long* qout = (Q && phase) ? a.DQ + col * a.GS : nullptr;
-  long long* vq = reinterpret_cast<long long*>(v);
   bool nanq = false;
   // FP64 tile bounds for k_boot_tiles (UQ set, fused phases): per 16-point tile the column's
   // maximum in units of 2^-8, rounded up; phase-2 columns store it minus their baseline
   // column's value (exact integers, so base + delta >= the column's maximum)
-  const bool uqf = !Q && a.UQ && phase;
+  const bool uqf = a.UQ && phase;
 #pragma unroll 1
   for (int j = 0; 64 * j < G; ++j) {
     const int k = lane + 64 * j;
@@ -363,18 +359,6 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
       }
       if (U) v[k] = r;  // the row of final values, for the stretch maxima below
       if (uqf && r != r) nanq = true;
-      if (qout) {
-        long long q = 0;
-        if (r != r)
-          nanq = true;
-        else if (r < -kQSat)
-          q = -(1LL << kQSatLog2);
-        else if (r < 0.0)
-          q = __double2ll_rn(r * 0x1p36);  // exact scaling by 2^kQFrac, one rounding
-        const long long d = qbase ? q - qbase[k] : q;
-        qout[k] = packq(d);
-        vq[k] = d;
-      }
     }
     if (uqf) {
       // this chunk's four 16-point tiles (one 16-lane row each): the maximum in units of
@@ -389,25 +373,6 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
           u -= unpacku(uqb ? uqb[t] : a.UQ[(long long)bc_u * kQTiles + t]);
         a.UQ[col * kQTiles + t] = packu(u);
       }
-    }
-  }
-  if (qout) {
-    if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
-    for (int k = G + lane; k < a.GS; k += 64) qout[k] = 0ull;
-    // per 16-point tile: the maximum of the stored values, rounded up to 2^-kQUFrac (two
-    // lanes per tile, 8 points each); tiles past the grid: 0
-    const int nt = (G + 15) / 16, t = lane >> 1;
-    long long m = LLONG_MIN;
-    if (t < nt)
-      for (int i = 0; i < 8; ++i) {
-        const int k = 16 * t + 8 * (lane & 1) + i;
-        if (k < G) m = vq[k] > m ? vq[k] : m;
-      }
-    const long long o = __shfl_xor(m, 1, 64);
-    m = o > m ? o : m;
-    if ((lane & 1) == 0) {
-      const int u = (t < nt) ? (int)(-((-m) >> (kQFrac - kQUFrac))) : 0;  // ceil(m / 2^28)
-      a.UQ[col * kQTiles + t] = packu(u);
     }
   }
   if (uqf) {
@@ -463,7 +428,7 @@ __device__ __forceinline__ void tables_tabs(double* etab, double (*ltab)[97]) {
 
 // Column-per-wave form, grid vectors read from global memory: phase 1 (one wave per
 // cell, its count-0 column) and grids too wide for the staged kernel.
-template <bool CT, bool Q>
+template <bool CT>
 __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   extern __shared__ double vrow[];  // [4 waves][GS]
   __shared__ double etab[64];
@@ -516,18 +481,16 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
           const long long co = (long long)lo * a.GS;
           const int bc = (phase == 2) ? a.base_col[lo] : -1;
           const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
-          tables_column<CT, Q>(a, cs, lo, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
-                               a.lcfp + co, nullptr, nullptr, a.theta + co, base, nullptr,
-                               vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
+          tables_column<CT>(a, cs, lo, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
+                            a.lcfp + co, nullptr, nullptr, a.theta + co, base, vrow + (long long)wid * a.GS, etab,
+                            lt, lane, a.GS);
         }
       }
       return;
     }
     if (phase == 2 && col == a.ncols) {  // the ELL pad column
-      for (int k = lane; k < a.GS; k += 64) {
+      for (int k = lane; k < a.GS; k += 64)
         if (a.D) a.D[col * a.GS + k] = 0.0;
-        if (a.DQ) a.DQ[col * a.GS + k] = 0ull;
-      }
       if (a.U && lane < kStretchSlots) a.U[col * kStretchSlots + lane] = 0.0;
       if (a.UQ && lane < kQTiles) a.UQ[col * kQTiles + lane] = 0u;
       return;
@@ -544,8 +507,9 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   const long long co = (long long)c * a.GS;
   const int bc = (phase == 2) ? a.base_col[c] : -1;
   const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
-  tables_column<CT, Q>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
-                       a.lcfp + co, nullptr, nullptr, a.theta + co, base, nullptr, vrow + (long long)wid * a.GS, etab, lt, lane, a.GS);
+  tables_column<CT>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
+                    a.lcfp + co, nullptr, nullptr, a.theta + co, base, vrow + (long long)wid * a.GS, etab, lt, lane,
+                    a.GS);
 }
 
 // Cell-staged form (phases 0 and 2, G <= kTabStagedG): one 8-wave block per task
@@ -556,7 +520,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
 // blocks fit a CU: (8 + 9) * G * 8 B = 54.5 KB at G = 401.
 constexpr int kTabStagedG = 448;
 constexpr int kTabWaves = 8;
-template <bool CT, bool Q>
+template <bool CT>
 __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TAB_WPE))) void k_tables_cell(TablesArgs a) {
   extern __shared__ double dyn[];  // vrow [8][G] | mu | P[4] | lcfpr | cfp | th | base, each G
   __shared__ double etab[64];
@@ -571,10 +535,8 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   const int phase = a.phase;
   if (c < 0) {  // the ELL pad column (phase 2)
     if (wid == 0) {
-      for (int k = lane; k < GS; k += 64) {
+      for (int k = lane; k < GS; k += 64)
         if (a.D) a.D[a.ncols * GS + k] = 0.0;
-        if (a.DQ) a.DQ[a.ncols * GS + k] = 0ull;
-      }
       if (a.U && lane < kStretchSlots) a.U[a.ncols * kStretchSlots + lane] = 0.0;
       if (a.UQ && lane < kQTiles) a.UQ[a.ncols * kQTiles + lane] = 0u;
     }
@@ -589,7 +551,7 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   double* sbase = sth + G;
   const long long co = (long long)c * GS;
   const int bc = (phase == 2) ? a.base_col[c] : -1;
-  if (bc >= 0 && !Q && a.UQ && threadIdx.x < kQTiles) suqb[threadIdx.x] = a.UQ[(long long)bc * kQTiles + threadIdx.x];
+  if (bc >= 0 && a.UQ && threadIdx.x < kQTiles) suqb[threadIdx.x] = a.UQ[(long long)bc * kQTiles + threadIdx.x];
   for (int k = threadIdx.x; k < G; k += 64 * kTabWaves) {
     smu[k] = a.mu[co + k];
     slr[k] = a.lcfpr[co + k];
@@ -602,22 +564,15 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
       sP[2 * G + k] = P[2 * GS + k];
       sP[3 * G + k] = P[3 * GS + k];
     }
-    if (bc >= 0) {
-      if (Q)
-        reinterpret_cast<long long*>(sbase)[k] = unpackq(a.DQ[(long long)bc * GS + k]);
-      else
-        sbase[k] = a.D[(long long)bc * GS + k];
-    }
+    if (bc >= 0) sbase[k] = a.D[(long long)bc * GS + k];
   }
   __syncthreads();
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
   const int zc = (phase == 2) ? a.zcol[c] : -1;
   for (int col = task.y + wid; col < task.z; col += kTabWaves) {
     if (col == zc) continue;  // done in phase 1
-    tables_column<CT, Q>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, nullptr, slc, (bc >= 0) ? suqb : nullptr, sth,
-                         (bc >= 0 && !Q) ? sbase : nullptr,
-                         (bc >= 0 && Q) ? reinterpret_cast<const long long*>(sbase) : nullptr, dyn + wid * G, etab,
-                         lt, lane, G);
+    tables_column<CT>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, nullptr, slc, (bc >= 0) ? suqb : nullptr, sth,
+                      (bc >= 0) ? sbase : nullptr, dyn + wid * G, etab, lt, lane, G);
   }
 }
 
@@ -1900,6 +1855,33 @@ __global__ __launch_bounds__(512) void k_boot2_list(
   }
 }
 
+// ------------------------------------------------------------------ baseline tile-bound sums
+// ZUq[set][l][t][Bp] = sum over the cells with a baseline column of W8[set][c][b] *
+// digit_l(UQ[bc][t]), l < 4: the baseline cells' part of k_boot_tiles' integer tile bounds.
+// Block per (set, 32 boots, chunk of kZChunk cells); thread = (tile, boot); global atomics
+// (exact integers, order-free; ZUq is zeroed first).
+constexpr int kZChunk = 64;
+__global__ __launch_bounds__(1024) void k_zuq(const unsigned* __restrict__ UQ, const int* __restrict__ base_col,
+                                              int ncells, const unsigned char* __restrict__ W8, int Bp,
+                                              int* __restrict__ ZUq) {
+  const int nch = (ncells + kZChunk - 1) / kZChunk;
+  const int t = threadIdx.x >> 5, b = blockIdx.x * 32 + (threadIdx.x & 31), set = blockIdx.y / nch;
+  const int c0 = (blockIdx.y % nch) * kZChunk, c1 = min(ncells, c0 + kZChunk);
+  const unsigned char* W = W8 + (long long)set * ncells * Bp + b;
+  int acc[4] = {0, 0, 0, 0};
+  for (int c = c0; c < c1; ++c) {
+    const int bc = base_col[c];
+    if (bc < 0) continue;
+    const int w = W[(long long)c * Bp];
+    const unsigned u = UQ[(long long)bc * kQTiles + t];
+#pragma unroll
+    for (int l = 0; l < 4; ++l) acc[l] += w * (int)(signed char)(u >> (8 * l));
+  }
+#pragma unroll
+  for (int l = 0; l < 4; ++l)
+    if (acc[l]) atomicAdd(ZUq + (((long long)set * 4 + l) * kQTiles + t) * Bp + b, acc[l]);
+}
+
 // ------------------------------------------------------------------ tile bootstrap
 // k_boot_tiles: k_boot2's FP64 bootstrap computed only where it matters, on 16-point grid
 // tiles chosen per (gene, boot slab) from exact integer bounds.  One wave per (gene, slab);
@@ -2334,6 +2316,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     atomicAdd(&stats[1], __builtin_popcount(done));
     atomicAdd(&stats[2], NT);
     atomicAdd(&stats[4], ng * ((n + 3) & ~3));
+    atomicAdd(&stats[6 + __builtin_popcount(done)], 1);  // histogram of tiles computed per slab
   }
 }
 
@@ -3103,9 +3086,8 @@ hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long
 
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   if (a.ncols <= 0 && a.phase != 2) return hipSuccess;
-  if (a.phase != 0 && ((!a.D && !a.DQ) || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
-  if (a.DQ && (!a.UQ || !a.nanflag || a.G > kTabStagedG)) return hipErrorInvalidValue;
-  if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG && a.const_theta && !a.DQ && a.colc && a.pq &&
+  if (a.phase != 0 && (!a.D || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
+  if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG && a.const_theta && a.colc && a.pq &&
       a.ncols > 0) {
     // register-row kernel, then the columns it leaves (rare; the launch exits at once unless
     // k_col_consts flagged one) by the column-per-wave kernel
@@ -3131,23 +3113,16 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
     const size_t shm = sizeof(double) * 4 * (size_t)a.GS;
     if (shm > 64 * 1024) return hipErrorInvalidValue;
     const long long nblk = std::min<long long>(1024, div_up(div_up(a.ncols, 64), 4));
-    hipLaunchKernelGGL((k_tables<true, false>), dim3(nblk), dim3(256), shm, s, b);
+    hipLaunchKernelGGL((k_tables<true>), dim3(nblk), dim3(256), shm, s, b);
     return hipGetLastError();
   }
   if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG) {
     const size_t shm = sizeof(double) * (kTabWaves + 9) * (size_t)a.G;
     const dim3 grid(a.ntasks), block(64 * kTabWaves);
-    if (a.const_theta) {
-      if (a.DQ)
-        hipLaunchKernelGGL((k_tables_cell<true, true>), grid, block, shm, s, a);
-      else
-        hipLaunchKernelGGL((k_tables_cell<true, false>), grid, block, shm, s, a);
-    } else {
-      if (a.DQ)
-        hipLaunchKernelGGL((k_tables_cell<false, true>), grid, block, shm, s, a);
-      else
-        hipLaunchKernelGGL((k_tables_cell<false, false>), grid, block, shm, s, a);
-    }
+    if (a.const_theta)
+      hipLaunchKernelGGL((k_tables_cell<true>), grid, block, shm, s, a);
+    else
+      hipLaunchKernelGGL((k_tables_cell<false>), grid, block, shm, s, a);
     return hipGetLastError();
   }
   const long long nwaves = a.phase == 1 ? a.ncells : a.phase == 2 ? a.ncols + 1 : a.ncols;
@@ -3155,17 +3130,20 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   const dim3 grid(div_up(nwaves, 4)), block(256);
   const size_t shm = sizeof(double) * 4 * (size_t)a.GS;
   if (shm > 64 * 1024) return hipErrorInvalidValue;
-  if (a.const_theta) {
-    if (a.DQ)
-      hipLaunchKernelGGL((k_tables<true, true>), grid, block, shm, s, a);
-    else
-      hipLaunchKernelGGL((k_tables<true, false>), grid, block, shm, s, a);
-  } else {
-    if (a.DQ)
-      hipLaunchKernelGGL((k_tables<false, true>), grid, block, shm, s, a);
-    else
-      hipLaunchKernelGGL((k_tables<false, false>), grid, block, shm, s, a);
-  }
+  if (a.const_theta)
+    hipLaunchKernelGGL((k_tables<true>), grid, block, shm, s, a);
+  else
+    hipLaunchKernelGGL((k_tables<false>), grid, block, shm, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_zuq(const unsigned* UQ, const int* base_col, int ncells, const unsigned char* W8, int Bp, int nsets,
+                      int* ZUq, hipStream_t s) {
+  if (Bp % 32) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(ZUq, 0, sizeof(int) * (size_t)nsets * 4 * kQTiles * Bp, s);
+  if (e != hipSuccess) return e;
+  const int nch = (ncells + kZChunk - 1) / kZChunk;
+  hipLaunchKernelGGL(k_zuq, dim3(Bp / 32, nsets * nch), dim3(1024), 0, s, UQ, base_col, ncells, W8, Bp, ZUq);
   return hipGetLastError();
 }
 

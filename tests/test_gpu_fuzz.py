@@ -7,9 +7,8 @@ Cases draw: genes 1-60, cells per group 1-35 (groups of unequal size), NA-group 
 counts from a zero-inflated negative binomial with occasional huge counts, models
 resampled from the es.mef (6-column) or knn (12-column: local theta, squared-logit
 concentration) fixtures, n.randomizations in {1, 2, 7, 20, 33}, n.cores in {1, 2, 5},
-prior length.out in {60, 401}.  Every case runs through the bootstrap kernels: the FP64
-k_boot2 (or k_boot_tiles from 200 cells), k_boot_tiles at every size (boot_tiles_cells 0) and the
-fixed-point int8-MFMA k_bootq (boot_q 2).
+prior length.out in {60, 401}.  Every case runs through the bootstrap kernels: k_boot2 (or
+k_boot_tiles from 200 cells), and k_boot_tiles at every size (boot_tiles_cells 0).
 """
 import numpy as np
 import pytest
@@ -43,7 +42,7 @@ def _case(seed):
         length_out=int(rng.choice([60, 400])))
 
 
-@pytest.mark.parametrize("opts", [{}, {"boot_tiles_cells": 0}, {"boot_q": 2}], ids=["default", "tiles", "q"])
+@pytest.mark.parametrize("opts", [{}, {"boot_tiles_cells": 0}], ids=["default", "tiles"])
 @pytest.mark.parametrize("seed", range(NCASES))
 def test_expression_difference_fuzz(seed, opts):
     from oracle import oracle as O
@@ -61,7 +60,6 @@ def test_expression_difference_fuzz(seed, opts):
                                              n_randomizations=kw["n_randomizations"], n_cores=kw["n_cores"],
                                              return_posteriors=True)
     finally:
-        ctx.set_option("boot_q", 0)
         ctx.set_option("boot_tiles_cells", 200)
     # the oracle takes factor codes (level order a < b, NA = -1), the api R-style labels
     codes = np.array([{"a": 0, "b": 1, None: -1}[v] for v in glist])

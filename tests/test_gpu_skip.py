@@ -4,16 +4,16 @@ The skipping is an optimisation that must not change results: a 64-point stretch
 left out of a boot slab when a rigorous upper bound of its row values stays more than 51
 below the exact row maximum (post-check), i.e. when every softmax term there falls under
 the e^-50 cut that zeroes it anyway; any slab that fails the check is recomputed whole.
-These tests run the same calls, for the bootstrap kernels (the fixed-point k_bootq with
-16-point tiles, boot_q = 2; the FP64 k_boot_tiles on bounded 16-point tiles, boot_q = 0; the
-FP64 k_boot2 with its 64-point stretch mask, boot_tiles = 0), with skipping on (default), off
-(boot_skip = 0), and forced onto the second-chance path so that the extra work really
-happens (its count is read back and must be > 0): a negative heuristic slack (skip_slack)
-that makes the masks drop tiles the post-check must reject, or k_boot_tiles limited to one
-register group (tile_groups = 1) so slabs needing more tiles go to k_boot2's redo launch --
-and compare every run with the oracle at the SURVEY §8(d) bar, and the runs of one
-arithmetic with each other bit for bit (the FP64 kernels share rows, maxima and
-tile-ordered sums).
+These tests run the same calls, for the bootstrap kernels (k_boot_tiles on bounded 16-point
+tiles, the default; k_boot2 with its 64-point stretch mask, boot_tiles = 0), with skipping on
+(default), off (boot_skip = 0), and forced onto the second-chance paths so that the extra work
+really happens (its count is read back and must be > 0): a negative heuristic slack
+(skip_slack) that makes the masks drop stretches the post-check must reject, k_boot_tiles
+limited to one register group (tile_groups = 1) so slabs needing more tiles go to k_boot2's
+redo launch, or a multiplicity limit of 1 (tile_max_mult) so the call, with its tables set up
+for the tile path, runs plain k_boot2 instead (the "multiplicity above 127" fallback) -- and
+compare every run with the oracle at the SURVEY §8(d) bar, and the runs with each other bit
+for bit (the kernels share rows, maxima and tile-ordered sums).
 """
 import math
 
@@ -34,8 +34,8 @@ def api():
 
 def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx = api.default_context()
-    ctx.set_option("boot_q", opts.get("boot_q", 2))
     ctx.set_option("boot_skip", opts.get("boot_skip", 1))
+    ctx.set_option("tile_max_mult", opts.get("tile_max_mult", 127))
     ctx.set_option("skip_slack", opts.get("skip_slack", math.nan))
     ctx.set_option("boot_tiles", opts.get("boot_tiles", 1))
     ctx.set_option("tile_groups", opts.get("tile_groups", 2))
@@ -47,9 +47,9 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     try:
         out = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=nrand,
                                              n_cores=ncores, return_posteriors=True)
-        stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo")}
+        stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo", "boot_path")}
     finally:
-        ctx.set_option("boot_q", 0)
+        ctx.set_option("tile_max_mult", 127)
         ctx.set_option("boot_skip", 1)
         ctx.set_option("skip_slack", math.nan)
         ctx.set_option("boot_tiles", 1)
@@ -69,29 +69,28 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
     ref = oracle.scde_expression_difference(models, counts, prior["x"], prior["y"], groups, n_randomizations=nrand,
                                             n_cores=ncores, return_posteriors=True)
     runs = {
-        "skip": {},
+        "tiles": {},
         "noskip": {"boot_skip": 0},
-        "forced-redo": {"skip_slack": -45.0},
-        "fp64": {"boot_q": 0},
-        "fp64-noskip": {"boot_q": 0, "boot_skip": 0},
-        "fp64-forced-redo": {"boot_q": 0, "tile_groups": 1},
-        "fp64-unordered": {"boot_q": 0, "tile_order": 0},
-        "fp64-stretch": {"boot_q": 0, "boot_tiles": 0},
-        "fp64-stretch-forced-redo": {"boot_q": 0, "boot_tiles": 0, "skip_slack": -45.0},
+        "tiles-forced-redo": {"tile_groups": 1},
+        "tiles-unordered": {"tile_order": 0},
+        "tiles-mult-fallback": {"tile_max_mult": 1},
+        "stretch": {"boot_tiles": 0},
+        "stretch-forced-redo": {"boot_tiles": 0, "skip_slack": -45.0},
     }
     got = {}
     for name, opts in runs.items():
         got[name], stats = _run(api, opts, models, counts, prior, groups, nrand, ncores)
-        if name == "fp64-noskip":
-            assert stats["skip_slabs"] == 0
-        elif name == "noskip":
-            assert stats["skip_slabs"] > 0 and stats["skip_kept"] == stats["skip_stretches"], stats
-        elif name == "fp64-forced-redo":  # one register group: slabs needing > 4 tiles all go to k_boot2
-            assert stats["skip_redo"] > 0, stats
+        if name == "noskip":
+            assert stats["skip_slabs"] == 0 and stats["boot_path"] == 0, stats
+        elif name == "tiles-mult-fallback":  # plain k_boot2 on the tile path's columns, no skipping
+            assert stats["boot_path"] == 0 and stats["skip_slabs"] == 0, stats
+        elif name == "tiles-forced-redo":  # one register group: slabs needing > 4 tiles go to k_boot2
+            assert stats["boot_path"] == 1 and stats["skip_redo"] > 0, stats
         else:
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
+            assert stats["boot_path"] == (0 if name.startswith("stretch") else 1), (name, stats)
         if name.endswith("forced-redo"):
-            assert stats["skip_redo"] > 0, stats  # the post-check really adds work
+            assert stats["skip_redo"] > 0, stats  # the second-chance path really adds work
         g = got[name]
         for i in range(2):
             assert_posterior_close(g["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"{name} jp{i}")
@@ -102,9 +101,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"], what=f"{name} Z")
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
-    for base, others in (("skip", ("noskip", "forced-redo")),
-                         ("fp64", ("fp64-noskip", "fp64-forced-redo", "fp64-unordered", "fp64-stretch",
-                                  "fp64-stretch-forced-redo"))):
+    for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-unordered", "tiles-mult-fallback",
+                                    "stretch", "stretch-forced-redo")),):
         for name in others:
             for i in range(2):
                 np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got[base]["joint.posteriors"][i])

@@ -12,5 +12,5 @@ for d in "$@"; do
 done
 wait
 for d in "$@"; do
-  hipcc -shared -fPIC --offload-arch=gfx950 -o ../../build_diag/libd$d.so ../../build_diag/kernels_d$d.o bootq.o engine.o bh.o prior.o wpca.o pagoda.o
+  hipcc -shared -fPIC --offload-arch=gfx950 -o ../../build_diag/libd$d.so ../../build_diag/kernels_d$d.o engine.o bh.o prior.o wpca.o pagoda.o
 done

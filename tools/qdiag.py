@@ -1,5 +1,5 @@
 """Bootstrap diagnostics on the GPU box: kept-tile statistics and per-slot kernel times of one
-config's DE call under a few context options (fixed-point vs FP64 kernels, skipping off).
+config's DE call under a few context options (tile vs stretch bootstrap, skipping off).
 
   python tools/qdiag.py [config] [option=value ...]
 """
@@ -49,11 +49,11 @@ def main():
             api.check(L.scde_posteriors_dev(ctx.handle, dc.ptr, NG, NG, P(cellidx), NC, P(mm), lt, sq, P(px), 401,
                                             100, 1, 0, NG, 1, 0, None, None, None, 0, P(jp), P(modes), None))
 
-    variants = [("tiles", {}), ("stretch", {"boot_tiles": 0}), ("q", {"boot_q": 2}), ("noskip", {"boot_skip": 0})]
+    variants = [("tiles", {}), ("stretch", {"boot_tiles": 0}), ("noskip", {"boot_skip": 0})]
     if extra:
         variants = [("custom", {k: float(v) for k, v in extra.items()})]
     for name, opts in variants:
-        for k, v in (("boot_q", 0), ("boot_skip", 1), ("boot_tiles", 1)):
+        for k, v in (("boot_skip", 1), ("boot_tiles", 1)):
             ctx.set_option(k, v)
         for k, v in opts.items():
             ctx.set_option(k, v)
