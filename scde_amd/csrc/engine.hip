@@ -220,13 +220,34 @@ struct scde_ctx {
     Buf cellidx, cmax, cmin, woff, bits, rank, nuniq, ucl, ucl_off, uci;
     std::vector<int> cmax_h, cmin_h, nuniq_h;
     std::vector<long long> woff_h, ucl_off_h;
-    const int* pin_in = nullptr;  // pinned landing area of the phase's device -> host copy
+    // pinned landing area of the phases' device -> host size read-backs: the set's own (not
+    // the shared staging arena), so no later staging can recycle it before the host reads it
+    int* pin_land = nullptr;
+    size_t pin_land_cap = 0;  // ints
+    const int* pin_in = nullptr;  // this phase's read-back (pin_land, or null: pageable fallback)
     std::vector<int4> tasks_h;  // cell-staged tables tasks (k_tables_cell)
     Buf tasks;
     bool ready = false;
+    int* landing(size_t n) {
+      if (n > pin_land_cap) {
+        if (pin_land) (void)hipHostFree(pin_land);
+        pin_land = nullptr;
+        pin_land_cap = 0;
+        if (hipHostMalloc(reinterpret_cast<void**>(&pin_land), sizeof(int) * n, hipHostMallocDefault) != hipSuccess) {
+          pin_land = nullptr;
+          (void)hipGetLastError();
+          return nullptr;
+        }
+        pin_land_cap = n;
+      }
+      return pin_land;
+    }
     void release() {
       Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci, &tasks};
       for (Buf* x : b) x->release();
+      if (pin_land) (void)hipHostFree(pin_land);
+      pin_land = nullptr;
+      pin_land_cap = 0;
     }
   } us[3];
   // profiling
@@ -360,9 +381,11 @@ char* pin_alloc(scde_ctx* cx, size_t bytes) {
   }
   size_t off = (cx->pin_off + 255) & ~size_t(255);
   if (off + bytes > kPinCap) {
-    // reuse from the start: every copy staged so far (on any of the context's streams) must
-    // have landed first
-    if (hipDeviceSynchronize() != hipSuccess) return nullptr;
+    // reuse from the start: every host -> device copy staged so far must have been read out of
+    // the arena first; they are issued on the context's own two streams only (device -> host
+    // read-backs land in each unique set's own area, never here)
+    if (hipStreamSynchronize(cx->stream) != hipSuccess) return nullptr;
+    if (cx->copy_stream && hipStreamSynchronize(cx->copy_stream) != hipSuccess) return nullptr;
     off = 0;
   }
   cx->pin_off = off + bytes;
@@ -397,7 +420,7 @@ int unique_phase1(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   HCHK(launch_cell_minmax(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.cmax.as<int>(), u.cmin.as<int>(), st));
   u.cmax_h.assign(C, 0);
   u.cmin_h.assign(C, 0);
-  int* h = reinterpret_cast<int*>(pin_alloc(cx, sizeof(int) * 2 * (size_t)C));
+  int* h = u.landing(2 * (size_t)C);
   u.pin_in = h;
   HCHK(hipMemcpyAsync(h ? h : u.cmax_h.data(), u.cmax.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
   HCHK(hipMemcpyAsync(h ? h + C : u.cmin_h.data(), u.cmin.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
@@ -426,7 +449,7 @@ int unique_phase2(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   HCHK(launch_rank(u.bits.as<unsigned long long>(), u.woff.as<long long>(), C, u.rank.as<int>(),
                    u.nuniq.as<int>(), st));
   u.nuniq_h.assign(C, 0);
-  int* h = reinterpret_cast<int*>(pin_alloc(cx, sizeof(int) * (size_t)C));
+  int* h = u.landing(2 * (size_t)C);  // phase 1's values were copied out by now
   u.pin_in = h;
   HCHK(hipMemcpyAsync(h ? h : u.nuniq_h.data(), u.nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
   return SCDE_OK;

@@ -85,6 +85,11 @@ def expression_difference(models, counts, prior, groups, n_randomizations=150, n
 
     world = dist.get_world_size(process_group)
     rank = dist.get_rank(process_group)
+    on_device = dist.get_backend(process_group) == "nccl"
+    import os
+    if on_device and world > 1 and os.environ.get("SCDE_SAME_DEVICE") == "1":
+        raise RuntimeError("SCDE_SAME_DEVICE=1 puts every rank on GPU 0, which RCCL does not allow: "
+                           "rehearse the multi-rank path with the gloo backend")
     mat, genes = api._align_counts(models, counts)
     N = mat.shape[0]
     codes = api._groups_vector(models, groups)
@@ -99,7 +104,6 @@ def expression_difference(models, counts, prior, groups, n_randomizations=150, n
     per = -(-N // world)
     buf = torch.zeros((per, 5), dtype=torch.float64)
     buf[: hi - lo] = torch.from_numpy(np.ascontiguousarray(rows))
-    on_device = dist.get_backend(process_group) == "nccl"
     if on_device:
         buf = buf.to(torch.device("cuda", ctx.device if ctx is not None else rank_device(rank)))
     parts = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
@@ -108,8 +112,8 @@ def expression_difference(models, counts, prior, groups, n_randomizations=150, n
         return None
     rows_all = torch.cat([parts[r][: (lambda b: b[1] - b[0])(shard_range(N, world, r))] for r in range(world)])
     res = rows_all.cpu().numpy()
-    if ctx is not None and N > 0:
-        # BH over all genes on rank 0's GPU (scde_bh_cz_dev)
+    if on_device and ctx is not None and N > 0:
+        # the rows are on rank 0's GPU already (RCCL gather): BH over all genes there (scde_bh_cz_dev)
         z = rows_all[:, 4].contiguous().to(torch.device("cuda", ctx.device))
         cz = torch.empty_like(z)
         torch.cuda.current_stream(z.device).synchronize()
@@ -117,6 +121,7 @@ def expression_difference(models, counts, prior, groups, n_randomizations=150, n
         ctx.synchronize()
         czh = cz.cpu().numpy()
     else:
+        # gloo (host tensors): the library's host BH, no device tensor needed
         czh = api._bh(res[:, 4])
     return api._result_frame(np.asfortranarray(res), czh, genes)
 
