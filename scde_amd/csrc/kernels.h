@@ -168,6 +168,7 @@ struct TileBootArgs {
                              // [6 + i] slabs that computed i tiles (i <= 28)
   const int* order;          // nullable: genes in this order (launch_gene_order)
   unsigned* pmask;           // [ngenes][P] tiles each slab's partial row holds (k_sum_partials reads those)
+  int pass8;                 // 1: k_boot_tiles8 (8 tiles, two points per lane, one pass); 0: k_boot_tiles (4 + 4)
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending

@@ -2320,6 +2320,322 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   }
 }
 
+// ------------------------------------------------------------------ tile bootstrap, one pass
+// k_boot_tiles8: k_boot_tiles with two grid points per lane, so one wave holds 8 tiles
+// (128 points) of its (gene, slab) in a single pass: the 8 tiles with the largest exact
+// integer bounds (the same bounds as k_boot_tiles), then a post-check that every other tile
+// stays below m'_b - 51, else the slab goes whole to k_boot2's fallback launch.  Per ELL entry
+// one 16-byte column load (points k0, k0 + 1) and one 16-byte multiplicity load (DPP
+// broadcast) feed 2 NB FMAs -- half the vector-memory instructions per FMA of the 4-tile
+// form, whose waves are bound by the texture addresser -- and no second register group.
+// Lane l: tile slot l >> 3 (8 lanes per tile, two tiles per 16-lane row), points
+// 16 tile + 2 (l & 7) and + 1.  Each (boot, point) row is the same fma chain as k_boot2's;
+// a tile's partial sum adds the lane's two points, then partners lane^1, ^2 and the 8-lane
+// mirror: the operand pairs of row16_sum, so sums, maxima, terms and jp rows are k_boot2's bits.
+__device__ __forceinline__ double pair8_sum(double p0, double p1) {
+  double v = p0 + p1;
+  v += dpp_d<kDppXor1>(v);
+  v += dpp_d<kDppXor2>(v);
+  v += dpp_d<kDppHalfMirror>(v);
+  return v;
+}
+
+// one entry into the two points' NB accumulators: boots 2J, 2J + 1 from lane J of wv
+template <int NB, int... J>
+__device__ __forceinline__ void fmac_entry2(double (&a0)[NB], double (&a1)[NB], const d2_t& wv, const d2_t& x,
+                                            std::integer_sequence<int, J...>) {
+  ((fmac_bcast<J>(a0[2 * J], wv.x, x.x), fmac_bcast<J>(a1[2 * J], wv.x, x.y),
+    fmac_bcast<J>(a0[2 * J + 1], wv.y, x.x), fmac_bcast<J>(a1[2 * J + 1], wv.y, x.y)),
+   ...);
+}
+
+#ifndef SCDE_TILE8_WPE
+#define SCDE_TILE8_WPE 4  // 2 x NB accumulators (80 VGPRs at NB = 20) + two 2-entry load buffers
+#endif
+template <int NB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_WPE))) void k_boot_tiles8(
+    const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
+    const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
+    int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
+    long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8p, int Bq,
+    const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
+    int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
+  static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
+  __shared__ float ubs[4][kTileMax * NB];  // [wave][tile][boot] bounds
+  __shared__ float fmx[4][2][32];          // [wave][.][boot] maxima
+  __shared__ double tsum[4][8][NB];        // [wave][tile slot][boot] partial sums
+  __shared__ double finv[4][32];
+  __shared__ double etab[64];
+  const int lane = threadIdx.x & 63;
+  const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
+  __syncthreads();
+  const int item = blockIdx.x * 4 + wsid;
+  if (item >= ngenes * P) return;
+  const int gi = item / P, p = item - gi * P, b0 = p * NB;
+  const int g = order ? order[gi] : gi;
+  if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
+    if (lane == 0) {
+      redo[(long long)g * P + p] = 1;
+      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
+      pmask[(long long)g * P + p] = ~0u;
+    }
+    return;
+  }
+  const int n = nnz[g];
+  const int NT = (G + 15) >> 4;
+  const int nlive = min(NB, nboot - b0);
+  const int r = lane & 15, h = lane >> 4;
+  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  const int set = wset ? wset[g] : 0;
+  float* ub = ubs[wsid];
+  // ---- 1. tile bounds: exactly k_boot_tiles' (see there)
+  if (SCDE_TILE_DIAG & 2) {  // timing build: rows without bounds (results wrong)
+    for (int i = lane; i < kTileMax * NB; i += 64) ub[i] = 0.0f;
+  } else {
+    const unsigned pstride = 32u * (unsigned)P;
+    const unsigned char* __restrict__ W8 = W8p + (long long)set * ncells * pstride + 32 * p;
+    const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
+    const int KP = (n + 63) & ~63;
+    for (int tg = 0; 16 * tg < NT; ++tg) {
+      const int t = 16 * tg + r;
+      i32x4 acc[2][4];
+#pragma unroll
+      for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+        for (int l = 0; l < 4; ++l)
+          acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + b0 + 16 * bt + 4 * h);
+      for (int e0 = 0; e0 < KP; e0 += 64) {
+        int cl[16], co[16];
+        const int4* E4 = reinterpret_cast<const int4*>(E + e0 + 16 * h);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int4 x = E4[q];
+          cl[2 * q] = x.x;
+          co[2 * q] = x.y;
+          cl[2 * q + 1] = x.z;
+          co[2 * q + 1] = x.w;
+        }
+        unsigned u[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) u[j] = UQ[(unsigned)(co[j] * kQTiles + t)];
+        i32x4 af[2];
+        unsigned lo4[4], hi4[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          unsigned w2[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            w2[i] = *reinterpret_cast<const unsigned short*>(W8 + (unsigned)(cl[4 * q + i] * pstride) + 2 * r);
+          const unsigned x01 = w2[0] | (w2[1] << 16), x23 = w2[2] | (w2[3] << 16);
+          lo4[q] = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
+          hi4[q] = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
+        }
+        af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
+        af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
+        unsigned pl[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+          const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
+          acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
+          acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
+        }
+      }
+      if (t < NT)
+#pragma unroll
+        for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int b = 16 * bt + 4 * h + q;
+            if (b < NB) {
+              const long long v =
+                  (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
+              const double x = (double)v * 0x1p-8;
+              float f = (float)x;
+              if ((double)f < x) f = nextafterf(f, INFINITY);
+              ub[t * NB + b] = f;
+            }
+          }
+    }
+  }
+#if SCDE_TILE_DIAG & 1
+  return;  // timing build: bounds only
+#endif
+  wave_sync();
+  // ---- 2. the tiles with the largest bound over the slab's live boots: 8 (4 when the tests
+  // force the fallback with maxgroups = 1), all of them when the grid has no more
+  float sc = -INFINITY;
+  if (lane < NT)
+    for (int b = 0; b < nlive; ++b) sc = fmaxf(sc, ub[lane * NB + b]);
+  const int nsel = min(maxgroups >= 2 ? 8 : 4, NT);
+  int tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned done = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j < nsel) {
+      float m = sc;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+      const unsigned long long bl = __ballot(lane < NT && !((done >> lane) & 1) && sc == m);
+      const int t = __ffsll((long long)bl) - 1;
+      tl[j] = t;
+      done |= 1u << t;
+      if (lane == t) sc = -INFINITY;
+    }
+  }
+  const int slot = lane >> 3, m2 = lane & 7;
+  int mytile = tl[0];
+#pragma unroll
+  for (int j = 1; j < 8; ++j) mytile = (slot == j) ? tl[j] : mytile;
+  const int k0 = 16 * mytile + 2 * m2;
+  const bool live = slot < nsel;
+  const bool l0 = live && k0 < G, l1 = live && k0 + 1 < G;
+  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
+  const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
+  // ---- rows: Z_b + sum_e W_be D_e at points k0, k0 + 1 (k0 even: 16-byte aligned pairs)
+  double a0[NB], a1[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const d2_t z = live ? *reinterpret_cast<const d2_t*>(Zs + (long long)(b0 + i) * GS + k0) : d2_t{0.0, 0.0};
+    a0[i] = l0 ? z.x : -INFINITY;
+    a1[i] = l1 ? z.y : -INFINITY;
+  }
+  {
+    constexpr int EB2 = 2;  // entries per batch: 2 x (column pair + multiplicity pair) loads
+    const unsigned doff = (unsigned)k0 * 8u;
+    const unsigned woff = (unsigned)(b0 + 2 * min(r, NB / 2 - 1)) * 8u;
+    d2_t v[EB2], vb[EB2], w[EB2], wb[EB2];
+    auto fetch = [&](int e0, int4& t) { t = *reinterpret_cast<const int4*>(E + e0); };
+    auto issue = [&](int4 t, d2_t (&x)[EB2], d2_t (&wv)[EB2]) {
+      asm volatile("" : "+s"(t.x), "+s"(t.y), "+s"(t.z), "+s"(t.w));
+      // 32-bit offsets: (ncols + 1) x GS and ncells x Bp are < 2^31 (checked by the launcher)
+      const double* d0 = D + (unsigned)(t.y * GS);
+      const double* d1 = D + (unsigned)(t.w * GS);
+      const double* w0 = W + (unsigned)(t.x * Bp);
+      const double* w1 = W + (unsigned)(t.z * Bp);
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[0]) : "v"(doff), "s"(d0));
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[0]) : "v"(woff), "s"(w0));
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[1]) : "v"(doff), "s"(d1));
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[1]) : "v"(woff), "s"(w1));
+    };
+    auto ready = [&](d2_t (&x)[EB2], d2_t (&wv)[EB2]) {  // all but the next batch's 4 loads have landed
+      asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
+    };
+    auto accumulate = [&](const d2_t (&x)[EB2], const d2_t (&wv)[EB2]) {
+#pragma unroll
+      for (int j = 0; j < EB2; ++j)
+        fmac_entry2<NB>(a0, a1, wv[j], x[j], std::make_integer_sequence<int, NB / 2>{});
+    };
+#pragma unroll
+    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(a0[i]), "+v"(a1[i]));
+    // rows are padded to a multiple of 64 entries plus 8 zero-column entries: every fetch and
+    // look-ahead batch stays inside the row
+    int4 ta, tb;
+    fetch(0, ta);
+    issue(ta, v, w);
+    fetch(EB2, tb);
+    const int n2 = (n + EB2 - 1) & ~(EB2 - 1);
+    int e0 = 0;
+    for (; e0 + 2 * EB2 <= n2; e0 += 2 * EB2) {
+      issue(tb, vb, wb);
+      fetch(e0 + 2 * EB2, ta);
+      ready(v, w);
+      accumulate(v, w);
+      issue(ta, v, w);
+      fetch(e0 + 3 * EB2, tb);
+      ready(vb, wb);
+      accumulate(vb, wb);
+    }
+    if (e0 < n2) {
+      issue(tb, vb, wb);
+      ready(v, w);
+      accumulate(v, w);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(wb[0]), "+v"(wb[1]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(w[0]), "+v"(w[1]));
+  }
+  {
+    double mx[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) mx[i] = gt_max(a0[i], a1[i]);
+    wave_max_partials_all<NB>(mx, &fmx[0][0][0], lane, 2 * wsid);
+  }
+  wave_sync();
+  // ---- 3. post-check: every tile not computed stays below the exact maxima minus 51
+  bool need = false;
+  if (lane < NT && !((done >> lane) & 1))
+    for (int b = 0; b < nlive; ++b) need |= (double)ub[lane * NB + b] >= (double)fmx[wsid][0][b] - 51.0;
+  if (SCDE_TILE_DIAG & 2) need = false;
+  if (__ballot(need)) {  // the whole slab goes to k_boot2's fallback launch
+    if (lane == 0) {
+      redo[(long long)g * P + p] = 1;
+      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
+      pmask[(long long)g * P + p] = ~0u;
+      if (stats) {
+        atomicAdd(&stats[3], 1);
+        atomicAdd(&stats[5], (n + 3) & ~3);
+      }
+    }
+    return;
+  }
+  if (lane < nlive && !(fabs((double)fmx[wsid][0][lane]) <= degen_thresh)) degen[g] = 1;
+  // ---- 4. softmax terms, tile partial sums, jp partial row
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const double m = (double)fmx[wsid][0][i];
+    const double d0 = a0[i] - m, d1 = a1[i] - m;
+    const bool n0 = l0 && d0 >= kBootExpCut, n1 = l1 && d1 >= kBootExpCut;
+    if (__builtin_amdgcn_ballot_w64(n0 || n1)) {
+      a0[i] = n0 ? exp_tab(d0, etab) : 0.0;
+      a1[i] = n1 ? exp_tab(d1, etab) : 0.0;
+    } else {
+      a0[i] = 0.0;
+      a1[i] = 0.0;
+    }
+    const double ps = pair8_sum(a0[i], a1[i]);
+    if (m2 == 0 && live) tsum[wsid][slot][i] = ps;
+  }
+  wave_sync();
+  if (lane < NB) {
+    double S = 0.0;
+    for (unsigned mm = done; mm; mm &= mm - 1) {
+      const int t = __builtin_ffs((int)mm) - 1;
+      int sl = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (tl[j] == t && j < nsel) sl = j;
+      S += tsum[wsid][sl][lane];
+    }
+    finv[wsid][lane] = (b0 + lane < nboot) ? 1.0 / (S * norm_mult) : 0.0;
+  }
+  wave_sync();
+  double* prow = part + (long long)p * part_stride + (long long)g * GS;
+  {
+    double j0 = 0.0, j1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      j0 = fma(a0[i], finv[wsid][i], j0);
+      j1 = fma(a1[i], finv[wsid][i], j1);
+    }
+    if (l1)
+      *reinterpret_cast<d2_t*>(prow + k0) = d2_t{j0, j1};
+    else if (l0)
+      prow[k0] = j0;
+  }
+  // tiles not computed stay unwritten: k_sum_partials reads only the tiles in pmask
+  if (lane == 0) pmask[(long long)g * P + p] = done;
+  if (stats && lane == 0) {
+    atomicAdd(&stats[0], 1);
+    atomicAdd(&stats[1], __builtin_popcount(done));
+    atomicAdd(&stats[2], NT);
+    atomicAdd(&stats[4], 2 * ((n + 1) & ~1));  // 8 tiles = two 4-tile groups' worth of FMAs
+    atomicAdd(&stats[6 + __builtin_popcount(done)], 1);
+  }
+}
+
 // jp[g, k] = sum over slabs p (in order) of part[p][g][k]
 // pmask (nullable, k_boot_tiles): per (gene, slab) the 16-point tiles written; the others
 // are zeros, read as +0.0, so the sums are those of full rows.
@@ -3328,10 +3644,16 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   const dim3 grid((unsigned)div_up(items, 4)), block(256);
 #define SCDE_BT(NBV)                                                                                             \
   case NBV:                                                                                                       \
-    hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,       \
-                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,       \
-                       a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
-                       a.redo, tb.stats, tb.order, tb.pmask);                                                   \
+    if (tb.pass8)                                                                                                 \
+      hipLaunchKernelGGL(k_boot_tiles8<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,    \
+                         a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,     \
+                         a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag,            \
+                         tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask);                                   \
+    else                                                                                                          \
+      hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,     \
+                         a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,     \
+                         a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag,            \
+                         tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask);                                   \
     break;
   switch (a.nb) {
     SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)
