@@ -202,8 +202,7 @@ struct scde_ctx {
   int opt_boot_tiles = 1;        // "boot_tiles": the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles)
   int opt_boot_tiles_cells = 200;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
                                    // rows are wide, most slabs need > 8 tiles, k_boot2's stretches win)
-  int opt_tile_groups = 2;       // "tile_groups": register groups of 4 tiles per k_boot_tiles wave (1 or 2)
-  int opt_tile_pass8 = 1;        // "tile_pass8": 1 = k_boot_tiles8 (8 tiles in one pass), 0 = k_boot_tiles (4 + 4)
+  int opt_tile_groups = 2;       // "tile_groups": 2 = k_boot_tiles computes 4 bound tiles, 1 = 2 (tests)
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
@@ -822,7 +821,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         tb.ZUq = cx->zubound.as<int>();
         tb.nanflag = cx->qflags.as<int>();
         tb.maxgroups = cx->opt_tile_groups;
-        tb.pass8 = cx->opt_tile_pass8;
         tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
         HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * N)));
         tb.pmask = cx->pmask.as<unsigned>();
@@ -1120,7 +1118,6 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "boot_tiles") ctx->opt_boot_tiles = value != 0;
   else if (n == "boot_tiles_cells") ctx->opt_boot_tiles_cells = (int)value;
   else if (n == "tile_groups") ctx->opt_tile_groups = (int)value;
-  else if (n == "tile_pass8") ctx->opt_tile_pass8 = (int)value;
   else if (n == "tile_max_mult") ctx->opt_tile_max_mult = (int)value;
   else if (n == "tile_order") ctx->opt_tile_order = value != 0;
   else return fail(SCDE_EARG, "unknown option '%s'", name);

@@ -84,7 +84,7 @@ struct TablesArgs {
   // stretch j, max_j T (phase 1) or max_j T - max_j T[baseline column] (phase 2; the
   // maximum itself where the cell has no baseline); 0 for the pad column.  [ncols + 1][8]
   double* U;
-  // k_boot_tiles' tile bounds (phase 2; nullable): per 16-point tile the column's maximum in
+  // k_boot_tiles' tile bounds (phase 2; nullable): per 32-point tile the column's maximum in
   // units of 2^-8, rounded up, as four balanced base-256 digits (packu); phase-2 columns
   // store it minus their baseline column's value.  Pad column: 0.  A NaN sets *nanflag.
   unsigned* UQ;            // [ncols + 1][kQTiles]
@@ -98,7 +98,8 @@ struct TablesArgs {
 };
 
 // ---- k_boot_tiles' integer tile bounds
-constexpr int kQTiles = 32;  // 16-point grid tiles per column (G <= 448 uses <= 28)
+constexpr int kQTiles = 16;  // 32-point bound tiles per column (G <= 448 uses <= 14)
+constexpr int kBTile = 32;   // grid points per bound tile
 __host__ __device__ inline unsigned packu(int u) { return ((unsigned)u + 0x80808080u) ^ 0x80808080u; }  // |u| < 2^31
 __host__ __device__ inline int unpacku(unsigned p) { return (int)((p ^ 0x80808080u) - 0x80808080u); }
 // ZUq[set][l][t][Bp]: the baseline cells' part of the tile bounds (four digits l)
@@ -159,16 +160,15 @@ struct TileBootArgs {
   const unsigned char* W8p;  // [nsets][ncells][P][32] draw multiplicities (<= 127): per slab the pairs
                              // (boot r, boot 16 + r) of its boots, r < 16 (0 past the slab's live boots)
   int Bq;                    // ZUq's boot stride: a multiple of 32, >= the last slab's first boot + 32
-  const unsigned* UQ;        // [ncols + 1][kQTiles] packed tile maxima (units of 2^-8, rounded up)
+  const unsigned* UQ;        // [ncols + 1][kQTiles] packed 32-point tile maxima (units of 2^-8, rounded up)
   const int* ZUq;            // [nsets][4][kQTiles][Bq] baseline tile-bound digit sums
   const int* nanflag;        // tables saw a NaN: every slab goes to k_boot2
-  int maxgroups;             // register groups of 4 tiles (1 or 2)
+  int maxgroups;             // 2: 4 bound tiles per pass (default), 1: 2 (tests force the fallback)
   int* stats;                // nullable: [0] slabs, [1] tiles computed, [2] tiles, [3] slabs left to k_boot2,
                              // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left,
                              // [6 + i] slabs that computed i tiles (i <= 28)
   const int* order;          // nullable: genes in this order (launch_gene_order)
   unsigned* pmask;           // [ngenes][P] tiles each slab's partial row holds (k_sum_partials reads those)
-  int pass8;                 // 1: k_boot_tiles8 (8 tiles, two points per lane, one pass); 0: k_boot_tiles (4 + 4)
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending

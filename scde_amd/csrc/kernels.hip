@@ -361,13 +361,14 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
       if (uqf && r != r) nanq = true;
     }
     if (uqf) {
-      // this chunk's four 16-point tiles (one 16-lane row each): the maximum in units of
-      // 2^-8, rounded up, floored at -2^29 (lanes past the grid and NaN lanes hold the
+      // this chunk's two 32-point bound tiles (two 16-lane rows each): the maximum in units
+      // of 2^-8, rounded up, floored at -2^29 (lanes past the grid and NaN lanes hold the
       // floor; ceil and the scaling are monotone, so this is ceil of the tile maximum)
       int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
-      const int t = 4 * j + (lane >> 4);
-      if ((lane & 15) == 0) {
-        if (16 * t >= G)
+      u = max(u, __shfl_xor(u, 16, 64));
+      const int t = 2 * j + (lane >> 5);
+      if ((lane & 31) == 0) {
+        if (kBTile * t >= G)
           u = 0;
         else if (bc_u >= 0)
           u -= unpacku(uqb ? uqb[t] : a.UQ[(long long)bc_u * kQTiles + t]);
@@ -377,7 +378,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   }
   if (uqf) {
     if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
-    const int t = 4 * ((G + 63) / 64) + lane;  // tiles past the chunks: 0
+    const int t = 2 * ((G + 63) / 64) + lane;  // tiles past the chunks: 0
     if (t < kQTiles) a.UQ[col * kQTiles + t] = 0u;
   }
   if (U) {
@@ -763,7 +764,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
   double* out = a.T ? a.T + col * a.GS : nullptr;
   double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
   const double minlp = a.minlogprob;
-  unsigned uqv = 0;  // lane t < 32: tile t's bound (BM == kBoundTiles)
+  unsigned uqv = 0;  // lane t < kQTiles: bound tile t's value (BM == kBoundTiles)
 #pragma unroll
   for (int j = 0; j < kTabChunks; ++j) {
     if (64 * j < G) {
@@ -796,11 +797,13 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       }
       r = in ? r : -INFINITY;
       if (BM == kBoundTiles) {
-        // this chunk's four 16-point tile maxima (one row each, rounded up to 2^-8, floor
-        // -2^29); lanes 4j..4j+3 collect them from rows 0..3 (lane 16 r)
+        // this chunk's two 32-point bound tiles (rows 0-1 and 2-3; row maxima rounded up to
+        // 2^-8, floor -2^29): lanes 2j, 2j + 1 collect both rows of their tile (lanes 32 i,
+        // 32 i + 16) and keep the larger
         const int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
-        const int g = __builtin_amdgcn_ds_bpermute(((lane - 4 * j) & 3) << 6, u);
-        uqv = ((lane >> 2) == j) ? (unsigned)g : uqv;
+        const int src = ((lane - 2 * j) & 1) << 7;
+        const int g0 = __builtin_amdgcn_ds_bpermute(src, u), g1 = __builtin_amdgcn_ds_bpermute(src + 64, u);
+        uqv = ((lane >> 1) == j) ? (unsigned)max(g0, g1) : uqv;
       }
       if (BM == kBoundStretch) {  // the stretch maximum (64 points = this chunk), f32 widened
         const float mf = wave_maxf((float)r);
@@ -816,7 +819,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
     if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
     if (lane < kQTiles) {
       int u = (int)uqv;
-      if (16 * lane >= G)
+      if (kBTile * lane >= G)
         u = 0;
       else if (bc_u >= 0)
         u -= unpacku(uqb[lane]);
@@ -1858,10 +1861,10 @@ __global__ __launch_bounds__(512) void k_boot2_list(
 // ------------------------------------------------------------------ baseline tile-bound sums
 // ZUq[set][l][t][Bp] = sum over the cells with a baseline column of W8[set][c][b] *
 // digit_l(UQ[bc][t]), l < 4: the baseline cells' part of k_boot_tiles' integer tile bounds.
-// Block per (set, 32 boots, chunk of kZChunk cells); thread = (tile, boot); global atomics
+// Block per (set, 32 boots, chunk of kZChunk cells); thread = (bound tile, boot); global atomics
 // (exact integers, order-free; ZUq is zeroed first).
 constexpr int kZChunk = 64;
-__global__ __launch_bounds__(1024) void k_zuq(const unsigned* __restrict__ UQ, const int* __restrict__ base_col,
+__global__ __launch_bounds__(32 * kQTiles) void k_zuq(const unsigned* __restrict__ UQ, const int* __restrict__ base_col,
                                               int ncells, const unsigned char* __restrict__ W8, int Bp,
                                               int* __restrict__ ZUq) {
   const int nch = (ncells + kZChunk - 1) / kZChunk;
@@ -1883,47 +1886,33 @@ __global__ __launch_bounds__(1024) void k_zuq(const unsigned* __restrict__ UQ, c
 }
 
 // ------------------------------------------------------------------ tile bootstrap
-// k_boot_tiles: k_boot2's FP64 bootstrap computed only where it matters, on 16-point grid
-// tiles chosen per (gene, boot slab) from exact integer bounds.  One wave per (gene, slab);
-// a block holds four consecutive (gene, slab) items, so a gene's slabs share the CU's
-// caches; the waves never synchronise with each other.
-//   1. bounds UB_bt = ZU_bt + sum_e W_be UQ_et for every boot and tile (UQ: the tables'
-//      per-tile column maxima in units of 2^-8, rounded up; ZU: the baseline cells' part),
-//      exact integers on the int8 matrix cores (4 balanced digits) -> LDS as f32 rounded up;
-//   2. the 4 tiles with the largest bound over the slab's live boots -> one register group
-//      (16 lanes per tile): rows Z_b + sum_e W_be D_e with k_boot2's arithmetic (scalar
-//      multiplicity operands, column look-ahead from asm), maxima m'_b (f32, as k_boot2);
-//   3. tiles not computed with UB_bt >= m'_b - 51 for some live boot: up to 4 more in a
-//      second register group; a slab needing more is left to k_boot2's redo launch;
-//   4. softmax terms, per-boot sums from 16-point tile partials in tile order (row16_sum),
-//      the jp partial row (zeros on the tiles not computed).
-// A tile left out has every row value <= UB_bt < m'_b - 51 <= m_b - 50, so all its terms
-// fall under the e^-50 cut; maxima, sums and jp rows are therefore bit for bit those of
-// k_boot2 with every stretch computed.
-constexpr int kTileMax = 28;  // G <= 448
+// k_boot_tiles: k_boot2's FP64 bootstrap computed only where it matters.  One wave per
+// (gene, slab of NB boots), four per block; the waves never synchronise with each other.
+//   1. bounds UB_bt = ZU_bt + sum_e W_be UQ_et for every boot and 32-point bound tile t (UQ:
+//      the tables' per-tile column maxima in units of 2^-8, rounded up; ZU: the baseline
+//      cells' part), exact integers on the int8 matrix cores (4 balanced digits), kept in LDS
+//      as f32 rounded up;
+//   2. the 4 bound tiles with the largest bound over the slab's live boots (8 sum tiles of 16
+//      points, 128 points): rows Z_b + sum_e W_be D_e with two grid points per lane, in
+//      k_boot2's arithmetic (the same fma chain per (boot, point)); maxima m'_b (f32);
+//   3. post-check: every bound tile not computed must have UB_bt < m'_b - 51 for every live
+//      boot, else the slab goes whole to k_boot2's fallback launch;
+//   4. softmax terms, per-boot sums from 16-point tile partials in tile order, the jp
+//      partial row (zeros on the tiles not computed).
+// A tile left out has every row value <= UB_bt < m'_b - 51 <= m_b - 50, so all its terms fall
+// under the e^-50 cut; maxima, sums and jp rows are therefore bit for bit those of k_boot2
+// with every point computed.  Per ELL entry one 16-byte column load (points k0, k0 + 1) and one
+// 16-byte multiplicity load (DPP broadcast) feed 2 NB FMAs: these waves are bound by the
+// vector-memory instruction rate (the texture addresser), not by the bytes.
+constexpr int kTileMax = 28;   // 16-point sum tiles, G <= 448
+constexpr int kBTileMax = 14;  // 32-point bound tiles, G <= 448
 #ifndef SCDE_TILE_DIAG
-#define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only
-#endif
-#ifndef SCDE_TILE_WPE
-// k_boot_tiles occupancy target (waves per SIMD): 128 VGPRs.  The row loop must not spill:
-// its look-ahead registers are written by asm loads the compiler believes complete at once,
-// so a spill or copy before the asm wait reads or reuses them early.  Builds at 5 and 6
-// waves per SIMD spilled there and faulted on the GPU; tests/test_kernel_resources.py
-// checks the loops of the shipped build for scratch traffic.
-#define SCDE_TILE_WPE 4
+#define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only, 2 = rows without bounds, 4 = no multiplicity loads
 #endif
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
-
-#ifndef SCDE_TILE_DPPW
-// k_boot_tiles' multiplicity operand: 1 = a vector load per entry (each 16-lane row holds the
-// slab's multiplicity pairs, lane j boots 2j and 2j + 1) broadcast to the row by DPP64
-// row_newbcast:j on the FMA itself; 0 = scalar loads (the FMA's SGPR operand).  Same value,
-// same fma, same bits either way.
-#define SCDE_TILE_DPPW 1
-#endif
 typedef double d2_t __attribute__((ext_vector_type(2)));
 
 // acc += (w on lane J of this lane's 16-lane row) * x, one v_fmac_f64 with a DPP64 source.
@@ -1935,403 +1924,8 @@ __device__ __forceinline__ void fmac_bcast(double& acc, double w, double x) {
                "n"(J));
 }
 
-// one entry into NB accumulators: boots 2j, 2j + 1 of the slab from lane j of wv
-template <int NB, int... J>
-__device__ __forceinline__ void fmac_entry(double (&acc)[NB], const d2_t& wv, double x,
-                                           std::integer_sequence<int, J...>) {
-  ((fmac_bcast<J>(acc[2 * J], wv.x, x), fmac_bcast<J>(acc[2 * J + 1], wv.y, x)), ...);
-}
-
-template <int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_tiles(
-    const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
-    const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
-    int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
-    long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8p, int Bq,
-    const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
-    int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
-  static_assert(NB % 4 == 0 && NB <= 32, "NB must be a multiple of 4, <= 32");
-  __shared__ float ubs[4][kTileMax * NB];  // [wave][tile][boot] bounds
-  __shared__ float fmx[4][2][32];          // [wave][group][boot] maxima
-  __shared__ double tsum[4][8][NB];        // [wave][tile slot][boot] partial sums
-  __shared__ double finv[4][32];
-  __shared__ double etab[64];
-  const int lane = threadIdx.x & 63;
-  const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
-  __syncthreads();
-  const int item = blockIdx.x * 4 + wsid;
-  if (item >= ngenes * P) return;
-  // genes in `order` (by expression): waves in flight then share columns and tiles in L2
-  const int gi = item / P, p = item - gi * P, b0 = p * NB;
-  const int g = order ? order[gi] : gi;
-  if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
-    if (lane == 0) {
-      redo[(long long)g * P + p] = 1;  // flag (k_boot2's full-grid redo launch) and list entry (k_boot2_list)
-      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
-      pmask[(long long)g * P + p] = ~0u;  // k_boot2 writes the whole row
-    }
-    return;
-  }
-  const int n = nnz[g];
-  const int NT = (G + 15) >> 4;
-  const int nlive = min(NB, nboot - b0);
-  const int r = lane & 15, h = lane >> 4;
-  const int2* __restrict__ E = ent + (long long)g * ent_stride;
-  const int set = wset ? wset[g] : 0;
-  float* ub = ubs[wsid];
-  // ---- 1. tile bounds (C layout of the 16x16x64 MFMA: tile 16 tg + r, boots 16 bt + 4 h + q);
-  // the A fragments are multiplicity bytes, cell-major, so each 16-lane row reads 16
-  // adjacent bytes
-  {
-    // W8p: [set][cell][slab][32] multiplicity bytes, pairs (r, 16 + r) of the slab's boots
-    const unsigned pstride = 32u * (unsigned)P;
-    const unsigned char* __restrict__ W8 = W8p + (long long)set * ncells * pstride + 32 * p;
-    const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
-    const int KP = (n + 63) & ~63;
-    for (int tg = 0; 16 * tg < NT; ++tg) {
-      const int t = 16 * tg + r;
-      i32x4 acc[2][4];
-#pragma unroll
-      for (int bt = 0; bt < 2; ++bt)
-#pragma unroll
-        for (int l = 0; l < 4; ++l)
-          acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + b0 + 16 * bt + 4 * h);
-      for (int e0 = 0; e0 < KP; e0 += 64) {
-        int cl[16], co[16];
-        const int4* E4 = reinterpret_cast<const int4*>(E + e0 + 16 * h);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int4 x = E4[q];
-          cl[2 * q] = x.x;
-          co[2 * q] = x.y;
-          cl[2 * q + 1] = x.z;
-          co[2 * q + 1] = x.w;
-        }
-        unsigned u[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) u[j] = UQ[(unsigned)(co[j] * kQTiles + t)];
-        i32x4 af[2];
-        // the slab's multiplicity pairs (boots r and 16 + r of the slab, one 16-bit load per
-        // entry from 32-bit offsets off a wave-uniform base), split into the two boot tiles'
-        // A fragments by v_perm_b32; ncells x P x 32 and (ncols + 1) x 32 are < 2^31
-        unsigned lo4[4], hi4[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          unsigned w2[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            w2[i] = *reinterpret_cast<const unsigned short*>(W8 + (unsigned)(cl[4 * q + i] * pstride) + 2 * r);
-          const unsigned x01 = w2[0] | (w2[1] << 16), x23 = w2[2] | (w2[3] << 16);
-          lo4[q] = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
-          hi4[q] = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
-        }
-        af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
-        af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
-        unsigned pl[4][4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
-#pragma unroll
-        for (int l = 0; l < 4; ++l) {
-          const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
-          acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
-          acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
-        }
-      }
-      if (t < NT)
-#pragma unroll
-        for (int bt = 0; bt < 2; ++bt)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int b = 16 * bt + 4 * h + q;
-            if (b < NB) {
-              const long long v =
-                  (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
-              const double x = (double)v * 0x1p-8;
-              float f = (float)x;
-              if ((double)f < x) f = nextafterf(f, INFINITY);
-              ub[t * NB + b] = f;
-            }
-          }
-    }
-  }
-#if SCDE_TILE_DIAG & 1
-  return;  // timing build: bounds only
-#endif
-  wave_sync();
-  // ---- 2. first group: the 4 tiles with the largest bound
-  float sc = -INFINITY;
-  if (lane < NT)
-    for (int b = 0; b < nlive; ++b) sc = fmaxf(sc, ub[lane * NB + b]);
-  int tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned done = 0;
-  const int n1 = min(4, NT);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    if (j < n1) {
-      float m = sc;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-      const unsigned long long bl = __ballot(lane < NT && !((done >> lane) & 1) && sc == m);
-      const int t = __ffsll((long long)bl) - 1;
-      tl[j] = t;
-      done |= 1u << t;
-      if (lane == t) sc = -INFINITY;
-    }
-  }
-  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
-  const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
-  constexpr int EB = SCDE_BOOT_EB;
-  static_assert(EB == 4, "the asm look-ahead assumes 4-entry batches");
-  // rows of one register group, in k_boot2's exact arithmetic (see k_boot2 for the asm)
-#if SCDE_TILE_DPPW
-  // Column and multiplicity loads both from asm (saddr form: the entry's column / cell row base
-  // in SGPRs, the lane's offset in a loop-invariant VGPR), waited with one explicit vmcnt: per
-  // batch 2 x EB loads, so vmcnt(2 EB) leaves only the next batch in flight.
-  const unsigned woff = (unsigned)(b0 + 2 * min(r, NB / 2 - 1)) * 8u;
-  auto rows = [&](double (&acc)[NB], int koff, bool live) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) acc[i] = live ? Zs[(long long)(b0 + i) * GS + koff] : -INFINITY;
-    const unsigned doff = (unsigned)koff * 8u;
-    double v[EB], vb[EB];
-    d2_t w[EB], wb[EB];
-    // the ELL entries (scalar loads, the only ones in the loop) are fetched one batch ahead of
-    // the batch whose loads they address, so their latency hides behind a batch of FMAs
-    auto fetch = [&](int e0, int4 (&t)[EB / 2]) {
-      const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
-#pragma unroll
-      for (int j = 0; j < EB / 2; ++j) t[j] = E4[j];
-    };
-    auto issue = [&](const int4 (&t4)[EB / 2], double (&x)[EB], d2_t (&wv)[EB]) {
-#pragma unroll
-      for (int j = 0; j < EB / 2; ++j) {
-        int4 t = t4[j];
-        // pins the address arithmetic (and the wait for the fetch) here, after the previous
-        // batch's FMAs, instead of where the compiler would hoist it
-        asm volatile("" : "+s"(t.x), "+s"(t.y), "+s"(t.z), "+s"(t.w));
-        // 32-bit offsets: (ncols + 1) x GS and ncells x Bp are < 2^31 (checked by the launcher)
-        const double* d0 = D + (unsigned)(t.y * GS);
-        const double* d1 = D + (unsigned)(t.w * GS);
-        const double* w0 = W + (unsigned)(t.x * Bp);
-        const double* w1 = W + (unsigned)(t.z * Bp);
-        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(x[2 * j]) : "v"(doff), "s"(d0));
-        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[2 * j]) : "v"(woff), "s"(w0));
-        asm volatile("global_load_dwordx2 %0, %1, %2" : "=v"(x[2 * j + 1]) : "v"(doff), "s"(d1));
-        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[2 * j + 1]) : "v"(woff), "s"(w1));
-      }
-    };
-    static_assert(EB == 4, "the vmcnt below counts 2 x 4 loads per batch");
-    auto ready = [&](double (&x)[EB], d2_t (&wv)[EB]) {  // all but the next batch's 8 loads have landed
-      asm volatile("s_waitcnt vmcnt(8)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(wv[0]), "+v"(wv[1]),
-                   "+v"(wv[2]), "+v"(wv[3]));
-    };
-    auto accumulate = [&](const double (&x)[EB], const d2_t (&wv)[EB]) {
-#pragma unroll
-      for (int j = 0; j < EB; ++j) fmac_entry<NB>(acc, wv[j], x[j], std::make_integer_sequence<int, NB / 2>{});
-    };
-#pragma unroll
-    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));
-    // rows are padded to a multiple of 64 entries plus 8 zero-column entries: every fetch and
-    // look-ahead batch below stays inside the row
-    int4 ta[EB / 2], tb[EB / 2];
-    fetch(0, ta);
-    issue(ta, v, w);
-    fetch(EB, tb);
-    const int n4 = (n + EB - 1) & ~(EB - 1);
-    int e0 = 0;
-    for (; e0 + 2 * EB <= n4; e0 += 2 * EB) {
-      issue(tb, vb, wb);
-      fetch(e0 + 2 * EB, ta);
-      ready(v, w);
-      accumulate(v, w);
-      issue(ta, v, w);
-      fetch(e0 + 3 * EB, tb);
-      ready(vb, wb);
-      accumulate(vb, wb);
-    }
-    if (e0 < n4) {
-      issue(tb, vb, wb);
-      ready(v, w);
-      accumulate(v, w);
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]), "+v"(wb[0]),
-                   "+v"(wb[1]), "+v"(wb[2]), "+v"(wb[3]));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(w[0]), "+v"(w[1]),
-                 "+v"(w[2]), "+v"(w[3]));
-  };
-#else
-  auto rows = [&](double (&acc)[NB], int koff, bool live) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) acc[i] = live ? Zs[(long long)(b0 + i) * GS + koff] : -INFINITY;
-    int cell[EB], cellb[EB];
-    double v[EB], vb[EB];
-    auto issue = [&](int e0, int (&c)[EB], double (&x)[EB]) {
-      const int4* __restrict__ E4 = reinterpret_cast<const int4*>(E + e0);
-#pragma unroll
-      for (int j = 0; j < EB / 2; ++j) {
-        const int4 t = E4[j];
-        c[2 * j] = t.x;
-        c[2 * j + 1] = t.z;
-        const double* p0 = D + (unsigned)(t.y * GS) + koff;
-        const double* p1 = D + (unsigned)(t.w * GS) + koff;
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j]) : "v"(p0));
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(x[2 * j + 1]) : "v"(p1));
-      }
-    };
-    auto ready = [&](double (&x)[EB]) {
-      asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]));
-    };
-    auto accumulate = [&](const int (&c)[EB], const double (&x)[EB]) {
-#pragma unroll
-      for (int i0 = 0; i0 < NB; i0 += 2) {
-        double2 w[EB];
-#pragma unroll
-        for (int j = 0; j < EB; ++j)
-          w[j] = *reinterpret_cast<const double2*>(W + (unsigned)(__builtin_amdgcn_readfirstlane(c[j]) * Bp) + b0 + i0);
-#pragma unroll
-        for (int j = 0; j < EB; ++j) {
-          acc[i0] = fma(w[j].x, x[j], acc[i0]);
-          acc[i0 + 1] = fma(w[j].y, x[j], acc[i0 + 1]);
-        }
-      }
-    };
-#pragma unroll
-    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(acc[i]));
-    issue(0, cell, v);
-    const int n4 = (n + EB - 1) & ~(EB - 1);
-    int e0 = 0;
-    for (; e0 + 2 * EB <= n4; e0 += 2 * EB) {
-      issue(e0 + EB, cellb, vb);
-      ready(v);
-      accumulate(cell, v);
-      issue(e0 + 2 * EB, cell, v);
-      ready(vb);
-      accumulate(cellb, vb);
-    }
-    if (e0 < n4) {
-      issue(e0 + EB, cellb, vb);
-      ready(v);
-      accumulate(cell, v);
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-  };
-#endif
-  double acc1[NB], acc2[NB];
-  const int k1 = 16 * tl[h] + r;
-  const bool live1 = h < n1 && k1 < G;
-  rows(acc1, k1, live1);
-  wave_max_partials_all<NB>(acc1, &fmx[0][0][0], lane, 2 * wsid);
-  wave_sync();
-  // ---- 3. tiles still needed against the exact maxima
-  bool need = false;
-  if (lane < NT && !((done >> lane) & 1))
-    for (int b = 0; b < nlive; ++b) need |= (double)ub[lane * NB + b] >= (double)fmx[wsid][0][b] - 51.0;
-  unsigned long long nm = __ballot(need);
-  const int cnt = __popcll(nm);
-  int ng = 1, n2 = 0;
-  if (cnt > 0) {
-    if (cnt > 4 || maxgroups < 2) {  // the whole slab goes to k_boot2's redo launch
-      if (lane == 0) {
-        redo[(long long)g * P + p] = 1;
-        redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
-        pmask[(long long)g * P + p] = ~0u;
-        if (stats) {
-          atomicAdd(&stats[3], 1);
-          atomicAdd(&stats[5], (n + 3) & ~3);
-        }
-      }
-      return;
-    }
-    n2 = cnt;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (j < n2) {
-        const int t = __ffsll((long long)nm) - 1;
-        nm &= nm - 1;
-        tl[4 + j] = t;
-        done |= 1u << t;
-      }
-    }
-    ng = 2;
-  }
-  const int k2 = 16 * tl[4 + h] + r;
-  const bool live2 = h < n2 && k2 < G;
-  if (ng == 2) {
-    rows(acc2, k2, live2);
-    wave_max_partials_all<NB>(acc2, &fmx[0][0][0], lane, 2 * wsid + 1);
-    wave_sync();
-    if (lane < NB) fmx[wsid][0][lane] = fmaxf(fmx[wsid][0][lane], fmx[wsid][1][lane]);
-    wave_sync();
-  }
-  if (lane < nlive && !(fabs((double)fmx[wsid][0][lane]) <= degen_thresh)) degen[g] = 1;
-  // ---- 4. softmax terms, tile partial sums, jp partial row
-  auto terms = [&](double (&acc)[NB], bool live, int slot0, int nt) {
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const double d = acc[i] - (double)fmx[wsid][0][i];
-      const bool nd = live && d >= kBootExpCut;
-      if (__builtin_amdgcn_ballot_w64(nd))
-        acc[i] = nd ? exp_tab(d, etab) : 0.0;
-      else
-        acc[i] = 0.0;
-      const double ps = row16_sum(acc[i]);
-      if (r == 0 && h < nt) tsum[wsid][slot0 + h][i] = ps;
-    }
-  };
-  terms(acc1, live1, 0, n1);
-  if (ng == 2) terms(acc2, live2, 4, n2);
-  wave_sync();
-  if (lane < NB) {
-    double S = 0.0;
-    for (unsigned m = done; m; m &= m - 1) {
-      const int t = __builtin_ffs((int)m) - 1;
-      int slot = 0;
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-        if (tl[s] == t && (s < n1 || (s >= 4 && s - 4 < n2))) slot = s;
-      S += tsum[wsid][slot][lane];
-    }
-    finv[wsid][lane] = (b0 + lane < nboot) ? 1.0 / (S * norm_mult) : 0.0;
-  }
-  wave_sync();
-  double* prow = part + (long long)p * part_stride + (long long)g * GS;
-  {
-    double jpv = 0.0;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) jpv = fma(acc1[i], finv[wsid][i], jpv);
-    if (live1) prow[k1] = jpv;
-  }
-  if (ng == 2) {
-    double jpv = 0.0;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) jpv = fma(acc2[i], finv[wsid][i], jpv);
-    if (live2) prow[k2] = jpv;
-  }
-  // tiles not computed stay unwritten: k_sum_partials reads only the tiles in pmask
-  if (lane == 0) pmask[(long long)g * P + p] = done;
-  if (stats && lane == 0) {
-    atomicAdd(&stats[0], 1);
-    atomicAdd(&stats[1], __builtin_popcount(done));
-    atomicAdd(&stats[2], NT);
-    atomicAdd(&stats[4], ng * ((n + 3) & ~3));
-    atomicAdd(&stats[6 + __builtin_popcount(done)], 1);  // histogram of tiles computed per slab
-  }
-}
-
-// ------------------------------------------------------------------ tile bootstrap, one pass
-// k_boot_tiles8: k_boot_tiles with two grid points per lane, so one wave holds 8 tiles
-// (128 points) of its (gene, slab) in a single pass: the 8 tiles with the largest exact
-// integer bounds (the same bounds as k_boot_tiles), then a post-check that every other tile
-// stays below m'_b - 51, else the slab goes whole to k_boot2's fallback launch.  Per ELL entry
-// one 16-byte column load (points k0, k0 + 1) and one 16-byte multiplicity load (DPP
-// broadcast) feed 2 NB FMAs -- half the vector-memory instructions per FMA of the 4-tile
-// form, whose waves are bound by the texture addresser -- and no second register group.
-// Lane l: tile slot l >> 3 (8 lanes per tile, two tiles per 16-lane row), points
-// 16 tile + 2 (l & 7) and + 1.  Each (boot, point) row is the same fma chain as k_boot2's;
-// a tile's partial sum adds the lane's two points, then partners lane^1, ^2 and the 8-lane
-// mirror: the operand pairs of row16_sum, so sums, maxima, terms and jp rows are k_boot2's bits.
+// A tile's partial sum: the lane's two points, then partners lane^1, ^2 and the 8-lane
+// mirror -- the operand pairs of row16_sum over 16 one-point lanes, so the same bits.
 __device__ __forceinline__ double pair8_sum(double p0, double p1) {
   double v = p0 + p1;
   v += dpp_d<kDppXor1>(v);
@@ -2349,11 +1943,16 @@ __device__ __forceinline__ void fmac_entry2(double (&a0)[NB], double (&a1)[NB], 
    ...);
 }
 
-#ifndef SCDE_TILE8_WPE
-#define SCDE_TILE8_WPE 4  // 2 x NB accumulators (80 VGPRs at NB = 20) + two 2-entry load buffers
+#ifndef SCDE_TILE_WPE
+// k_boot_tiles occupancy target (waves per SIMD): 2 x NB accumulators (80 VGPRs at NB = 20)
+// and two 2-entry load buffers fit 128 VGPRs.  The row loop must not spill: its look-ahead
+// registers are written by asm loads the compiler believes complete at once, so a spill or
+// copy before the asm wait reads or reuses them early (builds that did faulted on the GPU;
+// tests/test_kernel_resources.py checks the shipped ISA for it).
+#define SCDE_TILE_WPE 4
 #endif
 template <int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_WPE))) void k_boot_tiles8(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_tiles(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
     const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
@@ -2361,7 +1960,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
-  __shared__ float ubs[4][kTileMax * NB];  // [wave][tile][boot] bounds
+  __shared__ float ubs[4][kBTileMax * NB];  // [wave][bound tile][boot] bounds
   __shared__ float fmx[4][2][32];          // [wave][.][boot] maxima
   __shared__ double tsum[4][8][NB];        // [wave][tile slot][boot] partial sums
   __shared__ double finv[4][32];
@@ -2383,22 +1982,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
     return;
   }
   const int n = nnz[g];
-  const int NT = (G + 15) >> 4;
+  const int NT = (G + 15) >> 4, NTB = (G + 31) >> 5;  // 16-point sum tiles, 32-point bound tiles
   const int nlive = min(NB, nboot - b0);
   const int r = lane & 15, h = lane >> 4;
   const int2* __restrict__ E = ent + (long long)g * ent_stride;
   const int set = wset ? wset[g] : 0;
   float* ub = ubs[wsid];
-  // ---- 1. tile bounds: exactly k_boot_tiles' (see there)
+  // ---- 1. bound tiles (C layout of the 16x16x64 MFMA: bound tile r, boots 16 bt + 4 h + q); the
+  // A fragments are multiplicity bytes, cell-major, so each 16-lane row reads 16 adjacent bytes
   if (SCDE_TILE_DIAG & 2) {  // timing build: rows without bounds (results wrong)
-    for (int i = lane; i < kTileMax * NB; i += 64) ub[i] = 0.0f;
+    for (int i = lane; i < kBTileMax * NB; i += 64) ub[i] = 0.0f;
   } else {
     const unsigned pstride = 32u * (unsigned)P;
     const unsigned char* __restrict__ W8 = W8p + (long long)set * ncells * pstride + 32 * p;
     const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
     const int KP = (n + 63) & ~63;
-    for (int tg = 0; 16 * tg < NT; ++tg) {
-      const int t = 16 * tg + r;
+    {  // NTB <= 14 bound tiles: one 16-tile MFMA group
+      const int t = r;
       i32x4 acc[2][4];
 #pragma unroll
       for (int bt = 0; bt < 2; ++bt)
@@ -2444,7 +2044,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
           acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
         }
       }
-      if (t < NT)
+      if (t < NTB)
 #pragma unroll
         for (int bt = 0; bt < 2; ++bt)
 #pragma unroll
@@ -2465,33 +2065,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
   return;  // timing build: bounds only
 #endif
   wave_sync();
-  // ---- 2. the tiles with the largest bound over the slab's live boots: 8 (4 when the tests
-  // force the fallback with maxgroups = 1), all of them when the grid has no more
+  // ---- 2. the bound tiles with the largest bound over the slab's live boots: 4 (2 when the
+  // tests force the fallback with maxgroups = 1), all of them when the grid has no more
   float sc = -INFINITY;
-  if (lane < NT)
+  if (lane < NTB)
     for (int b = 0; b < nlive; ++b) sc = fmaxf(sc, ub[lane * NB + b]);
-  const int nsel = min(maxgroups >= 2 ? 8 : 4, NT);
-  int tl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  unsigned done = 0;
+  sc = (lane < NTB) ? sc : -INFINITY;
+  const int nsel = min(maxgroups >= 2 ? 4 : 2, NTB);
+  int tl[4] = {0, 0, 0, 0};
+  unsigned bdone = 0;  // bound tiles computed
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
+  for (int j = 0; j < 4; ++j) {
     if (j < nsel) {
+      // the 16 bound-tile scores sit in lanes 0..15: a 16-lane DPP max, read back from lane 0
       float m = sc;
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-      const unsigned long long bl = __ballot(lane < NT && !((done >> lane) & 1) && sc == m);
+      m = fmaxf(m, dpp_f<kDppXor1>(m));
+      m = fmaxf(m, dpp_f<kDppXor2>(m));
+      m = fmaxf(m, dpp_f<kDppHalfMirror>(m));
+      m = fmaxf(m, dpp_f<kDppMirror>(m));
+      m = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
+      const unsigned long long bl = __ballot(lane < NTB && !((bdone >> lane) & 1) && sc == m);
       const int t = __ffsll((long long)bl) - 1;
       tl[j] = t;
-      done |= 1u << t;
+      bdone |= 1u << t;
       if (lane == t) sc = -INFINITY;
     }
   }
-  const int slot = lane >> 3, m2 = lane & 7;
-  int mytile = tl[0];
+  // the 16-point sum tiles of the computed bound tiles
+  unsigned done = 0;
 #pragma unroll
-  for (int j = 1; j < 8; ++j) mytile = (slot == j) ? tl[j] : mytile;
+  for (int j = 0; j < 4; ++j)
+    if (j < nsel) done |= 3u << (2 * tl[j]);
+  done &= (NT >= 32) ? ~0u : ((1u << NT) - 1);
+  // lane l: sum tile slot l >> 3 = bound tile (l >> 4), half (l >> 3) & 1
+  const int slot = lane >> 3, m2 = lane & 7;
+  int mybt = tl[0];
+#pragma unroll
+  for (int j = 1; j < 4; ++j) mybt = ((slot >> 1) == j) ? tl[j] : mybt;
+  const int mytile = 2 * mybt + (slot & 1);
   const int k0 = 16 * mytile + 2 * m2;
-  const bool live = slot < nsel;
+  const bool live = (slot >> 1) < nsel;
   const bool l0 = live && k0 < G, l1 = live && k0 + 1 < G;
   const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
   const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
@@ -2517,12 +2130,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
       const double* w0 = W + (unsigned)(t.x * Bp);
       const double* w1 = W + (unsigned)(t.z * Bp);
       asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[0]) : "v"(doff), "s"(d0));
-      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[0]) : "v"(woff), "s"(w0));
+      if (!(SCDE_TILE_DIAG & 4)) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[0]) : "v"(woff), "s"(w0));
       asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[1]) : "v"(doff), "s"(d1));
-      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[1]) : "v"(woff), "s"(w1));
+      if (!(SCDE_TILE_DIAG & 4)) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[1]) : "v"(woff), "s"(w1));
     };
-    auto ready = [&](d2_t (&x)[EB2], d2_t (&wv)[EB2]) {  // all but the next batch's 4 loads have landed
-      asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
+    auto ready = [&](d2_t (&x)[EB2], d2_t (&wv)[EB2]) {  // all but the next batch's loads have landed
+      if (SCDE_TILE_DIAG & 4)  // timing build: multiplicities loaded once (results wrong)
+        asm volatile("s_waitcnt vmcnt(2)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
+      else
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
     };
     auto accumulate = [&](const d2_t (&x)[EB2], const d2_t (&wv)[EB2]) {
 #pragma unroll
@@ -2535,6 +2151,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
     // look-ahead batch stays inside the row
     int4 ta, tb;
     fetch(0, ta);
+    if (SCDE_TILE_DIAG & 4) {  // timing build: the first entry's multiplicities for every entry
+      const double* w0 = W + (unsigned)(ta.x * Bp);
+      w[0] = w[1] = wb[0] = wb[1] = *reinterpret_cast<const d2_t*>(w0 + woff / 8);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(wb[0]), "+v"(wb[1]));
+    }
     issue(ta, v, w);
     fetch(EB2, tb);
     const int n2 = (n + EB2 - 1) & ~(EB2 - 1);
@@ -2564,9 +2185,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
     wave_max_partials_all<NB>(mx, &fmx[0][0][0], lane, 2 * wsid);
   }
   wave_sync();
-  // ---- 3. post-check: every tile not computed stays below the exact maxima minus 51
+  // ---- 3. post-check: every bound tile not computed stays below the exact maxima minus 51
   bool need = false;
-  if (lane < NT && !((done >> lane) & 1))
+  if (lane < NTB && !((bdone >> lane) & 1))
     for (int b = 0; b < nlive; ++b) need |= (double)ub[lane * NB + b] >= (double)fmx[wsid][0][b] - 51.0;
   if (SCDE_TILE_DIAG & 2) need = false;
   if (__ballot(need)) {  // the whole slab goes to k_boot2's fallback launch
@@ -2605,8 +2226,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
       const int t = __builtin_ffs((int)mm) - 1;
       int sl = 0;
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (tl[j] == t && j < nsel) sl = j;
+      for (int j = 0; j < 4; ++j)
+        if (tl[j] == (t >> 1) && j < nsel) sl = 2 * j + (t & 1);
       S += tsum[wsid][sl][lane];
     }
     finv[wsid][lane] = (b0 + lane < nboot) ? 1.0 / (S * norm_mult) : 0.0;
@@ -2631,7 +2252,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE8_
     atomicAdd(&stats[0], 1);
     atomicAdd(&stats[1], __builtin_popcount(done));
     atomicAdd(&stats[2], NT);
-    atomicAdd(&stats[4], 2 * ((n + 1) & ~1));  // 8 tiles = two 4-tile groups' worth of FMAs
+    atomicAdd(&stats[4], 2 * ((n + 1) & ~1));  // 128 points = two 64-lane groups' worth of FMAs
     atomicAdd(&stats[6 + __builtin_popcount(done)], 1);
   }
 }
@@ -3459,7 +3080,7 @@ hipError_t launch_zuq(const unsigned* UQ, const int* base_col, int ncells, const
   hipError_t e = hipMemsetAsync(ZUq, 0, sizeof(int) * (size_t)nsets * 4 * kQTiles * Bp, s);
   if (e != hipSuccess) return e;
   const int nch = (ncells + kZChunk - 1) / kZChunk;
-  hipLaunchKernelGGL(k_zuq, dim3(Bp / 32, nsets * nch), dim3(1024), 0, s, UQ, base_col, ncells, W8, Bp, ZUq);
+  hipLaunchKernelGGL(k_zuq, dim3(Bp / 32, nsets * nch), dim3(32 * kQTiles), 0, s, UQ, base_col, ncells, W8, Bp, ZUq);
   return hipGetLastError();
 }
 
@@ -3644,16 +3265,10 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   const dim3 grid((unsigned)div_up(items, 4)), block(256);
 #define SCDE_BT(NBV)                                                                                             \
   case NBV:                                                                                                       \
-    if (tb.pass8)                                                                                                 \
-      hipLaunchKernelGGL(k_boot_tiles8<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,    \
-                         a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,     \
-                         a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag,            \
-                         tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask);                                   \
-    else                                                                                                          \
-      hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,     \
-                         a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,     \
-                         a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag,            \
-                         tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask);                                   \
+    hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,       \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,       \
+                       a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
+                       a.redo, tb.stats, tb.order, tb.pmask);                                                   \
     break;
   switch (a.nb) {
     SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)

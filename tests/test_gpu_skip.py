@@ -4,13 +4,12 @@ The skipping is an optimisation that must not change results: a 64-point stretch
 left out of a boot slab when a rigorous upper bound of its row values stays more than 51
 below the exact row maximum (post-check), i.e. when every softmax term there falls under
 the e^-50 cut that zeroes it anyway; any slab that fails the check is recomputed whole.
-These tests run the same calls, for the bootstrap kernels (k_boot_tiles8 on 8 bounded 16-point
-tiles, the default; the 4 + 4-tile k_boot_tiles, tile_pass8 = 0; k_boot2 with its 64-point
-stretch mask, boot_tiles = 0), with skipping on
+These tests run the same calls, for the bootstrap kernels (k_boot_tiles on 4 bounded 32-point
+tiles, the default; k_boot2 with its 64-point stretch mask, boot_tiles = 0), with skipping on
 (default), off (boot_skip = 0), and forced onto the second-chance paths so that the extra work
 really happens (its count is read back and must be > 0): a negative heuristic slack
-(skip_slack) that makes the masks drop stretches the post-check must reject, the tile kernels
-limited to 4 tiles (tile_groups = 1) so slabs needing more go to k_boot2's fallback launch, or a multiplicity limit of 1 (tile_max_mult) so the call, with its tables set up
+(skip_slack) that makes the masks drop stretches the post-check must reject, the tile kernel
+limited to 2 bound tiles (tile_groups = 1) so slabs needing more go to k_boot2's fallback launch, or a multiplicity limit of 1 (tile_max_mult) so the call, with its tables set up
 for the tile path, runs plain k_boot2 instead (the "multiplicity above 127" fallback) -- and
 compare every run with the oracle at the SURVEY §8(d) bar, and the runs with each other bit
 for bit (the kernels share rows, maxima and tile-ordered sums).
@@ -36,7 +35,6 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx = api.default_context()
     ctx.set_option("boot_skip", opts.get("boot_skip", 1))
     ctx.set_option("tile_max_mult", opts.get("tile_max_mult", 127))
-    ctx.set_option("tile_pass8", opts.get("tile_pass8", 1))
     ctx.set_option("skip_slack", opts.get("skip_slack", math.nan))
     ctx.set_option("boot_tiles", opts.get("boot_tiles", 1))
     ctx.set_option("tile_groups", opts.get("tile_groups", 2))
@@ -51,7 +49,6 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo", "boot_path")}
     finally:
         ctx.set_option("tile_max_mult", 127)
-        ctx.set_option("tile_pass8", 1)
         ctx.set_option("boot_skip", 1)
         ctx.set_option("skip_slack", math.nan)
         ctx.set_option("boot_tiles", 1)
@@ -76,8 +73,6 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-forced-redo": {"tile_groups": 1},
         "tiles-unordered": {"tile_order": 0},
         "tiles-mult-fallback": {"tile_max_mult": 1},
-        "tiles4": {"tile_pass8": 0},
-        "tiles4-forced-redo": {"tile_pass8": 0, "tile_groups": 1},
         "stretch": {"boot_tiles": 0},
         "stretch-forced-redo": {"boot_tiles": 0, "skip_slack": -45.0},
     }
@@ -88,7 +83,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
             assert stats["skip_slabs"] == 0 and stats["boot_path"] == 0, stats
         elif name == "tiles-mult-fallback":  # plain k_boot2 on the tile path's columns, no skipping
             assert stats["boot_path"] == 0 and stats["skip_slabs"] == 0, stats
-        elif name.endswith("tiles-forced-redo") or name == "tiles4-forced-redo":  # 4 tiles: the rest go to k_boot2
+        elif name == "tiles-forced-redo":  # 2 bound tiles (64 points): slabs needing more go to k_boot2
             assert stats["boot_path"] == 1 and stats["skip_redo"] > 0, stats
         else:
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
@@ -106,7 +101,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-unordered", "tiles-mult-fallback",
-                                    "tiles4", "tiles4-forced-redo", "stretch", "stretch-forced-redo")),):
+                                    "stretch", "stretch-forced-redo")),):
         for name in others:
             for i in range(2):
                 np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got[base]["joint.posteriors"][i])
