@@ -121,8 +121,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "boot_tiles"    1/0  the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles; default 1)
  *   "boot_tiles_cells"  the cell count from which it is used (default 200; below: k_boot2's
  *                   64-point stretch mask)
- *   "tile_groups"   register groups of 4 tiles per k_boot_tiles wave, 1 or 2 (default 2; slabs
- *                   needing more go to k_boot2 whole -- tests force that with 1)
+ *   "tile_groups"   32-point grid tiles k_boot_tiles computes per slab, 1..4 (default 4; slabs
+ *                   needing more go to k_boot2 whole -- tests force that with 2)
  *   "tile_max_mult" the largest draw multiplicity the tile path takes (default 127, the int8 bound
  *                   operand; a call with a larger one runs plain k_boot2 on the same columns --
  *                   tests force that fallback with a small value)

@@ -202,7 +202,7 @@ struct scde_ctx {
   int opt_boot_tiles = 1;        // "boot_tiles": the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles)
   int opt_boot_tiles_cells = 200;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
                                    // rows are wide, most slabs need > 8 tiles, k_boot2's stretches win)
-  int opt_tile_groups = 2;       // "tile_groups": 2 = k_boot_tiles computes 4 bound tiles, 1 = 2 (tests)
+  int opt_tile_groups = 4;       // "tile_groups": 32-point bound tiles k_boot_tiles computes per slab (1..4)
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)

@@ -163,7 +163,7 @@ struct TileBootArgs {
   const unsigned* UQ;        // [ncols + 1][kQTiles] packed 32-point tile maxima (units of 2^-8, rounded up)
   const int* ZUq;            // [nsets][4][kQTiles][Bq] baseline tile-bound digit sums
   const int* nanflag;        // tables saw a NaN: every slab goes to k_boot2
-  int maxgroups;             // 2: 4 bound tiles per pass (default), 1: 2 (tests force the fallback)
+  int maxgroups;             // 32-point bound tiles computed per slab, 1..4 (4; tests force the fallback with fewer)
   int* stats;                // nullable: [0] slabs, [1] tiles computed, [2] tiles, [3] slabs left to k_boot2,
                              // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left,
                              // [6 + i] slabs that computed i tiles (i <= 28)

@@ -800,10 +800,11 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
         // this chunk's two 32-point bound tiles (rows 0-1 and 2-3; row maxima rounded up to
         // 2^-8, floor -2^29): lanes 2j, 2j + 1 collect both rows of their tile (lanes 32 i,
         // 32 i + 16) and keep the larger
-        const int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
-        const int src = ((lane - 2 * j) & 1) << 7;
-        const int g0 = __builtin_amdgcn_ds_bpermute(src, u), g1 = __builtin_amdgcn_ds_bpermute(src + 64, u);
-        uqv = ((lane >> 1) == j) ? (unsigned)max(g0, g1) : uqv;
+        int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
+        const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+        u = max((int)sw[0], (int)sw[1]);  // rows 0-1 | rows 2-3: the bound tile's maximum on every lane
+        const int g = __builtin_amdgcn_ds_bpermute(((lane - 2 * j) & 1) << 7, u);
+        uqv = ((lane >> 1) == j) ? (unsigned)g : uqv;
       }
       if (BM == kBoundStretch) {  // the stretch maximum (64 points = this chunk), f32 widened
         const float mf = wave_maxf((float)r);
@@ -1907,7 +1908,8 @@ __global__ __launch_bounds__(32 * kQTiles) void k_zuq(const unsigned* __restrict
 constexpr int kTileMax = 28;   // 16-point sum tiles, G <= 448
 constexpr int kBTileMax = 14;  // 32-point bound tiles, G <= 448
 #ifndef SCDE_TILE_DIAG
-#define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only, 2 = rows without bounds, 4 = no multiplicity loads
+#define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only, 2 = rows without bounds, 4 = no multiplicity loads,
+                          // 8 = every column load from the entry-0 column (cache-resident)
 #endif
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2065,13 +2067,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   return;  // timing build: bounds only
 #endif
   wave_sync();
-  // ---- 2. the bound tiles with the largest bound over the slab's live boots: 4 (2 when the
-  // tests force the fallback with maxgroups = 1), all of them when the grid has no more
+  // ---- 2. the bound tiles with the largest bound over the slab's live boots: maxgroups (4; the
+  // tests force the fallback with fewer), all of them when the grid has no more
   float sc = -INFINITY;
   if (lane < NTB)
     for (int b = 0; b < nlive; ++b) sc = fmaxf(sc, ub[lane * NB + b]);
   sc = (lane < NTB) ? sc : -INFINITY;
-  const int nsel = min(maxgroups >= 2 ? 4 : 2, NTB);
+  const int nsel = min(max(1, min(maxgroups, 4)), NTB);  // bound tiles computed: 4 (tests: fewer)
   int tl[4] = {0, 0, 0, 0};
   unsigned bdone = 0;  // bound tiles computed
 #pragma unroll
@@ -2122,11 +2124,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     const unsigned woff = (unsigned)(b0 + 2 * min(r, NB / 2 - 1)) * 8u;
     d2_t v[EB2], vb[EB2], w[EB2], wb[EB2];
     auto fetch = [&](int e0, int4& t) { t = *reinterpret_cast<const int4*>(E + e0); };
+    const int col0 = __builtin_amdgcn_readfirstlane(E[0].y);  // timing build 8: every load from this column
+    (void)col0;
     auto issue = [&](int4 t, d2_t (&x)[EB2], d2_t (&wv)[EB2]) {
       asm volatile("" : "+s"(t.x), "+s"(t.y), "+s"(t.z), "+s"(t.w));
       // 32-bit offsets: (ncols + 1) x GS and ncells x Bp are < 2^31 (checked by the launcher)
-      const double* d0 = D + (unsigned)(t.y * GS);
-      const double* d1 = D + (unsigned)(t.w * GS);
+      const double* d0 = D + (unsigned)(((SCDE_TILE_DIAG & 8) ? col0 : t.y) * GS);
+      const double* d1 = D + (unsigned)(((SCDE_TILE_DIAG & 8) ? col0 : t.w) * GS);
       const double* w0 = W + (unsigned)(t.x * Bp);
       const double* w1 = W + (unsigned)(t.z * Bp);
       asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[0]) : "v"(doff), "s"(d0));

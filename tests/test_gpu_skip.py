@@ -9,7 +9,7 @@ tiles, the default; k_boot2 with its 64-point stretch mask, boot_tiles = 0), wit
 (default), off (boot_skip = 0), and forced onto the second-chance paths so that the extra work
 really happens (its count is read back and must be > 0): a negative heuristic slack
 (skip_slack) that makes the masks drop stretches the post-check must reject, the tile kernel
-limited to 2 bound tiles (tile_groups = 1) so slabs needing more go to k_boot2's fallback launch, or a multiplicity limit of 1 (tile_max_mult) so the call, with its tables set up
+limited to 2 bound tiles (tile_groups = 2) so slabs needing more go to k_boot2's fallback launch, or a multiplicity limit of 1 (tile_max_mult) so the call, with its tables set up
 for the tile path, runs plain k_boot2 instead (the "multiplicity above 127" fallback) -- and
 compare every run with the oracle at the SURVEY §8(d) bar, and the runs with each other bit
 for bit (the kernels share rows, maxima and tile-ordered sums).
@@ -37,7 +37,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("tile_max_mult", opts.get("tile_max_mult", 127))
     ctx.set_option("skip_slack", opts.get("skip_slack", math.nan))
     ctx.set_option("boot_tiles", opts.get("boot_tiles", 1))
-    ctx.set_option("tile_groups", opts.get("tile_groups", 2))
+    ctx.set_option("tile_groups", opts.get("tile_groups", 4))
     ctx.set_option("boot_tiles_cells", opts.get("boot_tiles_cells", 0))
     ctx.set_option("tile_order", opts.get("tile_order", 1))
     ctx.set_option("skip_stats", 1)
@@ -52,7 +52,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("boot_skip", 1)
         ctx.set_option("skip_slack", math.nan)
         ctx.set_option("boot_tiles", 1)
-        ctx.set_option("tile_groups", 2)
+        ctx.set_option("tile_groups", 4)
         ctx.set_option("boot_tiles_cells", 200)
         ctx.set_option("tile_order", 1)
         ctx.set_option("skip_stats", 0)
@@ -70,7 +70,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
     runs = {
         "tiles": {},
         "noskip": {"boot_skip": 0},
-        "tiles-forced-redo": {"tile_groups": 1},
+        "tiles-forced-redo": {"tile_groups": 2},
         "tiles-unordered": {"tile_order": 0},
         "tiles-mult-fallback": {"tile_max_mult": 1},
         "stretch": {"boot_tiles": 0},
