@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdarg>
@@ -208,6 +209,9 @@ struct scde_ctx {
   int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
+  // host wall time of scde_expression_difference_{dev,host} phases (ms, summed over calls):
+  // setup, unique tables (incl. their syncs), posteriors enqueued, ratio + results read back
+  double st_host_ms[4] = {0, 0, 0, 0};
   // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
   // stretches x 64 lanes x slab boots x entries)
   double st_boot_f64_fma = 0;
@@ -1134,6 +1138,10 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "boot_path") *value = ctx->st_boot_path;
   else if (n == "skip_redo") *value = ctx->st_skip_redo;
   else if (n == "degen") *value = ctx->st_degen;
+  else if (n == "host_setup_ms") *value = ctx->st_host_ms[0];
+  else if (n == "host_unique_ms") *value = ctx->st_host_ms[1];
+  else if (n == "host_post_ms") *value = ctx->st_host_ms[2];
+  else if (n == "host_tail_ms") *value = ctx->st_host_ms[3];
   else if (n.rfind("tiles_", 0) == 0 && atoi(n.c_str() + 6) >= 0 && atoi(n.c_str() + 6) <= 28)
     *value = ctx->st_tile_hist[atoi(n.c_str() + 6)];
   else return fail(SCDE_EARG, "unknown statistic '%s'", name);
@@ -1143,6 +1151,7 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
 int scde_ctx_reset_stats(scde_ctx* ctx) {
   if (!ctx) return fail(SCDE_EARG, "null argument");
   ctx->st_skip_slabs = ctx->st_skip_kept = ctx->st_skip_stretches = ctx->st_skip_redo = ctx->st_degen = 0;
+  for (double& x : ctx->st_host_ms) x = 0;
   ctx->st_boot_f64_fma = 0;
   for (double& x : ctx->st_tile_hist) x = 0;
   return SCDE_OK;
@@ -1576,6 +1585,12 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
   HCHK(hipSetDevice(ctx->device));
   hipStream_t st = ctx->stream;
   const int C = p->ncells, G = p->ngrid;
+  using hclock = std::chrono::steady_clock;
+  auto hlap = [&, t = hclock::now()](int slot) mutable {
+    const auto now = hclock::now();
+    ctx->st_host_ms[slot] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  };
   // split cells by group (R/functions.R:372-374, tapply over levels)
   std::vector<int> idx[2];
   for (int c = 0; c < C; ++c)
@@ -1617,6 +1632,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     s.jp_g = G;  // gene-major rows for the ratio kernel
     s.jp_k = 1;
   }
+  hlap(0);
   if (up) {
     // group by group, each after its columns have arrived (the first range ends with the
     // last cell of the group whose cells end first)
@@ -1632,6 +1648,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       UniqueSet* up[1] = {&ctx->us[gi]};
       if (k == 0) {
         RCHK(build_unique_sets(ctx, sp, up, 1));
+        hlap(1);
       } else {
         // the second group's unique sets on the copy stream, behind its own upload: their two
         // host syncs then wait for its small kernels, not for the first group's posterior
@@ -1644,8 +1661,10 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         RCHK(rc);
         HCHK(hipEventRecord(ctx->uq_ev, ctx->copy_stream));
         HCHK(hipStreamWaitEvent(ctx->stream, ctx->uq_ev, 0));
+        hlap(1);
       }
       RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
+      hlap(2);
     }
   } else {
     // both groups' unique tables first (two host syncs, GPU otherwise idle), then the
@@ -1654,7 +1673,9 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     const PostSpec* sp[2] = {&specs[0], &specs[1]};
     UniqueSet* up[2] = {&ctx->us[0], &ctx->us[1]};
     RCHK(build_unique_sets(ctx, sp, up, 2));
+    hlap(1);
     for (int gi = 0; gi < 2; ++gi) RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
+    hlap(2);
   }
   // ratio posterior + summary
   const std::vector<double> diffv = ratio_diffv(p->prior_x, G);
@@ -1709,7 +1730,9 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     RCHK(ctx->sync());
     transpose_rows_to_colmajor(tmp.data(), ngenes, G, jp2);
   }
-  return ctx->sync();
+  const int rc = ctx->sync();
+  hlap(3);
+  return rc;
 }
 
 // Batch-corrected scde.expression.difference (R/functions.R:321-399), device resident:

@@ -1963,6 +1963,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
   __shared__ float ubs[4][kBTileMax * NB];  // [wave][bound tile][boot] bounds
+  __shared__ unsigned bstage[4][1024 + 512];  // [wave] bound staging: 16 x 64 tile words | 16 x 32 pair words
   __shared__ float fmx[4][2][32];          // [wave][.][boot] maxima
   __shared__ double tsum[4][8][NB];        // [wave][tile slot][boot] partial sums
   __shared__ double finv[4][32];
@@ -1990,78 +1991,91 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   const int2* __restrict__ E = ent + (long long)g * ent_stride;
   const int set = wset ? wset[g] : 0;
   float* ub = ubs[wsid];
-  // ---- 1. bound tiles (C layout of the 16x16x64 MFMA: bound tile r, boots 16 bt + 4 h + q); the
-  // A fragments are multiplicity bytes, cell-major, so each 16-lane row reads 16 adjacent bytes
+  // ---- 1. bound tiles (C layout of the 16x16x64 MFMA: bound tile r, boots 16 bt + 4 h + q).  Per
+  // 64-entry chunk each lane loads one entry's data with wide loads -- its (cell, column), the
+  // column's 16 tile bounds (64 B) and the cell's 16 multiplicity pairs of this slab (32 B) --
+  // and writes them transposed into the wave's LDS area; the MFMA fragments are then contiguous
+  // LDS reads: 7 vector-memory instructions per chunk instead of 40 single-entry gathers.
   if (SCDE_TILE_DIAG & 2) {  // timing build: rows without bounds (results wrong)
     for (int i = lane; i < kBTileMax * NB; i += 64) ub[i] = 0.0f;
   } else {
     const unsigned pstride = 32u * (unsigned)P;
     const unsigned char* __restrict__ W8 = W8p + (long long)set * ncells * pstride + 32 * p;
     const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
+    unsigned* sq = &bstage[wsid][0];      // [tile t][entry l] tile bounds (64 x 16 words)
+    unsigned* sw = &bstage[wsid][1024];   // [pair r][entry l / 2] multiplicity pairs (two entries a word)
     const int KP = (n + 63) & ~63;
-    {  // NTB <= 14 bound tiles: one 16-tile MFMA group
-      const int t = r;
-      i32x4 acc[2][4];
+    const int t = r;
+    i32x4 acc[2][4];
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+      for (int l = 0; l < 4; ++l)
+        acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + b0 + 16 * bt + 4 * h);
+    for (int e0 = 0; e0 < KP; e0 += 64) {
+      const int2 en = E[e0 + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
+      const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
+      const uint4 q0 = uq[0], q1 = uq[1], q2 = uq[2], q3 = uq[3];
+      const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * pstride));
+      const uint4 w0 = wp[0], w1 = wp[1];
+      wave_sync();  // the previous chunk's fragment reads are done before the area is rewritten
+      const unsigned qv[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                               q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+      for (int tt = 0; tt < 16; ++tt) sq[tt * 64 + lane] = qv[tt];
+      // pairs (boot j, boot 16 + j) as 16-bit words: two entries per 32-bit LDS word
+      const unsigned wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      unsigned short* sw16 = reinterpret_cast<unsigned short*>(sw);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        sw16[(2 * j) * 64 + lane] = (unsigned short)(wv[j] & 0xffffu);
+        sw16[(2 * j + 1) * 64 + lane] = (unsigned short)(wv[j] >> 16);
+      }
+      wave_sync();
+      // B fragment: tile t's words of entries 16 h .. 16 h + 15
+      const uint4* bq = reinterpret_cast<const uint4*>(sq + t * 64 + 16 * h);
+      const uint4 b0v = bq[0], b1v = bq[1], b2v = bq[2], b3v = bq[3];
+      const unsigned u[16] = {b0v.x, b0v.y, b0v.z, b0v.w, b1v.x, b1v.y, b1v.z, b1v.w,
+                              b2v.x, b2v.y, b2v.z, b2v.w, b3v.x, b3v.y, b3v.z, b3v.w};
+      // A fragments: pair r of entries 16 h .. 16 h + 15 (two entries a word)
+      const uint4* aw = reinterpret_cast<const uint4*>(sw + r * 32 + 8 * h);
+      const uint4 a0v = aw[0], a1v = aw[1];
+      const unsigned x2[8] = {a0v.x, a0v.y, a0v.z, a0v.w, a1v.x, a1v.y, a1v.z, a1v.w};
+      i32x4 af[2];
+      unsigned lo4[4], hi4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        lo4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x06040200u);
+        hi4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x07050301u);
+      }
+      af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
+      af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
+      unsigned pl[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
+#pragma unroll
+      for (int l = 0; l < 4; ++l) {
+        const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
+        acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
+        acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
+      }
+    }
+    if (t < NTB)
 #pragma unroll
       for (int bt = 0; bt < 2; ++bt)
 #pragma unroll
-        for (int l = 0; l < 4; ++l)
-          acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + b0 + 16 * bt + 4 * h);
-      for (int e0 = 0; e0 < KP; e0 += 64) {
-        int cl[16], co[16];
-        const int4* E4 = reinterpret_cast<const int4*>(E + e0 + 16 * h);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int4 x = E4[q];
-          cl[2 * q] = x.x;
-          co[2 * q] = x.y;
-          cl[2 * q + 1] = x.z;
-          co[2 * q + 1] = x.w;
-        }
-        unsigned u[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) u[j] = UQ[(unsigned)(co[j] * kQTiles + t)];
-        i32x4 af[2];
-        unsigned lo4[4], hi4[4];
-#pragma unroll
         for (int q = 0; q < 4; ++q) {
-          unsigned w2[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            w2[i] = *reinterpret_cast<const unsigned short*>(W8 + (unsigned)(cl[4 * q + i] * pstride) + 2 * r);
-          const unsigned x01 = w2[0] | (w2[1] << 16), x23 = w2[2] | (w2[3] << 16);
-          lo4[q] = __builtin_amdgcn_perm(x23, x01, 0x06040200u);
-          hi4[q] = __builtin_amdgcn_perm(x23, x01, 0x07050301u);
-        }
-        af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
-        af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
-        unsigned pl[4][4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
-#pragma unroll
-        for (int l = 0; l < 4; ++l) {
-          const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
-          acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
-          acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
-        }
-      }
-      if (t < NTB)
-#pragma unroll
-        for (int bt = 0; bt < 2; ++bt)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int b = 16 * bt + 4 * h + q;
-            if (b < NB) {
-              const long long v =
-                  (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
-              const double x = (double)v * 0x1p-8;
-              float f = (float)x;
-              if ((double)f < x) f = nextafterf(f, INFINITY);
-              ub[t * NB + b] = f;
-            }
+          const int b = 16 * bt + 4 * h + q;
+          if (b < NB) {
+            const long long v =
+                (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
+            const double x = (double)v * 0x1p-8;
+            float f = (float)x;
+            if ((double)f < x) f = nextafterf(f, INFINITY);
+            ub[t * NB + b] = f;
           }
-    }
+        }
   }
 #if SCDE_TILE_DIAG & 1
   return;  // timing build: bounds only

@@ -64,6 +64,11 @@ def main():
         st = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo", "degen")}
         hist = [int(ctx.stat(f"tiles_{i}")) for i in range(29)]
         ctx.set_option("skip_stats", 0)
+        ctx.reset_stats()
+        for _ in range(3):  # host phases without the profiling events
+            run()
+        ctx.synchronize()
+        host = {k: round(ctx.stat(f"host_{k}_ms") / 3, 3) for k in ("setup", "unique", "post", "tail")}
         ctx.set_profiling(True)
         ctx.reset_kernel_times()
         for _ in range(3):
@@ -76,6 +81,7 @@ def main():
               f"degen {st['degen']:.0f} ms/step {kt}", flush=True)
         if any(hist):
             print("   tiles/slab histogram:", {i: h for i, h in enumerate(hist) if h}, flush=True)
+        print("   host ms/step by phase:", host, flush=True)
 
 
 if __name__ == "__main__":
