@@ -451,6 +451,8 @@ def main():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="readiness study, one process: time rank 0's shard of a strong split over this many "
                          "ranks (no collective; not the metric)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="context option for a study run (scde_ctx_set_option); the defaults are the product")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config])
     cpu_sample = cfg["cpu_sample"] if args.cpu_sample is None else args.cpu_sample
@@ -498,6 +500,9 @@ def main():
         cfg["batch"] = synthetic_batch(cfg["seed"], NC, cfg["nbatch"])
     zero_frac = float(np.mean(counts == 0))
     ctx = api.Context(device)
+    for o in args.opt:
+        k, v = o.split("=", 1)
+        ctx.set_option(k, float(v))
     # the prior is an input of the measured path: computed once, on the GPU,
     # from the whole data set (so every rank of a strong-scaling run holds the same grid)
     dcp = api.DeviceCounts(ctx, counts_all)

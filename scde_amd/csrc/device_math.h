@@ -474,19 +474,26 @@ __device__ __noinline__ double bd0_series_fast(double x, double np) {
 // bd0 = (x - np) v + 2 x v sum_{j>=1} w^j / (2j + 1) (src: R nmath bd0, the loop R runs until
 // the sum stops changing).  Nine terms leave a tail below 2e-17 of the first, so the result
 // matches the loop to rounding, with no loop, no early exit and no divergence.
+// fma as one VOP3 v_fma_f64 (the same rounding as fma()): with the coefficient held in a
+// VGPR pair across the loop, the compiler's v_fmac form would first copy it into the
+// accumulator (one v_mov_b64 per Horner step)
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 __device__ __forceinline__ double bd0_poly(double x, double np) {
   const double d = x - np;
   const double v = d / (x + np);
   const double w = v * v;
-  double P = 1.0 / 19;
-  P = fma(P, w, 1.0 / 17);
-  P = fma(P, w, 1.0 / 15);
-  P = fma(P, w, 1.0 / 13);
-  P = fma(P, w, 1.0 / 11);
-  P = fma(P, w, 1.0 / 9);
-  P = fma(P, w, 1.0 / 7);
-  P = fma(P, w, 1.0 / 5);
-  P = fma(P, w, 1.0 / 3);
+  double P = fma3(1.0 / 19, w, 1.0 / 17);
+  P = fma3(P, w, 1.0 / 15);
+  P = fma3(P, w, 1.0 / 13);
+  P = fma3(P, w, 1.0 / 11);
+  P = fma3(P, w, 1.0 / 9);
+  P = fma3(P, w, 1.0 / 7);
+  P = fma3(P, w, 1.0 / 5);
+  P = fma3(P, w, 1.0 / 3);
   P *= w;
   return fma(2.0 * x * v, P, d * v);
 }

@@ -169,6 +169,7 @@ struct scde_ctx {
   hipStream_t copy_stream = nullptr;
   hipEvent_t up_ev[2] = {nullptr, nullptr};
   hipEvent_t uq_ev = nullptr;  // the second group's unique sets (built on copy_stream) are ready
+  hipEvent_t modes_ev = nullptr;  // run_posterior's posterior modes are computed (they need the tables only)
   // Pinned staging arena for the small per-call transfers (cell lists, offsets, draws,
   // multiplicities, tasks; the unique builder's size read-backs).  A pageable copy is staged
   // by the runtime and costs 20-40 us of host latency each; from pinned memory it is a plain
@@ -324,6 +325,7 @@ struct scde_ctx {
     if (stream) (void)hipStreamDestroy(stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (uq_ev) (void)hipEventDestroy(uq_ev);
+    if (modes_ev) (void)hipEventDestroy(modes_ev);
     if (pin) (void)hipHostFree(pin);
     for (auto& e : up_ev)
       if (e) (void)hipEventDestroy(e);
@@ -364,6 +366,7 @@ struct PostSpec {
   double* jp = nullptr;
   long long jp_g = 0, jp_k = 0;
   double* modes = nullptr;  // ngenes x ncells col-major
+  bool modes_early = false;  // modes right after the tables, with cx->modes_ev recorded (copy_modes_out)
   double* post = nullptr;   // ncells blocks of ngenes x G col-major
   bool use_baseline = true;
   int rand_kind = 0;
@@ -691,6 +694,16 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     HCHK(launch_tables(ta, st));
   }
   cx->mark_end(SLOT_TABLES, ev);
+  // ---- individual posterior modes (src/jpmatLogBoot.cpp:277-296): argmax of each cell's table
+  // column, known as soon as the tables are; computed here so the caller's read-back of the
+  // (ngenes x ncells) matrix overlaps the bootstrap
+  const bool want_modes = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
+  if (want_modes && s.modes && s.modes_early) {
+    HCHK(launch_modes(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->maxi.as<int>(),
+                      cx->mag.as<double>(), s.modes, 1, N, st));
+    if (!cx->modes_ev) HCHK(hipEventCreateWithFlags(&cx->modes_ev, hipEventDisableTiming));
+    HCHK(hipEventRecord(cx->modes_ev, st));
+  }
   if (fused && s.nboot > 0) {
     make_draws(s, Bp, draws, W, ndraw);
     maxw = 0;
@@ -925,8 +938,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     HCHK(launch_boot_exact(xa, st));
   }
   // ---- individual outputs (src/jpmatLogBoot.cpp:277-328)
-  const bool want_modes = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
-  if (want_modes && s.modes)
+  if (want_modes && s.modes && !s.modes_early)
     HCHK(launch_modes(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->maxi.as<int>(),
                       cx->mag.as<double>(), s.modes, 1, N, st));
   if (want_post && s.post)
@@ -1189,6 +1201,16 @@ int scde_d2h(scde_ctx* ctx, void* dst, const void* src, int64_t bytes) {
 }
 
 // ------------------------------------------------------------------ layer 1
+// The posterior-mode matrix (ngenes x ncells doubles: 480 MB at config 4) to the host on the
+// copy stream, after run_posterior's modes_ev: issued once every kernel of the call is queued
+// (a pageable read-back can hold the host thread until it is done), it overlaps the bootstrap.
+static int copy_modes_out(scde_ctx* cx, double* host, const double* dev, size_t n) {
+  if (!cx->copy_stream) HCHK(hipStreamCreateWithFlags(&cx->copy_stream, hipStreamNonBlocking));
+  HCHK(hipStreamWaitEvent(cx->copy_stream, cx->modes_ev, 0));
+  HCHK(hipMemcpyAsync(host, dev, sizeof(double) * n, hipMemcpyDeviceToHost, cx->copy_stream));
+  return SCDE_OK;
+}
+
 static int logboot_common(bool batch, const double* models, int ncells, const int* ucl_vals, const int64_t* ucl_off,
                           const int* counti, int ngenes, const double* magnitudes, int ngrid, const int* batch_vals,
                           const int64_t* batch_off, const int* composition, int nbatch, int nboot, int seed,
@@ -1239,6 +1261,7 @@ static int logboot_common(bool batch, const double* models, int ncells, const in
   if (want_modes) {
     HCHK(cx->jpB.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * ncells)));
     s.modes = cx->jpB.as<double>();
+    s.modes_early = ngenes > 0;
   }
   if (want_post) {
     HCHK(cx->outbuf.ensure(sizeof(double) * std::max<size_t>(1, NG * ncells)));
@@ -1246,11 +1269,11 @@ static int logboot_common(bool batch, const double* models, int ncells, const in
   }
   cx->us[0].ready = false;
   RCHK(run_posterior(cx, s, cx->us[0]));
+  if (s.modes_early) RCHK(copy_modes_out(cx, modes, s.modes, (size_t)ngenes * ncells));
   if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, cx->stream));
-  if (want_modes && ngenes)
-    HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * ngenes * ncells, hipMemcpyDeviceToHost, cx->stream));
   if (want_post && NG)
     HCHK(hipMemcpyAsync(post, s.post, sizeof(double) * NG * ncells, hipMemcpyDeviceToHost, cx->stream));
+  if (s.modes_early) HCHK(hipStreamSynchronize(cx->copy_stream));
   return cx->sync();
 }
 
@@ -1525,6 +1548,7 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
   if (want_modes) {
     HCHK(ctx->jpB.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * ncells_sel)));
     s.modes = ctx->jpB.as<double>();
+    s.modes_early = ngenes > 0;
   }
   if (want_post) {
     HCHK(ctx->outbuf.ensure(sizeof(double) * std::max<size_t>(1, NG * ncells_sel)));
@@ -1532,11 +1556,11 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
   }
   ctx->us[0].ready = false;
   RCHK(run_posterior(ctx, s, ctx->us[0]));
+  if (s.modes_early) RCHK(copy_modes_out(ctx, modes, s.modes, (size_t)ngenes * ncells_sel));
   if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, ctx->stream));
-  if (want_modes && ngenes)
-    HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * ngenes * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
   if (want_post && NG)
     HCHK(hipMemcpyAsync(post, s.post, sizeof(double) * NG * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
+  if (s.modes_early) HCHK(hipStreamSynchronize(ctx->copy_stream));
   return ctx->sync();
 }
 

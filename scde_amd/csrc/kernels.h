@@ -8,7 +8,7 @@
 #define SCDE_BOOT_ASMLD 1  // k_boot2 column look-ahead issued from asm with explicit vmcnt waits
 #endif
 #ifndef SCDE_TABREG_WPE
-#define SCDE_TABREG_WPE 2  // k_tables_reg occupancy target (waves per SIMD; 4-wave blocks, two per CU)
+#define SCDE_TABREG_WPE 3  // k_tables_reg occupancy target (waves per SIMD; 4-wave blocks)
 #endif
 #ifndef SCDE_TABREG_G401
 #define SCDE_TABREG_G401 1  // k_tables_reg specialised for the default 401-point grid

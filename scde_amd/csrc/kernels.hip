@@ -597,9 +597,16 @@ __device__ unsigned long long g_kt_stamp[16];
     if (lane == 0) atomicAdd(&g_kt_stamp[i], (unsigned long long)(t_ - kt0_));           \
     kt0_ = t_;                                                                           \
   } while (0)
+#define KT_EVENT(i, c)                                                                   \
+  do {                                                                                   \
+    if (__builtin_amdgcn_ballot_w64(c) && lane == 0) atomicAdd(&g_kt_stamp[i], 1ull);    \
+  } while (0)
 #else
 #define KT_STAMP(i) \
   do {              \
+  } while (0)
+#define KT_EVENT(i, c) \
+  do {                 \
   } while (0)
 #endif
 constexpr int kTabChunks = kTabStagedG / 64;
@@ -687,6 +694,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       double lpr = sl[(kRowP + 2) * kRS + 64 * j], lqr = sl[(kRowP + 3) * kRS + 64 * j];
       const double muv = sl[kRowMu * kRS + 64 * j], mnext = sl[kRowMu * kRS + 64 * j + 1];
       const bool over = in && ((!last && x > muv && x < mnext) || (last && x > muv));
+      KT_EVENT(12, over);
       if (__builtin_amdgcn_ballot_w64(over)) {
         pr = over ? po : pr;
         qr = over ? 1 - po : qr;
@@ -697,6 +705,10 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       // nq finite -- the fast form's full validity condition
       const double np = nf.n * pr, nq = nf.n * qr;
       const bool bad = in && !(np > 0.0 && nq > 0.0 && pr <= 1.0);
+      KT_EVENT(11, bad);
+      KT_EVENT(8, in && fabs(nf.X - np) < 0.1 * (nf.X + np));
+      KT_EVENT(9, in && nf.X != nf.n && fabs(nf.nx - nq) < 0.1 * (nf.nx + nq));
+      KT_EVENT(13, in);
       double nb = (SCDE_KT_DIAG & 1) ? lpr * x + lqr : dnbinom_fast(nf, pr, qr, lpr, lqr);
       badm |= bad ? (1u << j) : 0u;
       nb += sl[kRowLcfpr * kRS + 64 * j];
@@ -749,6 +761,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       const bool in = k < G;
       v[j] -= maxp;  // t1
       double e = sl[kRowCfp * kRS + 64 * j] * E;
+      KT_EVENT(14, in && v[j] > -60.0);
       if (!(SCDE_KT_DIAG & 2) && __builtin_amdgcn_ballot_w64(in && v[j] > -60.0)) e += exp_tab(fmax(v[j], -746.0), etab);
       ls += in ? e : 0.0;
     }
@@ -775,6 +788,8 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       const bool tiny = !(hi >= -665.0);
       const bool mixed = !tiny && !(hi - lo > 37.5);
       double r = hi - lsum;
+      KT_EVENT(10, in && (tiny || mixed));
+      KT_EVENT(15, in && tiny);
       if (__builtin_amdgcn_ballot_w64(in && (tiny || mixed))) {
         const double e = fma(sl[kRowCfp * kRS + 64 * j], E, exp_tab(fmax(t1, -746.0), etab));
         const double rm = (SCDE_KT_DIAG & 4) ? e - lsum : log_tab(tiny ? e / s : e, lt) - (tiny ? 0.0 : lsum);
@@ -1917,6 +1932,23 @@ __device__ __forceinline__ void wave_sync() {
 }
 typedef double d2_t __attribute__((ext_vector_type(2)));
 
+// Logical block of hardware block b under round-robin XCD dispatch (block b runs on XCD
+// b % 8): runs of K consecutive logical blocks -- a gene's slabs, and genes adjacent in the
+// count-sum order, which share low-count columns -- go to one XCD and run there at about the
+// same time, meeting each other's D columns in its L2; the runs rotate over the XCDs, so
+// every XCD walks the count-sum order (the work gradient) at the same pace.  Hardware
+// blocks g 8K + 8 i + x (x < 8, i < K) take logical g 8K + K x + i; a last partial group
+// keeps the identity (a bijection for any n).
+#ifndef SCDE_XCD_RUN
+#define SCDE_XCD_RUN 16
+#endif
+__device__ __forceinline__ int xcd_block(int b, int n) {
+  constexpr int K = SCDE_XCD_RUN;
+  if (K <= 1 || b >= n / (8 * K) * (8 * K)) return b;
+  const int r = b % (8 * K);
+  return b - r + (r & 7) * K + (r >> 3);
+}
+
 // acc += (w on lane J of this lane's 16-lane row) * x, one v_fmac_f64 with a DPP64 source.
 // w must come from a load, never from a VALU write in the two preceding instructions (the
 // DPP read hazard; tests/test_kernel_resources.py checks the shipped ISA).
@@ -1953,8 +1985,11 @@ __device__ __forceinline__ void fmac_entry2(double (&a0)[NB], double (&a1)[NB], 
 // tests/test_kernel_resources.py checks the shipped ISA for it).
 #define SCDE_TILE_WPE 4
 #endif
-template <int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_tiles(
+// WB waves per block (4; one item each).  Measured and not kept: a gene's 5 slabs as the 5
+// waves of one block (the slabs' column loads did not meet in L1: the same L1 -> L2 request
+// count, boot 12.5 -> 14.6 ms at config 4).
+template <int NB, int WB>
+__global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_tiles(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
     const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
@@ -1962,17 +1997,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
-  __shared__ float ubs[4][kBTileMax * NB];  // [wave][bound tile][boot] bounds
-  __shared__ unsigned bstage[4][1024 + 512];  // [wave] bound staging: 16 x 64 tile words | 16 x 32 pair words
-  __shared__ float fmx[4][2][32];          // [wave][.][boot] maxima
-  __shared__ double tsum[4][8][NB];        // [wave][tile slot][boot] partial sums
-  __shared__ double finv[4][32];
+  __shared__ float ubs[WB][kBTileMax * NB];  // [wave][bound tile][boot] bounds
+#ifdef SCDE_TILE_TEST_WB1
+  __shared__ unsigned bstage[WB][64];  // hazard-test builds: the LDS that would cap occupancy (never run)
+#else
+  __shared__ unsigned bstage[WB][1024 + 512];  // [wave] bound staging: 16 x 64 tile words | 16 x 32 pair words
+#endif
+  __shared__ float fmx[WB][2][32];          // [wave][.][boot] maxima
+  __shared__ double tsum[WB][8][NB];        // [wave][tile slot][boot] partial sums
+  __shared__ double finv[WB][32];
   __shared__ double etab[64];
   const int lane = threadIdx.x & 63;
   const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
   __syncthreads();
-  const int item = blockIdx.x * 4 + wsid;
+  const int item = xcd_block(blockIdx.x, gridDim.x) * WB + wsid;
   if (item >= ngenes * P) return;
   const int gi = item / P, p = item - gi * P, b0 = p * NB;
   const int g = order ? order[gi] : gi;
@@ -2274,6 +2313,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     atomicAdd(&stats[6 + __builtin_popcount(done)], 1);
   }
 }
+
+#ifdef SCDE_TILE_TEST_WB1
+// hazard-test builds only (tests/test_kernel_resources.py), never run: one-wave blocks with a
+// token bound-staging area, whose LDS no longer caps occupancy at 4 waves per SIMD, so
+// SCDE_TILE_WPE = 6 squeezes the row loop's registers as the faulting round-2 builds were
+template __global__ void k_boot_tiles<20, 1>(const double* __restrict__, const int2* __restrict__, const int* __restrict__,
+                                             int, const double* __restrict__, int, int, const int* __restrict__,
+                                             const double* __restrict__, int, int, int, int, double, double,
+                                             double* __restrict__, long long, int* __restrict__, int,
+                                             const unsigned char* __restrict__, int, const unsigned* __restrict__,
+                                             const int* __restrict__, const int* __restrict__, int, int* __restrict__,
+                                             int* __restrict__, const int* __restrict__, unsigned* __restrict__);
+#endif
 
 // jp[g, k] = sum over slabs p (in order) of part[p][g][k]
 // pmask (nullable, k_boot_tiles): per (gene, slab) the 16-point tiles written; the others
@@ -3280,13 +3332,14 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   hipError_t e = hipMemsetAsync(a.redo, 0, sizeof(int) * ((size_t)a.ngenes * P + 1), s);
   if (e != hipSuccess) return e;
   const long long items = (long long)a.ngenes * P;
-  const dim3 grid((unsigned)div_up(items, 4)), block(256);
-#define SCDE_BT(NBV)                                                                                             \
-  case NBV:                                                                                                       \
-    hipLaunchKernelGGL(k_boot_tiles<NBV>, grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,       \
-                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,       \
-                       a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, \
-                       a.redo, tb.stats, tb.order, tb.pmask);                                                   \
+  constexpr int WB = 4;
+  const dim3 grid((unsigned)div_up(items, WB)), block(64 * WB);
+#define SCDE_BT(NBV)                                                                                              \
+  case NBV:                                                                                                        \
+    hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,  \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
+                       a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups,  \
+                       a.redo, tb.stats, tb.order, tb.pmask);                                                    \
     break;
   switch (a.nb) {
     SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)

@@ -184,18 +184,19 @@ def test_dpp_broadcast_sources_not_fresh_valu_results(isa):
 
 def test_hazard_check_rejects_a_faulting_build(tmp_path):
     """k_boot_tiles built for 6 waves per SIMD (the occupancy that faulted on the GPU in round 2,
-    DESIGN.md §4.0): the compiler spills or copies inside the look-ahead loop, and the check
-    must report it."""
+    DESIGN.md §4.0), as one-wave blocks (SCDE_TILE_TEST_WB1: the shipped blocks' LDS caps
+    occupancy at 4 waves per SIMD, which would leave the registers unsqueezed): the compiler
+    spills or copies inside the look-ahead loop, and the check must report it."""
     hipcc = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
     if not os.path.exists(hipcc):
         pytest.skip("hipcc not found")
     out = tmp_path / "k6.s"
     r = subprocess.run([hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
-                        "-S", "-DSCDE_TILE_WPE=6", "-I" + os.path.join(ROOT, "include"),
+                        "-S", "-DSCDE_TILE_WPE=6", "-DSCDE_TILE_TEST_WB1", "-I" + os.path.join(ROOT, "include"),
                         "-o", str(out), os.path.join(CSRC, "kernels.hip")], capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     found = []
-    for sym, body in _bodies(out.read_text(), "k_boot_tilesILi20E"):
+    for sym, body in _bodies(out.read_text(), "k_boot_tilesILi20ELi1E"):
         lines, spans = _loop_spans(body)
         for a, b in spans:
             found += vmcnt_hazards(lines[a:b + 1])

@@ -54,6 +54,10 @@ def main():
     print(f"columns {ncol}  cycles/column (s_memtime ticks) total {tot / ncol:.0f}")
     for i, n in enumerate(PHASES):
         print(f"  {n:24s} {buf[i] / ncol:9.0f}  {100 * buf[i] / max(tot, 1):5.1f}%")
+    print("chunk events per column (waves whose ballot is non-zero):")
+    for i, n in [(13, "chunks"), (12, "own-count point"), (11, "bad lanes"), (8, "bd0 series X"),
+                 (9, "bd0 series n-x"), (14, "loop2 exp"), (10, "loop3 mixed|tiny"), (15, "loop3 tiny")]:
+        print(f"  {n:24s} {buf[i] / ncol:7.3f}")
 
 
 if __name__ == "__main__":
