@@ -128,13 +128,17 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   tests force that fallback with a small value)
  *   "tile_order"    1/0  k_boot_tiles takes the genes in order of their count sums, so waves in
  *                   flight share columns and tiles in L2 (default 1; results are the same)
+ *   "pair_cells"    the cell count from which k_boot_tiles runs two slabs per wave with two
+ *                   bound tiles each (default 1000: wide calls, narrow posteriors); slabs that need
+ *                   more take a four-tile pass (results are the same)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
  *   "ratio_window"  k_ratio_summary register window 4, 5, 7 or 8;  "ratio_block" 64, 128, 256
  *   "wpca_ms"       1/0  the multi-start npcs = 1 weighted-PCA kernel
  * Statistics: "skip_slabs", "skip_stretches", "skip_kept", "skip_redo", "degen", "tiles_<i>"
- * (k_boot_tiles slabs computing i tiles) (with skip_stats); "boot_f64_fma" (FP64 lane FMAs the
+ * (k_boot_tiles slabs computing i tiles), "pair_redo" (slabs a pair pass left to the four-tile
+ * pass) (with skip_stats); "boot_f64_fma" (FP64 lane FMAs the
  * bootstrap kernels issued), also with skip_stats; "boot_path": the bootstrap kernel of the last
  * posterior (0 k_boot2, 1 k_boot_tiles, 3 the general k_boot). */
 int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);

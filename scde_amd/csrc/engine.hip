@@ -192,7 +192,7 @@ struct scde_ctx {
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
-  Buf gkey, gkey2, gidx, gorder, gwork, pmask;
+  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 30 + 0.4 C); tests force redo slabs
@@ -208,6 +208,8 @@ struct scde_ctx {
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
+  int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
+                                 // tiles each; the posterior narrows with the cells, most slabs need two)
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // host wall time of scde_expression_difference_{dev,host} phases (ms, summed over calls):
@@ -216,6 +218,7 @@ struct scde_ctx {
   // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
   // stretches x 64 lanes x slab boots x entries)
   double st_boot_f64_fma = 0;
+  double st_pair_redo = 0;  // slabs a pair pass of k_boot_tiles left to the four-tile list pass
   double st_boot_path = -1;  // the bootstrap kernel of the last posterior: 0 k_boot2, 1 k_boot_tiles, 3 general
   static constexpr int kQMaxTilesHost = 28;
   double st_tile_hist[kQMaxTilesHost + 1] = {0};
@@ -313,7 +316,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask};
+                 &w8t,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
@@ -841,6 +844,11 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
         HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * N)));
         tb.pmask = cx->pmask.as<unsigned>();
+        tb.pairs = (C >= cx->opt_pair_cells && P >= 2) ? 1 : 0;
+        if (tb.pairs) {
+          HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * N)));
+          tb.wide = cx->pwide.as<int>();
+        }
         if (cx->opt_tile_order && N > 1) {
           HCHK(cx->gkey.ensure(sizeof(unsigned) * N));
           HCHK(cx->gkey2.ensure(sizeof(unsigned) * N));
@@ -865,6 +873,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
           cx->st_skip_kept += h[3];
           cx->st_skip_stretches += h[4];
           cx->st_skip_redo += h[5];
+          cx->st_pair_redo += h[37];
           cx->st_boot_f64_fma += (double)h[6] * 64.0 * nb + (double)h[7] * nb * (double)round_up(G, 64);
         }
       } else {
@@ -1136,6 +1145,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "tile_groups") ctx->opt_tile_groups = (int)value;
   else if (n == "tile_max_mult") ctx->opt_tile_max_mult = (int)value;
   else if (n == "tile_order") ctx->opt_tile_order = value != 0;
+  else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
 }
@@ -1149,6 +1159,7 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "boot_f64_fma") *value = ctx->st_boot_f64_fma;
   else if (n == "boot_path") *value = ctx->st_boot_path;
   else if (n == "skip_redo") *value = ctx->st_skip_redo;
+  else if (n == "pair_redo") *value = ctx->st_pair_redo;
   else if (n == "degen") *value = ctx->st_degen;
   else if (n == "host_setup_ms") *value = ctx->st_host_ms[0];
   else if (n == "host_unique_ms") *value = ctx->st_host_ms[1];
@@ -1163,6 +1174,7 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
 int scde_ctx_reset_stats(scde_ctx* ctx) {
   if (!ctx) return fail(SCDE_EARG, "null argument");
   ctx->st_skip_slabs = ctx->st_skip_kept = ctx->st_skip_stretches = ctx->st_skip_redo = ctx->st_degen = 0;
+  ctx->st_pair_redo = 0;
   for (double& x : ctx->st_host_ms) x = 0;
   ctx->st_boot_f64_fma = 0;
   for (double& x : ctx->st_tile_hist) x = 0;

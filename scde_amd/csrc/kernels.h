@@ -166,9 +166,12 @@ struct TileBootArgs {
   int maxgroups;             // 32-point bound tiles computed per slab, 1..4 (4; tests force the fallback with fewer)
   int* stats;                // nullable: [0] slabs, [1] tiles computed, [2] tiles, [3] slabs left to k_boot2,
                              // [4] sum of groups x entries (FMA count / (64 nb)), [5] entries of the slabs left,
-                             // [6 + i] slabs that computed i tiles (i <= 28)
+                             // [6 + i] slabs that computed i tiles (i <= 28), [35] slabs a pair pass left
   const int* order;          // nullable: genes in this order (launch_gene_order)
   unsigned* pmask;           // [ngenes][P] tiles each slab's partial row holds (k_sum_partials reads those)
+  int pairs = 0;             // a wave per two slabs of a gene, two bound tiles each (wide cells: most slabs
+                             // need two); slabs needing more take a four-tile pass over `wide`
+  int* wide = nullptr;       // [1 + ngenes * P] pair mode's list: [0] length, then g * P + p
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending

@@ -189,7 +189,8 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
 }
 
 #ifndef SCDE_KT_DIAG
-#define SCDE_KT_DIAG 0  // timing-only builds: 1 trivial dnbinom, 2 no exp, 4 no log, 8 no stores
+#define SCDE_KT_DIAG 0  // timing-only builds: 1 trivial dnbinom, 2 no exp, 4 no log, 8 no stores, 16 loop 1
+                        // only, 32 staging and constants only, 64 no tile bounds
 #endif
 constexpr int kStretchSlots = 8;  // per-column stretch bounds: ceil(G / 64) <= 7 used
 __device__ __forceinline__ float gt_maxf(float a, float b) { return (b > a) ? b : a; }
@@ -811,7 +812,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
         dout[k] = r;
       }
       r = in ? r : -INFINITY;
-      if (BM == kBoundTiles) {
+      if (BM == kBoundTiles && !(SCDE_KT_DIAG & 64)) {
         // this chunk's two 32-point bound tiles (rows 0-1 and 2-3; row maxima rounded up to
         // 2^-8, floor -2^29): lanes 2j, 2j + 1 collect both rows of their tile (lanes 32 i,
         // 32 i + 16) and keep the larger
@@ -1995,49 +1996,83 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8p, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
-    int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask) {
+    int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask,
+    int pairs, const int* __restrict__ ilist, int* __restrict__ wide) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
-  __shared__ float ubs[WB][kBTileMax * NB];  // [wave][bound tile][boot] bounds
+  __shared__ float ubs[WB][kBTileMax * NB];  // [wave][bound tile][boot] slab A's bounds
 #ifdef SCDE_TILE_TEST_WB1
   __shared__ unsigned bstage[WB][64];  // hazard-test builds: the LDS that would cap occupancy (never run)
 #else
   __shared__ unsigned bstage[WB][1024 + 512];  // [wave] bound staging: 16 x 64 tile words | 16 x 32 pair words
 #endif
-  __shared__ float fmx[WB][2][32];          // [wave][.][boot] maxima
-  __shared__ double tsum[WB][8][NB];        // [wave][tile slot][boot] partial sums
-  __shared__ double finv[WB][32];
+  __shared__ float fmx[WB][2][32];          // [wave][slab][boot] maxima
   __shared__ double etab[64];
   const int lane = threadIdx.x & 63;
   const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
   __syncthreads();
-  const int item = xcd_block(blockIdx.x, gridDim.x) * WB + wsid;
-  if (item >= ngenes * P) return;
-  const int gi = item / P, p = item - gi * P, b0 = p * NB;
-  const int g = order ? order[gi] : gi;
+  // the bound staging area, once the bound loops are done: slab B's bounds | tile partial sums
+  // [slot][boot] | 1 / (S nboot) [slab][boot] (the shipped 4-wave block stays under 40 KB of LDS:
+  // four blocks, 16 waves per CU)
+#ifndef SCDE_TILE_TEST_WB1
+  static_assert(2 * ((kBTileMax * NB + 1) / 2) + 2 * (8 * NB + 2 * 32) <= (int)(sizeof(bstage[0]) / 4),
+                "the staging area must hold slab B's bounds, the tile sums and the normalisers");
+#endif
+  float* const ubB = reinterpret_cast<float*>(&bstage[wsid][0]);
+  double* const tsum = reinterpret_cast<double*>(&bstage[wsid][2 * ((kBTileMax * NB + 1) / 2)]);
+  double* const finv = tsum + 8 * NB;
+  // ---- the wave's slabs: (gene, slab) items; in pair mode (gene, slab pair) items, slabs 2i
+  // and 2i + 1 side by side (a last odd slab alone, all four bound tiles); in list mode the
+  // slabs a pair pass could not finish, all four bound tiles each
+  const int idx = xcd_block(blockIdx.x, gridDim.x) * WB + wsid;
+  int g, pA, pB = -1;
+  if (ilist) {
+    if (idx >= ilist[0]) return;
+    const int it = ilist[1 + idx];
+    g = it / P;
+    pA = it - g * P;
+  } else if (pairs) {
+    const int PP = (P + 1) >> 1;
+    if (idx >= ngenes * PP) return;
+    const int gi = idx / PP, pi = idx - gi * PP;
+    g = order ? order[gi] : gi;
+    pA = 2 * pi;
+    pB = (2 * pi + 1 < P) ? 2 * pi + 1 : -1;
+  } else {
+    if (idx >= ngenes * P) return;
+    const int gi = idx / P;
+    g = order ? order[gi] : gi;
+    pA = idx - gi * P;
+  }
+  const bool pr = pB >= 0;  // two slabs: rows 0-1 slab A's two best bound tiles, rows 2-3 slab B's
+  const int nsl = pr ? 2 : 1;
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
-    if (lane == 0) {
-      redo[(long long)g * P + p] = 1;
-      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
-      pmask[(long long)g * P + p] = ~0u;
+    if (lane < nsl) {
+      const int q = (long long)g * P + (lane ? pB : pA);
+      redo[q] = 1;
+      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = q;
+      pmask[q] = ~0u;
     }
     return;
   }
   const int n = nnz[g];
   const int NT = (G + 15) >> 4, NTB = (G + 31) >> 5;  // 16-point sum tiles, 32-point bound tiles
-  const int nlive = min(NB, nboot - b0);
   const int r = lane & 15, h = lane >> 4;
   const int2* __restrict__ E = ent + (long long)g * ent_stride;
   const int set = wset ? wset[g] : 0;
-  float* ub = ubs[wsid];
   // ---- 1. bound tiles (C layout of the 16x16x64 MFMA: bound tile r, boots 16 bt + 4 h + q).  Per
   // 64-entry chunk each lane loads one entry's data with wide loads -- its (cell, column), the
   // column's 16 tile bounds (64 B) and the cell's 16 multiplicity pairs of this slab (32 B) --
   // and writes them transposed into the wave's LDS area; the MFMA fragments are then contiguous
   // LDS reads: 7 vector-memory instructions per chunk instead of 40 single-entry gathers.
-  if (SCDE_TILE_DIAG & 2) {  // timing build: rows without bounds (results wrong)
-    for (int i = lane; i < kBTileMax * NB; i += 64) ub[i] = 0.0f;
-  } else {
+#pragma unroll 1
+  for (int sl = 0; sl < nsl; ++sl) {
+    const int p = sl ? pB : pA, b0 = p * NB;
+    float* ub = sl ? ubB : ubs[wsid];
+    if (SCDE_TILE_DIAG & 2) {  // timing build: rows without bounds (results wrong)
+      for (int i = lane; i < kBTileMax * NB; i += 64) ub[i] = 0.0f;
+      continue;
+    }
     const unsigned pstride = 32u * (unsigned)P;
     const unsigned char* __restrict__ W8 = W8p + (long long)set * ncells * pstride + 32 * p;
     const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
@@ -2120,47 +2155,68 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   return;  // timing build: bounds only
 #endif
   wave_sync();
-  // ---- 2. the bound tiles with the largest bound over the slab's live boots: maxgroups (4; the
-  // tests force the fallback with fewer), all of them when the grid has no more
-  float sc = -INFINITY;
-  if (lane < NTB)
-    for (int b = 0; b < nlive; ++b) sc = fmaxf(sc, ub[lane * NB + b]);
-  sc = (lane < NTB) ? sc : -INFINITY;
-  const int nsel = min(max(1, min(maxgroups, 4)), NTB);  // bound tiles computed: 4 (tests: fewer)
+  const int b0A = pA * NB, b0B = pr ? pB * NB : 0;
+  const int nliveA = min(NB, nboot - b0A), nliveB = pr ? min(NB, nboot - b0B) : 0;
+  // ---- 2. per slab the bound tiles with the largest bound over its live boots: four (one
+  // slab; maxgroups, the tests force the fallback with fewer), two each (a pair); all of them
+  // when the grid has no more
+  float scA = -INFINITY, scB = -INFINITY;
+  if (lane < NTB) {
+    for (int b = 0; b < nliveA; ++b) scA = fmaxf(scA, ubs[wsid][lane * NB + b]);
+    for (int b = 0; b < nliveB; ++b) scB = fmaxf(scB, ubB[lane * NB + b]);
+  }
+  const int nsel = pr ? min(2, NTB) : min(max(1, min(maxgroups, 4)), NTB);  // tiles per slab
   int tl[4] = {0, 0, 0, 0};
-  unsigned bdone = 0;  // bound tiles computed
+  unsigned bdA = 0, bdB = 0;  // bound tiles computed, per slab
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    if (j < nsel) {
+    const bool onB = pr && j >= 2;
+    if ((pr ? (j & 1) : j) < nsel) {
       // the 16 bound-tile scores sit in lanes 0..15: a 16-lane DPP max, read back from lane 0
+      const float sc = onB ? scB : scA;
       float m = sc;
       m = fmaxf(m, dpp_f<kDppXor1>(m));
       m = fmaxf(m, dpp_f<kDppXor2>(m));
       m = fmaxf(m, dpp_f<kDppHalfMirror>(m));
       m = fmaxf(m, dpp_f<kDppMirror>(m));
       m = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(m)));
-      const unsigned long long bl = __ballot(lane < NTB && !((bdone >> lane) & 1) && sc == m);
+      const unsigned bd = onB ? bdB : bdA;
+      const unsigned long long bl = __ballot(lane < NTB && !((bd >> lane) & 1) && sc == m);
       const int t = __ffsll((long long)bl) - 1;
       tl[j] = t;
-      bdone |= 1u << t;
-      if (lane == t) sc = -INFINITY;
+      if (onB) {
+        bdB |= 1u << t;
+        if (lane == t) scB = -INFINITY;
+      } else {
+        bdA |= 1u << t;
+        if (lane == t) scA = -INFINITY;
+      }
     }
   }
-  // the 16-point sum tiles of the computed bound tiles
-  unsigned done = 0;
+  // the 16-point sum tiles of the computed bound tiles, per slab
+  const unsigned ntmask = (NT >= 32) ? ~0u : ((1u << NT) - 1);
+  unsigned doneA = 0, doneB = 0;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (j < nsel) done |= 3u << (2 * tl[j]);
-  done &= (NT >= 32) ? ~0u : ((1u << NT) - 1);
-  // lane l: sum tile slot l >> 3 = bound tile (l >> 4), half (l >> 3) & 1
-  const int slot = lane >> 3, m2 = lane & 7;
+  for (int j = 0; j < 4; ++j) {
+    if ((pr ? (j & 1) : j) >= nsel) continue;
+    if (pr && j >= 2)
+      doneB |= 3u << (2 * tl[j]);
+    else
+      doneA |= 3u << (2 * tl[j]);
+  }
+  doneA &= ntmask;
+  doneB &= ntmask;
+  // lane l: row l >> 4 = one bound tile of one slab; sum tile slot l >> 3 (its half l >> 3 & 1)
+  const int slot = lane >> 3, m2 = lane & 7, row = lane >> 4;
   int mybt = tl[0];
 #pragma unroll
-  for (int j = 1; j < 4; ++j) mybt = ((slot >> 1) == j) ? tl[j] : mybt;
+  for (int j = 1; j < 4; ++j) mybt = (row == j) ? tl[j] : mybt;
+  const int mys = (pr && row >= 2) ? 1 : 0;  // the lane's slab
   const int mytile = 2 * mybt + (slot & 1);
   const int k0 = 16 * mytile + 2 * m2;
-  const bool live = (slot >> 1) < nsel;
+  const bool live = (pr ? (row & 1) : row) < nsel;
   const bool l0 = live && k0 < G, l1 = live && k0 + 1 < G;
+  const int b0 = mys ? b0B : b0A;
   const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
   const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
   // ---- rows: Z_b + sum_e W_be D_e at points k0, k0 + 1 (k0 even: 16-byte aligned pairs)
@@ -2235,37 +2291,60 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     }
     asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(w[0]), "+v"(w[1]));
   }
-  {
+  // per slab maxima m'_b (f32) over its lanes -> fmx[wsid][slab]
+#pragma unroll 1
+  for (int sl = 0; sl < nsl; ++sl) {
     double mx[NB];
 #pragma unroll
-    for (int i = 0; i < NB; ++i) mx[i] = gt_max(a0[i], a1[i]);
-    wave_max_partials_all<NB>(mx, &fmx[0][0][0], lane, 2 * wsid);
+    for (int i = 0; i < NB; ++i) mx[i] = (mys == sl) ? gt_max(a0[i], a1[i]) : -INFINITY;
+    wave_max_partials_all<NB>(mx, &fmx[0][0][0], lane, 2 * wsid + sl);
   }
   wave_sync();
-  // ---- 3. post-check: every bound tile not computed stays below the exact maxima minus 51
-  bool need = false;
-  if (lane < NTB && !((bdone >> lane) & 1))
-    for (int b = 0; b < nlive; ++b) need |= (double)ub[lane * NB + b] >= (double)fmx[wsid][0][b] - 51.0;
-  if (SCDE_TILE_DIAG & 2) need = false;
-  if (__ballot(need)) {  // the whole slab goes to k_boot2's fallback launch
-    if (lane == 0) {
-      redo[(long long)g * P + p] = 1;
-      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = g * P + p;
-      pmask[(long long)g * P + p] = ~0u;
-      if (stats) {
-        atomicAdd(&stats[3], 1);
-        atomicAdd(&stats[5], (n + 3) & ~3);
+  // ---- 3. post-check per slab: every bound tile not computed stays below the exact maxima
+  // minus 51; a slab that fails goes whole to the four-tile list pass (pair mode) or to
+  // k_boot2's fallback launch
+  unsigned failm = 0;
+#pragma unroll 1
+  for (int sl = 0; sl < nsl; ++sl) {
+    const unsigned bd = sl ? bdB : bdA;
+    const int nl = sl ? nliveB : nliveA;
+    bool need = false;
+    if (lane < NTB && !((bd >> lane) & 1))
+      for (int b = 0; b < nl; ++b) need |= (double)(sl ? ubB : ubs[wsid])[lane * NB + b] >= (double)fmx[wsid][sl][b] - 51.0;
+    if (SCDE_TILE_DIAG & 2) need = false;
+    if (__ballot(need)) {
+      failm |= 1u << sl;
+      if (lane == 0) {
+        const int q = g * P + (sl ? pB : pA);
+        if (pr) {
+          wide[1 + atomicAdd(&wide[0], 1)] = q;
+          if (stats) atomicAdd(&stats[35], 1);
+        } else {
+          redo[q] = 1;
+          redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = q;
+          pmask[q] = ~0u;
+          if (stats) {
+            atomicAdd(&stats[3], 1);
+            atomicAdd(&stats[5], (n + 3) & ~3);
+          }
+        }
       }
     }
-    return;
   }
-  if (lane < nlive && !(fabs((double)fmx[wsid][0][lane]) <= degen_thresh)) degen[g] = 1;
-  // ---- 4. softmax terms, tile partial sums, jp partial row
+  if (stats && lane == 0) atomicAdd(&stats[4], 2 * ((n + 1) & ~1));  // 128 points = two 64-lane groups' FMAs
+  if (failm == (pr ? 3u : 1u)) return;
+  const bool mine = !((failm >> mys) & 1);  // the lane's slab is finished here
+  if (lane < nsl && !((failm >> lane) & 1)) {
+    const int nl = lane ? nliveB : nliveA;
+    for (int b = 0; b < nl; ++b)
+      if (!(fabs((double)fmx[wsid][lane][b]) <= degen_thresh)) degen[g] = 1;
+  }
+  // ---- 4. softmax terms, tile partial sums, jp partial rows
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const double m = (double)fmx[wsid][0][i];
+    const double m = (double)fmx[wsid][mys][i];
     const double d0 = a0[i] - m, d1 = a1[i] - m;
-    const bool n0 = l0 && d0 >= kBootExpCut, n1 = l1 && d1 >= kBootExpCut;
+    const bool n0 = mine && l0 && d0 >= kBootExpCut, n1 = mine && l1 && d1 >= kBootExpCut;
     if (__builtin_amdgcn_ballot_w64(n0 || n1)) {
       a0[i] = n0 ? exp_tab(d0, etab) : 0.0;
       a1[i] = n1 ? exp_tab(d1, etab) : 0.0;
@@ -2274,29 +2353,36 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
       a1[i] = 0.0;
     }
     const double ps = pair8_sum(a0[i], a1[i]);
-    if (m2 == 0 && live) tsum[wsid][slot][i] = ps;
+    if (m2 == 0 && live) tsum[slot * NB + i] = ps;
   }
   wave_sync();
-  if (lane < NB) {
-    double S = 0.0;
-    for (unsigned mm = done; mm; mm &= mm - 1) {
-      const int t = __builtin_ffs((int)mm) - 1;
-      int sl = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (tl[j] == (t >> 1) && j < nsel) sl = 2 * j + (t & 1);
-      S += tsum[wsid][sl][lane];
-    }
-    finv[wsid][lane] = (b0 + lane < nboot) ? 1.0 / (S * norm_mult) : 0.0;
-  }
-  wave_sync();
-  double* prow = part + (long long)p * part_stride + (long long)g * GS;
   {
+    // lanes 0..NB-1: slab A's boots, 32..32+NB-1: slab B's; S over the slab's tiles in tile order
+    const int sl = lane >> 5, b = lane & 31;
+    if (sl < nsl && b < NB && !((failm >> sl) & 1)) {
+      const unsigned dn = sl ? doneB : doneA;
+      double S = 0.0;
+      for (unsigned mm = dn; mm; mm &= mm - 1) {
+        const int t = __builtin_ffs((int)mm) - 1;
+        int sslot = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool js = pr && j >= 2;
+          if (tl[j] == (t >> 1) && (pr ? (j & 1) : j) < nsel && (int)js == sl) sslot = 2 * j + (t & 1);
+        }
+        S += tsum[sslot * NB + b];
+      }
+      finv[sl * 32 + b] = ((sl ? b0B : b0A) + b < nboot) ? 1.0 / (S * norm_mult) : 0.0;
+    }
+  }
+  wave_sync();
+  if (mine) {
+    double* prow = part + (long long)(mys ? pB : pA) * part_stride + (long long)g * GS;
     double j0 = 0.0, j1 = 0.0;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-      j0 = fma(a0[i], finv[wsid][i], j0);
-      j1 = fma(a1[i], finv[wsid][i], j1);
+      j0 = fma(a0[i], finv[mys * 32 + i], j0);
+      j1 = fma(a1[i], finv[mys * 32 + i], j1);
     }
     if (l1)
       *reinterpret_cast<d2_t*>(prow + k0) = d2_t{j0, j1};
@@ -2304,13 +2390,15 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
       prow[k0] = j0;
   }
   // tiles not computed stay unwritten: k_sum_partials reads only the tiles in pmask
-  if (lane == 0) pmask[(long long)g * P + p] = done;
-  if (stats && lane == 0) {
-    atomicAdd(&stats[0], 1);
-    atomicAdd(&stats[1], __builtin_popcount(done));
-    atomicAdd(&stats[2], NT);
-    atomicAdd(&stats[4], 2 * ((n + 1) & ~1));  // 128 points = two 64-lane groups' worth of FMAs
-    atomicAdd(&stats[6 + __builtin_popcount(done)], 1);
+  if (lane < nsl && !((failm >> lane) & 1)) {
+    const unsigned dn = lane ? doneB : doneA;
+    pmask[(long long)g * P + (lane ? pB : pA)] = dn;
+    if (stats) {
+      atomicAdd(&stats[0], 1);
+      atomicAdd(&stats[1], __builtin_popcount(dn));
+      atomicAdd(&stats[2], NT);
+      atomicAdd(&stats[6 + __builtin_popcount(dn)], 1);
+    }
   }
 }
 
@@ -2324,7 +2412,8 @@ template __global__ void k_boot_tiles<20, 1>(const double* __restrict__, const i
                                              double* __restrict__, long long, int* __restrict__, int,
                                              const unsigned char* __restrict__, int, const unsigned* __restrict__,
                                              const int* __restrict__, const int* __restrict__, int, int* __restrict__,
-                                             int* __restrict__, const int* __restrict__, unsigned* __restrict__);
+                                             int* __restrict__, const int* __restrict__, unsigned* __restrict__, int,
+                                             const int* __restrict__, int* __restrict__);
 #endif
 
 // jp[g, k] = sum over slabs p (in order) of part[p][g][k]
@@ -3332,14 +3421,29 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   hipError_t e = hipMemsetAsync(a.redo, 0, sizeof(int) * ((size_t)a.ngenes * P + 1), s);
   if (e != hipSuccess) return e;
   const long long items = (long long)a.ngenes * P;
+  // pair mode: a wave per two slabs of a gene, two bound tiles each; the slabs that need more
+  // go to a four-tile pass over the compacted list `wide` ([0] length, then g * P + p)
+  const bool pairs = tb.pairs && P >= 2 && tb.wide;
+  if (pairs) {
+    e = hipMemsetAsync(tb.wide, 0, sizeof(int), s);
+    if (e != hipSuccess) return e;
+  }
   constexpr int WB = 4;
-  const dim3 grid((unsigned)div_up(items, WB)), block(64 * WB);
+  const long long items1 = pairs ? (long long)a.ngenes * ((P + 1) / 2) : items;
+  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : 0;  // slabs a pair pass may leave
 #define SCDE_BT(NBV)                                                                                              \
   case NBV:                                                                                                        \
-    hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), grid, block, 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,  \
-                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
-                       a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups,  \
-                       a.redo, tb.stats, tb.order, tb.pmask);                                                    \
+    hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
+                       a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,      \
+                       a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq,      \
+                       tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask, pairs ? 1 : 0, \
+                       nullptr, tb.wide);                                                                        \
+    if (pairs)                                                                                                     \
+      hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items2, WB)), dim3(64 * WB), 0, s, a.D,   \
+                         a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,    \
+                         a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq,    \
+                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask, 0,        \
+                         tb.wide, nullptr);                                                                      \
     break;
   switch (a.nb) {
     SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)

@@ -9,7 +9,9 @@ tiles, the default; k_boot2 with its 64-point stretch mask, boot_tiles = 0), wit
 (default), off (boot_skip = 0), and forced onto the second-chance paths so that the extra work
 really happens (its count is read back and must be > 0): a negative heuristic slack
 (skip_slack) that makes the masks drop stretches the post-check must reject, the tile kernel
-limited to 2 bound tiles (tile_groups = 2) so slabs needing more go to k_boot2's fallback launch, or a multiplicity limit of 1 (tile_max_mult) so the call, with its tables set up
+limited to 2 bound tiles (tile_groups = 2) so slabs needing more go to k_boot2's fallback launch,
+the pair mode (two slabs per wave, two bound tiles each; pair_cells = 1) whose slabs needing more
+take the four-tile list pass, or a multiplicity limit of 1 (tile_max_mult) so the call, with its tables set up
 for the tile path, runs plain k_boot2 instead (the "multiplicity above 127" fallback) -- and
 compare every run with the oracle at the SURVEY §8(d) bar, and the runs with each other bit
 for bit (the kernels share rows, maxima and tile-ordered sums).
@@ -40,13 +42,15 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("tile_groups", opts.get("tile_groups", 4))
     ctx.set_option("boot_tiles_cells", opts.get("boot_tiles_cells", 0))
     ctx.set_option("tile_order", opts.get("tile_order", 1))
+    ctx.set_option("pair_cells", opts.get("pair_cells", 1000))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
     try:
         out = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=nrand,
                                              n_cores=ncores, return_posteriors=True)
-        stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo", "boot_path")}
+        stats = {k: ctx.stat(k) for k in ("skip_slabs", "skip_kept", "skip_stretches", "skip_redo", "boot_path",
+                                          "pair_redo")}
     finally:
         ctx.set_option("tile_max_mult", 127)
         ctx.set_option("boot_skip", 1)
@@ -55,6 +59,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("tile_groups", 4)
         ctx.set_option("boot_tiles_cells", 200)
         ctx.set_option("tile_order", 1)
+        ctx.set_option("pair_cells", 1000)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -72,6 +77,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "noskip": {"boot_skip": 0},
         "tiles-forced-redo": {"tile_groups": 2},
         "tiles-unordered": {"tile_order": 0},
+        "tiles-pairs": {"pair_cells": 1},
+        "tiles-pairs-redo": {"pair_cells": 1, "tile_groups": 2},
         "tiles-mult-fallback": {"tile_max_mult": 1},
         "stretch": {"boot_tiles": 0},
         "stretch-forced-redo": {"boot_tiles": 0, "skip_slack": -45.0},
@@ -85,6 +92,12 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
             assert stats["boot_path"] == 0 and stats["skip_slabs"] == 0, stats
         elif name == "tiles-forced-redo":  # 2 bound tiles (64 points): slabs needing more go to k_boot2
             assert stats["boot_path"] == 1 and stats["skip_redo"] > 0, stats
+        elif name == "tiles-pairs":
+            # two slabs per wave, two bound tiles each: at these cell counts many slabs need more and
+            # take the four-tile list pass
+            assert stats["boot_path"] == 1 and stats["skip_slabs"] > 0 and stats["pair_redo"] > 0, stats
+        elif name == "tiles-pairs-redo":  # the list pass limited to two tiles too: k_boot2 takes the rest
+            assert stats["boot_path"] == 1 and stats["pair_redo"] > 0 and stats["skip_redo"] > 0, stats
         else:
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
             assert stats["boot_path"] == (0 if name.startswith("stretch") else 1), (name, stats)
@@ -100,8 +113,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"], what=f"{name} Z")
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
-    for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-unordered", "tiles-mult-fallback",
-                                    "stretch", "stretch-forced-redo")),):
+    for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-unordered", "tiles-pairs",
+                                    "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
         for name in others:
             for i in range(2):
                 np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got[base]["joint.posteriors"][i])
