@@ -9,7 +9,7 @@ for lib in "$@"; do
     opts=""; name=${lib%%:*}
     if [[ "$lib" == *:* ]]; then for o in $(echo ${lib#*:} | tr , ' '); do opts="$opts --opt $o"; done; fi
     if [ "$name" = main ]; then env=""; else env="SCDE_LIB=diag/lib$name.so"; fi
-    env $env timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 --cpu-workers 0 $opts \
+    env $env timeout -k 10 200 python bench.py --config $c --steps ${STEPS:-10} --warmup 2 --cpu-sample 0 --cpu-workers 0 $opts \
       > "$out/$lib.$c.log" 2>&1 || { tail -5 "$out/$lib.$c.log"; exit 1; }
     python - "$out/$lib.$c.log" "$lib" "$c" <<'PY'
 import json, sys
