@@ -500,8 +500,11 @@ __device__ __forceinline__ double bd0_poly(double x, double np) {
 
 // L = log x - log np (precomputed as log x - log n - log p).  The series region is taken
 // with a wave-uniform branch: only waves with a lane in it evaluate the polynomial.
+#ifndef SCDE_BD0_DIAG
+#define SCDE_BD0_DIAG 0  // timing-only builds: 1 = never the series (results wrong)
+#endif
 __device__ __forceinline__ double bd0_fast(double x, double np, double L) {
-  const bool ser = fabs(x - np) < 0.1 * (x + np);
+  const bool ser = !(SCDE_BD0_DIAG & 1) && fabs(x - np) < 0.1 * (x + np);
   double b = x * L + np - x;
   if (__builtin_amdgcn_ballot_w64(ser)) {
     const double sv = bd0_poly(x, np);
