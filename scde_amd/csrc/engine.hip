@@ -170,6 +170,11 @@ struct scde_ctx {
   hipEvent_t up_ev[2] = {nullptr, nullptr};
   hipEvent_t uq_ev = nullptr;  // the second group's unique sets (built on copy_stream) are ready
   hipEvent_t modes_ev = nullptr;  // run_posterior's posterior modes are computed (they need the tables only)
+  // run_posterior's bootstrap set-up (draw uploads, ELL rows, baseline bound sums, Z, gene
+  // order) needs only the count-0 columns: it runs on aux_stream after p1_ev (phase 1 of the
+  // tables), beside phase 2, and the bootstrap waits for aux_ev
+  hipStream_t aux_stream = nullptr;
+  hipEvent_t p1_ev = nullptr, aux_ev = nullptr;
   // Pinned staging arena for the small per-call transfers (cell lists, offsets, draws,
   // multiplicities, tasks; the unique builder's size read-backs).  A pageable copy is staged
   // by the runtime and costs 20-40 us of host latency each; from pinned memory it is a plain
@@ -329,6 +334,9 @@ struct scde_ctx {
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (uq_ev) (void)hipEventDestroy(uq_ev);
     if (modes_ev) (void)hipEventDestroy(modes_ev);
+    if (p1_ev) (void)hipEventDestroy(p1_ev);
+    if (aux_ev) (void)hipEventDestroy(aux_ev);
+    if (aux_stream) (void)hipStreamDestroy(aux_stream);
     if (pin) (void)hipHostFree(pin);
     for (auto& e : up_ev)
       if (e) (void)hipEventDestroy(e);
@@ -396,22 +404,24 @@ char* pin_alloc(scde_ctx* cx, size_t bytes) {
     // read-backs land in each unique set's own area, never here)
     if (hipStreamSynchronize(cx->stream) != hipSuccess) return nullptr;
     if (cx->copy_stream && hipStreamSynchronize(cx->copy_stream) != hipSuccess) return nullptr;
+    if (cx->aux_stream && hipStreamSynchronize(cx->aux_stream) != hipSuccess) return nullptr;
     off = 0;
   }
   cx->pin_off = off + bytes;
   return cx->pin + off;
 }
 
-int upload(scde_ctx* cx, Buf& b, const void* src, size_t bytes) {
+int upload_on(scde_ctx* cx, Buf& b, const void* src, size_t bytes, hipStream_t st) {
   HCHK(b.ensure(bytes));
   if (!bytes) return SCDE_OK;
   if (char* h = pin_alloc(cx, bytes)) {
     std::memcpy(h, src, bytes);
     src = h;
   }
-  HCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, cx->stream));
+  HCHK(hipMemcpyAsync(b.p, src, bytes, hipMemcpyHostToDevice, st));
   return SCDE_OK;
 }
+int upload(scde_ctx* cx, Buf& b, const void* src, size_t bytes) { return upload_on(cx, b, src, bytes, cx->stream); }
 
 // Build ucl/uci for the selected cells on device (R/functions.R:609-610).  Unique
 // counts come out sorted ascending rather than in first-appearance order; the order
@@ -691,6 +701,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   if (fused) {
     ta.phase = 1;
     HCHK(launch_tables(ta, st));
+    if (!cx->p1_ev) HCHK(hipEventCreateWithFlags(&cx->p1_ev, hipEventDisableTiming));
+    HCHK(hipEventRecord(cx->p1_ev, st));
     ta.phase = 2;
     HCHK(launch_tables(ta, st));
   } else {
@@ -729,8 +741,17 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     HCHK(hipMemsetAsync(s.jp, 0, sizeof(double) * (size_t)N * G, st));
   } else {
     if (!fused) make_draws(s, Bp, draws, W, ndraw);
-    RCHK(upload(cx, cx->Wt, W.data(), sizeof(double) * W.size()));
-    RCHK(upload(cx, cx->draws, draws.data(), sizeof(int) * draws.size()));
+    // the set-up below reads only phase 1's count-0 columns (fused path): on the aux stream,
+    // beside phase 2 of the tables
+    hipStream_t sa = st;
+    if (fused) {
+      if (!cx->aux_stream) HCHK(hipStreamCreateWithFlags(&cx->aux_stream, hipStreamNonBlocking));
+      if (!cx->aux_ev) HCHK(hipEventCreateWithFlags(&cx->aux_ev, hipEventDisableTiming));
+      sa = cx->aux_stream;
+      HCHK(hipStreamWaitEvent(sa, cx->p1_ev, 0));
+    }
+    RCHK(upload_on(cx, cx->Wt, W.data(), sizeof(double) * W.size(), sa));
+    RCHK(upload_on(cx, cx->draws, draws.data(), sizeof(int) * draws.size(), sa));
     if (!fused) {
       HCHK(cx->base_col.ensure(sizeof(int) * C));
       HCHK(launch_base_cols(u.ucl.as<int>(), u.ucl_off.as<long long>(), C, cx->has_clamp.as<unsigned char>(),
@@ -749,7 +770,22 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     // the baseline columns: T (slow path) or the fused D buffer, which holds T there
     const double* Tbase = fused ? cx->E.as<double>() : cx->T.as<double>();
     HCHK(launch_ell(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->base_col.as<int>(), stride,
-                    (int)ncols, tpath ? 64 : 8, cx->ent.as<int2>(), cx->nnz.as<int>(), st));
+                    (int)ncols, tpath ? 64 : 8, cx->ent.as<int2>(), cx->nnz.as<int>(), sa));
+    // tile path: genes in order of their count sums (waves in flight share columns in L2)
+    const bool have_order = tpath && fast && cx->opt_tile_order && N > 1;
+    if (have_order) {
+      HCHK(cx->gkey.ensure(sizeof(unsigned) * N));
+      HCHK(cx->gkey2.ensure(sizeof(unsigned) * N));
+      HCHK(cx->gidx.ensure(sizeof(int) * N));
+      HCHK(cx->gorder.ensure(sizeof(int) * N));
+      size_t wb = 0;
+      HCHK(launch_gene_order(nullptr, nullptr, N, nullptr, nullptr, nullptr, &wb, sa));
+      HCHK(cx->gwork.ensure(std::max<size_t>(wb, 1)));
+      HCHK(launch_gene_key(cx->ent.as<int2>(), cx->nnz.as<int>(), stride, u.ucl.as<int>(), N, cx->gkey.as<unsigned>(),
+                           cx->gidx.as<int>(), sa));
+      HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), N, cx->gkey2.as<unsigned>(),
+                             cx->gorder.as<int>(), cx->gwork.p, &wb, sa));
+    }
     if (tpath) {
       // byte multiplicities [set][cell][boot] (baseline bound sums and the tile bounds)
       // and, for the tile bounds' A fragments, per slab the pairs (boot r, boot 16 + r) of its nb
@@ -768,27 +804,31 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
               w8p[(((size_t)set * C + c) * P + p) * 32 + slot] = (unsigned char)wr[b];
             }
         }
-      RCHK(upload(cx, cx->w8, w8.data(), w8.size()));
-      RCHK(upload(cx, cx->w8t, w8p.data(), w8p.size()));
+      RCHK(upload_on(cx, cx->w8, w8.data(), w8.size(), sa));
+      RCHK(upload_on(cx, cx->w8t, w8p.data(), w8p.size(), sa));
       HCHK(cx->zubound.ensure(sizeof(int) * (size_t)nsets * 4 * kQTiles * Bt));
       HCHK(launch_zuq(cx->ubound.as<unsigned>(), cx->base_col.as<int>(), C, cx->w8.as<unsigned char>(), Bt, nsets,
-                      cx->zubound.as<int>(), st));
+                      cx->zubound.as<int>(), sa));
     }
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
     HCHK(launch_baseline_z(Tbase, G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
-                           cx->Z.as<double>(), st));
+                           cx->Z.as<double>(), sa));
     if (stretch_skip) {
       HCHK(cx->zubound.ensure(sizeof(double) * 8 * (size_t)nsets * Bp));
       HCHK(launch_stretch_zu(cx->ubound.as<double>(), cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
-                             cx->zubound.as<double>(), st));
+                             cx->zubound.as<double>(), sa));
     }
     cx->mark_end(SLOT_OTHER, ev);
     if (nsets > 1) {
       if ((int)s.wset.size() != N) return fail(SCDE_EINTERNAL, "wset size mismatch");
-      RCHK(upload(cx, cx->wset, s.wset.data(), sizeof(int) * N));
+      RCHK(upload_on(cx, cx->wset, s.wset.data(), sizeof(int) * N, sa));
     }
     HCHK(cx->degen.ensure(sizeof(int) * std::max(1, N)));
-    HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, N), st));
+    HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, N), sa));
+    if (sa != st) {  // the bootstrap waits for the set-up and for phase 2
+      HCHK(hipEventRecord(cx->aux_ev, sa));
+      HCHK(hipStreamWaitEvent(st, cx->aux_ev, 0));
+    }
     const int* wset_d = nsets > 1 ? cx->wset.as<int>() : nullptr;
     const double thresh = 16777216.0;  // 2^24: beyond this the sums' rounding order matters
     ev = cx->mark_begin(SLOT_BOOT);
@@ -849,20 +889,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
           HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * N)));
           tb.wide = cx->pwide.as<int>();
         }
-        if (cx->opt_tile_order && N > 1) {
-          HCHK(cx->gkey.ensure(sizeof(unsigned) * N));
-          HCHK(cx->gkey2.ensure(sizeof(unsigned) * N));
-          HCHK(cx->gidx.ensure(sizeof(int) * N));
-          HCHK(cx->gorder.ensure(sizeof(int) * N));
-          size_t wb = 0;
-          HCHK(launch_gene_order(nullptr, nullptr, N, nullptr, nullptr, nullptr, &wb, st));
-          HCHK(cx->gwork.ensure(std::max<size_t>(wb, 1)));
-          HCHK(launch_gene_key(cx->ent.as<int2>(), cx->nnz.as<int>(), stride, u.ucl.as<int>(), N,
-                               cx->gkey.as<unsigned>(), cx->gidx.as<int>(), st));
-          HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), N, cx->gkey2.as<unsigned>(),
-                                 cx->gorder.as<int>(), cx->gwork.p, &wb, st));
-          tb.order = cx->gorder.as<int>();
-        }
+        if (have_order) tb.order = cx->gorder.as<int>();
         HCHK(launch_boot_tiles(b2, tb, st));
         if (cx->opt_skip_stats) {
           int h[40];
