@@ -443,7 +443,8 @@ def main():
                     help="multi-GPU: strong = one fixed gene set split over the ranks (configs 3/4 default), "
                          "weak = a full gene set per rank")
     ap.add_argument("--cpu-sample", type=int, default=None, help="genes timed on the CPU baseline (0 = skip)")
-    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="no HIP-event stage times and no counter step (rocprofv3 runs: tools/profile.sh)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL, the real path) or gloo (CPU gather; rehearsal with ranks sharing one GPU)")
     ap.add_argument("--cpu-workers", type=int, default=16,
@@ -618,14 +619,19 @@ def main():
     ctx.set_profiling(False)
 
     # arithmetic the bootstrap kernels issue in one step (one extra untimed step with the
-    # context's counters on): FP64 lane FMAs of k_boot_tiles / k_boot2
-    ctx.set_option("skip_stats", 1)
-    ctx.reset_stats()
-    run(dc.ptr)
-    ctx.synchronize()
-    step_fma = ctx.stat("boot_f64_fma")
-    stage_name = BOOT_STAGES.get(int(ctx.stat("boot_path")), "bootstrap stage")
-    ctx.set_option("skip_stats", 0)
+    # context's counters on): FP64 lane FMAs of k_boot_tiles / k_boot2.  Not in --no-profile
+    # runs (tools/profile.sh's rocprofv3 passes): the counters' atomics slow that step's
+    # kernels 2x, which would skew rocprof's per-kernel averages
+    step_fma = None
+    stage_name = "bootstrap stage"
+    if not args.no_profile:
+        ctx.set_option("skip_stats", 1)
+        ctx.reset_stats()
+        run(dc.ptr)
+        ctx.synchronize()
+        step_fma = ctx.stat("boot_f64_fma")
+        stage_name = BOOT_STAGES.get(int(ctx.stat("boot_path")), "bootstrap stage")
+        ctx.set_option("skip_stats", 0)
 
     total_genes = NTOT * args.steps
     value = total_genes / dt
