@@ -503,11 +503,33 @@ __device__ __forceinline__ double bd0_poly(double x, double np) {
 #ifndef SCDE_BD0_DIAG
 #define SCDE_BD0_DIAG 0  // timing-only builds: 1 = never the series (results wrong)
 #endif
+// bd0 in the series region from L = log(x / np) itself, with no division: x = np e^L gives
+// bd0 = np psi(L), psi(L) = L e^L - e^L + 1 = sum_{k>=2} (k - 1) L^k / k!.  In the region
+// |v| < 0.1, |L| < log(1.1 / 0.9) = 0.2007, and the terms through k = 13 leave a tail below
+// 1.2e-18 of the first.  Its error is np |L| |dL| <= 0.2 np |dL| for an error dL of L (a
+// few ulps of log x and log np), a fifth of what x L + np - x carries outside the region.
+#ifndef SCDE_BD0_PSI
+#define SCDE_BD0_PSI 1
+#endif
+__device__ __forceinline__ double bd0_psi(double np, double L) {
+  double P = fma3(12.0 / 6227020800.0, L, 11.0 / 479001600.0);
+  P = fma3(P, L, 10.0 / 39916800.0);
+  P = fma3(P, L, 9.0 / 3628800.0);
+  P = fma3(P, L, 8.0 / 362880.0);
+  P = fma3(P, L, 7.0 / 40320.0);
+  P = fma3(P, L, 6.0 / 5040.0);
+  P = fma3(P, L, 5.0 / 720.0);
+  P = fma3(P, L, 4.0 / 120.0);
+  P = fma3(P, L, 3.0 / 24.0);
+  P = fma3(P, L, 2.0 / 6.0);
+  P = fma3(P, L, 0.5);
+  return np * ((L * L) * P);
+}
 __device__ __forceinline__ double bd0_fast(double x, double np, double L) {
   const bool ser = !(SCDE_BD0_DIAG & 1) && fabs(x - np) < 0.1 * (x + np);
   double b = x * L + np - x;
   if (__builtin_amdgcn_ballot_w64(ser)) {
-    const double sv = bd0_poly(x, np);
+    const double sv = SCDE_BD0_PSI ? bd0_psi(np, L) : bd0_poly(x, np);
     b = ser ? sv : b;
   }
   return b;
