@@ -213,6 +213,7 @@ struct scde_ctx {
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
+  int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
   int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
                                  // tiles each; the posterior narrows with the cells, most slabs need two)
   // statistics (scde_ctx_get_stat)
@@ -230,11 +231,12 @@ struct scde_ctx {
   // ucl/uci of a cell subset (R/functions.R:609-610); one set per group so both groups'
   // unique tables can be built up front, with their host syncs, before the heavy kernels
   struct UniqueSet {
-    Buf cellidx, cmax, cmin, woff, bits, rank, nuniq, ucl, ucl_off, uci;
+    Buf cellidx, cmax, cmin, woff, bits, rank, nuniq, ucl, ucl_off, uci, flags;
     std::vector<int> cmax_h, cmin_h, nuniq_h;
     std::vector<long long> woff_h, ucl_off_h;
     // pinned landing area of the phases' device -> host size read-backs: the set's own (not
     // the shared staging arena), so no later staging can recycle it before the host reads it
+    int fixed_flags = 0;  // unique_phase12_fixed's flags when no pinned landing area exists
     int* pin_land = nullptr;
     size_t pin_land_cap = 0;  // ints
     const int* pin_in = nullptr;  // this phase's read-back (pin_land, or null: pageable fallback)
@@ -256,7 +258,7 @@ struct scde_ctx {
       return pin_land;
     }
     void release() {
-      Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci, &tasks};
+      Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci, &flags, &tasks};
       for (Buf* x : b) x->release();
       if (pin_land) (void)hipHostFree(pin_land);
       pin_land = nullptr;
@@ -492,13 +494,59 @@ int unique_phase3(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   return SCDE_OK;
 }
 
+// Phases 1 and 2 in one, without the per-cell maxima: every cell gets a bitmap of
+// kUniqueFixedWords words (counts below 65,536); k_mark flags a negative count or one past the
+// bitmap, and such a set is rebuilt with exact widths (phases 1-2).  One host sync per build.
+constexpr long long kUniqueFixedWords = 1024;
+int unique_phase12_fixed(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
+  const int C = s.ncells, N = s.ngenes;
+  hipStream_t st = cx->stream;
+  RCHK(upload(cx, u.cellidx, s.cellidx_host, sizeof(int) * C));
+  u.woff_h.resize(C + 1);
+  for (int c = 0; c <= C; ++c) u.woff_h[c] = (long long)c * kUniqueFixedWords;
+  RCHK(upload(cx, u.woff, u.woff_h.data(), sizeof(long long) * (C + 1)));
+  HCHK(u.bits.ensure(sizeof(unsigned long long) * u.woff_h[C]));
+  HCHK(hipMemsetAsync(u.bits.p, 0, sizeof(unsigned long long) * u.woff_h[C], st));
+  HCHK(u.flags.ensure(sizeof(int)));
+  HCHK(hipMemsetAsync(u.flags.p, 0, sizeof(int), st));
+  HCHK(launch_mark(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.woff.as<long long>(),
+                   u.bits.as<unsigned long long>(), st, u.flags.as<int>()));
+  HCHK(u.rank.ensure(sizeof(int) * u.woff_h[C]));
+  HCHK(u.nuniq.ensure(sizeof(int) * C));
+  HCHK(launch_rank(u.bits.as<unsigned long long>(), u.woff.as<long long>(), C, u.rank.as<int>(),
+                   u.nuniq.as<int>(), st));
+  u.nuniq_h.assign(C, 0);
+  u.fixed_flags = 0;
+  int* h = u.landing(2 * (size_t)C + 1);
+  u.pin_in = h;
+  HCHK(hipMemcpyAsync(h ? h : u.nuniq_h.data(), u.nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+  HCHK(hipMemcpyAsync(h ? h + C : &u.fixed_flags, u.flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  return SCDE_OK;
+}
+
 // ns (1 or 2) cell subsets of the same device counts
 int build_unique_sets(scde_ctx* cx, const PostSpec* const* s, UniqueSet* const* u, int ns) {
   hipEvent_t ev = cx->mark_begin(SLOT_UNIQUE);
-  for (int i = 0; i < ns; ++i) RCHK(unique_phase1(cx, *s[i], *u[i]));
-  HCHK(hipStreamSynchronize(cx->stream));
-  for (int i = 0; i < ns; ++i) RCHK(unique_phase2(cx, *s[i], *u[i]));
-  HCHK(hipStreamSynchronize(cx->stream));
+  if (ns < 1 || ns > 4) return fail(SCDE_EINTERNAL, "unique sets per build: 1..4");
+  bool exact[4] = {true, true, true, true};
+  if (cx->opt_unique_fixed) {
+    for (int i = 0; i < ns; ++i) RCHK(unique_phase12_fixed(cx, *s[i], *u[i]));
+    HCHK(hipStreamSynchronize(cx->stream));
+    for (int i = 0; i < ns; ++i) {
+      const int fl = u[i]->pin_in ? u[i]->pin_in[s[i]->ncells] : u[i]->fixed_flags;
+      exact[i] = fl != 0;  // a count outside [0, 65536): the exact build (and its error message)
+    }
+  }
+  bool any_exact = false;
+  for (int i = 0; i < ns; ++i) any_exact = any_exact || exact[i];
+  if (any_exact) {
+    for (int i = 0; i < ns; ++i)
+      if (exact[i]) RCHK(unique_phase1(cx, *s[i], *u[i]));
+    HCHK(hipStreamSynchronize(cx->stream));
+    for (int i = 0; i < ns; ++i)
+      if (exact[i]) RCHK(unique_phase2(cx, *s[i], *u[i]));
+    HCHK(hipStreamSynchronize(cx->stream));
+  }
   for (int i = 0; i < ns; ++i) RCHK(unique_phase3(cx, *s[i], *u[i]));
   cx->mark_end(SLOT_UNIQUE, ev);
   return SCDE_OK;
@@ -1173,6 +1221,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "tile_max_mult") ctx->opt_tile_max_mult = (int)value;
   else if (n == "tile_order") ctx->opt_tile_order = value != 0;
   else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
+  else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
 }

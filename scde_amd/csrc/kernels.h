@@ -260,7 +260,8 @@ hipError_t launch_post(const int* uci, long long ld_uci, int ngenes, int c, cons
 hipError_t launch_cell_minmax(const int* counts, long long ld, long long g0, int ngenes, int ncells,
                               const int* cellidx, int* cmax, int* cmin, hipStream_t s);
 hipError_t launch_mark(const int* counts, long long ld, long long g0, int ngenes, int ncells, const int* cellidx,
-                       const long long* woff, unsigned long long* bits, hipStream_t s);
+                       const long long* woff, unsigned long long* bits, hipStream_t s,
+                       int* flags = nullptr);
 hipError_t launch_rank(const unsigned long long* bits, const long long* woff, int ncells, int* rank, int* nuniq,
                        hipStream_t s);
 hipError_t launch_fill_ucl(const unsigned long long* bits, const long long* woff, int ncells, const int* rank,

@@ -2635,19 +2635,26 @@ template <int KM, int MW>
 __global__ __launch_bounds__(256) void k_mark(const int* __restrict__ counts, long long ld, long long g0,
                                               int ngenes, const int* __restrict__ cellidx,
                                               const long long* __restrict__ woff,
-                                              unsigned long long* __restrict__ bits) {
+                                              unsigned long long* __restrict__ bits, int* __restrict__ flags) {
   __shared__ unsigned long long lw[MW];
   const int c = blockIdx.y;
   if (threadIdx.x < MW) lw[threadIdx.x] = 0ull;
   __syncthreads();
   const int* __restrict__ col = counts + (long long)cellidx[c] * ld + g0;
   unsigned long long* __restrict__ cb = bits + woff[c];
+  // flags (fixed-width bitmaps, cmax unknown): bit 0 a negative count, bit 1 a count past the
+  // cell's bitmap (the caller rebuilds with exact widths); such counts are not marked
+  const long long width = flags ? woff[c + 1] - woff[c] : 0;
   const int base = blockIdx.x * (256 * KM) + threadIdx.x;
 #pragma unroll
   for (int j = 0; j < KM; ++j) {
     const int g = base + j * 256;
-    const bool valid = g < ngenes;
+    bool valid = g < ngenes;
     const int x = valid ? col[g] : 0;
+    if (flags && valid && (x < 0 || (x >> 6) >= width)) {
+      atomicOr(flags, x < 0 ? 1 : 2);
+      valid = false;
+    }
     // count 0 (the common case) by ballot: one LDS atomic per wave instead of up to 64
     if (__ballot(valid && x == 0) && (threadIdx.x & 63) == 0) atomicOr(&lw[0], 1ull);
     if (valid && x != 0) {
@@ -3554,11 +3561,11 @@ hipError_t launch_cell_minmax(const int* counts, long long ld, long long g0, int
 }
 
 hipError_t launch_mark(const int* counts, long long ld, long long g0, int ngenes, int ncells, const int* cellidx,
-                       const long long* woff, unsigned long long* bits, hipStream_t s) {
+                       const long long* woff, unsigned long long* bits, hipStream_t s, int* flags) {
   const long long n = (long long)ngenes * ncells;
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL((k_mark<8, 16>), dim3(div_up(ngenes, 256 * 8), ncells), dim3(256), 0, s, counts, ld, g0,
-                     ngenes, cellidx, woff, bits);
+                     ngenes, cellidx, woff, bits, flags);
   return hipGetLastError();
 }
 
