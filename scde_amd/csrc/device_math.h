@@ -601,7 +601,7 @@ __device__ inline dd dd_add_d(dd a, double b) {
 }
 __device__ inline double dd_to_d(dd a) { return __dadd_rn(a.hi, a.lo); }
 
-// int8 matrix-core helpers (k_bootq rows and bounds, k_boot_tiles bounds)
+// int8 matrix-core helpers (k_boot_tiles bounds)
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ i32x4 mfma_i8(i32x4 a, i32x4 b, i32x4 c) {

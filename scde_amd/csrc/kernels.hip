@@ -999,7 +999,7 @@ __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ 
       n[i] += __popcll(m);
     }
   }
-  // padto 64: k_bootq reads whole 64-entry steps; k_boot_tiles' FP64 loop also looks one
+  // padto 64: k_boot_tiles' bounds read whole 64-entry steps; its FP64 loop also looks one
   // 4-entry batch past its last batch, hence the extra 8
 #pragma unroll
   for (int i = 0; i < GPW; ++i) {
