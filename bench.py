@@ -164,7 +164,7 @@ def add_profile_fields(roof: dict, prof, stage_s=None):
     roof["rocprof_stage_ms"] = prof["avg_ms"]
     t = stage_s if stage_s else prof["avg_ms"] / 1e3
     roof["counter_bytes_frac"] = prof["traffic_bytes"] / t / 1e9 / HBM_PEAK_GBS
-    roof["time_base"] = ("HIP events around the stage in this run" if stage_s else
+    roof["time_base"] = ("HIP events around the stage in this run (its lanes = 1 pass)" if stage_s else
                          "rocprofv3 kernel durations of the committed profile")
     if prof.get("wait_frac") is not None:
         roof["wait_frac"] = prof["wait_frac"]
@@ -612,11 +612,23 @@ def main():
 
     # the metric: host-resident counts -> host-resident result table
     dt = timed()
-    # device-resident rate and per-kernel HIP-event times (counts already in HBM)
+    # device-resident rate (counts already in HBM), product settings
     dc = api.DeviceCounts(ctx, counts)
-    dt_dev = timed(dc.ptr, profile=not args.no_profile)
+    dt_dev = timed(dc.ptr)
+    # per-stage HIP-event times from a separate pass with the two groups' posteriors one after
+    # the other (option lanes = 1): concurrent lanes share the CUs, and a stage's time would then
+    # include the other group's kernels.  tools/profile.sh's rocprof runs pass --opt lanes=1 too,
+    # so its per-kernel averages describe the same launches.
+    if not args.no_profile:
+        ctx.set_option("lanes", 1)
+        timed(dc.ptr, profile=True)
     kt = ctx.kernel_times()
     ctx.set_profiling(False)
+    for o in args.opt:  # back to the run's settings
+        k, v = o.split("=", 1)
+        ctx.set_option(k, float(v))
+    if not any(o.startswith("lanes=") for o in args.opt):
+        ctx.set_option("lanes", 2)
 
     # arithmetic the bootstrap kernels issue in one step (one extra untimed step with the
     # context's counters on): FP64 lane FMAs of k_boot_tiles / k_boot2.  Not in --no-profile

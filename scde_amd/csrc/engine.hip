@@ -216,6 +216,14 @@ struct scde_ctx {
   int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
   int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
                                  // tiles each; the posterior narrows with the cells, most slabs need two)
+  double opt_pipeline_mb = 48;  // "pipeline_mb": host-count DE calls from this many MB of counts upload in two
+                                // column ranges, each group starting once its cells are in HBM
+  int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
+                                 // group on `peer`, its own streams and workspace) or one after the other (1)
+  // the second lane of a DE call: a context on the same device, created on first use; its
+  // options are copied from this one per call and its timings/statistics merged back
+  scde_ctx* peer = nullptr;
+  hipEvent_t lane_ev[2] = {nullptr, nullptr};  // [0] this stream -> peer, [1] peer -> this stream
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // host wall time of scde_expression_difference_{dev,host} phases (ms, summed over calls):
@@ -302,6 +310,15 @@ struct scde_ctx {
   }
   int sync() {
     HCHK(hipStreamSynchronize(stream));
+    if (peer) {  // the peer lane's timings count as this context's
+      RCHK(peer->sync());
+      for (int i = 0; i < NSLOTS; ++i) {
+        ms[i] += peer->ms[i];
+        launches[i] += peer->launches[i];
+        peer->ms[i] = 0;
+        peer->launches[i] = 0;
+      }
+    }
     for (auto& p : pending) {
       float t = 0.f;
       if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) {
@@ -315,6 +332,12 @@ struct scde_ctx {
     return SCDE_OK;
   }
   ~scde_ctx() {
+    if (peer) {
+      (void)hipStreamSynchronize(peer->stream);
+      delete peer;
+    }
+    for (auto& e : lane_ev)
+      if (e) (void)hipEventDestroy(e);
     Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &pq, &colc, &T,      &E,      &maxi,
                   &has_clamp, &base_col, &zcol, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
                   &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw, &ubound, &zubound, &smask, &subuf, &sredo};
@@ -1222,6 +1245,8 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "tile_order") ctx->opt_tile_order = value != 0;
   else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
+  else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
+  else if (n == "lanes") ctx->opt_lanes = value >= 2 ? 2 : 1;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
 }
@@ -1677,9 +1702,59 @@ static int upload_range(scde_ctx* ctx, const HostUpload& h, int k) {
   return SCDE_OK;
 }
 
-// up (nullable): the host-count entry's upload.  With it the groups run one after the other,
+// The second lane of a DE call (opt_lanes = 2): the peer context runs the second group's
+// posterior on its own streams and workspace, concurrently with the first group's on this
+// context's stream.  Both groups' launches then share the CUs: the second group's small set-up
+// kernels and its tables fill the first group's tails instead of waiting behind them.
+static int lane_peer(scde_ctx* cx, scde_ctx** out) {
+  if (!cx->peer) {
+    scde_ctx* p = nullptr;
+    RCHK(scde_ctx_create(cx->device, &p));
+    cx->peer = p;
+    for (auto& e : cx->lane_ev)
+      if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  scde_ctx* p = cx->peer;
+  p->opt_boot_skip = cx->opt_boot_skip;
+  p->opt_skip_slack = cx->opt_skip_slack;
+  p->opt_boot_nb = cx->opt_boot_nb;
+  p->opt_skip_stats = cx->opt_skip_stats;
+  p->opt_ratio_window = cx->opt_ratio_window;
+  p->opt_ratio_block = cx->opt_ratio_block;
+  p->opt_wpca_ms = cx->opt_wpca_ms;
+  p->opt_boot_tiles = cx->opt_boot_tiles;
+  p->opt_boot_tiles_cells = cx->opt_boot_tiles_cells;
+  p->opt_tile_groups = cx->opt_tile_groups;
+  p->opt_tile_max_mult = cx->opt_tile_max_mult;
+  p->opt_tile_order = cx->opt_tile_order;
+  p->opt_unique_fixed = cx->opt_unique_fixed;
+  p->opt_pair_cells = cx->opt_pair_cells;
+  p->profile = cx->profile;
+  *out = p;
+  return SCDE_OK;
+}
+
+// the peer's statistics added into the context's (and cleared on the peer)
+static void merge_peer_stats(scde_ctx* cx) {
+  scde_ctx* p = cx->peer;
+  if (!p) return;
+  cx->st_skip_slabs += p->st_skip_slabs;
+  cx->st_skip_kept += p->st_skip_kept;
+  cx->st_skip_stretches += p->st_skip_stretches;
+  cx->st_skip_redo += p->st_skip_redo;
+  cx->st_degen += p->st_degen;
+  cx->st_pair_redo += p->st_pair_redo;
+  cx->st_boot_f64_fma += p->st_boot_f64_fma;
+  for (int i = 0; i <= scde_ctx::kQMaxTilesHost; ++i) cx->st_tile_hist[i] += p->st_tile_hist[i];
+  if (p->st_boot_path >= 0) cx->st_boot_path = p->st_boot_path;
+  (void)scde_ctx_reset_stats(p);
+  p->st_boot_path = -1;
+}
+
+// up (nullable): the host-count entry's upload.  With it the groups start one after the other,
 // each once its columns are in HBM; without, both unique tables are built first (their host
-// syncs back to back), then the two posteriors.
+// syncs back to back), then the two posteriors.  With two lanes the second group's posterior
+// runs on the peer context, beside the first's.
 static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const scde_de_params* p,
                   double* results, double* jp1, double* jp2, double* ratio, const HostUpload* up);
 
@@ -1745,6 +1820,8 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     s.jp_k = 1;
   }
   hlap(0);
+  scde_ctx* lane = ctx;  // the context that runs the second group's posterior
+  if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
   if (up) {
     // group by group, each after its columns have arrived (the first range ends with the
     // last cell of the group whose cells end first)
@@ -1761,6 +1838,17 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       if (k == 0) {
         RCHK(build_unique_sets(ctx, sp, up, 1));
         hlap(1);
+      } else if (lane != ctx) {
+        // the second group on the peer lane, behind its own upload: its unique sets' host
+        // sync waits for its small kernels only, and its posterior runs beside the first's
+        HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
+        RCHK(build_unique_sets(lane, sp, up, 1));
+        hlap(1);
+        RCHK(run_posterior(lane, specs[gi], ctx->us[gi]));
+        HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
+        HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+        hlap(2);
+        continue;
       } else {
         // the second group's unique sets on the copy stream, behind its own upload: their two
         // host syncs then wait for its small kernels, not for the first group's posterior
@@ -1786,7 +1874,16 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     UniqueSet* up[2] = {&ctx->us[0], &ctx->us[1]};
     RCHK(build_unique_sets(ctx, sp, up, 2));
     hlap(1);
-    for (int gi = 0; gi < 2; ++gi) RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
+    if (lane != ctx) {
+      HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
+      HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
+    }
+    RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
+    RCHK(run_posterior(lane, specs[1], ctx->us[1]));
+    if (lane != ctx) {
+      HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
+      HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+    }
     hlap(2);
   }
   // ratio posterior + summary
@@ -1843,6 +1940,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     transpose_rows_to_colmajor(tmp.data(), ngenes, G, jp2);
   }
   const int rc = ctx->sync();
+  merge_peer_stats(ctx);
   hlap(3);
   return rc;
 }
@@ -2061,7 +2159,7 @@ int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld
   // Small matrices upload in one piece and keep the batched unique-table build: the
   // per-group build costs two extra host syncs, which a short transfer does not repay
   // (20k x 200 counts: 5.20 vs 5.59 ms per call; 20k x 1,000: 11.19 vs 10.60)
-  constexpr size_t kPipelineBytes = size_t(48) << 20;
+  const size_t kPipelineBytes = (size_t)std::max(0.0, ctx->opt_pipeline_mb) * (size_t(1) << 20);
   if (ngenes == 0 || sizeof(int) * (size_t)ngenes * C < kPipelineBytes) {
     const int* dev = nullptr;
     RCHK(stage_counts(ctx, counts, ld, ngenes, C, &dev));

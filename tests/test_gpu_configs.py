@@ -98,9 +98,9 @@ def test_config5_ms1_kernel_3000_cells():
 def test_config3_host_pipeline_equals_device_resident(api):
     """Full config 3 (20,000 x 1,000: an 80 MB matrix, above the 48 MB pipelining threshold):
     scde_expression_difference_host uploads the counts in two column ranges and builds the
-    second group's unique sets on its copy stream beside the first group's posterior
-    (engine.hip de_run); the table must equal, bit for bit, the device-resident entry on the
-    same counts (one stream, no pipelining)."""
+    second group's unique sets and posterior on the peer lane beside the first group's
+    (engine.hip de_run, lanes = 2); the table must equal, bit for bit, the device-resident entry
+    on the same counts with the groups one after the other (lanes = 1, no pipelining)."""
     import ctypes
     import bench
     from scde_amd._lib import DEParams, check, lib
@@ -127,9 +127,11 @@ def test_config3_host_pipeline_equals_device_resident(api):
     dc = api.DeviceCounts(ctx, mat)
     try:
         dev = np.zeros((N, 6), order="F")
+        ctx.set_option("lanes", 1)
         check(lib().scde_expression_difference_dev(ctx.handle, dc.ptr, N, N, ctypes.byref(params), vp(dev), None,
                                                    None, None))
     finally:
+        ctx.set_option("lanes", 2)
         dc.free()
     assert np.isfinite(host[:, :4]).all()
     np.testing.assert_array_equal(host, dev)

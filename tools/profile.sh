@@ -4,7 +4,7 @@
 # pass 0: kernel trace + stats; passes 1-3: PMC counters (each in its own run, no trace domains).
 set -e
 OUT=${1:-gpurun_out/prof}; shift || true
-ARGS=${@:-"--steps 3 --warmup 1 --cpu-sample 0 --no-profile"}
+ARGS=${@:-"--steps 3 --warmup 1 --cpu-sample 0 --no-profile --opt lanes=1"}
 export TMPDIR=/tmp
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 bench.py $ARGS > $OUT/trace.log 2>&1
