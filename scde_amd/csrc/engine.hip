@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -120,6 +121,26 @@ struct Buf {
     if (e == hipSuccess) cap = want;
     return e;
   }
+  // ensure(bytes), or with keep: grown (25% headroom) keeping the contents -- after a device
+  // synchronisation, as any stream may still write or read the old allocation (rare: the
+  // buffers are grow-only and reused across calls)
+  hipError_t grow(bool keep, size_t bytes) {
+    if (!keep || !p) return ensure(bytes);
+    if (bytes <= cap) return hipSuccess;
+    const size_t want = bytes + bytes / 4;
+    void* q = nullptr;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMalloc(&q, want);
+    if (e == hipSuccess) e = hipMemcpy(q, p, cap, hipMemcpyDeviceToDevice);
+    if (e != hipSuccess) {
+      if (q) (void)hipFree(q);
+      return e;
+    }
+    (void)hipFree(p);
+    p = q;
+    cap = want;
+    return hipSuccess;
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -218,12 +239,15 @@ struct scde_ctx {
                                  // tiles each; the posterior narrows with the cells, most slabs need two)
   double opt_pipeline_mb = 48;  // "pipeline_mb": host-count DE calls from this many MB of counts upload in two
                                 // column ranges, each group starting once its cells are in HBM
+  int opt_pieces = 4;           // "pieces": the first group's columns of a pipelined host-count DE call upload
+                                // in this many pieces, each piece's unique sets and tables starting as it lands
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                  // group on `peer`, its own streams and workspace) or one after the other (1)
   // the second lane of a DE call: a context on the same device, created on first use; its
   // options are copied from this one per call and its timings/statistics merged back
   scde_ctx* peer = nullptr;
   hipEvent_t lane_ev[2] = {nullptr, nullptr};  // [0] this stream -> peer, [1] peer -> this stream
+  hipEvent_t piece_ev[8] = {nullptr};           // run_posterior's pieces: unique sets built
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // host wall time of scde_expression_difference_{dev,host} phases (ms, summed over calls):
@@ -251,6 +275,13 @@ struct scde_ctx {
     std::vector<int4> tasks_h;  // cell-staged tables tasks (k_tables_cell)
     Buf tasks;
     bool ready = false;
+    // a piece of a larger set (run_posterior's pieces): phase 3 writes the unique counts into
+    // into->ucl from column into_col0 on (grown to an estimate of the whole set's columns,
+    // into_cap_hint) and the count indices into into->uci from cell into_c0 on; its own ucl_off
+    // (from 0) serves the piece's tables launch
+    UniqueSet* into = nullptr;
+    long long into_col0 = 0, into_cap_hint = 0;
+    int into_c0 = 0;
     int* landing(size_t n) {
       if (n > pin_land_cap) {
         if (pin_land) (void)hipHostFree(pin_land);
@@ -273,6 +304,8 @@ struct scde_ctx {
       pin_land_cap = 0;
     }
   } us[3];
+  static constexpr int kMaxPieces = 8;
+  UniqueSet upc[kMaxPieces];  // run_posterior's pieces
   // profiling
   bool profile = false;
   struct Pending {
@@ -338,6 +371,8 @@ struct scde_ctx {
     }
     for (auto& e : lane_ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : piece_ev)
+      if (e) (void)hipEventDestroy(e);
     Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &pq, &colc, &T,      &E,      &maxi,
                   &has_clamp, &base_col, &zcol, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
                   &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw, &ubound, &zubound, &smask, &subuf, &sredo};
@@ -349,6 +384,7 @@ struct scde_ctx {
                  &w8t,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
+    for (auto& u : upc) u.release();
     for (void* p : user_allocs) (void)hipFree(p);
     for (auto& p : pending) {
       (void)hipEventDestroy(p.a);
@@ -406,6 +442,15 @@ struct PostSpec {
   double* post = nullptr;   // ncells blocks of ngenes x G col-major
   bool use_baseline = true;
   int rand_kind = 0;
+  // counts arriving in pieces (de_run's host-count pipeline): piece j holds this spec's cells
+  // [piece_c[j], piece_c[j + 1]) and is in HBM once piece_ready(j) returned and piece_stream
+  // reached the point it recorded; run_posterior builds each piece's unique sets on
+  // piece_stream and launches its tables as it arrives (piece_ev: one event per piece)
+  int npieces = 0;
+  const int* piece_c = nullptr;
+  std::function<int(int)> piece_ready;
+  hipStream_t piece_stream = nullptr;
+  hipEvent_t* piece_ev = nullptr;
 };
 
 constexpr size_t kPinCap = size_t(16) << 20;  // the arena
@@ -507,12 +552,23 @@ int unique_phase3(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   u.ucl_off_h.assign(C + 1, 0);
   for (int c = 0; c < C; ++c) u.ucl_off_h[c + 1] = u.ucl_off_h[c] + u.nuniq_h[c];
   RCHK(upload(cx, u.ucl_off, u.ucl_off_h.data(), sizeof(long long) * (C + 1)));
-  HCHK(u.ucl.ensure(sizeof(int) * std::max<long long>(1, u.ucl_off_h[C])));
+  int* ucl = nullptr;
+  int* uci = nullptr;
+  if (u.into) {  // a piece: into the whole set's arrays (uci sized by the caller)
+    const long long need = std::max(u.into_col0 + u.ucl_off_h[C], u.into_cap_hint);
+    HCHK(u.into->ucl.grow(u.into_col0 > 0, sizeof(int) * std::max<long long>(1, need)));
+    ucl = u.into->ucl.as<int>() + u.into_col0;
+    uci = u.into->uci.as<int>() + (size_t)N * u.into_c0;
+  } else {
+    HCHK(u.ucl.ensure(sizeof(int) * std::max<long long>(1, u.ucl_off_h[C])));
+    HCHK(u.uci.ensure(sizeof(int) * std::max<long long>(1, (long long)N * C)));
+    ucl = u.ucl.as<int>();
+    uci = u.uci.as<int>();
+  }
   HCHK(launch_fill_ucl(u.bits.as<unsigned long long>(), u.woff.as<long long>(), C, u.rank.as<int>(),
-                       u.ucl_off.as<long long>(), u.ucl.as<int>(), st));
-  HCHK(u.uci.ensure(sizeof(int) * std::max<long long>(1, (long long)N * C)));
+                       u.ucl_off.as<long long>(), ucl, st));
   HCHK(launch_uci(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.woff.as<long long>(),
-                  u.bits.as<unsigned long long>(), u.rank.as<int>(), u.uci.as<int>(), st));
+                  u.bits.as<unsigned long long>(), u.rank.as<int>(), uci, st));
   u.ready = true;
   return SCDE_OK;
 }
@@ -616,7 +672,10 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
   }
 }
 
-int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
+// rest (nullable): return once the tables are queued, with the remaining work (modes, draws,
+// bootstrap, outputs) in *rest, to be run later on the same stream -- de_run queues both groups'
+// tables before either bootstrap, so the second lane's tables start at once
+int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<int()>* rest = nullptr) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
   // column stride: >= the k_boot2 block (lanes never read past a column); 512 keeps
   // columns 4 KiB-aligned
@@ -650,8 +709,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
                         cx->mu.as<double>(), cx->lcfp.as<double>(), cx->lcfpr.as<double>(), cx->theta.as<double>(),
                         cx->cellscal.as<double>(), s.localtheta ? nullptr : cx->pq.as<double>(), st));
   cx->mark_end(SLOT_OTHER, ev);
-  // ---- unique counts (prebuilt by build_unique_sets when u.ready)
+  // ---- unique counts (prebuilt by build_unique_sets when u.ready; piece by piece with the
+  // tables below when the counts arrive in pieces)
   std::vector<long long>& ucl_off_h = u.ucl_off_h;
+  const bool pieces = s.npieces > 0 && !s.ucl_host;
   if (s.ucl_host) {
     ucl_off_h.assign(s.ucl_off_host, s.ucl_off_host + C + 1);
     if (ucl_off_h[0] != 0) return fail(SCDE_EARG, "ucl_off[0] must be 0");
@@ -667,24 +728,225 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
         if (col[g] < 0 || col[g] >= nu) return fail(SCDE_EARG, "counti[%d,%d]=%d out of range [0,%lld)", g, c, col[g], nu);
     }
     RCHK(upload(cx, u.uci, s.uci_host, sizeof(int) * std::max<long long>(1, (long long)N * C)));
-  } else if (!u.ready) {
+  } else if (!u.ready && !pieces) {
     const PostSpec* sp[1] = {&s};
     UniqueSet* up[1] = {&u};
     RCHK(build_unique_sets(cx, sp, up, 1));
   }
   u.ready = false;  // consumed by this call
-  const long long ncols = ucl_off_h[C];
   // ---- K1 tables
   // Bootstrap path with G <= 1024 (k_boot2): the tables kernel writes the baseline-delta
   // columns D directly (phase 1: count-0 columns and base_col, phase 2: the rest); T itself
   // is kept only when individual posteriors are returned.
   const bool boot_path = s.nboot > 0 && (s.batch_call || !s.ensemble);
-  // k_boot2 forms column and multiplicity-row offsets in 32 bits: past that, the general kernel
-  const bool fast = ((G + 63) / 64) * 64 <= 1024 && (ncols + 1) * (long long)GS < (1LL << 31) &&
-                    (long long)C * round_up(std::max(s.nboot, 1), 32) < (1LL << 31);
-  const bool fused = boot_path && fast;
+  // the launch plan; its column-count conditions are checked again once the count is known
+  // (pieces: the tables launch piece by piece before the last piece has arrived)
+  struct Plan {
+    bool fast, fused, keep_T, tpath, stretch_skip;
+    bool operator==(const Plan& o) const {
+      return fast == o.fast && fused == o.fused && keep_T == o.keep_T && tpath == o.tpath &&
+             stretch_skip == o.stretch_skip;
+    }
+  };
   const bool want_post = s.batch_call ? (s.postflag == 2) : (s.postflag == 2 || s.postflag == 3);
-  const bool keep_T = !fused || (want_post && s.post);
+  // k_boot2 forms column and multiplicity-row offsets in 32 bits: past that, the general kernel
+  auto make_plan = [&](long long nc) {
+    Plan p{};
+    p.fast = ((G + 63) / 64) * 64 <= 1024 && (nc + 1) * (long long)GS < (1LL << 31) &&
+             (long long)C * round_up(std::max(s.nboot, 1), 32) < (1LL << 31);
+    p.fused = boot_path && p.fast;
+    p.keep_T = !p.fused || (want_post && s.post);
+    int nbp = p.fast ? boot2_nb(s.nboot) : 16;
+    if (p.fast) {
+      const int v = cx->opt_boot_nb;  // tuning option: a multiple of 4 in [4, 32]
+      if (v >= 4 && v <= 32 && v % 4 == 0) nbp = v;
+    }
+    // k_boot_tiles: G <= 448, nb <= 20, multiplicities <= 127 (int8), int32 digit sums.  The
+    // tables are set up for it before the draws exist; should a multiplicity exceed 127 (a
+    // cell drawn 128 times in one boot), plain k_boot2 runs on the same D columns instead.
+    p.tpath = p.fused && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
+              C >= cx->opt_boot_tiles_cells && nbp <= 20 && C < 100000 && (nc + 1) * (long long)GS < (1LL << 31);
+    // k_boot2 grid-stretch skipping (G <= 448: at most 7 stretches of 64 points); the
+    // tables kernel emits the per-column stretch maxima
+    p.stretch_skip = p.fused && !p.tpath && G <= 448 && cx->opt_boot_skip;
+    return p;
+  };
+  // pieces: planned for the smallest column count (every condition holds for fewer columns)
+  const Plan plan0 = make_plan(pieces ? 0 : ucl_off_h[C]);
+  const bool want_maxi = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
+  TablesArgs ta{};
+  // buffers for `cap` columns (pieces: grown keeping what earlier pieces wrote) and the
+  // launch arguments over the whole column range
+  auto setup_tables = [&](const Plan& p, long long cap, bool keep) -> int {
+    const size_t ncap = (size_t)std::max<long long>(1, cap);
+    if (p.keep_T) HCHK(cx->T.grow(keep, sizeof(double) * ncap * GS));
+    HCHK(cx->maxi.grow(keep, sizeof(int) * ncap));
+    HCHK(cx->has_clamp.grow(keep, ncap));
+    if (p.tpath) HCHK(cx->ubound.grow(keep, sizeof(unsigned) * kQTiles * (ncap + 1)));
+    if (p.fused) {
+      HCHK(cx->E.grow(keep, sizeof(double) * (ncap + 1) * GS));
+      if (p.stretch_skip) HCHK(cx->ubound.grow(keep, sizeof(double) * 8 * (ncap + 1)));
+    }
+    if (!s.localtheta) HCHK(cx->colc.grow(keep, sizeof(double) * (kColc * ncap + 1)));  // + the slow-column flag
+    ta.ucl = u.ucl.as<int>();
+    ta.ucl_off = u.ucl_off.as<long long>();
+    ta.ncells = C;
+    ta.G = G;
+    ta.GS = GS;
+    ta.mu = cx->mu.as<double>();
+    ta.lcfp = cx->lcfp.as<double>();
+    ta.lcfpr = cx->lcfpr.as<double>();
+    ta.theta = cx->theta.as<double>();
+    ta.cellscal = cx->cellscal.as<double>();
+    ta.minlogprob = -1 * DBL_MAX / C / 1.1;
+    ta.T = p.keep_T ? cx->T.as<double>() : nullptr;
+    ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
+    ta.has_clamp = cx->has_clamp.as<unsigned char>();
+    ta.const_theta = s.localtheta ? 0 : 1;
+    ta.pq = s.localtheta ? nullptr : cx->pq.as<double>();
+    ta.colc = s.localtheta ? nullptr : cx->colc.as<double>();
+    ta.use_baseline = s.use_baseline ? 1 : 0;
+    ta.UQ = p.tpath ? cx->ubound.as<unsigned>() : nullptr;
+    ta.nanflag = p.tpath ? cx->qflags.as<int>() : nullptr;
+    ta.D = p.fused ? cx->E.as<double>() : nullptr;
+    ta.zcol = p.fused ? cx->zcol.as<int>() : nullptr;
+    ta.base_col = p.fused ? cx->base_col.as<int>() : nullptr;
+    ta.U = p.stretch_skip ? cx->ubound.as<double>() : nullptr;
+    return SCDE_OK;
+  };
+  // the tables of cells [c0, c1), whose columns [col0, col0 + nc) are described by the
+  // cell-local offsets off_h (device copy off_d, from 0); last: the pad column's task and p1_ev
+  auto launch_tables_range = [&](const Plan& p, int c0, int c1, long long col0, const long long* off_d,
+                                 const std::vector<long long>& off_h, bool last, UniqueSet& tu) -> int {
+    const int Cc = c1 - c0;
+    const long long nc = off_h[Cc];
+    TablesArgs tc = ta;
+    tc.ucl = ta.ucl + col0;
+    tc.ucl_off = off_d;
+    tc.ncols = nc;
+    tc.ncells = Cc;
+    const size_t co = (size_t)c0 * GS;
+    tc.mu = ta.mu + co;
+    tc.lcfp = ta.lcfp + co;
+    tc.lcfpr = ta.lcfpr + co;
+    tc.theta = ta.theta + co;
+    tc.cellscal = ta.cellscal + 2 * (size_t)c0;
+    if (tc.pq) tc.pq = ta.pq + 4 * co;
+    if (tc.T) tc.T = ta.T + (size_t)col0 * GS;
+    if (tc.maxi) tc.maxi = ta.maxi + col0;
+    tc.has_clamp = ta.has_clamp + col0;
+    if (tc.colc) tc.colc = ta.colc + (size_t)kColc * col0;
+    if (tc.UQ) tc.UQ = ta.UQ + (size_t)kQTiles * col0;
+    if (tc.U) tc.U = ta.U + (size_t)8 * col0;
+    if (tc.D) tc.D = ta.D + (size_t)col0 * GS;
+    if (tc.zcol) tc.zcol = ta.zcol + c0;
+    if (tc.base_col) tc.base_col = ta.base_col + c0;
+    tc.col_base = (int)col0;
+    // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
+    if (G <= 448 && nc > 0) {
+      constexpr long long kTaskCols = kTabTaskCols;
+      tu.tasks_h.clear();
+      for (int c = 0; c < Cc; ++c)
+        for (long long b = off_h[c]; b < off_h[c + 1]; b += kTaskCols)
+          tu.tasks_h.push_back(make_int4(c, (int)b, (int)std::min(b + kTaskCols, off_h[c + 1]), 0));
+      if (p.fused && last) tu.tasks_h.push_back(make_int4(-1, 0, 0, 0));  // the ELL pad column
+      RCHK(upload(cx, tu.tasks, tu.tasks_h.data(), sizeof(int4) * tu.tasks_h.size()));
+      tc.tasks = tu.tasks.as<int4>();
+      tc.ntasks = (int)tu.tasks_h.size();
+    }
+    hipEvent_t evt = cx->mark_begin(SLOT_TABLES);
+    if (!s.localtheta && nc > 0)
+      HCHK(launch_col_consts(tc.ucl, off_d, nc, Cc, tc.theta, GS, tc.cellscal,
+                             cx->colc.as<double>() + (size_t)kColc * col0, st));
+    if (p.fused) {
+      tc.phase = 1;
+      HCHK(launch_tables(tc, st));
+      if (last) {
+        if (!cx->p1_ev) HCHK(hipEventCreateWithFlags(&cx->p1_ev, hipEventDisableTiming));
+        HCHK(hipEventRecord(cx->p1_ev, st));
+      }
+      tc.phase = 2;
+      HCHK(launch_tables(tc, st));
+    } else {
+      HCHK(launch_tables(tc, st));
+    }
+    cx->mark_end(SLOT_TABLES, evt);
+    return SCDE_OK;
+  };
+  if (plan0.tpath) {
+    HCHK(cx->qflags.ensure(sizeof(int) * 40));
+    HCHK(hipMemsetAsync(cx->qflags.p, 0, sizeof(int) * 40, st));
+  }
+  if (plan0.fused) {
+    HCHK(cx->base_col.ensure(sizeof(int) * std::max(1, C)));
+    HCHK(cx->zcol.ensure(sizeof(int) * std::max(1, C)));
+  }
+  bool tables_done = false;
+  if (pieces) {
+    // piece j: cells [piece_c[j], piece_c[j+1]) of this spec; its unique sets are built (on
+    // the copy stream, beside the previous piece's tables) into u's arrays at the running
+    // column offset, then its tables launch
+    HCHK(u.uci.ensure(sizeof(int) * std::max<long long>(1, (long long)N * C)));
+    ucl_off_h.assign(C + 1, 0);
+    long long col0 = 0;
+    int jlast = 0;
+    for (int j = 0; j < s.npieces; ++j)
+      if (s.piece_c[j + 1] > s.piece_c[j]) jlast = j;
+    for (int j = 0; j < s.npieces; ++j) {
+      const int c0 = s.piece_c[j], c1 = s.piece_c[j + 1];
+      RCHK(s.piece_ready(j));
+      if (c1 == c0) continue;
+      UniqueSet& pu = cx->upc[j];
+      PostSpec ps;
+      ps.ncells = c1 - c0;
+      ps.counts_dev = s.counts_dev;
+      ps.ld = s.ld;
+      ps.cellidx_host = s.cellidx_host + c0;
+      ps.ngenes = N;
+      pu.into = &u;
+      pu.into_col0 = col0;
+      pu.into_c0 = c0;
+      pu.into_cap_hint = j == 0 ? 0 : (long long)((double)col0 / c0 * C * 1.1);
+      const PostSpec* sp[1] = {&ps};
+      UniqueSet* up[1] = {&pu};
+      const hipStream_t main = cx->stream;
+      cx->stream = s.piece_stream;
+      const int rc = build_unique_sets(cx, sp, up, 1);
+      cx->stream = main;
+      pu.into = nullptr;
+      RCHK(rc);
+      HCHK(hipEventRecord(s.piece_ev[j], s.piece_stream));
+      HCHK(hipStreamWaitEvent(st, s.piece_ev[j], 0));
+      for (int c = c0; c < c1; ++c) ucl_off_h[c + 1] = col0 + pu.ucl_off_h[c - c0 + 1];
+      const long long nc = pu.ucl_off_h[c1 - c0];
+      // capacity for this piece plus an estimate of the rest (grown keeping the columns so far)
+      const long long est = std::max<long long>(col0 + nc, (long long)((double)(col0 + nc) / c1 * C * 1.1));
+      RCHK(setup_tables(plan0, est, j > 0));
+      RCHK(launch_tables_range(plan0, c0, c1, col0, pu.ucl_off.as<long long>(), pu.ucl_off_h, j == jlast, pu));
+      col0 += nc;
+    }
+    RCHK(upload(cx, u.ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
+    ta.ucl_off = u.ucl_off.as<long long>();
+    tables_done = make_plan(col0) == plan0;  // else: the whole tables again, planned for col0 columns
+  }
+  const long long ncols = ucl_off_h[C];
+  const Plan plan = make_plan(ncols);
+  const bool fast = plan.fast, fused = plan.fused, keep_T = plan.keep_T, stretch_skip = plan.stretch_skip;
+  bool tpath = plan.tpath;
+  ta.ncols = ncols;
+  if (!tables_done) {
+    if (plan.tpath && !plan0.tpath) {
+      HCHK(cx->qflags.ensure(sizeof(int) * 40));
+      HCHK(hipMemsetAsync(cx->qflags.p, 0, sizeof(int) * 40, st));
+    }
+    if (plan.fused) {
+      HCHK(cx->base_col.ensure(sizeof(int) * std::max(1, C)));
+      HCHK(cx->zcol.ensure(sizeof(int) * std::max(1, C)));
+    }
+    RCHK(setup_tables(plan, ncols, false));
+    ta.ncols = ncols;
+    RCHK(launch_tables_range(plan, 0, C, 0, u.ucl_off.as<long long>(), ucl_off_h, true, u));
+  }
   std::vector<int> draws;
   std::vector<double> W;
   int ndraw = 0, maxw = 0;
@@ -699,87 +961,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
   }
   const int Bp = (int)round_up(std::max(s.nboot, 1), nb);
-  // k_boot_tiles: G <= 448, nb <= 20, multiplicities <= 127 (int8), int32 digit sums.  The
-  // tables are set up for it before the draws exist; should a multiplicity exceed 127 (a
-  // cell drawn 128 times in one boot), plain k_boot2 runs on the same D columns instead.
-  bool tpath = fused && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
-               C >= cx->opt_boot_tiles_cells && nb <= 20 && C < 100000 && (ncols + 1) * (long long)GS < (1LL << 31);
   const int Bt = (int)round_up(Bp, 32) + 32;  // byte multiplicity rows: the last slab reads 32 boots
-  if (keep_T) HCHK(cx->T.ensure(sizeof(double) * std::max<long long>(1, ncols) * GS));
-  HCHK(cx->maxi.ensure(sizeof(int) * std::max<long long>(1, ncols)));
-  HCHK(cx->has_clamp.ensure(std::max<long long>(1, ncols)));
-  const bool want_maxi = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
-  TablesArgs ta{};
-  ta.ucl = u.ucl.as<int>();
-  ta.ucl_off = u.ucl_off.as<long long>();
-  ta.ncols = ncols;
-  ta.ncells = C;
-  ta.G = G;
-  ta.GS = GS;
-  ta.mu = cx->mu.as<double>();
-  ta.lcfp = cx->lcfp.as<double>();
-  ta.lcfpr = cx->lcfpr.as<double>();
-  ta.theta = cx->theta.as<double>();
-  ta.cellscal = cx->cellscal.as<double>();
-  ta.minlogprob = -1 * DBL_MAX / C / 1.1;
-  ta.T = keep_T ? cx->T.as<double>() : nullptr;
-  ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
-  ta.has_clamp = cx->has_clamp.as<unsigned char>();
-  ta.const_theta = s.localtheta ? 0 : 1;
-  ta.pq = s.localtheta ? nullptr : cx->pq.as<double>();
-  ta.use_baseline = s.use_baseline ? 1 : 0;
-  // k_boot2 grid-stretch skipping (G <= 448: at most 7 stretches of 64 points); the
-  // tables kernel emits the per-column stretch maxima.  SCDE_BOOT_SKIP=0 disables it.
-  const bool stretch_skip = fused && !tpath && G <= 448 && cx->opt_boot_skip;
-  if (tpath) {
-    HCHK(cx->qflags.ensure(sizeof(int) * 40));
-    HCHK(hipMemsetAsync(cx->qflags.p, 0, sizeof(int) * 40, st));
-    HCHK(cx->ubound.ensure(sizeof(unsigned) * kQTiles * (size_t)(ncols + 1)));
-    ta.UQ = cx->ubound.as<unsigned>();
-    ta.nanflag = cx->qflags.as<int>();
-  }
-  if (fused) {
-    HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
-    HCHK(cx->base_col.ensure(sizeof(int) * std::max(1, C)));
-    HCHK(cx->zcol.ensure(sizeof(int) * std::max(1, C)));
-    ta.D = cx->E.as<double>();
-    ta.zcol = cx->zcol.as<int>();
-    ta.base_col = cx->base_col.as<int>();
-    if (stretch_skip) {
-      HCHK(cx->ubound.ensure(sizeof(double) * 8 * (size_t)(ncols + 1)));
-      ta.U = cx->ubound.as<double>();
-    }
-  }
-  // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
-  if (G <= 448 && ncols > 0) {
-    constexpr long long kTaskCols = kTabTaskCols;
-    u.tasks_h.clear();
-    for (int c = 0; c < C; ++c)
-      for (long long b = ucl_off_h[c]; b < ucl_off_h[c + 1]; b += kTaskCols)
-        u.tasks_h.push_back(make_int4(c, (int)b, (int)std::min(b + kTaskCols, ucl_off_h[c + 1]), 0));
-    if (fused) u.tasks_h.push_back(make_int4(-1, 0, 0, 0));  // the ELL pad column
-    RCHK(upload(cx, u.tasks, u.tasks_h.data(), sizeof(int4) * u.tasks_h.size()));
-    ta.tasks = u.tasks.as<int4>();
-    ta.ntasks = (int)u.tasks_h.size();
-  }
-  ev = cx->mark_begin(SLOT_TABLES);
-  if (!s.localtheta && ncols > 0) {
-    HCHK(cx->colc.ensure(sizeof(double) * (kColc * (size_t)ncols + 1)));  // + the slow-column flag
-    HCHK(launch_col_consts(u.ucl.as<int>(), u.ucl_off.as<long long>(), ncols, C, cx->theta.as<double>(), GS,
-                           cx->cellscal.as<double>(), cx->colc.as<double>(), st));
-    ta.colc = cx->colc.as<double>();
-  }
-  if (fused) {
-    ta.phase = 1;
-    HCHK(launch_tables(ta, st));
-    if (!cx->p1_ev) HCHK(hipEventCreateWithFlags(&cx->p1_ev, hipEventDisableTiming));
-    HCHK(hipEventRecord(cx->p1_ev, st));
-    ta.phase = 2;
-    HCHK(launch_tables(ta, st));
-  } else {
-    HCHK(launch_tables(ta, st));
-  }
-  cx->mark_end(SLOT_TABLES, ev);
+  auto rest_fn = [=, &s, &u]() mutable -> int {
   // ---- individual posterior modes (src/jpmatLogBoot.cpp:277-296): argmax of each cell's table
   // column, known as soon as the tables are; computed here so the caller's read-back of the
   // (ngenes x ncells) matrix overlaps the bootstrap
@@ -1053,6 +1236,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
       HCHK(launch_post(u.uci.as<int>(), N, N, c, u.ucl_off.as<long long>(), cx->T.as<double>(), G, GS,
                        s.post + (size_t)c * N * G, 1, N, st));
   return SCDE_OK;
+  };
+  if (rest) {
+    *rest = rest_fn;
+    return SCDE_OK;
+  }
+  return rest_fn();
 }
 
 std::mutex g_default_mu;
@@ -1246,6 +1435,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
+  else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
   else if (n == "lanes") ctx->opt_lanes = value >= 2 ? 2 : 1;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
@@ -1614,12 +1804,55 @@ int scde_ratio_summary(const double* pmat1, const double* pmat2, int nrows, int 
 }
 
 // ------------------------------------------------------------------ layer 2
+// Host counts for de_run: copied in two column ranges on the context's copy stream.  A
+// pageable copy returns only once its data has left the host buffer, so the second range is
+// issued after the first group's kernels are queued: its transfer then overlaps them.
+struct HostUpload {
+  const int* counts;
+  int64_t ld;
+  int ngenes, cut, C;
+};
+// columns [lo, hi) of the host counts into counts_in, on the copy stream
+static int upload_cols(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
+  const size_t row = sizeof(int) * (size_t)h.ngenes;
+  if (hi > lo) {
+    char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
+    const int* src = h.counts + (size_t)h.ld * lo;
+    if (h.ld == h.ngenes)
+      HCHK(hipMemcpyAsync(dst, src, row * (hi - lo), hipMemcpyHostToDevice, ctx->copy_stream));
+    else
+      HCHK(hipMemcpy2DAsync(dst, row, src, sizeof(int) * (size_t)h.ld, row, hi - lo, hipMemcpyHostToDevice,
+                            ctx->copy_stream));
+  }
+  return SCDE_OK;
+}
+
+// up (nullable): the host-count entry's upload, in pieces of the selected cells (cellidx
+// strictly increasing), each piece's unique sets and tables starting as it lands
+static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const int* cellidx,
+                          int ncells_sel, const double* models_sel, int local_theta, int square_logit_conc,
+                          const double* prior_x, int ngrid, int nboot, int n_cores, int64_t gene_offset,
+                          int64_t ngenes_total, int return_post, int ensemble, const int* batch_vals,
+                          const int64_t* batch_off, const int* composition, int nbatch, double* jp, double* modes,
+                          double* post, const HostUpload* up);
+
 int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const int* cellidx,
                         int ncells_sel, const double* models_sel, int local_theta, int square_logit_conc,
                         const double* prior_x, int ngrid, int nboot, int n_cores, int64_t gene_offset,
                         int64_t ngenes_total, int return_post, int ensemble, const int* batch_vals,
                         const int64_t* batch_off, const int* composition, int nbatch, double* jp, double* modes,
                         double* post) {
+  return posteriors_run(ctx, counts_dev, ld, ngenes, cellidx, ncells_sel, models_sel, local_theta, square_logit_conc,
+                        prior_x, ngrid, nboot, n_cores, gene_offset, ngenes_total, return_post, ensemble, batch_vals,
+                        batch_off, composition, nbatch, jp, modes, post, nullptr);
+}
+
+static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, const int* cellidx,
+                          int ncells_sel, const double* models_sel, int local_theta, int square_logit_conc,
+                          const double* prior_x, int ngrid, int nboot, int n_cores, int64_t gene_offset,
+                          int64_t ngenes_total, int return_post, int ensemble, const int* batch_vals,
+                          const int64_t* batch_off, const int* composition, int nbatch, double* jp, double* modes,
+                          double* post, const HostUpload* up) {
   if (!ctx || !counts_dev || !cellidx || !models_sel || !prior_x || !jp) return fail(SCDE_EARG, "null argument");
   if (ngenes < 0 || ncells_sel <= 0 || ngrid <= 0) return fail(SCDE_EARG, "bad dimensions");
   HCHK(hipSetDevice(ctx->device));
@@ -1668,6 +1901,21 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
     s.post = ctx->outbuf.as<double>();
   }
   ctx->us[0].ready = false;
+  std::vector<int> piece_c, piece_col;
+  if (up) {
+    const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
+    for (int j = 0; j <= K; ++j) piece_c.push_back((int)((long long)ncells_sel * j / K));
+    piece_col.push_back(0);  // piece j uploads columns [piece_col[j], piece_col[j + 1])
+    for (int j = 0; j < K; ++j)
+      piece_col.push_back(piece_c[j + 1] > piece_c[j] ? cellidx[piece_c[j + 1] - 1] + 1 : piece_col.back());
+    for (int j = 0; j < K; ++j)
+      if (!ctx->piece_ev[j]) HCHK(hipEventCreateWithFlags(&ctx->piece_ev[j], hipEventDisableTiming));
+    s.npieces = K;
+    s.piece_c = piece_c.data();
+    s.piece_stream = ctx->copy_stream;
+    s.piece_ev = ctx->piece_ev;
+    s.piece_ready = [&](int j) { return upload_cols(ctx, *up, piece_col[j], piece_col[j + 1]); };
+  }
   RCHK(run_posterior(ctx, s, ctx->us[0]));
   if (s.modes_early) RCHK(copy_modes_out(ctx, modes, s.modes, (size_t)ngenes * ncells_sel));
   if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, ctx->stream));
@@ -1677,14 +1925,6 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
   return ctx->sync();
 }
 
-// Host counts for de_run: copied in two column ranges on the context's copy stream.  A
-// pageable copy returns only once its data has left the host buffer, so the second range is
-// issued after the first group's kernels are queued: its transfer then overlaps them.
-struct HostUpload {
-  const int* counts;
-  int64_t ld;
-  int ngenes, cut, C;
-};
 static int upload_range(scde_ctx* ctx, const HostUpload& h, int k) {
   const size_t row = sizeof(int) * (size_t)h.ngenes;
   const int lo = k == 0 ? 0 : h.cut, hi = k == 0 ? h.cut : h.C;
@@ -1829,10 +2069,37 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     for (int c : idx[0]) max0 = std::max(max0, c);
     for (int c : idx[1]) max1 = std::max(max1, c);
     const int first = max0 <= max1 ? 0 : 1;
+    // the first group's range in pieces: each piece's unique sets and tables start as it lands
+    const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
+    std::vector<int> piece_c;
+    if (K > 1) {
+      const std::vector<int>& ix = idx[first];
+      for (int j = 0; j <= K; ++j) {
+        const int a = (int)((long long)up->cut * j / K);
+        piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
+      }
+      for (int j = 0; j < K; ++j)
+        if (!ctx->piece_ev[j]) HCHK(hipEventCreateWithFlags(&ctx->piece_ev[j], hipEventDisableTiming));
+    }
     for (int k = 0; k < 2; ++k) {
       const int gi = k == 0 ? first : 1 - first;
-      RCHK(upload_range(ctx, *up, k));
       ctx->us[gi].ready = false;
+      if (k == 0 && K > 1) {
+        PostSpec& sf = specs[gi];
+        sf.npieces = K;
+        sf.piece_c = piece_c.data();
+        sf.piece_stream = ctx->copy_stream;
+        sf.piece_ev = ctx->piece_ev;
+        sf.piece_ready = [&, K](int j) {
+          const int lo = (int)((long long)up->cut * j / K), hi = (int)((long long)up->cut * (j + 1) / K);
+          return upload_cols(ctx, *up, lo, hi);
+        };
+        hlap(1);
+        RCHK(run_posterior(ctx, sf, ctx->us[gi]));
+        hlap(2);
+        continue;
+      }
+      RCHK(upload_range(ctx, *up, k));
       const PostSpec* sp[1] = {&specs[gi]};
       UniqueSet* up[1] = {&ctx->us[gi]};
       if (k == 0) {
@@ -1878,8 +2145,17 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
       HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
     }
-    RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
-    RCHK(run_posterior(lane, specs[1], ctx->us[1]));
+    if (lane != ctx) {
+      // both groups' tables first, then both bootstraps
+      std::function<int()> rest0, rest1;
+      RCHK(run_posterior(ctx, specs[0], ctx->us[0], &rest0));
+      RCHK(run_posterior(lane, specs[1], ctx->us[1], &rest1));
+      RCHK(rest0());
+      RCHK(rest1());
+    } else {
+      RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
+      RCHK(run_posterior(ctx, specs[1], ctx->us[1]));
+    }
     if (lane != ctx) {
       HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
       HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
@@ -2205,6 +2481,26 @@ int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngene
   if (!cellidx) return fail(SCDE_EARG, "null argument");
   for (int i = 0; i < ncells_sel; ++i)
     if (cellidx[i] < 0 || cellidx[i] >= ncells_total) return fail(SCDE_EARG, "cell index %d out of range", cellidx[i]);
+  if (!ctx) RCHK(default_ctx(&ctx));
+  bool increasing = ncells_sel > 0;
+  for (int i = 1; i < ncells_sel && increasing; ++i) increasing = cellidx[i] > cellidx[i - 1];
+  if (ngenes > 0 && counts && ld >= ngenes && increasing && ctx->opt_pieces > 1 &&
+      sizeof(int) * (size_t)ngenes * ncells_total >= (size_t)std::max(0.0, ctx->opt_pipeline_mb) * (size_t(1) << 20)) {
+    // the selected cells' columns in pieces on the copy stream, each piece's unique sets and
+    // tables starting as it lands
+    HCHK(hipSetDevice(ctx->device));
+    if (!ctx->copy_stream) HCHK(hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    for (auto& e : ctx->up_ev)
+      if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HCHK(ctx->counts_in.ensure(sizeof(int) * (size_t)ngenes * ncells_total));
+    // the previous call's kernels may still read counts_in: the copies wait for them
+    HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
+    HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
+    const HostUpload h{counts, ld, ngenes, 0, ncells_total};
+    return posteriors_run(ctx, ctx->counts_in.as<int>(), ngenes, ngenes, cellidx, ncells_sel, models_sel, local_theta,
+                          square_logit_conc, prior_x, ngrid, nboot, n_cores, gene_offset, ngenes_total, return_post,
+                          ensemble, batch_vals, batch_off, composition, nbatch, jp, modes, post, &h);
+  }
   const int* dev = nullptr;
   RCHK(stage_counts(ctx, counts, ld, ngenes, ncells_total, &dev));
   return scde_posteriors_dev(ctx, dev, ngenes, ngenes, cellidx, ncells_sel, models_sel, local_theta,

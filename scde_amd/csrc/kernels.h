@@ -75,6 +75,10 @@ struct TablesArgs {
   double* D;      // [ncols + 1][GS]
   int* zcol;      // [ncells] count-0 column or -1
   int* base_col;  // [ncells]
+  // chunked launches (the host-count pipeline): every column array above (ucl, T, maxi,
+  // has_clamp, D, U, UQ, colc) and the per-cell arrays start at the chunk's first column / cell;
+  // zcol and base_col hold global column indices, col_base = the chunk's first global column
+  int col_base;
   // Cell-staged tables (phases 0 and 2, G <= 448): per block {cell, first column, end
   // column, 0}; one task with cell -1 writes the ELL pad column (phase 2).  Null: the
   // column-per-wave kernel.

@@ -198,6 +198,18 @@ __device__ __forceinline__ float gt_maxf(float a, float b) { return (b > a) ? b 
 // One (cell, unique count) column, one wavefront, lanes over grid points.  The per-cell
 // grid vectors (mu, pq, lcfpr, lcfp, theta) and the baseline column come in as pointers:
 // global memory (k_tables) or an LDS copy staged once per cell (k_tables_cell).
+
+// base_col / zcol hold global column indices; a chunked tables launch (TablesArgs::col_base)
+// sees its columns from col_base on as 0, 1, ...
+__device__ __forceinline__ int tab_base_col(const TablesArgs& a, int c) {
+  const int b = a.base_col[c];
+  return b >= 0 ? b - a.col_base : -1;
+}
+__device__ __forceinline__ int tab_zcol(const TablesArgs& a, int c) {
+  const int z = a.zcol[c];
+  return z >= 0 ? z - a.col_base : -1;
+}
+
 template <bool CT>
 __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col, int c, int phase,
                                               const double* __restrict__ mu, const double* __restrict__ P,
@@ -313,7 +325,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   double* out = a.T ? a.T + col * a.GS : nullptr;
   // fused delta (phase 2): D = T - T[baseline column of the cell], as k_delta computes it
   double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
-  const int bc_u = (phase == 2) ? a.base_col[c] : -1;
+  const int bc_u = (phase == 2) ? tab_base_col(a, c) : -1;
   // per 64-point stretch j (grid points 64j .. 64j+63, one k_boot2 wave each): the
   // column's maximum, for k_boot2's stretch bounds (U: raw maxima for phase-1 columns,
   // maxima minus the cell's baseline-column maxima for phase-2 columns)
@@ -416,7 +428,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
   }
   const unsigned long long anyc = __ballot(clamp);
   if (lane == 0) a.has_clamp[col] = anyc ? 1 : 0;
-  if (phase == 1 && lane == 0) a.base_col[c] = (a.use_baseline && !anyc) ? (int)col : -1;
+  if (phase == 1 && lane == 0) a.base_col[c] = (a.use_baseline && !anyc) ? (int)col + a.col_base : -1;
 }
 
 __device__ __forceinline__ void tables_tabs(double* etab, double (*ltab)[97]) {
@@ -458,7 +470,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
         break;
       }
     }
-    if (lane == 0) a.zcol[c] = (int)zc;
+    if (lane == 0) a.zcol[c] = zc >= 0 ? (int)zc + a.col_base : -1;
     if (zc < 0) {
       if (lane == 0) a.base_col[c] = -1;
       return;
@@ -479,9 +491,9 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
             const int mid = (lo + hi) >> 1;
             if (a.ucl_off[mid] <= cs) lo = mid; else hi = mid;
           }
-          if (phase == 2 && cs == a.zcol[lo]) continue;  // done in phase 1
+          if (phase == 2 && cs == tab_zcol(a, lo)) continue;  // done in phase 1
           const long long co = (long long)lo * a.GS;
-          const int bc = (phase == 2) ? a.base_col[lo] : -1;
+          const int bc = (phase == 2) ? tab_base_col(a, lo) : -1;
           const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
           tables_column<CT>(a, cs, lo, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
                             a.lcfp + co, nullptr, nullptr, a.theta + co, base, vrow + (long long)wid * a.GS, etab,
@@ -504,10 +516,10 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
       if (a.ucl_off[mid] <= col) lo = mid; else hi = mid;
     }
     c = lo;
-    if (phase == 2 && col == a.zcol[c]) return;  // done in phase 1
+    if (phase == 2 && col == tab_zcol(a, c)) return;  // done in phase 1
   }
   const long long co = (long long)c * a.GS;
-  const int bc = (phase == 2) ? a.base_col[c] : -1;
+  const int bc = (phase == 2) ? tab_base_col(a, c) : -1;
   const double* base = (bc >= 0 && a.D) ? a.D + (long long)bc * a.GS : nullptr;
   tables_column<CT>(a, col, c, phase, a.mu + co, (CT && a.pq) ? a.pq + 4 * co : nullptr, a.lcfpr + co,
                     a.lcfp + co, nullptr, nullptr, a.theta + co, base, vrow + (long long)wid * a.GS, etab, lt, lane,
@@ -552,7 +564,7 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   double* sth = slc + G;
   double* sbase = sth + G;
   const long long co = (long long)c * GS;
-  const int bc = (phase == 2) ? a.base_col[c] : -1;
+  const int bc = (phase == 2) ? tab_base_col(a, c) : -1;
   if (bc >= 0 && a.UQ && threadIdx.x < kQTiles) suqb[threadIdx.x] = a.UQ[(long long)bc * kQTiles + threadIdx.x];
   for (int k = threadIdx.x; k < G; k += 64 * kTabWaves) {
     smu[k] = a.mu[co + k];
@@ -570,7 +582,7 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   }
   __syncthreads();
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
-  const int zc = (phase == 2) ? a.zcol[c] : -1;
+  const int zc = (phase == 2) ? tab_zcol(a, c) : -1;
   for (int col = task.y + wid; col < task.z; col += kTabWaves) {
     if (col == zc) continue;  // done in phase 1
     tables_column<CT>(a, col, c, phase, smu, haveP ? sP : nullptr, slr, nullptr, slc, (bc >= 0) ? suqb : nullptr, sth,
@@ -896,7 +908,7 @@ __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_
     return;
   }
   const long long co = (long long)c * GS;
-  const int bc = (phase == 2) ? a.base_col[c] : -1;
+  const int bc = (phase == 2) ? tab_base_col(a, c) : -1;
   if (bc >= 0 && a.UQ && threadIdx.x < kQTiles) suqb[threadIdx.x] = a.UQ[(long long)bc * kQTiles + threadIdx.x];
   const double* P = a.pq + 4 * co;
   for (int k = threadIdx.x; k < kRS; k += 64 * kTabRegWaves) {
@@ -914,7 +926,7 @@ __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_
   }
   __syncthreads();
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
-  const int zc = (phase == 2) ? a.zcol[c] : -1;
+  const int zc = (phase == 2) ? tab_zcol(a, c) : -1;
   const double theta = a.theta[co];
   const double maxcfp = a.cellscal[2 * c];
   for (int col = task.y + wid; col < task.z; col += kTabRegWaves) {

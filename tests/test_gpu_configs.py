@@ -97,8 +97,9 @@ def test_config5_ms1_kernel_3000_cells():
 
 def test_config3_host_pipeline_equals_device_resident(api):
     """Full config 3 (20,000 x 1,000: an 80 MB matrix, above the 48 MB pipelining threshold):
-    scde_expression_difference_host uploads the counts in two column ranges and builds the
-    second group's unique sets and posterior on the peer lane beside the first group's
+    scde_expression_difference_host uploads the counts in two column ranges, the first in pieces
+    whose unique sets and tables start as each lands (option pieces), and builds the second
+    group's unique sets and posterior on the peer lane beside the first group's
     (engine.hip de_run, lanes = 2); the table must equal, bit for bit, the device-resident entry
     on the same counts with the groups one after the other (lanes = 1, no pipelining)."""
     import ctypes
@@ -120,10 +121,18 @@ def test_config3_host_pipeline_equals_device_resident(api):
     params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, len(px), 100, 1,
                       0, N, 0.0, api.get_rand_kind(), 1)
     vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
-    host = np.zeros((N, 6), order="F")
-    for _ in range(2):  # the second call reuses the context's buffers and streams
-        check(lib().scde_expression_difference_host(ctx.handle, vp(mat), N, N, ctypes.byref(params), vp(host), None,
-                                                    None, None))
+    hosts = []
+    try:
+        # the first group's columns in 4 (default), 3 (uneven) pieces or one; the repeat reuses the
+        # context's buffers and streams
+        for pieces in (4, 4, 3, 1, 8):
+            ctx.set_option("pieces", pieces)
+            host = np.zeros((N, 6), order="F")
+            check(lib().scde_expression_difference_host(ctx.handle, vp(mat), N, N, ctypes.byref(params), vp(host),
+                                                        None, None, None))
+            hosts.append(host)
+    finally:
+        ctx.set_option("pieces", 4)
     dc = api.DeviceCounts(ctx, mat)
     try:
         dev = np.zeros((N, 6), order="F")
@@ -133,5 +142,6 @@ def test_config3_host_pipeline_equals_device_resident(api):
     finally:
         ctx.set_option("lanes", 2)
         dc.free()
-    assert np.isfinite(host[:, :4]).all()
-    np.testing.assert_array_equal(host, dev)
+    for host in hosts:
+        assert np.isfinite(host[:, :4]).all()
+        np.testing.assert_array_equal(host, dev)

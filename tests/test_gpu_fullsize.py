@@ -83,6 +83,20 @@ def test_config4_1000_gene_slice_modes(api):
     api.set_rand("glibc")
     got = api.scde_posteriors(models, sub, prior, n_randomizations=100, return_individual_posterior_modes=True,
                               n_cores=1)
+    # the host entry's piece pipeline (forced below its 48 MB threshold): the same bits
+    ctx = api.default_context()
+    try:
+        for pieces in (3, 8):
+            ctx.set_option("pipeline_mb", 0)
+            ctx.set_option("pieces", pieces)
+            api.set_rand("glibc")
+            pip = api.scde_posteriors(models, sub, prior, n_randomizations=100,
+                                      return_individual_posterior_modes=True, n_cores=1)
+            np.testing.assert_array_equal(pip["jp"], got["jp"])
+            np.testing.assert_array_equal(pip["modes"], got["modes"])
+    finally:
+        ctx.set_option("pipeline_mb", 48)
+        ctx.set_option("pieces", 4)
     px = np.asarray(prior["x"])
     w = _workers()
     bounds = np.linspace(0, n, w + 1).astype(int)
