@@ -134,6 +134,13 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "pair_cells"    the cell count from which k_boot_tiles runs two slabs per wave with two
  *                   bound tiles each (default 1000: wide calls, narrow posteriors); slabs that need
  *                   more take a four-tile pass (results are the same)
+ *   "lanes"         2/1  a DE call's second group runs on a peer context (its own streams and
+ *                   workspace, same device) beside the first (default 2), or after it (1; bench's
+ *                   per-stage timing pass and the rocprof runs use 1); results are the same
+ *   "pipeline_mb"   host-count DE / scde.posteriors calls whose matrix has at least this many MB
+ *                   upload on a copy stream in column pieces that the kernels follow (default 48)
+ *   "pieces"        pieces of that upload (the DE call's first group; the posteriors call's
+ *                   selected cells), 1..8 (default 4); results are the same
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
