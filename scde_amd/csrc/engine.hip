@@ -2433,8 +2433,8 @@ int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld
   if (ngenes < 0 || C <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
   HCHK(hipSetDevice(ctx->device));
   // Small matrices upload in one piece and keep the batched unique-table build: the
-  // per-group build costs two extra host syncs, which a short transfer does not repay
-  // (20k x 200 counts: 5.20 vs 5.59 ms per call; 20k x 1,000: 11.19 vs 10.60)
+  // per-group build costs extra host syncs, which a short transfer does not repay (two lanes,
+  // pipeline_mb 48 vs 0: 2,500 x 1,000 counts 1.84 vs 2.29 ms per call, 20k x 200 4.66 vs 4.87)
   const size_t kPipelineBytes = (size_t)std::max(0.0, ctx->opt_pipeline_mb) * (size_t(1) << 20);
   if (ngenes == 0 || sizeof(int) * (size_t)ngenes * C < kPipelineBytes) {
     const int* dev = nullptr;
