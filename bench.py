@@ -436,8 +436,8 @@ def cpu_model() -> str:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="3", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", default=None, choices=["strong", "weak"],
                     help="multi-GPU: strong = one fixed gene set split over the ranks (configs 3/4 default), "
