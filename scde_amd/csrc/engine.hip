@@ -306,6 +306,8 @@ struct scde_ctx {
   } us[3];
   static constexpr int kMaxPieces = 8;
   UniqueSet upc[kMaxPieces];  // run_posterior's pieces
+  UniqueSet task_us;          // run_posterior's tables tasks (unpieced): per context, so lanes sharing a
+                              // unique set never write one tasks buffer
   // profiling
   bool profile = false;
   struct Pending {
@@ -385,6 +387,7 @@ struct scde_ctx {
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (auto& u : upc) u.release();
+    task_us.release();
     for (void* p : user_allocs) (void)hipFree(p);
     for (auto& p : pending) {
       (void)hipEventDestroy(p.a);
@@ -945,7 +948,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     }
     RCHK(setup_tables(plan, ncols, false));
     ta.ncols = ncols;
-    RCHK(launch_tables_range(plan, 0, C, 0, u.ucl_off.as<long long>(), ucl_off_h, true, u));
+    RCHK(launch_tables_range(plan, 0, C, 0, u.ucl_off.as<long long>(), ucl_off_h, true, cx->task_us));
   }
   std::vector<int> draws;
   std::vector<double> W;
@@ -2318,11 +2321,30 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     UniqueSet* up[3] = {&ctx->us[0], &ctx->us[1], &ctx->us[2]};
     RCHK(build_unique_sets(ctx, sp, up, 3));
   }
-  RCHK(run_posterior(ctx, sb[0], ctx->us[2]));
-  ctx->us[2].ready = true;  // same cells, same counts: reuse for the second batch run
-  RCHK(run_posterior(ctx, sb[1], ctx->us[2]));
-  RCHK(run_posterior(ctx, sg[0], ctx->us[0]));
-  RCHK(run_posterior(ctx, sg[1], ctx->us[1]));
+  scde_ctx* lane = ctx;  // the second batch posterior and the second group's run on the peer lane
+  if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
+  if (lane != ctx) {
+    HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
+    HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
+    std::function<int()> rest0, rest1;
+    RCHK(run_posterior(ctx, sb[0], ctx->us[2], &rest0));
+    ctx->us[2].ready = true;  // same cells, same counts: reuse for the second batch run
+    RCHK(run_posterior(lane, sb[1], ctx->us[2], &rest1));
+    RCHK(rest0());
+    RCHK(rest1());
+    RCHK(run_posterior(ctx, sg[0], ctx->us[0], &rest0));
+    RCHK(run_posterior(lane, sg[1], ctx->us[1], &rest1));
+    RCHK(rest0());
+    RCHK(rest1());
+    HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
+    HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+  } else {
+    RCHK(run_posterior(ctx, sb[0], ctx->us[2]));
+    ctx->us[2].ready = true;  // same cells, same counts: reuse for the second batch run
+    RCHK(run_posterior(ctx, sb[1], ctx->us[2]));
+    RCHK(run_posterior(ctx, sg[0], ctx->us[0]));
+    RCHK(run_posterior(ctx, sg[1], ctx->us[1]));
+  }
   // three ratio posteriors + summaries
   const std::vector<double> dv1 = ratio_diffv(p->prior_x, G);
   const int m = 2 * G - 1, m2 = 2 * m - 1;
@@ -2397,7 +2419,9 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     RCHK(ctx->sync());
     transpose_rows_to_colmajor(tmp.data(), N, G, out);
   }
-  return ctx->sync();
+  const int rc = ctx->sync();
+  merge_peer_stats(ctx);
+  return rc;
 }
 
 // ------------------------------------------------------------------ host-count entry points

@@ -317,6 +317,20 @@ def test_batch_corrected_difference(api, oracle, ncores, nlev):
             np.testing.assert_array_equal(got[k].to_numpy(), want[k], err_msg=f"{table}.{k}")
         assert_z_close(got["Z"].to_numpy(), want["Z"], what=f"{table}.Z")
         assert_z_close(got["cZ"].to_numpy(), want["cZ"], what=f"{table}.cZ")
+    # the four posteriors on two lanes (default) or one after the other: the same bits
+    ctx = api.default_context()
+    try:
+        ctx.set_option("lanes", 1)
+        one = api.scde_expression_difference(models, counts, prior, groups=groups, batch=batch, n_randomizations=10,
+                                             n_cores=ncores, return_posteriors=True)
+    finally:
+        ctx.set_option("lanes", 2)
+    for i in range(2):
+        np.testing.assert_array_equal(one["joint.posteriors"][i], out["joint.posteriors"][i])
+    for key in ("difference.posterior", "batch.adjusted.difference.posterior"):
+        np.testing.assert_array_equal(one[key].values, out[key].values)
+    for table in ("batch.effect", "results", "batch.adjusted"):
+        np.testing.assert_array_equal(one[table].to_numpy(dtype=float), out[table].to_numpy(dtype=float))
 
 
 def test_batch_device_matches_composition(api):
