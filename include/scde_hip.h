@@ -138,7 +138,7 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   workspace, same device) beside the first (default 2), or after it (1; bench's
  *                   per-stage timing pass and the rocprof runs use 1); results are the same
  *   "pipeline_mb"   host-count DE / scde.posteriors calls whose matrix has at least this many MB
- *                   upload on a copy stream in column pieces that the kernels follow (default 48)
+ *                   upload on a copy stream in column pieces that the kernels follow (default 32)
  *   "pieces"        pieces of that upload (the DE call's first group; the posteriors call's
  *                   selected cells), 1..8 (default 4); results are the same
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)

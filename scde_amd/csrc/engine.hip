@@ -237,7 +237,7 @@ struct scde_ctx {
   int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
   int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
                                  // tiles each; the posterior narrows with the cells, most slabs need two)
-  double opt_pipeline_mb = 48;  // "pipeline_mb": host-count DE calls from this many MB of counts upload in two
+  double opt_pipeline_mb = 32;  // "pipeline_mb": host-count DE calls from this many MB of counts upload in two
                                 // column ranges, each group starting once its cells are in HBM
   int opt_pieces = 4;           // "pieces": the first group's columns of a pipelined host-count DE call upload
                                 // in this many pieces, each piece's unique sets and tables starting as it lands
@@ -2458,7 +2458,9 @@ int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld
   HCHK(hipSetDevice(ctx->device));
   // Small matrices upload in one piece and keep the batched unique-table build: the
   // per-group build costs extra host syncs, which a short transfer does not repay (two lanes,
-  // pipeline_mb 48 vs 0: 2,500 x 1,000 counts 1.84 vs 2.29 ms per call, 20k x 200 4.66 vs 4.87)
+  // one piece vs pipelined: 2,500 x 1,000 counts 1.84 vs 2.29 ms per call, 5,000 x 1,000 2.89-2.92
+  // vs 3.20-3.22, 20k x 200 4.66 vs 4.87; from 32 MB the pipeline wins: 10,000 x 1,000
+  // 4.72-4.92 vs 5.00-5.14)
   const size_t kPipelineBytes = (size_t)std::max(0.0, ctx->opt_pipeline_mb) * (size_t(1) << 20);
   if (ngenes == 0 || sizeof(int) * (size_t)ngenes * C < kPipelineBytes) {
     const int* dev = nullptr;

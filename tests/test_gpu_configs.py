@@ -96,7 +96,7 @@ def test_config5_ms1_kernel_3000_cells():
 
 
 def test_config3_host_pipeline_equals_device_resident(api):
-    """Full config 3 (20,000 x 1,000: an 80 MB matrix, above the 48 MB pipelining threshold):
+    """Full config 3 (20,000 x 1,000: an 80 MB matrix, above the 32 MB pipelining threshold):
     scde_expression_difference_host uploads the counts in two column ranges, the first in pieces
     whose unique sets and tables start as each lands (option pieces), and builds the second
     group's unique sets and posterior on the peer lane beside the first group's
@@ -112,7 +112,7 @@ def test_config3_host_pipeline_equals_device_resident(api):
     prior = expression_prior(models, counts, length_out=bench.LENGTH_OUT)
     mat = np.asfortranarray(counts, dtype=np.int32)
     N, C = mat.shape
-    assert mat.nbytes >= 48 << 20
+    assert mat.nbytes >= 32 << 20
     codes = np.ascontiguousarray(np.asarray(groups), np.int32)
     mm, lt, sq = model_matrix(models)
     px = np.ascontiguousarray(prior["x"], np.float64)

@@ -83,7 +83,7 @@ def test_config4_1000_gene_slice_modes(api):
     api.set_rand("glibc")
     got = api.scde_posteriors(models, sub, prior, n_randomizations=100, return_individual_posterior_modes=True,
                               n_cores=1)
-    # the host entry's piece pipeline (forced below its 48 MB threshold): the same bits
+    # the host entry's piece pipeline (forced below its 32 MB threshold): the same bits
     ctx = api.default_context()
     try:
         for pieces in (3, 8):
@@ -95,7 +95,7 @@ def test_config4_1000_gene_slice_modes(api):
             np.testing.assert_array_equal(pip["jp"], got["jp"])
             np.testing.assert_array_equal(pip["modes"], got["modes"])
     finally:
-        ctx.set_option("pipeline_mb", 48)
+        ctx.set_option("pipeline_mb", 32)
         ctx.set_option("pieces", 4)
     px = np.asarray(prior["x"])
     w = _workers()

@@ -45,7 +45,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("pair_cells", opts.get("pair_cells", 1000))
     ctx.set_option("unique_fixed", opts.get("unique_fixed", 1))
     ctx.set_option("lanes", opts.get("lanes", 2))
-    ctx.set_option("pipeline_mb", opts.get("pipeline_mb", 48))
+    ctx.set_option("pipeline_mb", opts.get("pipeline_mb", 32))
     ctx.set_option("pieces", opts.get("pieces", 4))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
@@ -66,7 +66,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("pair_cells", 1000)
         ctx.set_option("unique_fixed", 1)
         ctx.set_option("lanes", 2)
-        ctx.set_option("pipeline_mb", 48)
+        ctx.set_option("pipeline_mb", 32)
         ctx.set_option("pieces", 4)
         ctx.set_option("skip_stats", 0)
     return out, stats
