@@ -452,6 +452,8 @@ def main():
     ap.add_argument("--shard-of", type=int, default=1,
                     help="readiness study, one process: time rank 0's shard of a strong split over this many "
                          "ranks (no collective; not the metric)")
+    ap.add_argument("--trace-host", action="store_true",
+                    help="end with a second host-count pass (tools/tl_shard.sh: the traced last step is a host step)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="context option for a study run (scde_ctx_set_option); the defaults are the product")
     args = ap.parse_args()
@@ -645,6 +647,8 @@ def main():
         stage_name = BOOT_STAGES.get(int(ctx.stat("boot_path")), "bootstrap stage")
         ctx.set_option("skip_stats", 0)
 
+    if args.trace_host:
+        timed()
     total_genes = NTOT * args.steps
     value = total_genes / dt
     boot_ms, boot_n = kt["boot"]

@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <functional>
+#include <thread>
 #include <memory>
 #include <mutex>
 #include <numeric>
@@ -241,6 +243,8 @@ struct scde_ctx {
                                 // column ranges, each group starting once its cells are in HBM
   int opt_pieces = 4;           // "pieces": the first group's columns of a pipelined host-count DE call upload
                                 // in this many pieces, each piece's unique sets and tables starting as it lands
+  int opt_lane_prio = 1;        // "lane_prio": the peer lane's streams at the device's highest priority (set
+                                // before the peer's first use)
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                  // group on `peer`, its own streams and workspace) or one after the other (1)
   // the second lane of a DE call: a context on the same device, created on first use; its
@@ -248,6 +252,21 @@ struct scde_ctx {
   scde_ctx* peer = nullptr;
   hipEvent_t lane_ev[2] = {nullptr, nullptr};  // [0] this stream -> peer, [1] peer -> this stream
   hipEvent_t piece_ev[8] = {nullptr};           // run_posterior's pieces: unique sets built
+  hipEvent_t piece_up_ev[8] = {nullptr};        // the pieces' uploads landed (upload worker)
+  hipStream_t uq_stream = nullptr;              // the pieces' and the second group's unique builds
+  int stream_prio = 0;  // priority of streams this context creates (the peer lane: the device's highest)
+  // host-count upload thread (created on first use, lives with the context): a pageable copy
+  // blocks its calling thread for the whole transfer, so the pieces go up from here, back to
+  // back, while the caller builds unique sets and queues kernels
+  struct Uploader {
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    bool stop = false, busy = false;
+    long long job = 0;
+    std::function<int(int)> issue;  // issue(j): upload range j and record its event
+    int nranges = 0, issued = 0, err = 0;
+  } upl;
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // host wall time of scde_expression_difference_{dev,host} phases (ms, summed over calls):
@@ -367,6 +386,14 @@ struct scde_ctx {
     return SCDE_OK;
   }
   ~scde_ctx() {
+    if (upl.th.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(upl.m);
+        upl.stop = true;
+      }
+      upl.cv.notify_all();
+      upl.th.join();
+    }
     if (peer) {
       (void)hipStreamSynchronize(peer->stream);
       delete peer;
@@ -375,6 +402,9 @@ struct scde_ctx {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : piece_ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : piece_up_ev)
+      if (e) (void)hipEventDestroy(e);
+    if (uq_stream) (void)hipStreamDestroy(uq_stream);
     Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &pq, &colc, &T,      &E,      &maxi,
                   &has_clamp, &base_col, &zcol, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
                   &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw, &ubound, &zubound, &smask, &subuf, &sredo};
@@ -934,7 +964,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   }
   const long long ncols = ucl_off_h[C];
   const Plan plan = make_plan(ncols);
-  const bool fast = plan.fast, fused = plan.fused, keep_T = plan.keep_T, stretch_skip = plan.stretch_skip;
+  const bool fast = plan.fast, fused = plan.fused, stretch_skip = plan.stretch_skip;
   bool tpath = plan.tpath;
   ta.ncols = ncols;
   if (!tables_done) {
@@ -1002,7 +1032,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // beside phase 2 of the tables
     hipStream_t sa = st;
     if (fused) {
-      if (!cx->aux_stream) HCHK(hipStreamCreateWithFlags(&cx->aux_stream, hipStreamNonBlocking));
+      if (!cx->aux_stream) HCHK(hipStreamCreateWithPriority(&cx->aux_stream, hipStreamNonBlocking, cx->stream_prio));
       if (!cx->aux_ev) HCHK(hipEventCreateWithFlags(&cx->aux_ev, hipEventDisableTiming));
       sa = cx->aux_stream;
       HCHK(hipStreamWaitEvent(sa, cx->p1_ev, 0));
@@ -1439,6 +1469,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
+  else if (n == "lane_prio") ctx->opt_lane_prio = value != 0;
   else if (n == "lanes") ctx->opt_lanes = value >= 2 ? 2 : 1;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
@@ -1807,9 +1838,9 @@ int scde_ratio_summary(const double* pmat1, const double* pmat2, int nrows, int 
 }
 
 // ------------------------------------------------------------------ layer 2
-// Host counts for de_run: copied in two column ranges on the context's copy stream.  A
-// pageable copy returns only once its data has left the host buffer, so the second range is
-// issued after the first group's kernels are queued: its transfer then overlaps them.
+// Host counts of a host-count entry (de_run: the first group's range in pieces, then the
+// second group's range; posteriors_run: the selected cells in pieces), copied on the context's
+// copy stream by an UploadWorker.
 struct HostUpload {
   const int* counts;
   int64_t ld;
@@ -1829,6 +1860,83 @@ static int upload_cols(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   }
   return SCDE_OK;
 }
+
+// The host-count uploads of one call, issued back to back from a worker thread: a pageable
+// copy blocks its calling thread for the whole transfer, so issued from the caller's thread
+// each piece would wait for the previous piece's unique-set build (a host sync) and PCIe would
+// sit idle in between.  Column ranges [cols[j], cols[j+1]) go up on the copy stream in order,
+// each followed by evs[j]; wait(n) returns once the first n are issued (their events recorded).
+struct UploadWorker {
+  scde_ctx* ctx = nullptr;
+  int start(scde_ctx* c, const HostUpload& h, std::vector<int> cols, std::vector<hipEvent_t> evs) {
+    ctx = c;
+    auto& u = c->upl;
+    if (!u.th.joinable()) {
+      u.th = std::thread([c] {
+        auto& q = c->upl;
+        (void)hipSetDevice(c->device);
+        long long seen = 0;
+        std::unique_lock<std::mutex> lk(q.m);
+        for (;;) {
+          q.cv.wait(lk, [&] { return q.stop || q.job != seen; });
+          if (q.stop) return;
+          seen = q.job;
+          const int n = q.nranges;
+          auto issue = q.issue;
+          lk.unlock();
+          int rc = SCDE_OK;
+          for (int j = 0; j < n && rc == SCDE_OK; ++j) {
+            rc = issue(j);
+            std::lock_guard<std::mutex> g(q.m);
+            if (rc != SCDE_OK) q.err = rc; else ++q.issued;
+            q.cv.notify_all();
+          }
+          lk.lock();
+          q.busy = false;
+          q.cv.notify_all();
+        }
+      });
+    }
+    std::lock_guard<std::mutex> lk(u.m);
+    u.issue = [c, h, cols = std::move(cols), evs = std::move(evs)](int j) -> int {
+      RCHK(upload_cols(c, h, cols[j], cols[j + 1]));
+      HCHK(hipEventRecord(evs[j], c->copy_stream));
+      return SCDE_OK;
+    };
+    u.nranges = (int)evs.size();
+    u.issued = 0;
+    u.err = 0;
+    u.busy = true;
+    ++u.job;
+    u.cv.notify_all();
+    return SCDE_OK;
+  }
+  int wait(int n) {
+    auto& u = ctx->upl;
+    std::unique_lock<std::mutex> lk(u.m);
+    u.cv.wait(lk, [&] { return u.issued >= n || u.err != 0 || !u.busy; });
+    if (u.err) return fail(u.err, "count upload failed");
+    return u.issued >= n ? SCDE_OK : fail(SCDE_EINTERNAL, "upload range %d never issued", n - 1);
+  }
+  // the job is finished (every range issued or failed) before the call returns: the next call's
+  // job, and the caller's buffers, must not overlap it
+  ~UploadWorker() {
+    if (!ctx) return;
+    auto& u = ctx->upl;
+    std::unique_lock<std::mutex> lk(u.m);
+    u.cv.wait(lk, [&] { return !u.busy; });
+  }
+};
+
+static int ensure_piece_streams(scde_ctx* ctx) {
+  if (!ctx->uq_stream) HCHK(hipStreamCreateWithFlags(&ctx->uq_stream, hipStreamNonBlocking));
+  for (int j = 0; j < scde_ctx::kMaxPieces; ++j) {
+    if (!ctx->piece_ev[j]) HCHK(hipEventCreateWithFlags(&ctx->piece_ev[j], hipEventDisableTiming));
+    if (!ctx->piece_up_ev[j]) HCHK(hipEventCreateWithFlags(&ctx->piece_up_ev[j], hipEventDisableTiming));
+  }
+  return SCDE_OK;
+}
+
 
 // up (nullable): the host-count entry's upload, in pieces of the selected cells (cellidx
 // strictly increasing), each piece's unique sets and tables starting as it lands
@@ -1905,19 +2013,24 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
   }
   ctx->us[0].ready = false;
   std::vector<int> piece_c, piece_col;
+  UploadWorker uw;
   if (up) {
     const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
     for (int j = 0; j <= K; ++j) piece_c.push_back((int)((long long)ncells_sel * j / K));
     piece_col.push_back(0);  // piece j uploads columns [piece_col[j], piece_col[j + 1])
     for (int j = 0; j < K; ++j)
       piece_col.push_back(piece_c[j + 1] > piece_c[j] ? cellidx[piece_c[j + 1] - 1] + 1 : piece_col.back());
-    for (int j = 0; j < K; ++j)
-      if (!ctx->piece_ev[j]) HCHK(hipEventCreateWithFlags(&ctx->piece_ev[j], hipEventDisableTiming));
+    RCHK(ensure_piece_streams(ctx));
+    RCHK(uw.start(ctx, *up, piece_col, std::vector<hipEvent_t>(ctx->piece_up_ev, ctx->piece_up_ev + K)));
     s.npieces = K;
     s.piece_c = piece_c.data();
-    s.piece_stream = ctx->copy_stream;
+    s.piece_stream = ctx->uq_stream;
     s.piece_ev = ctx->piece_ev;
-    s.piece_ready = [&](int j) { return upload_cols(ctx, *up, piece_col[j], piece_col[j + 1]); };
+    s.piece_ready = [&](int j) {
+      RCHK(uw.wait(j + 1));
+      HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
+      return SCDE_OK;
+    };
   }
   RCHK(run_posterior(ctx, s, ctx->us[0]));
   if (s.modes_early) RCHK(copy_modes_out(ctx, modes, s.modes, (size_t)ngenes * ncells_sel));
@@ -1926,23 +2039,6 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
     HCHK(hipMemcpyAsync(post, s.post, sizeof(double) * NG * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
   if (s.modes_early) HCHK(hipStreamSynchronize(ctx->copy_stream));
   return ctx->sync();
-}
-
-static int upload_range(scde_ctx* ctx, const HostUpload& h, int k) {
-  const size_t row = sizeof(int) * (size_t)h.ngenes;
-  const int lo = k == 0 ? 0 : h.cut, hi = k == 0 ? h.cut : h.C;
-  if (hi > lo) {
-    char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
-    const int* src = h.counts + (size_t)h.ld * lo;
-    if (h.ld == h.ngenes)
-      HCHK(hipMemcpyAsync(dst, src, row * (hi - lo), hipMemcpyHostToDevice, ctx->copy_stream));
-    else
-      HCHK(hipMemcpy2DAsync(dst, row, src, sizeof(int) * (size_t)h.ld, row, hi - lo, hipMemcpyHostToDevice,
-                            ctx->copy_stream));
-  }
-  HCHK(hipEventRecord(ctx->up_ev[k], ctx->copy_stream));
-  HCHK(hipStreamWaitEvent(ctx->stream, ctx->up_ev[k], 0));
-  return SCDE_OK;
 }
 
 // The second lane of a DE call (opt_lanes = 2): the peer context runs the second group's
@@ -1954,6 +2050,17 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
     scde_ctx* p = nullptr;
     RCHK(scde_ctx_create(cx->device, &p));
     cx->peer = p;
+    // the peer lane starts later than the first group (its counts and unique sets come
+    // second) and its small set-up kernels would queue behind the first group's bootstrap
+    // waves: its streams get the device's highest priority
+    if (cx->opt_lane_prio) {
+      int lo = 0, hi = 0;
+      HCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      p->stream_prio = hi;
+      HCHK(hipStreamDestroy(p->stream));
+      p->stream = nullptr;
+      HCHK(hipStreamCreateWithPriority(&p->stream, hipStreamNonBlocking, hi));
+    }
     for (auto& e : cx->lane_ev)
       if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
@@ -2072,68 +2179,67 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     for (int c : idx[0]) max0 = std::max(max0, c);
     for (int c : idx[1]) max1 = std::max(max1, c);
     const int first = max0 <= max1 ? 0 : 1;
-    // the first group's range in pieces: each piece's unique sets and tables start as it lands
+    // the first group's range in pieces, then the second group's range, uploaded back to back by
+    // a worker thread: each piece's unique sets and tables start as it lands
     const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
-    std::vector<int> piece_c;
-    if (K > 1) {
-      const std::vector<int>& ix = idx[first];
-      for (int j = 0; j <= K; ++j) {
-        const int a = (int)((long long)up->cut * j / K);
-        piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
-      }
-      for (int j = 0; j < K; ++j)
-        if (!ctx->piece_ev[j]) HCHK(hipEventCreateWithFlags(&ctx->piece_ev[j], hipEventDisableTiming));
+    std::vector<int> piece_c, cols;
+    const std::vector<int>& ix = idx[first];
+    for (int j = 0; j <= K; ++j) {
+      const int a = (int)((long long)up->cut * j / K);
+      cols.push_back(a);
+      piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
     }
-    for (int k = 0; k < 2; ++k) {
-      const int gi = k == 0 ? first : 1 - first;
+    cols.push_back(up->C);
+    RCHK(ensure_piece_streams(ctx));
+    std::vector<hipEvent_t> evs(ctx->piece_up_ev, ctx->piece_up_ev + K);
+    evs.push_back(ctx->up_ev[1]);
+    UploadWorker uw;
+    RCHK(uw.start(ctx, *up, cols, evs));
+    {
+      const int gi = first;
       ctx->us[gi].ready = false;
-      if (k == 0 && K > 1) {
-        PostSpec& sf = specs[gi];
-        sf.npieces = K;
-        sf.piece_c = piece_c.data();
-        sf.piece_stream = ctx->copy_stream;
-        sf.piece_ev = ctx->piece_ev;
-        sf.piece_ready = [&, K](int j) {
-          const int lo = (int)((long long)up->cut * j / K), hi = (int)((long long)up->cut * (j + 1) / K);
-          return upload_cols(ctx, *up, lo, hi);
-        };
-        hlap(1);
-        RCHK(run_posterior(ctx, sf, ctx->us[gi]));
-        hlap(2);
-        continue;
-      }
-      RCHK(upload_range(ctx, *up, k));
+      PostSpec& sf = specs[gi];
+      sf.npieces = K;
+      sf.piece_c = piece_c.data();
+      sf.piece_stream = ctx->uq_stream;
+      sf.piece_ev = ctx->piece_ev;
+      sf.piece_ready = [&](int j) {
+        RCHK(uw.wait(j + 1));
+        HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
+        return SCDE_OK;
+      };
+      hlap(1);
+      RCHK(run_posterior(ctx, sf, ctx->us[gi]));
+      hlap(2);
+    }
+    {
+      // the second group, once its range is in HBM: its unique sets on the peer lane (or on
+      // the unique stream with one lane), so their host sync waits for its small kernels only
+      const int gi = 1 - first;
+      ctx->us[gi].ready = false;
+      RCHK(uw.wait(K + 1));
       const PostSpec* sp[1] = {&specs[gi]};
-      UniqueSet* up[1] = {&ctx->us[gi]};
-      if (k == 0) {
-        RCHK(build_unique_sets(ctx, sp, up, 1));
-        hlap(1);
-      } else if (lane != ctx) {
-        // the second group on the peer lane, behind its own upload: its unique sets' host
-        // sync waits for its small kernels only, and its posterior runs beside the first's
+      UniqueSet* usp[1] = {&ctx->us[gi]};
+      if (lane != ctx) {
         HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
-        RCHK(build_unique_sets(lane, sp, up, 1));
+        RCHK(build_unique_sets(lane, sp, usp, 1));
         hlap(1);
         RCHK(run_posterior(lane, specs[gi], ctx->us[gi]));
         HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
         HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
-        hlap(2);
-        continue;
       } else {
-        // the second group's unique sets on the copy stream, behind its own upload: their two
-        // host syncs then wait for its small kernels, not for the first group's posterior
-        // still running on the main stream, and its tables queue before that posterior ends
         if (!ctx->uq_ev) HCHK(hipEventCreateWithFlags(&ctx->uq_ev, hipEventDisableTiming));
+        HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->up_ev[1], 0));
         const hipStream_t main = ctx->stream;
-        ctx->stream = ctx->copy_stream;
-        const int rc = build_unique_sets(ctx, sp, up, 1);
+        ctx->stream = ctx->uq_stream;
+        const int rc = build_unique_sets(ctx, sp, usp, 1);
         ctx->stream = main;
         RCHK(rc);
-        HCHK(hipEventRecord(ctx->uq_ev, ctx->copy_stream));
+        HCHK(hipEventRecord(ctx->uq_ev, ctx->uq_stream));
         HCHK(hipStreamWaitEvent(ctx->stream, ctx->uq_ev, 0));
         hlap(1);
+        RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
       }
-      RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
       hlap(2);
     }
   } else {
