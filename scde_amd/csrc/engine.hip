@@ -187,6 +187,7 @@ enum {
 struct scde_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t home_stream = nullptr;  // `stream` as created (unique builds swap `stream` for a while)
   // host-count entry points: the count upload runs on its own stream, in column chunks, so
   // the first group's kernels start before the second group's columns have arrived
   hipStream_t copy_stream = nullptr;
@@ -503,11 +504,13 @@ char* pin_alloc(scde_ctx* cx, size_t bytes) {
   size_t off = (cx->pin_off + 255) & ~size_t(255);
   if (off + bytes > kPinCap) {
     // reuse from the start: every host -> device copy staged so far must have been read out of
-    // the arena first; they are issued on the context's own two streams only (device -> host
+    // the arena first; they are issued on the context's own streams only (device -> host
     // read-backs land in each unique set's own area, never here)
     if (hipStreamSynchronize(cx->stream) != hipSuccess) return nullptr;
+    if (cx->home_stream && hipStreamSynchronize(cx->home_stream) != hipSuccess) return nullptr;
     if (cx->copy_stream && hipStreamSynchronize(cx->copy_stream) != hipSuccess) return nullptr;
     if (cx->aux_stream && hipStreamSynchronize(cx->aux_stream) != hipSuccess) return nullptr;
+    if (cx->uq_stream && hipStreamSynchronize(cx->uq_stream) != hipSuccess) return nullptr;
     off = 0;
   }
   cx->pin_off = off + bytes;
@@ -1403,6 +1406,7 @@ int scde_ctx_create(int device, scde_ctx** out) {
     delete c;
     return fail(SCDE_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
+  c->home_stream = c->stream;
   *out = c;
   return SCDE_OK;
 }
@@ -2060,6 +2064,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
       HCHK(hipStreamDestroy(p->stream));
       p->stream = nullptr;
       HCHK(hipStreamCreateWithPriority(&p->stream, hipStreamNonBlocking, hi));
+      p->home_stream = p->stream;
     }
     for (auto& e : cx->lane_ev)
       if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
