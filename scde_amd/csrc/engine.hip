@@ -1901,13 +1901,16 @@ struct UploadWorker {
         }
       });
     }
+    const int nranges = (int)evs.size();  // (before the vectors move into the closure)
+    if ((int)cols.size() != nranges + 1) return fail(SCDE_EINTERNAL, "upload ranges: %d bounds for %d events",
+                                                     (int)cols.size(), nranges);
     std::lock_guard<std::mutex> lk(u.m);
     u.issue = [c, h, cols = std::move(cols), evs = std::move(evs)](int j) -> int {
       RCHK(upload_cols(c, h, cols[j], cols[j + 1]));
       HCHK(hipEventRecord(evs[j], c->copy_stream));
       return SCDE_OK;
     };
-    u.nranges = (int)evs.size();
+    u.nranges = nranges;
     u.issued = 0;
     u.err = 0;
     u.busy = true;
