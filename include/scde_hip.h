@@ -137,6 +137,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "lanes"         2/1  a DE call's second group runs on a peer context (its own streams and
  *                   workspace, same device) beside the first (default 2), or after it (1; bench's
  *                   per-stage timing pass and the rocprof runs use 1); results are the same
+ *   "lane_prio"     1/0  the peer lane's streams at the device's highest priority (default 0; set
+ *                   before the first DE call)
  *   "pipeline_mb"   host-count DE / scde.posteriors calls whose matrix has at least this many MB
  *                   upload on a copy stream in column pieces that the kernels follow (default 32)
  *   "pieces"        pieces of that upload (the DE call's first group; the posteriors call's

@@ -244,8 +244,9 @@ struct scde_ctx {
                                 // column ranges, each group starting once its cells are in HBM
   int opt_pieces = 4;           // "pieces": the first group's columns of a pipelined host-count DE call upload
                                 // in this many pieces, each piece's unique sets and tables starting as it lands
-  int opt_lane_prio = 1;        // "lane_prio": the peer lane's streams at the device's highest priority (set
-                                // before the peer's first use)
+  int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
+                                // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
+                                // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                  // group on `peer`, its own streams and workspace) or one after the other (1)
   // the second lane of a DE call: a context on the same device, created on first use; its
