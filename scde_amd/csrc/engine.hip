@@ -247,6 +247,8 @@ struct scde_ctx {
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
+  int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
+                                // the second group's tables
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                  // group on `peer`, its own streams and workspace) or one after the other (1)
   // the second lane of a DE call: a context on the same device, created on first use; its
@@ -1475,6 +1477,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
   else if (n == "lane_prio") ctx->opt_lane_prio = value != 0;
+  else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
   else if (n == "lanes") ctx->opt_lanes = value >= 2 ? 2 : 1;
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
@@ -2204,6 +2207,11 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     evs.push_back(ctx->up_ev[1]);
     UploadWorker uw;
     RCHK(uw.start(ctx, *up, cols, evs));
+    // two lanes: the first group's bootstrap is queued only after the second group's tables, so
+    // those (and their small set-up kernels) do not wait behind its waves; the first group's
+    // tables end about when the second group's range lands anyway
+    const bool defer = lane != ctx && ctx->opt_defer_boot;
+    std::function<int()> rest0, rest1;
     {
       const int gi = first;
       ctx->us[gi].ready = false;
@@ -2218,7 +2226,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         return SCDE_OK;
       };
       hlap(1);
-      RCHK(run_posterior(ctx, sf, ctx->us[gi]));
+      RCHK(run_posterior(ctx, sf, ctx->us[gi], defer ? &rest0 : nullptr));
       hlap(2);
     }
     {
@@ -2233,7 +2241,11 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
         RCHK(build_unique_sets(lane, sp, usp, 1));
         hlap(1);
-        RCHK(run_posterior(lane, specs[gi], ctx->us[gi]));
+        RCHK(run_posterior(lane, specs[gi], ctx->us[gi], defer ? &rest1 : nullptr));
+        if (defer) {
+          RCHK(rest0());
+          RCHK(rest1());
+        }
         HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
         HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
       } else {
