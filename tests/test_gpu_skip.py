@@ -47,6 +47,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("lanes", opts.get("lanes", 2))
     ctx.set_option("pipeline_mb", opts.get("pipeline_mb", 32))
     ctx.set_option("pieces", opts.get("pieces", 4))
+    ctx.set_option("defer_boot", opts.get("defer_boot", 0))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -68,6 +69,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("lanes", 2)
         ctx.set_option("pipeline_mb", 32)
         ctx.set_option("pieces", 4)
+        ctx.set_option("defer_boot", 0)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -89,6 +91,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "one-lane": {"lanes": 1},
         "pipelined-pieces": {"pipeline_mb": 0, "pieces": 3},
         "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1},
+        "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1},
         "tiles-pairs": {"pair_cells": 1},
         "tiles-pairs-redo": {"pair_cells": 1, "tile_groups": 2},
         "tiles-mult-fallback": {"tile_max_mult": 1},
@@ -126,7 +129,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
-                                    "pipelined-one-lane", "tiles-pairs",
+                                    "pipelined-one-lane", "pipelined-deferred", "tiles-pairs",
                                     "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
         for name in others:
             for i in range(2):
