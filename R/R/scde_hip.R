@@ -63,8 +63,13 @@ scde.expression.difference <- function(models, counts, prior, groups = NULL, bat
         batch <- as.factor(batch)
         if (length(batch) != nrow(models)) stop("arguments must have same length")
         bm <- .scde.model.matrix(batch.models)
-        if (bm$localtheta != m$localtheta || bm$squarelogit != m$squarelogit || nrow(bm$mm) != nrow(m$mm)) {
-            # batch.models of another model type: the reference glue over the layer-1 symbols
+        if (bm$localtheta != m$localtheta || bm$squarelogit != m$squarelogit || nrow(bm$mm) != nrow(m$mm) ||
+            !identical(rownames(batch.models), rownames(models))) {
+            # batch.models of another model type, or of other cells / another row order: the
+            # reference's batch posteriors reorder the counts by rownames(batch.models) and pair
+            # batch[i] with batch.models row i (R/functions.R:356, 570, 573-574), which the fused
+            # call (one count matrix in models' order) does not express -- the reference glue over
+            # the layer-1 symbols
             return(.scde.ref.expression.difference(models, counts, prior, groups, batch, n.randomizations, n.cores,
                                                    batch.models, return.posteriors, expectation, verbose))
         }
@@ -111,13 +116,14 @@ scde.expression.difference <- function(models, counts, prior, groups = NULL, bat
 scde.posteriors <- function(models, counts, prior, n.randomizations = 100, batch = NULL, composition = NULL,
                             return.individual.posteriors = FALSE, return.individual.posterior.modes = FALSE,
                             ensemble.posterior = FALSE, n.cores = 20) {
-    if (!is.null(batch)) {
-        return(.scde.ref.posteriors(models, counts, prior, n.randomizations, batch, composition,
-                                    return.individual.posteriors, return.individual.posterior.modes,
-                                    ensemble.posterior, n.cores))
-    }
     if (!all(rownames(models) %in% colnames(counts))) {
         stop("ERROR: provided count data does not cover all of the cells specified in the model matrix")
+    }
+    batchil <- NULL
+    if (!is.null(batch)) {  # R/functions.R:568-571: batch-sampled posteriors
+        if (is.null(composition)) stop("ERROR: group composition must be provided if the batch argument is passed")
+        batchil <- tapply(c(1:nrow(models)) - 1, batch, I)
+        composition <- as.integer(composition)
     }
     counts <- as.matrix(counts[, match(rownames(models), colnames(counts)), drop = FALSE])
     storage.mode(counts) <- "integer"
@@ -130,8 +136,13 @@ scde.posteriors <- function(models, counts, prior, n.randomizations = 100, batch
     }
     m <- .scde.model.matrix(models)
     m$mm[, 5] <- pmax(m$mm[, 5], 1e-10)
+    if (any(models$corr.a < 1e-10)) {  # R/functions.R:579-583
+        cat("WARNING: the following cells have negatively-correlated or 0-slope fits: ",
+            paste(rownames(models)[models$corr.a < 1e-10], collapse = " "), ". Setting slopes to 1e-10.\n")
+    }
     x <- .Call("scde_hip_posteriors", m$mm, counts, prior$x, n.randomizations, n.cores, m$localtheta, m$squarelogit,
-               postflag, ensemble.posterior, PACKAGE = "scde")
+               postflag, ensemble.posterior, batchil, composition, PACKAGE = "scde")
+    if (!is.null(batch) && postflag == 3) postflag <- 0  # the reference's batch call returns jp only
     name.jp <- function(j) {
         rownames(j) <- rownames(counts)
         colnames(j) <- as.character(exp(marginals))

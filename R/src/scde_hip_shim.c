@@ -37,6 +37,7 @@ static void flatten_ilist(SEXP l, int **vals, int64_t **off) {
   for (R_xlen_t i = 0; i < n; i++) { tot += XLENGTH(VECTOR_ELT(l, i)); (*off)[i + 1] = tot; }
   *vals = (int *) R_alloc(tot > 0 ? tot : 1, sizeof(int));
   for (R_xlen_t i = 0; i < n; i++) {
+    if (XLENGTH(VECTOR_ELT(l, i)) == 0) continue;  /* tapply's NULL for an empty level */
     SEXP v = PROTECT(Rf_coerceVector(VECTOR_ELT(l, i), INTSXP));
     memcpy(*vals + (*off)[i], INTEGER(v), sizeof(int) * XLENGTH(v));
     UNPROTECT(1);
@@ -348,28 +349,44 @@ SEXP scde_hip_expression_difference_batch(SEXP Models, SEXP BatchModels, SEXP Co
   return out;
 }
 
+/* scde.posteriors (R/functions.R:566-669) in one call.  BatchIL / Composition: R_NilValue, or the
+ * reference's batchil <- tapply(c(1:nrow(models)) - 1, batch, I) (0-based model rows per batch
+ * level, R/functions.R:570) and the composition vector (draws per boot per level, 568-569), as
+ * the reference passes them to logBootBatchPosterior (613, 635).  As there, a batch call returns
+ * modes for postflag 1 and the individual posteriors for postflag 2 only (src/jpmatLogBoot.cpp:
+ * 499-530); postflag 3 returns jp. */
 SEXP scde_hip_posteriors(SEXP Models, SEXP Counts, SEXP PriorX, SEXP Nboot, SEXP NCores, SEXP LocalTheta,
-                         SEXP SquareLogitConc, SEXP PostFlag, SEXP Ensemble) {
+                         SEXP SquareLogitConc, SEXP PostFlag, SEXP Ensemble, SEXP BatchIL, SEXP Composition) {
   SEXP mm = PROTECT(Rf_coerceVector(Models, REALSXP)), px = PROTECT(Rf_coerceVector(PriorX, REALSXP));
   SEXP ci = PROTECT(Rf_coerceVector(Counts, INTSXP));
   const int *counts = INTEGER(ci);
   const int ngenes = Rf_nrows(Counts), ncells = Rf_ncols(Counts), G = XLENGTH(px);
   const int postflag = as_int(PostFlag);
+  const int batch = BatchIL != R_NilValue;
+  int *bv = NULL, nbatch = 0; int64_t *bo = NULL;
+  SEXP comp = PROTECT(batch ? Rf_coerceVector(Composition, INTSXP) : R_NilValue);
+  if (batch) {
+    nbatch = (int) XLENGTH(comp);
+    if (XLENGTH(BatchIL) != nbatch) Rf_error("scde_hip: composition has %d levels, batch %d", nbatch, (int) XLENGTH(BatchIL));
+    flatten_ilist(BatchIL, &bv, &bo);
+  }
   int *cellidx = (int *) R_alloc(ncells, sizeof(int));
   for (int c = 0; c < ncells; c++) cellidx[c] = c;
+  const int want_modes = batch ? postflag == 1 : (postflag == 1 || postflag == 3);
+  const int want_post = batch ? postflag == 2 : (postflag == 2 || postflag == 3);
   SEXP jp = PROTECT(Rf_allocMatrix(REALSXP, ngenes, G));
-  SEXP modes = (postflag == 1 || postflag == 3) ? Rf_allocMatrix(REALSXP, ngenes, ncells) : R_NilValue;
+  SEXP modes = want_modes ? Rf_allocMatrix(REALSXP, ngenes, ncells) : R_NilValue;
   PROTECT(modes);
   SEXP post = R_NilValue; double *pbuf = NULL;
-  if (postflag == 2 || postflag == 3) post = alloc_post(ncells, ngenes, G, &pbuf);
+  if (want_post) post = alloc_post(ncells, ngenes, G, &pbuf);
   PROTECT(post);
   chk(scde_posteriors_host(NULL, counts, ngenes, ngenes, ncells, cellidx, ncells, REAL(mm), as_int(LocalTheta),
                            as_int(SquareLogitConc), REAL(px), G, as_int(Nboot), as_int(NCores), 0, ngenes, postflag,
-                           as_int(Ensemble), NULL, NULL, NULL, 0, REAL(jp), modes == R_NilValue ? NULL : REAL(modes),
-                           pbuf));
+                           as_int(Ensemble), bv, bo, batch ? INTEGER(comp) : NULL, nbatch, REAL(jp),
+                           modes == R_NilValue ? NULL : REAL(modes), pbuf));
   if (post != R_NilValue) fill_post(post, pbuf, ncells, ngenes, G);
-  SEXP out = pack(jp, modes, post, postflag);
-  UNPROTECT(6);
+  SEXP out = pack(jp, modes, post, batch ? ((postflag == 1 || postflag == 2) ? postflag : 0) : postflag);
+  UNPROTECT(7);
   return out;
 }
 

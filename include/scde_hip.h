@@ -31,6 +31,9 @@ extern "C" {
 #define SCDE_EARG 1   /* invalid argument / shape */
 #define SCDE_EHIP 2   /* HIP runtime error (no device, launch failure, OOM) */
 #define SCDE_EINTERNAL 3
+#define SCDE_EFORK 4  /* a GPU entry in a process forked after this library initialised HIP
+                         in its parent (R's mclapply after an n.cores = 1 call): the child
+                         cannot use the inherited runtime; nothing was run */
 
 const char* scde_last_error(void);
 int scde_version(void); /* 100 * major + minor */
@@ -136,7 +139,11 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   more take a four-tile pass (results are the same)
  *   "lanes"         2/1  a DE call's second group runs on a peer context (its own streams and
  *                   workspace, same device) beside the first (default 2), or after it (1; bench's
- *                   per-stage timing pass and the rocprof runs use 1); results are the same
+ *                   per-stage timing pass and the rocprof runs use 1); results are the same.
+ *                   Memory: the peer holds a second grow-only workspace (tables, deltas, slab
+ *                   partials, joint posterior: about 2.3 GB at 20k genes x 500 cells per group,
+ *                   DESIGN.md section 3), so two lanes roughly double a DE call's device
+ *                   footprint; setting 1 releases the peer and its workspace
  *   "lane_prio"     1/0  the peer lane's streams at the device's highest priority (default 0; set
  *                   before the first DE call)
  *   "pipeline_mb"   host-count DE / scde.posteriors calls whose matrix has at least this many MB

@@ -16,7 +16,9 @@
 #include <condition_variable>
 #include <functional>
 #include <thread>
+#include <atomic>
 #include <memory>
+#include <unistd.h>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -40,6 +42,34 @@ int fail(int code, const char* fmt, ...) {
   g_err = buf;
   return code;
 }
+
+// Fork guard (SURVEY.md §8(b) threading row).  The reference's R glue forks mclapply
+// workers that each make their own .Call (R/functions.R:606-617), and with n.cores = 1 (or
+// N <= n.cores) it calls in the R parent itself (629-637), so a session can initialise HIP
+// in the parent and fork later.  A HIP runtime is not fork-safe: a child must not touch the
+// state it inherited.  g_hip_pid records the process that made this library's first HIP
+// call; any GPU entry in another process (a fork child of it) fails with SCDE_EFORK before
+// any HIP call.  A process forked *before* that first call (mclapply from a fresh session)
+// sees 0 and initialises its own runtime, as tests/test_fork.py checks.
+std::atomic<pid_t> g_hip_pid{0};
+
+int fork_guard() {
+  const pid_t me = getpid();
+  pid_t p = g_hip_pid.load(std::memory_order_acquire);
+  if (p == me) return SCDE_OK;
+  if (p == 0 && g_hip_pid.compare_exchange_strong(p, me)) return SCDE_OK;
+  if (p == me) return SCDE_OK;
+  return fail(SCDE_EFORK,
+              "HIP was initialised by process %d before this process (%d) was forked from it; a forked child "
+              "cannot use the inherited GPU runtime. Run scde with n.cores = 1 in the parent (the fused entries "
+              "honour n.cores for seeding only), or make the first GPU call in the child",
+              (int)p, (int)me);
+}
+
+#define FORK_GUARD()                      \
+  do {                                    \
+    if (int fg_ = fork_guard()) return fg_; \
+  } while (0)
 
 #define HCHK(expr)                                                                     \
   do {                                                                                 \
@@ -107,12 +137,19 @@ struct PlatformRand {
   }
 };
 
+// Reallocations of an existing workspace buffer (grow-only, so early calls only): each one is
+// a hipFree, which waits for the device, plus -- for grow(keep) -- a copy after the owning
+// context's streams are synchronised.  Counted process-wide (stat "buf_reallocs") so a
+// regression that reallocates in steady state shows.
+std::atomic<long long> g_buf_reallocs{0};
+
 struct Buf {
   void* p = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t bytes) {
     if (bytes <= cap && p) return hipSuccess;
     if (p) {
+      g_buf_reallocs.fetch_add(1, std::memory_order_relaxed);
       hipError_t e = hipFree(p);
       p = nullptr;
       cap = 0;
@@ -123,15 +160,18 @@ struct Buf {
     if (e == hipSuccess) cap = want;
     return e;
   }
-  // ensure(bytes), or with keep: grown (25% headroom) keeping the contents -- after a device
-  // synchronisation, as any stream may still write or read the old allocation (rare: the
-  // buffers are grow-only and reused across calls)
-  hipError_t grow(bool keep, size_t bytes) {
+  // ensure(bytes), or with keep: grown (25% headroom) keeping the contents, after
+  // sync_streams() has drained every stream of the owning context that may still write or
+  // read the old allocation (scoped to that context: the peer lane, other contexts and torch
+  // streams keep running)
+  template <class SyncStreams>
+  hipError_t grow(bool keep, size_t bytes, SyncStreams&& sync_streams) {
     if (!keep || !p) return ensure(bytes);
     if (bytes <= cap) return hipSuccess;
     const size_t want = bytes + bytes / 4;
     void* q = nullptr;
-    hipError_t e = hipDeviceSynchronize();
+    g_buf_reallocs.fetch_add(1, std::memory_order_relaxed);
+    hipError_t e = sync_streams();
     if (e == hipSuccess) e = hipMalloc(&q, want);
     if (e == hipSuccess) e = hipMemcpy(q, p, cap, hipMemcpyDeviceToDevice);
     if (e != hipSuccess) {
@@ -270,6 +310,7 @@ struct scde_ctx {
     long long job = 0;
     std::function<int(int)> issue;  // issue(j): upload range j and record its event
     int nranges = 0, issued = 0, err = 0;
+    std::string err_msg;  // the worker thread's error text (its g_err is its own)
   } upl;
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
@@ -279,6 +320,8 @@ struct scde_ctx {
   // arithmetic the bootstrap kernels issued (skip_stats runs): FP64 lane FMAs of k_boot2 (kept
   // stretches x 64 lanes x slab boots x entries)
   double st_boot_f64_fma = 0;
+  double st_stream_syncs = 0;  // grow(keep) drains of this context's streams (scoped, never the device)
+  double st_arena_syncs = 0;   // pinned-arena wraps (this context's streams drained)
   double st_pair_redo = 0;  // slabs a pair pass of k_boot_tiles left to the four-tile list pass
   double st_boot_path = -1;  // the bootstrap kernel of the last posterior: 0 k_boot2, 1 k_boot_tiles, 3 general
   static constexpr int kQMaxTilesHost = 28;
@@ -441,6 +484,17 @@ struct scde_ctx {
   }
 };
 
+// every stream of the context that touches its workspace (grow(keep) drains these, not the device)
+hipError_t ctx_streams_sync(scde_ctx* cx) {
+  for (hipStream_t st : {cx->stream, cx->home_stream, cx->copy_stream, cx->aux_stream, cx->uq_stream}) {
+    if (!st) continue;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return e;
+  }
+  cx->st_stream_syncs += 1;
+  return hipSuccess;
+}
+
 namespace {
 
 // ------------------------------------------------------------------ posterior spec
@@ -514,6 +568,7 @@ char* pin_alloc(scde_ctx* cx, size_t bytes) {
     if (cx->copy_stream && hipStreamSynchronize(cx->copy_stream) != hipSuccess) return nullptr;
     if (cx->aux_stream && hipStreamSynchronize(cx->aux_stream) != hipSuccess) return nullptr;
     if (cx->uq_stream && hipStreamSynchronize(cx->uq_stream) != hipSuccess) return nullptr;
+    cx->st_arena_syncs += 1;
     off = 0;
   }
   cx->pin_off = off + bytes;
@@ -595,7 +650,8 @@ int unique_phase3(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   int* uci = nullptr;
   if (u.into) {  // a piece: into the whole set's arrays (uci sized by the caller)
     const long long need = std::max(u.into_col0 + u.ucl_off_h[C], u.into_cap_hint);
-    HCHK(u.into->ucl.grow(u.into_col0 > 0, sizeof(int) * std::max<long long>(1, need)));
+    auto cx_sync = [cx] { return ctx_streams_sync(cx); };
+    HCHK(u.into->ucl.grow(u.into_col0 > 0, sizeof(int) * std::max<long long>(1, need), cx_sync));
     ucl = u.into->ucl.as<int>() + u.into_col0;
     uci = u.into->uci.as<int>() + (size_t)N * u.into_c0;
   } else {
@@ -816,17 +872,18 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   TablesArgs ta{};
   // buffers for `cap` columns (pieces: grown keeping what earlier pieces wrote) and the
   // launch arguments over the whole column range
+  auto cx_sync = [cx] { return ctx_streams_sync(cx); };
   auto setup_tables = [&](const Plan& p, long long cap, bool keep) -> int {
     const size_t ncap = (size_t)std::max<long long>(1, cap);
-    if (p.keep_T) HCHK(cx->T.grow(keep, sizeof(double) * ncap * GS));
-    HCHK(cx->maxi.grow(keep, sizeof(int) * ncap));
-    HCHK(cx->has_clamp.grow(keep, ncap));
-    if (p.tpath) HCHK(cx->ubound.grow(keep, sizeof(unsigned) * kQTiles * (ncap + 1)));
+    if (p.keep_T) HCHK(cx->T.grow(keep, sizeof(double) * ncap * GS, cx_sync));
+    HCHK(cx->maxi.grow(keep, sizeof(int) * ncap, cx_sync));
+    HCHK(cx->has_clamp.grow(keep, ncap, cx_sync));
+    if (p.tpath) HCHK(cx->ubound.grow(keep, sizeof(unsigned) * kQTiles * (ncap + 1), cx_sync));
     if (p.fused) {
-      HCHK(cx->E.grow(keep, sizeof(double) * (ncap + 1) * GS));
-      if (p.stretch_skip) HCHK(cx->ubound.grow(keep, sizeof(double) * 8 * (ncap + 1)));
+      HCHK(cx->E.grow(keep, sizeof(double) * (ncap + 1) * GS, cx_sync));
+      if (p.stretch_skip) HCHK(cx->ubound.grow(keep, sizeof(double) * 8 * (ncap + 1), cx_sync));
     }
-    if (!s.localtheta) HCHK(cx->colc.grow(keep, sizeof(double) * (kColc * ncap + 1)));  // + the slow-column flag
+    if (!s.localtheta) HCHK(cx->colc.grow(keep, sizeof(double) * (kColc * ncap + 1), cx_sync));  // + the slow-column flag
     ta.ucl = u.ucl.as<int>();
     ta.ucl_off = u.ucl_off.as<long long>();
     ta.ncells = C;
@@ -945,7 +1002,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       pu.into = &u;
       pu.into_col0 = col0;
       pu.into_c0 = c0;
-      pu.into_cap_hint = j == 0 ? 0 : (long long)((double)col0 / c0 * C * 1.1);
+      pu.into_cap_hint = c0 > 0 ? (long long)((double)col0 / c0 * C * 1.1) : 0;  // leading pieces may be empty
       const PostSpec* sp[1] = {&ps};
       UniqueSet* up[1] = {&pu};
       const hipStream_t main = cx->stream;
@@ -1396,6 +1453,7 @@ int scde_get_rand_kind(void) { return g_rand_kind; }
 int scde_version(void) { return 100; }
 
 int scde_ctx_create(int device, scde_ctx** out) {
+  FORK_GUARD();
   if (!out) return fail(SCDE_EARG, "null out");
   int n = 0;
   HCHK(hipGetDeviceCount(&n));
@@ -1415,6 +1473,7 @@ int scde_ctx_create(int device, scde_ctx** out) {
 }
 
 void scde_ctx_destroy(scde_ctx* ctx) {
+  if (fork_guard() != SCDE_OK) return;  // a forked child leaves the parent's context alone
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
@@ -1426,6 +1485,7 @@ void scde_ctx_destroy(scde_ctx* ctx) {
 }
 
 int scde_ctx_synchronize(scde_ctx* ctx) {
+  FORK_GUARD();
   if (!ctx) return fail(SCDE_EARG, "null ctx");
   HCHK(hipSetDevice(ctx->device));
   return ctx->sync();
@@ -1438,6 +1498,7 @@ int scde_ctx_set_profiling(scde_ctx* ctx, int on) {
 }
 
 int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslots) {
+  FORK_GUARD();
   if (!ctx) return fail(SCDE_EARG, "null ctx");
   RCHK(ctx->sync());
   for (int i = 0; i < nslots && i < NSLOTS; ++i) {
@@ -1448,6 +1509,7 @@ int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslo
 }
 
 int scde_ctx_reset_kernel_times(scde_ctx* ctx) {
+  FORK_GUARD();
   if (!ctx) return fail(SCDE_EARG, "null ctx");
   RCHK(ctx->sync());
   for (int i = 0; i < NSLOTS; ++i) {
@@ -1478,7 +1540,16 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
   else if (n == "lane_prio") ctx->opt_lane_prio = value != 0;
   else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
-  else if (n == "lanes") ctx->opt_lanes = value >= 2 ? 2 : 1;
+  else if (n == "lanes") {
+    ctx->opt_lanes = value >= 2 ? 2 : 1;
+    if (ctx->opt_lanes == 1 && ctx->peer) {  // one lane: the peer's workspace goes back to the device
+      FORK_GUARD();
+      HCHK(hipSetDevice(ctx->device));
+      RCHK(ctx->sync());
+      delete ctx->peer;
+      ctx->peer = nullptr;
+    }
+  }
   else return fail(SCDE_EARG, "unknown option '%s'", name);
   return SCDE_OK;
 }
@@ -1494,6 +1565,9 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "skip_redo") *value = ctx->st_skip_redo;
   else if (n == "pair_redo") *value = ctx->st_pair_redo;
   else if (n == "degen") *value = ctx->st_degen;
+  else if (n == "stream_syncs") *value = ctx->st_stream_syncs + (ctx->peer ? ctx->peer->st_stream_syncs : 0);
+  else if (n == "arena_syncs") *value = ctx->st_arena_syncs + (ctx->peer ? ctx->peer->st_arena_syncs : 0);
+  else if (n == "buf_reallocs") *value = (double)g_buf_reallocs.load();
   else if (n == "host_setup_ms") *value = ctx->st_host_ms[0];
   else if (n == "host_unique_ms") *value = ctx->st_host_ms[1];
   else if (n == "host_post_ms") *value = ctx->st_host_ms[2];
@@ -1508,6 +1582,8 @@ int scde_ctx_reset_stats(scde_ctx* ctx) {
   if (!ctx) return fail(SCDE_EARG, "null argument");
   ctx->st_skip_slabs = ctx->st_skip_kept = ctx->st_skip_stretches = ctx->st_skip_redo = ctx->st_degen = 0;
   ctx->st_pair_redo = 0;
+  ctx->st_stream_syncs = ctx->st_arena_syncs = 0;
+  if (ctx->peer) ctx->peer->st_stream_syncs = ctx->peer->st_arena_syncs = 0;
   for (double& x : ctx->st_host_ms) x = 0;
   ctx->st_boot_f64_fma = 0;
   for (double& x : ctx->st_tile_hist) x = 0;
@@ -1515,6 +1591,7 @@ int scde_ctx_reset_stats(scde_ctx* ctx) {
 }
 
 int scde_dev_alloc(scde_ctx* ctx, int64_t bytes, void** dptr) {
+  FORK_GUARD();
   if (!ctx || !dptr || bytes < 0) return fail(SCDE_EARG, "bad args");
   HCHK(hipSetDevice(ctx->device));
   HCHK(hipMalloc(dptr, std::max<int64_t>(bytes, 1)));
@@ -1523,6 +1600,7 @@ int scde_dev_alloc(scde_ctx* ctx, int64_t bytes, void** dptr) {
 }
 
 int scde_dev_free(scde_ctx* ctx, void* dptr) {
+  FORK_GUARD();
   if (!ctx) return fail(SCDE_EARG, "null ctx");
   auto it = std::find(ctx->user_allocs.begin(), ctx->user_allocs.end(), dptr);
   if (it == ctx->user_allocs.end()) return fail(SCDE_EARG, "pointer not owned by this context");
@@ -1532,6 +1610,7 @@ int scde_dev_free(scde_ctx* ctx, void* dptr) {
 }
 
 int scde_h2d(scde_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+  FORK_GUARD();
   if (!ctx) return fail(SCDE_EARG, "null ctx");
   HCHK(hipSetDevice(ctx->device));
   HCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -1539,6 +1618,7 @@ int scde_h2d(scde_ctx* ctx, void* dst, const void* src, int64_t bytes) {
 }
 
 int scde_d2h(scde_ctx* ctx, void* dst, const void* src, int64_t bytes) {
+  FORK_GUARD();
   if (!ctx) return fail(SCDE_EARG, "null ctx");
   HCHK(hipSetDevice(ctx->device));
   HCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -1626,6 +1706,7 @@ int scde_logBootPosterior(const double* models, int ncells, const int* ucl_vals,
                           const int* counti, int ngenes, const double* magnitudes, int ngrid, int nboot, int seed,
                           int return_post, int local_theta, int square_logit_conc, int ensemble, double* jp,
                           double* modes, double* post) {
+  FORK_GUARD();
   return logboot_common(false, models, ncells, ucl_vals, ucl_off, counti, ngenes, magnitudes, ngrid, nullptr,
                         nullptr, nullptr, 0, nboot, seed, return_post, local_theta, square_logit_conc, ensemble, jp,
                         modes, post);
@@ -1636,6 +1717,7 @@ int scde_logBootBatchPosterior(const double* models, int ncells, const int* ucl_
                                const int* batch_vals, const int64_t* batch_off, const int* composition, int nbatch,
                                int nboot, int seed, int return_post, int local_theta, int square_logit_conc,
                                double* jp, double* modes, double* post) {
+  FORK_GUARD();
   if (!batch_vals || !batch_off || !composition) return fail(SCDE_EARG, "null batch input");
   return logboot_common(true, models, ncells, ucl_vals, ucl_off, counti, ngenes, magnitudes, ngrid, batch_vals,
                         batch_off, composition, nbatch, nboot, seed, return_post, local_theta, square_logit_conc, 0,
@@ -1755,11 +1837,13 @@ static int jpmat_common(const double* const* mats, int nmat, const int* type_off
 }
 
 int scde_jpmatLogBoot(const double* const* mats, int nmat, int nrows, int ncols, int nboot, int seed, double* out) {
+  FORK_GUARD();
   return jpmat_common(mats, nmat, nullptr, nullptr, 0, nrows, ncols, nboot, seed, out);
 }
 
 int scde_jpmatLogBatchBoot(const double* const* mats, const int* type_off, const int* comp, int ntypes, int nrows,
                            int ncols, int nboot, int seed, double* out) {
+  FORK_GUARD();
   if (!type_off || !comp || ntypes <= 0) return fail(SCDE_EARG, "bad jpmatLogBatchBoot arguments");
   return jpmat_common(mats, type_off[ntypes], type_off, comp, ntypes, nrows, ncols, nboot, seed, out);
 }
@@ -1808,6 +1892,7 @@ static int ratio_common(const double* pmat1, const double* pmat2, int nrows, int
 }
 
 int scde_distribution_summary(const double* rpost, int nrows, int m, const double* diffv, int zi, double* res) {
+  FORK_GUARD();
   if (!rpost || !diffv || !res || nrows < 0 || m < 1 || (m % 2) == 0) return fail(SCDE_EARG, "bad summary arguments");
   if (zi < 0 || zi >= m) return fail(SCDE_EARG, "zi out of range");
   scde_ctx* cx = nullptr;
@@ -1836,12 +1921,14 @@ int scde_distribution_summary(const double* rpost, int nrows, int m, const doubl
 }
 
 int scde_matSlideMult(const double* m1, const double* m2, int nrows, int ncols, double* out) {
+  FORK_GUARD();
   if (!out) return fail(SCDE_EARG, "null out");
   return ratio_common(m1, m2, nrows, ncols, nullptr, nullptr, 0, 0, out, nullptr);
 }
 
 int scde_ratio_summary(const double* pmat1, const double* pmat2, int nrows, int n, const double* prior_y,
                        const double* diffv, int zi, double* ratio, double* res) {
+  FORK_GUARD();
   return ratio_common(pmat1, pmat2, nrows, n, prior_y, diffv, zi, 1, ratio, res);
 }
 
@@ -1896,7 +1983,12 @@ struct UploadWorker {
           for (int j = 0; j < n && rc == SCDE_OK; ++j) {
             rc = issue(j);
             std::lock_guard<std::mutex> g(q.m);
-            if (rc != SCDE_OK) q.err = rc; else ++q.issued;
+            if (rc != SCDE_OK) {
+              q.err = rc;
+              q.err_msg = g_err;  // g_err is thread-local: hand the worker's message to the caller
+            } else {
+              ++q.issued;
+            }
             q.cv.notify_all();
           }
           lk.lock();
@@ -1917,6 +2009,7 @@ struct UploadWorker {
     u.nranges = nranges;
     u.issued = 0;
     u.err = 0;
+    u.err_msg.clear();
     u.busy = true;
     ++u.job;
     u.cv.notify_all();
@@ -1926,7 +2019,7 @@ struct UploadWorker {
     auto& u = ctx->upl;
     std::unique_lock<std::mutex> lk(u.m);
     u.cv.wait(lk, [&] { return u.issued >= n || u.err != 0 || !u.busy; });
-    if (u.err) return fail(u.err, "count upload failed");
+    if (u.err) return fail(u.err, "count upload failed: %s", u.err_msg.c_str());
     return u.issued >= n ? SCDE_OK : fail(SCDE_EINTERNAL, "upload range %d never issued", n - 1);
   }
   // the job is finished (every range issued or failed) before the call returns: the next call's
@@ -1964,6 +2057,7 @@ int scde_posteriors_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ng
                         int64_t ngenes_total, int return_post, int ensemble, const int* batch_vals,
                         const int64_t* batch_off, const int* composition, int nbatch, double* jp, double* modes,
                         double* post) {
+  FORK_GUARD();
   return posteriors_run(ctx, counts_dev, ld, ngenes, cellidx, ncells_sel, models_sel, local_theta, square_logit_conc,
                         prior_x, ngrid, nboot, n_cores, gene_offset, ngenes_total, return_post, ensemble, batch_vals,
                         batch_off, composition, nbatch, jp, modes, post, nullptr);
@@ -2123,6 +2217,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
 int scde_expression_difference_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes,
                                    const scde_de_params* p, double* results, double* jp1, double* jp2,
                                    double* ratio) {
+  FORK_GUARD();
   return de_run(ctx, counts_dev, ld, ngenes, p, results, jp1, jp2, ratio, nullptr);
 }
 
@@ -2359,6 +2454,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
                                          const scde_de_params* p, const double* batch_models,
                                          const int* batch_codes, int nbatch, double* results, double* jp1,
                                          double* jp2, double* ratio, double* adj_ratio, double* batch_ratio) {
+  FORK_GUARD();
   if (!ctx || !counts_dev || !p || !p->models || !p->groups || !p->prior_x || !p->prior_y || !batch_codes ||
       !results)
     return fail(SCDE_EARG, "null argument");
@@ -2577,6 +2673,7 @@ static int stage_counts(scde_ctx*& ctx, const int* counts, int64_t ld, int ngene
 int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngenes,
                                     const scde_de_params* p, double* results, double* jp1, double* jp2,
                                     double* ratio) {
+  FORK_GUARD();
   if (!p || !p->groups) return fail(SCDE_EARG, "null argument");
   if (!ctx) RCHK(default_ctx(&ctx));
   if (!counts) return fail(SCDE_EARG, "null argument");
@@ -2618,6 +2715,7 @@ int scde_expression_difference_batch_host(scde_ctx* ctx, const int* counts, int6
                                           const scde_de_params* p, const double* batch_models,
                                           const int* batch_codes, int nbatch, double* results, double* jp1,
                                           double* jp2, double* ratio, double* adj_ratio, double* batch_ratio) {
+  FORK_GUARD();
   if (!p) return fail(SCDE_EARG, "null argument");
   const int* dev = nullptr;
   RCHK(stage_counts(ctx, counts, ld, ngenes, p->ncells, &dev));
@@ -2631,6 +2729,7 @@ int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngene
                          int64_t gene_offset, int64_t ngenes_total, int return_post, int ensemble,
                          const int* batch_vals, const int64_t* batch_off, const int* composition, int nbatch,
                          double* jp, double* modes, double* post) {
+  FORK_GUARD();
   if (!cellidx) return fail(SCDE_EARG, "null argument");
   for (int i = 0; i < ncells_sel; ++i)
     if (cellidx[i] < 0 || cellidx[i] >= ncells_total) return fail(SCDE_EARG, "cell index %d out of range", cellidx[i]);
@@ -2703,6 +2802,7 @@ int scde_pagoda_varnorm_weights_dev(scde_ctx* ctx, const int* counts_dev, int64_
                                     const double* prior_x, int ngrid, int nboot, int n_cores, const int* batch_codes,
                                     int nbatch, int use_expected_value, double* modes, double* matw,
                                     double* bmatw) {
+  FORK_GUARD();
   if (!ctx || !counts_dev || !models || !prior_x || !modes || !matw) return fail(SCDE_EARG, "null argument");
   if (ngenes < 0 || ncells <= 0 || ngrid <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
   const bool batch = batch_codes && nbatch > 1;
@@ -2769,6 +2869,7 @@ int scde_pagoda_varnorm_weights_host(scde_ctx* ctx, const int* counts, int64_t l
                                      const double* prior_x, int ngrid, int nboot, int n_cores,
                                      const int* batch_codes, int nbatch, int use_expected_value, double* modes,
                                      double* matw, double* bmatw) {
+  FORK_GUARD();
   const int* dev = nullptr;
   RCHK(stage_counts(ctx, counts, ld, ngenes, ncells, &dev));
   return scde_pagoda_varnorm_weights_dev(ctx, dev, ngenes, ngenes, ncells, models, local_theta, square_logit_conc,
@@ -2782,6 +2883,7 @@ int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, 
                               const double* models, int square_logit_conc, int length_out, double pseudo_count,
                               double bw, double max_quantile, const double* max_value, double* x, double* y,
                               double* lp, double* grid_weight, double* max_value_out) {
+  FORK_GUARD();
   if (!ctx || !counts_dev || !models || !x || !y) return fail(SCDE_EARG, "null argument");
   if (ngenes <= 0 || ncells <= 0 || ld < ngenes) return fail(SCDE_EARG, "bad dimensions");
   // density grid n <= 4096: k_prior_conv stages y and the 2n kernel values in LDS (96 KiB of 160)
@@ -2868,6 +2970,7 @@ int scde_expression_prior_dev(scde_ctx* ctx, const int* counts_dev, int64_t ld, 
 }
 
 int scde_bh_cz_dev(scde_ctx* ctx, const double* z_dev, int64_t n, double* cz_dev) {
+  FORK_GUARD();
   if (!ctx || n < 0 || (n > 0 && (!z_dev || !cz_dev))) return fail(SCDE_EARG, "bad arguments");
   if (n > 0x7fffffff) return fail(SCDE_EARG, "n too large");
   if (n == 0) return SCDE_OK;
@@ -3075,6 +3178,7 @@ int scde_bwpca_batch_dev(scde_ctx* ctx, const double* M_dev, const double* W_dev
                          const int* perms, int64_t nperms, const int64_t* start_off, const double* starts,
                          int64_t nstart_vals, int smooth, double em_tol, int em_maxiter, double* rotation,
                          double* scores, double* scoreweights, double* colmeans, double* stats, int* iterations) {
+  FORK_GUARD();
   if (!ctx || !M_dev || !W_dev) return fail(SCDE_EARG, "null argument");
   if (nprob < 0 || ncells <= 0 || ld < ncells || mcols <= 0) return fail(SCDE_EARG, "bad dimensions");
   if (nprob == 0) return SCDE_OK;
@@ -3274,6 +3378,7 @@ int scde_baileyWPCA(const double* mat, const double* matw, int n, int d, int npc
                     double em_tol, int em_maxiter, const double* starts, int nshuffles, const int* perms,
                     double* rotation, double* scores, double* scoreweights, double* var, double* totvar,
                     double* randvar) {
+  FORK_GUARD();
   if (!mat || !matw || !starts || !rotation || !scores || !var || !totvar) return fail(SCDE_EARG, "null argument");
   if (n <= 0 || d <= 0) return fail(SCDE_EARG, "bad dimensions");
   if (nshuffles < 0 || (nshuffles > 0 && (!perms || !randvar))) return fail(SCDE_EARG, "bad shuffles");
@@ -3313,6 +3418,7 @@ int scde_baileyWPCA(const double* mat, const double* matw, int n, int d, int npc
 // ------------------------------------------------------------------ PAGODA helpers
 // .Call("winsorizeMatrix", Mat, Trim) (src/pagoda.cpp:6-31; pagoda.h:5).  mat: nrow x ncol.
 int scde_winsorizeMatrix(const double* mat, int nrow, int ncol, double trim, double* out) {
+  FORK_GUARD();
   if (!mat || !out) return fail(SCDE_EARG, "null argument");
   if (nrow < 0 || ncol < 0) return fail(SCDE_EARG, "bad dimensions");
   const size_t nel = (size_t)nrow * ncol;
@@ -3339,6 +3445,7 @@ int scde_winsorizeMatrix(const double* mat, int nrow, int ncol, double trim, dou
 // .Call("matWCorr", Mat, Matw) (src/pagoda.cpp:41-65; pagoda.h:6).  mat, matw: nrow x ncol;
 // out: ncol x ncol (identity diagonal, c(j, i) for j > i, upper triangle 0).
 int scde_matWCorr(const double* mat, const double* matw, int nrow, int ncol, double* out) {
+  FORK_GUARD();
   if (!mat || !matw || !out) return fail(SCDE_EARG, "null argument");
   if (nrow < 0 || ncol < 0) return fail(SCDE_EARG, "bad dimensions");
   if (ncol == 0) return SCDE_OK;
@@ -3358,6 +3465,7 @@ int scde_matWCorr(const double* mat, const double* matw, int nrow, int ncol, dou
 // .Call("matCorr", X, Y) = arma::cor(x, y) (src/pagoda.cpp:33-38; pagoda.h:8).  x: nrow x nx,
 // y: nrow x ny; out: nx x ny.
 int scde_matCorr(const double* x, int nrow, int nx, const double* y, int ny, double* out) {
+  FORK_GUARD();
   if (!x || !y || !out) return fail(SCDE_EARG, "null argument");
   if (nrow < 0 || nx < 0 || ny < 0) return fail(SCDE_EARG, "bad dimensions");
   if ((size_t)nx * ny == 0) return SCDE_OK;
@@ -3378,6 +3486,7 @@ int scde_matCorr(const double* x, int nrow, int nx, const double* y, int ny, dou
 // gene indices idx[off[p] .. off[p+1]) (increasing), values val[...].  r: np x np
 // correlations over the shared genes (1 on the diagonal); n: np x np union sizes (0 on it).
 int scde_plSemicompleteCor2(int np, const int64_t* off, const int* idx, const double* val, double* r, int* n) {
+  FORK_GUARD();
   if (np < 0 || (np > 0 && (!off || !r || !n))) return fail(SCDE_EARG, "null argument");
   if (np == 0) return SCDE_OK;
   const int64_t tot = off[np];

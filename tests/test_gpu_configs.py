@@ -14,7 +14,7 @@ The oracle is the C restatement (oracle/scde_oracle.c, oracle/bwpca_oracle.c).
 import numpy as np
 import pytest
 
-from conftest import assert_posterior_close, assert_z_close
+from conftest import assert_cz_close, assert_posterior_close, assert_z_close
 
 pytestmark = pytest.mark.gpu
 
@@ -58,7 +58,9 @@ def test_config3_slice_full_bootstrap(api, oracle, ncores):
         for i in range(2):
             assert_posterior_close(got["joint.posteriors"][i], ref["joint.posteriors"][i], what=f"jp{i}")
         assert_posterior_close(got["difference.posterior"].values, ref["difference.posterior"], what="ratio")
-        assert_z_close(got["results"]["cZ"].to_numpy(), ref["results"]["cZ"], what="cZ")
+        assert_z_close(got["results"]["Z"].to_numpy(), ref["results"]["Z"])
+        assert_cz_close(got["results"]["cZ"].to_numpy(), ref["results"]["cZ"], got["results"]["Z"].to_numpy(),
+                        ref["results"]["Z"])
 
 
 def test_config4_slice_modes_full_bootstrap(api, oracle):

@@ -17,7 +17,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import assert_posterior_close, assert_z_close
+from conftest import assert_cz_close, assert_posterior_close, assert_z_close
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -59,7 +59,7 @@ def test_config3_whole_table_vs_oracle(api, oracle):
     for j, k in enumerate(("lb", "mle", "ub", "ce")):
         np.testing.assert_array_equal(res[k].to_numpy(), want[:, j], err_msg=k)
     assert_z_close(res["Z"].to_numpy(), want[:, 4], what="Z")
-    assert_z_close(res["cZ"].to_numpy(), want[:, 5], what="cZ")
+    assert_cz_close(res["cZ"].to_numpy(), want[:, 5], res["Z"].to_numpy(), want[:, 4], what="cZ")
     # posteriors of a window across the first chunk boundary (two draw lists), live oracle
     lo, hi = 1226, 1274
     ref = oracle.scde_expression_difference(models, np.ascontiguousarray(counts[lo:hi]), prior["x"], prior["y"],
@@ -133,4 +133,4 @@ def test_config2b_slice_b100(api, oracle):
         for k in ("lb", "mle", "ub", "ce"):
             np.testing.assert_array_equal(got[k].to_numpy(), want[k], err_msg=f"{table}.{k}")
         assert_z_close(got["Z"].to_numpy(), want["Z"], what=f"{table}.Z")
-        assert_z_close(got["cZ"].to_numpy(), want["cZ"], what=f"{table}.cZ")
+        assert_cz_close(got["cZ"].to_numpy(), want["cZ"], got["Z"].to_numpy(), want["Z"], what=f"{table}.cZ")

@@ -13,7 +13,7 @@ k_boot_tiles from 200 cells), and k_boot_tiles at every size (boot_tiles_cells 0
 import numpy as np
 import pytest
 
-from conftest import assert_posterior_close, assert_z_close, golden
+from conftest import assert_cz_close, assert_posterior_close, assert_z_close, golden
 
 pytestmark = pytest.mark.gpu
 
@@ -73,4 +73,4 @@ def test_expression_difference_fuzz(seed, opts):
     for k in ("lb", "mle", "ub", "ce"):
         np.testing.assert_array_equal(res[k].to_numpy(), ref["results"][k], err_msg=f"{k} {kw}")
     assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"])
-    assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what="cZ")
+    assert_cz_close(res["cZ"].to_numpy(), ref["results"]["cZ"], res["Z"].to_numpy(), ref["results"]["Z"])

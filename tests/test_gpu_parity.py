@@ -5,7 +5,7 @@ grid-valued outputs (lb/mle/ub/ce, modes) exact; matSlideMult bit-exact."""
 import numpy as np
 import pytest
 
-from conftest import assert_posterior_close, assert_z_close, golden
+from conftest import assert_cz_close, assert_posterior_close, assert_z_close, golden
 
 pytestmark = pytest.mark.gpu
 
@@ -184,7 +184,7 @@ def test_expression_difference_golden(api):
     for k in ("lb", "mle", "ub", "ce"):
         np.testing.assert_array_equal(res[k].to_numpy(), g[k], err_msg=k)
     assert_z_close(res["Z"].to_numpy(), g["Z"])
-    assert_z_close(res["cZ"].to_numpy(), g["cZ"], what="cZ")
+    assert_cz_close(res["cZ"].to_numpy(), g["cZ"], res["Z"].to_numpy(), g["Z"])
 
 
 def test_vignette_table_on_gpu(api):
@@ -316,7 +316,7 @@ def test_batch_corrected_difference(api, oracle, ncores, nlev):
         for k in ("lb", "mle", "ub", "ce"):
             np.testing.assert_array_equal(got[k].to_numpy(), want[k], err_msg=f"{table}.{k}")
         assert_z_close(got["Z"].to_numpy(), want["Z"], what=f"{table}.Z")
-        assert_z_close(got["cZ"].to_numpy(), want["cZ"], what=f"{table}.cZ")
+        assert_cz_close(got["cZ"].to_numpy(), want["cZ"], got["Z"].to_numpy(), want["Z"], what=f"{table}.cZ")
     # the four posteriors on two lanes (default) or one after the other: the same bits
     ctx = api.default_context()
     try:
@@ -426,7 +426,7 @@ def test_expression_difference_config3_shape(api, oracle):
     for k in ("lb", "mle", "ub", "ce"):
         np.testing.assert_array_equal(res[k].to_numpy(), ref["results"][k], err_msg=k)
     assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"])
-    assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what="cZ")
+    assert_cz_close(res["cZ"].to_numpy(), ref["results"]["cZ"], res["Z"].to_numpy(), ref["results"]["Z"])
 
 
 def test_posteriors_modes_config4_shape(api, oracle):
@@ -464,4 +464,4 @@ def test_expression_difference_grid_sizes(api, oracle, length_out):
     for k in ("lb", "mle", "ub", "ce"):
         np.testing.assert_array_equal(res[k].to_numpy(), ref["results"][k], err_msg=k)
     assert_z_close(res["Z"].to_numpy(), ref["results"]["Z"])
-    assert_z_close(res["cZ"].to_numpy(), ref["results"]["cZ"], what="cZ")
+    assert_cz_close(res["cZ"].to_numpy(), ref["results"]["cZ"], res["Z"].to_numpy(), ref["results"]["Z"])
