@@ -259,7 +259,7 @@ struct scde_ctx {
   // host-count entry points: the call's counts staged here (grow-only, reused across calls)
   Buf counts_in;
   // fixed-point bootstrap: byte multiplicities, flags/counters
-  Buf w8, w8t, qflags;
+  Buf w8, w8t, w8g, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
   Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
@@ -278,6 +278,10 @@ struct scde_ctx {
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
   int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
+  int opt_gene_blocks = 1;       // "gene_blocks": k_boot_gene (a 4-wave block per gene's slab group, rows shared
+                                 // by its slabs) instead of one k_boot_tiles wave per slab; not with pair mode
+  int opt_gene_rows = 4;         // "gene_rows": rows per slab k_boot_gene gives each slab at most (tests force its
+                                 // four-tile list pass with fewer)
   int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
                                  // tiles each; the posterior narrows with the cells, most slabs need two)
   double opt_pipeline_mb = 32;  // "pipeline_mb": host-count DE calls from this many MB of counts upload in two
@@ -460,7 +464,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide};
+                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (auto& u : upc) u.release();
@@ -1057,7 +1061,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     if (v >= 4 && v <= 32 && v % 4 == 0) nb = v;
   }
   const int Bp = (int)round_up(std::max(s.nboot, 1), nb);
-  const int Bt = (int)round_up(Bp, 32) + 32;  // byte multiplicity rows: the last slab reads 32 boots
+  const int Bt = (int)round_up(Bp, 32) + 128;  // byte multiplicity rows: the last gene group reads 128 boots
   auto rest_fn = [=, &s, &u]() mutable -> int {
   // ---- individual posterior modes (src/jpmatLogBoot.cpp:277-296): argmax of each cell's table
   // column, known as soon as the tables are; computed here so the caller's read-back of the
@@ -1136,6 +1140,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), N, cx->gkey2.as<unsigned>(),
                              cx->gorder.as<int>(), cx->gwork.p, &wb, sa));
     }
+    // k_boot_gene (not with pair mode): groups of gene_sg slabs per 4-wave block
+    const int gene_sg = (tpath && cx->opt_gene_blocks && !(C >= cx->opt_pair_cells && (s.nboot + nb - 1) / nb >= 2))
+                            ? std::min({(s.nboot + nb - 1) / nb, 8, 128 / nb})
+                            : 0;
     if (tpath) {
       // byte multiplicities [set][cell][boot] (baseline bound sums and the tile bounds)
       // and, for the tile bounds' A fragments, per slab the pairs (boot r, boot 16 + r) of its nb
@@ -1156,6 +1164,25 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         }
       RCHK(upload_on(cx, cx->w8, w8.data(), w8.size(), sa));
       RCHK(upload_on(cx, cx->w8t, w8p.data(), w8p.size(), sa));
+      if (gene_sg > 0) {  // k_boot_gene: per (cell, group of gene_sg slabs) four 32-boot windows as pair slots
+        const int NGR = (P + gene_sg - 1) / gene_sg;
+        std::vector<unsigned char> w8g((size_t)nsets * C * NGR * 128, 0);
+        for (int set = 0; set < nsets; ++set)
+          for (int c = 0; c < C; ++c) {
+            const double* wr = W.data() + ((size_t)set * C + c) * Bp;
+            for (int gr = 0; gr < NGR; ++gr) {
+              const int gb0 = gr * gene_sg * nb, gnb = std::min(gene_sg, P - gr * gene_sg) * nb;
+              for (int j = 0; j < gnb && j < 128; ++j) {
+                const int b = gb0 + j;
+                if (b >= Bp) break;
+                const int w = j >> 5, jj = j & 31;
+                const size_t slot = (jj < 16) ? 2 * jj : 2 * (jj - 16) + 1;
+                w8g[(((size_t)set * C + c) * NGR + gr) * 128 + 32 * w + slot] = (unsigned char)wr[b];
+              }
+            }
+          }
+        RCHK(upload_on(cx, cx->w8g, w8g.data(), w8g.size(), sa));
+      }
       HCHK(cx->zubound.ensure(sizeof(int) * (size_t)nsets * 4 * kQTiles * Bt));
       HCHK(launch_zuq(cx->ubound.as<unsigned>(), cx->base_col.as<int>(), C, cx->w8.as<unsigned char>(), Bt, nsets,
                       cx->zubound.as<int>(), sa));
@@ -1238,6 +1265,14 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         if (tb.pairs) {
           HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * N)));
           tb.wide = cx->pwide.as<int>();
+        }
+        if (gene_sg > 0) {
+          HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * N)));
+          tb.wide = cx->pwide.as<int>();
+          tb.gene = 1;
+          tb.SG = gene_sg;
+          tb.kcap = cx->opt_gene_rows;
+          tb.W8g = cx->w8g.as<unsigned char>();
         }
         if (have_order) tb.order = cx->gorder.as<int>();
         HCHK(launch_boot_tiles(b2, tb, st));
@@ -1535,6 +1570,8 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "tile_max_mult") ctx->opt_tile_max_mult = (int)value;
   else if (n == "tile_order") ctx->opt_tile_order = value != 0;
   else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
+  else if (n == "gene_blocks") ctx->opt_gene_blocks = value != 0;
+  else if (n == "gene_rows") ctx->opt_gene_rows = std::max(1, std::min(4, (int)value));
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
@@ -2185,6 +2222,8 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_tile_order = cx->opt_tile_order;
   p->opt_unique_fixed = cx->opt_unique_fixed;
   p->opt_pair_cells = cx->opt_pair_cells;
+  p->opt_gene_blocks = cx->opt_gene_blocks;
+  p->opt_gene_rows = cx->opt_gene_rows;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;

@@ -38,7 +38,7 @@ namespace scde {
 // k_col_consts record per column: [n or -1, n - x, stirlerr sum, 0.5 lf, log(size/(size+x)),
 // log X - log n, log(n - X) - log n, dpois_log(x, failure rate), log po, log(1 - po)] with
 // po = size / (size + x) (the count's own grid point), padded to 10 doubles
-constexpr int kColc = 10;
+constexpr int kColc = 11;
 // columns per task of the cell-staged tables kernels (k_tables_reg stages a task's column
 // constants in LDS: tasks must not exceed this)
 #ifndef SCDE_TAB_TASK_COLS
@@ -176,6 +176,12 @@ struct TileBootArgs {
   int pairs = 0;             // a wave per two slabs of a gene, two bound tiles each (wide cells: most slabs
                              // need two); slabs needing more take a four-tile pass over `wide`
   int* wide = nullptr;       // [1 + ngenes * P] pair mode's list: [0] length, then g * P + p
+  int gene = 0;              // k_boot_gene: a 4-wave block per (gene, group of SG slabs), 16 rows shared
+                             // by the group's slabs (not with pairs); failures take the list pass over `wide`
+  int SG = 0;                // slabs per group (<= 8, SG x nb <= 128)
+  int kcap = 4;              // rows per slab at most (tests force the list pass with fewer)
+  const unsigned char* W8g = nullptr;  // [nsets][ncells][groups][4 windows][32] the group's boots 32 w + j
+                                       // as pair slots (boot 32 w + j, 32 w + 16 + j), 0 past its boots
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending

@@ -186,8 +186,16 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
   const double size = theta[(long long)lo * GS], po = size / (size + x);
   o[8] = log(po);
   o[9] = log(1 - po);
+  // the closed form's column constant (k_tables_reg, SCDE_NB_CLOSED): dnbinom(x; size, p) =
+  // log(size / (size + x)) + dbinom_raw(size, n, p, q) and, as bd0(y, n r) = y log(y / n) - y log r
+  // + n r - y with p + q = 1, dbinom_raw = S - lf / 2 - size log(size / n) - nx log(nx / n)
+  // + size log p + nx log q: everything but the last two terms is this constant
+  o[10] = f.ok ? ((f.lp + f.S) - f.hlf) - f.X * f.lXn - f.nx * f.lnxn : 0.0;
 }
 
+#ifndef SCDE_NB_CLOSED
+#define SCDE_NB_CLOSED 1  // k_tables_reg: the NB log-pmf in closed form (0: nmath's saddle-point form)
+#endif
 #ifndef SCDE_KT_DIAG
 #define SCDE_KT_DIAG 0  // timing-only builds: 1 trivial dnbinom, 2 no exp, 4 no log, 8 no stores, 16 loop 1
                         // only, 32 staging and constants only, 64 no tile bounds
@@ -722,11 +730,22 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       KT_EVENT(8, in && fabs(nf.X - np) < 0.1 * (nf.X + np));
       KT_EVENT(9, in && nf.X != nf.n && fabs(nf.nx - nq) < 0.1 * (nf.nx + nq));
       KT_EVENT(13, in);
-      double nb = (SCDE_KT_DIAG & 1) ? lpr * x + lqr : dnbinom_fast(nf, pr, qr, lpr, lqr);
-      badm |= bad ? (1u << j) : 0u;
+      double nb;
+      if (SCDE_NB_CLOSED) {
+        // log dnbinom(x; size, p_k) = C + size log p_k + x log q_k (C: the column constant;
+        // count 0: size log p_k, as the x == n branch of dbinom_raw).  p_k, q_k are the same
+        // rounded values the saddle-point form takes, log p_k and log q_k the staged logs;
+        // q_k = 0 (grid point 0) gives -inf for x > 0 and 0 for x = 0, as dbinom_raw.  Against
+        // the saddle-point form the difference is below 2e-11 absolute at counts of 5,000 and
+        // means of 10^5 (log space), far under the 1e-6 parity bar.
+        nb = (x == 0.0) ? nf.X * lpr : fma(x, lqr, fma(nf.X, lpr, cc[10]));
+      } else {
+        nb = (SCDE_KT_DIAG & 1) ? lpr * x + lqr : dnbinom_fast(nf, pr, qr, lpr, lqr);
+        badm |= bad ? (1u << j) : 0u;
+      }
       nb += sl[kRowLcfpr * kRS + 64 * j];
       v[j] = in ? nb : -INFINITY;
-      lmax = gt_max(lmax, bad ? -INFINITY : v[j]);
+      lmax = gt_max(lmax, (!SCDE_NB_CLOSED && bad) ? -INFINITY : v[j]);
     }
   }
   if (__builtin_amdgcn_ballot_w64(badm != 0)) {
@@ -2001,6 +2020,180 @@ __device__ __forceinline__ void fmac_entry2(double (&a0)[NB], double (&a1)[NB], 
 // WB waves per block (4; one item each).  Measured and not kept: a gene's 5 slabs as the 5
 // waves of one block (the slabs' column loads did not meet in L1: the same L1 -> L2 request
 // count, boot 12.5 -> 14.6 ms at config 4).
+// One bound pass (step 1 of k_boot_tiles / k_boot_gene): UB_bt = ZU_bt + sum_e W_be UQ_et for the
+// 32 boot slots of one pair-interleaved multiplicity block (boots j and 16 + j in the bytes of pair
+// slot j) and every 32-point bound tile t < NTB, exact integers on the int8 matrix cores (C layout
+// of the 16x16x64 MFMA: bound tile r, boots 16 bt + 4 h + q), written rounded up to f32 as
+// ub[t * ustride + b] for b < nbout.  W8: cell 0's block (cell c at W8 + c * cstride); ZU: the
+// baseline digit sums of boot slot 0 (digit l, tile t at ZU + (l * kQTiles + t) * Bq); stage: the
+// wave's 1536-word LDS area.  Per 64-entry chunk each lane loads one entry's data with wide loads
+// -- its (cell, column), the column's 16 tile bounds (64 B) and the cell's 16 multiplicity pairs
+// (32 B) -- and writes them transposed into the staging area; the MFMA fragments are then
+// contiguous LDS reads: 7 vector-memory instructions per chunk instead of 40 single-entry gathers.
+__device__ __forceinline__ void tile_bound_pass(const int2* __restrict__ E, int n, const unsigned* __restrict__ UQ,
+                                                const unsigned char* __restrict__ W8, unsigned cstride,
+                                                const int* __restrict__ ZU, int Bq, unsigned* stage, float* ub,
+                                                int ustride, int nbout, int NTB, int lane) {
+  const int r = lane & 15, h = lane >> 4;
+  unsigned* sq = stage;         // [tile t][entry l] tile bounds (64 x 16 words)
+  unsigned* sw = stage + 1024;  // [pair r][entry l / 2] multiplicity pairs (two entries a word)
+  const int KP = (n + 63) & ~63;
+  const int t = r;
+  i32x4 acc[2][4];
+#pragma unroll
+  for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+      acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + 16 * bt + 4 * h);
+  for (int e0 = 0; e0 < KP; e0 += 64) {
+    const int2 en = E[e0 + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
+    const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
+    const uint4 q0 = uq[0], q1 = uq[1], q2 = uq[2], q3 = uq[3];
+    const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * cstride));
+    const uint4 w0 = wp[0], w1 = wp[1];
+    wave_sync();  // the previous chunk's fragment reads are done before the area is rewritten
+    const unsigned qv[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                             q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) sq[tt * 64 + lane] = qv[tt];
+    // pairs (boot j, boot 16 + j) as 16-bit words: two entries per 32-bit LDS word
+    const unsigned wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    unsigned short* sw16 = reinterpret_cast<unsigned short*>(sw);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sw16[(2 * j) * 64 + lane] = (unsigned short)(wv[j] & 0xffffu);
+      sw16[(2 * j + 1) * 64 + lane] = (unsigned short)(wv[j] >> 16);
+    }
+    wave_sync();
+    // B fragment: tile t's words of entries 16 h .. 16 h + 15
+    const uint4* bq = reinterpret_cast<const uint4*>(sq + t * 64 + 16 * h);
+    const uint4 b0v = bq[0], b1v = bq[1], b2v = bq[2], b3v = bq[3];
+    const unsigned u[16] = {b0v.x, b0v.y, b0v.z, b0v.w, b1v.x, b1v.y, b1v.z, b1v.w,
+                            b2v.x, b2v.y, b2v.z, b2v.w, b3v.x, b3v.y, b3v.z, b3v.w};
+    // A fragments: pair r of entries 16 h .. 16 h + 15 (two entries a word)
+    const uint4* aw = reinterpret_cast<const uint4*>(sw + r * 32 + 8 * h);
+    const uint4 a0v = aw[0], a1v = aw[1];
+    const unsigned x2[8] = {a0v.x, a0v.y, a0v.z, a0v.w, a1v.x, a1v.y, a1v.z, a1v.w};
+    i32x4 af[2];
+    unsigned lo4[4], hi4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      lo4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x06040200u);
+      hi4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x07050301u);
+    }
+    af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
+    af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
+    unsigned pl[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
+      acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
+      acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
+    }
+  }
+  if (t < NTB)
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b = 16 * bt + 4 * h + q;
+        if (b < nbout) {
+          const long long v =
+              (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
+          const double x = (double)v * 0x1p-8;
+          float f = (float)x;
+          if ((double)f < x) f = nextafterf(f, INFINITY);
+          ub[t * ustride + b] = f;
+        }
+      }
+}
+
+// The rows of k_boot_tiles / k_boot_gene: a0/a1[i] = Z_b + sum_e W_be D_e at points k0, k0 + 1 of
+// boot b = b0 + i (k0 even: 16-byte aligned pairs; -inf where the point is dead).  Per ELL entry
+// one 16-byte column load (both points) and one 16-byte multiplicity load (boots 2J, 2J + 1 on
+// lane J of each 16-lane row), then 2 NB v_fmac_f64_dpp row_newbcast:J; loads are issued from
+// inline asm in saddr form one batch (2 entries) ahead and waited with an explicit vmcnt, over
+// two register buffers.  Each 16-lane row may belong to another slab (b0) and tile (k0).
+template <int NB>
+__device__ __forceinline__ void tile_rows(double (&a0)[NB], double (&a1)[NB], const double* __restrict__ D,
+                                          const int2* __restrict__ E, int n, const double* __restrict__ W,
+                                          const double* __restrict__ Zs, int GS, int Bp, int b0, int k0, int r,
+                                          bool live, bool l0, bool l1) {
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const d2_t z = live ? *reinterpret_cast<const d2_t*>(Zs + (long long)(b0 + i) * GS + k0) : d2_t{0.0, 0.0};
+    a0[i] = l0 ? z.x : -INFINITY;
+    a1[i] = l1 ? z.y : -INFINITY;
+  }
+  {
+    constexpr int EB2 = 2;  // entries per batch: 2 x (column pair + multiplicity pair) loads
+    const unsigned doff = (unsigned)k0 * 8u;
+    const unsigned woff = (unsigned)(b0 + 2 * min(r, NB / 2 - 1)) * 8u;
+    d2_t v[EB2], vb[EB2], w[EB2], wb[EB2];
+    auto fetch = [&](int e0, int4& t) { t = *reinterpret_cast<const int4*>(E + e0); };
+    const int col0 = __builtin_amdgcn_readfirstlane(E[0].y);  // timing build 8: every load from this column
+    (void)col0;
+    auto issue = [&](int4 t, d2_t (&x)[EB2], d2_t (&wv)[EB2]) {
+      asm volatile("" : "+s"(t.x), "+s"(t.y), "+s"(t.z), "+s"(t.w));
+      // 32-bit offsets: (ncols + 1) x GS and ncells x Bp are < 2^31 (checked by the launcher)
+      const double* d0 = D + (unsigned)(((SCDE_TILE_DIAG & 8) ? col0 : t.y) * GS);
+      const double* d1 = D + (unsigned)(((SCDE_TILE_DIAG & 8) ? col0 : t.w) * GS);
+      const double* w0 = W + (unsigned)(t.x * Bp);
+      const double* w1 = W + (unsigned)(t.z * Bp);
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[0]) : "v"(doff), "s"(d0));
+      if (!(SCDE_TILE_DIAG & 4)) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[0]) : "v"(woff), "s"(w0));
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[1]) : "v"(doff), "s"(d1));
+      if (!(SCDE_TILE_DIAG & 4)) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[1]) : "v"(woff), "s"(w1));
+    };
+    auto ready = [&](d2_t (&x)[EB2], d2_t (&wv)[EB2]) {  // all but the next batch's loads have landed
+      if (SCDE_TILE_DIAG & 4)  // timing build: multiplicities loaded once (results wrong)
+        asm volatile("s_waitcnt vmcnt(2)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
+      else
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
+    };
+    auto accumulate = [&](const d2_t (&x)[EB2], const d2_t (&wv)[EB2]) {
+#pragma unroll
+      for (int j = 0; j < EB2; ++j)
+        fmac_entry2<NB>(a0, a1, wv[j], x[j], std::make_integer_sequence<int, NB / 2>{});
+    };
+#pragma unroll
+    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(a0[i]), "+v"(a1[i]));
+    // rows are padded to a multiple of 64 entries plus 8 zero-column entries: every fetch and
+    // look-ahead batch stays inside the row
+    int4 ta, tb;
+    fetch(0, ta);
+    if (SCDE_TILE_DIAG & 4) {  // timing build: the first entry's multiplicities for every entry
+      const double* w0 = W + (unsigned)(ta.x * Bp);
+      w[0] = w[1] = wb[0] = wb[1] = *reinterpret_cast<const d2_t*>(w0 + woff / 8);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(wb[0]), "+v"(wb[1]));
+    }
+    issue(ta, v, w);
+    fetch(EB2, tb);
+    const int n2 = (n + EB2 - 1) & ~(EB2 - 1);
+    int e0 = 0;
+    for (; e0 + 2 * EB2 <= n2; e0 += 2 * EB2) {
+      issue(tb, vb, wb);
+      fetch(e0 + 2 * EB2, ta);
+      ready(v, w);
+      accumulate(v, w);
+      issue(ta, v, w);
+      fetch(e0 + 3 * EB2, tb);
+      ready(vb, wb);
+      accumulate(vb, wb);
+    }
+    if (e0 < n2) {
+      issue(tb, vb, wb);
+      ready(v, w);
+      accumulate(v, w);
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(wb[0]), "+v"(wb[1]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(w[0]), "+v"(w[1]));
+  }
+}
+
 template <int NB, int WB>
 __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_tiles(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
@@ -2069,7 +2262,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   }
   const int n = nnz[g];
   const int NT = (G + 15) >> 4, NTB = (G + 31) >> 5;  // 16-point sum tiles, 32-point bound tiles
-  const int r = lane & 15, h = lane >> 4;
+  const int r = lane & 15;
   const int2* __restrict__ E = ent + (long long)g * ent_stride;
   const int set = wset ? wset[g] : 0;
   // ---- 1. bound tiles (C layout of the 16x16x64 MFMA: bound tile r, boots 16 bt + 4 h + q).  Per
@@ -2087,81 +2280,8 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     }
     const unsigned pstride = 32u * (unsigned)P;
     const unsigned char* __restrict__ W8 = W8p + (long long)set * ncells * pstride + 32 * p;
-    const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq;
-    unsigned* sq = &bstage[wsid][0];      // [tile t][entry l] tile bounds (64 x 16 words)
-    unsigned* sw = &bstage[wsid][1024];   // [pair r][entry l / 2] multiplicity pairs (two entries a word)
-    const int KP = (n + 63) & ~63;
-    const int t = r;
-    i32x4 acc[2][4];
-#pragma unroll
-    for (int bt = 0; bt < 2; ++bt)
-#pragma unroll
-      for (int l = 0; l < 4; ++l)
-        acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + b0 + 16 * bt + 4 * h);
-    for (int e0 = 0; e0 < KP; e0 += 64) {
-      const int2 en = E[e0 + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
-      const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
-      const uint4 q0 = uq[0], q1 = uq[1], q2 = uq[2], q3 = uq[3];
-      const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * pstride));
-      const uint4 w0 = wp[0], w1 = wp[1];
-      wave_sync();  // the previous chunk's fragment reads are done before the area is rewritten
-      const unsigned qv[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
-                               q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
-#pragma unroll
-      for (int tt = 0; tt < 16; ++tt) sq[tt * 64 + lane] = qv[tt];
-      // pairs (boot j, boot 16 + j) as 16-bit words: two entries per 32-bit LDS word
-      const unsigned wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-      unsigned short* sw16 = reinterpret_cast<unsigned short*>(sw);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        sw16[(2 * j) * 64 + lane] = (unsigned short)(wv[j] & 0xffffu);
-        sw16[(2 * j + 1) * 64 + lane] = (unsigned short)(wv[j] >> 16);
-      }
-      wave_sync();
-      // B fragment: tile t's words of entries 16 h .. 16 h + 15
-      const uint4* bq = reinterpret_cast<const uint4*>(sq + t * 64 + 16 * h);
-      const uint4 b0v = bq[0], b1v = bq[1], b2v = bq[2], b3v = bq[3];
-      const unsigned u[16] = {b0v.x, b0v.y, b0v.z, b0v.w, b1v.x, b1v.y, b1v.z, b1v.w,
-                              b2v.x, b2v.y, b2v.z, b2v.w, b3v.x, b3v.y, b3v.z, b3v.w};
-      // A fragments: pair r of entries 16 h .. 16 h + 15 (two entries a word)
-      const uint4* aw = reinterpret_cast<const uint4*>(sw + r * 32 + 8 * h);
-      const uint4 a0v = aw[0], a1v = aw[1];
-      const unsigned x2[8] = {a0v.x, a0v.y, a0v.z, a0v.w, a1v.x, a1v.y, a1v.z, a1v.w};
-      i32x4 af[2];
-      unsigned lo4[4], hi4[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        lo4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x06040200u);
-        hi4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x07050301u);
-      }
-      af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
-      af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
-      unsigned pl[4][4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
-#pragma unroll
-      for (int l = 0; l < 4; ++l) {
-        const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
-        acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
-        acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
-      }
-    }
-    if (t < NTB)
-#pragma unroll
-      for (int bt = 0; bt < 2; ++bt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int b = 16 * bt + 4 * h + q;
-          if (b < NB) {
-            const long long v =
-                (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
-            const double x = (double)v * 0x1p-8;
-            float f = (float)x;
-            if ((double)f < x) f = nextafterf(f, INFINITY);
-            ub[t * NB + b] = f;
-          }
-        }
+    const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq + b0;
+    tile_bound_pass(E, n, UQ, W8, pstride, ZU, Bq, &bstage[wsid][0], ub, NB, NB, NTB, lane);
   }
 #if SCDE_TILE_DIAG & 1
   return;  // timing build: bounds only
@@ -2233,76 +2353,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
   // ---- rows: Z_b + sum_e W_be D_e at points k0, k0 + 1 (k0 even: 16-byte aligned pairs)
   double a0[NB], a1[NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const d2_t z = live ? *reinterpret_cast<const d2_t*>(Zs + (long long)(b0 + i) * GS + k0) : d2_t{0.0, 0.0};
-    a0[i] = l0 ? z.x : -INFINITY;
-    a1[i] = l1 ? z.y : -INFINITY;
-  }
-  {
-    constexpr int EB2 = 2;  // entries per batch: 2 x (column pair + multiplicity pair) loads
-    const unsigned doff = (unsigned)k0 * 8u;
-    const unsigned woff = (unsigned)(b0 + 2 * min(r, NB / 2 - 1)) * 8u;
-    d2_t v[EB2], vb[EB2], w[EB2], wb[EB2];
-    auto fetch = [&](int e0, int4& t) { t = *reinterpret_cast<const int4*>(E + e0); };
-    const int col0 = __builtin_amdgcn_readfirstlane(E[0].y);  // timing build 8: every load from this column
-    (void)col0;
-    auto issue = [&](int4 t, d2_t (&x)[EB2], d2_t (&wv)[EB2]) {
-      asm volatile("" : "+s"(t.x), "+s"(t.y), "+s"(t.z), "+s"(t.w));
-      // 32-bit offsets: (ncols + 1) x GS and ncells x Bp are < 2^31 (checked by the launcher)
-      const double* d0 = D + (unsigned)(((SCDE_TILE_DIAG & 8) ? col0 : t.y) * GS);
-      const double* d1 = D + (unsigned)(((SCDE_TILE_DIAG & 8) ? col0 : t.w) * GS);
-      const double* w0 = W + (unsigned)(t.x * Bp);
-      const double* w1 = W + (unsigned)(t.z * Bp);
-      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[0]) : "v"(doff), "s"(d0));
-      if (!(SCDE_TILE_DIAG & 4)) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[0]) : "v"(woff), "s"(w0));
-      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(x[1]) : "v"(doff), "s"(d1));
-      if (!(SCDE_TILE_DIAG & 4)) asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wv[1]) : "v"(woff), "s"(w1));
-    };
-    auto ready = [&](d2_t (&x)[EB2], d2_t (&wv)[EB2]) {  // all but the next batch's loads have landed
-      if (SCDE_TILE_DIAG & 4)  // timing build: multiplicities loaded once (results wrong)
-        asm volatile("s_waitcnt vmcnt(2)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
-      else
-        asm volatile("s_waitcnt vmcnt(4)" : "+v"(x[0]), "+v"(x[1]), "+v"(wv[0]), "+v"(wv[1]));
-    };
-    auto accumulate = [&](const d2_t (&x)[EB2], const d2_t (&wv)[EB2]) {
-#pragma unroll
-      for (int j = 0; j < EB2; ++j)
-        fmac_entry2<NB>(a0, a1, wv[j], x[j], std::make_integer_sequence<int, NB / 2>{});
-    };
-#pragma unroll
-    for (int i = 0; i < NB; ++i) asm volatile("" : "+v"(a0[i]), "+v"(a1[i]));
-    // rows are padded to a multiple of 64 entries plus 8 zero-column entries: every fetch and
-    // look-ahead batch stays inside the row
-    int4 ta, tb;
-    fetch(0, ta);
-    if (SCDE_TILE_DIAG & 4) {  // timing build: the first entry's multiplicities for every entry
-      const double* w0 = W + (unsigned)(ta.x * Bp);
-      w[0] = w[1] = wb[0] = wb[1] = *reinterpret_cast<const d2_t*>(w0 + woff / 8);
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(w[0]), "+v"(w[1]), "+v"(wb[0]), "+v"(wb[1]));
-    }
-    issue(ta, v, w);
-    fetch(EB2, tb);
-    const int n2 = (n + EB2 - 1) & ~(EB2 - 1);
-    int e0 = 0;
-    for (; e0 + 2 * EB2 <= n2; e0 += 2 * EB2) {
-      issue(tb, vb, wb);
-      fetch(e0 + 2 * EB2, ta);
-      ready(v, w);
-      accumulate(v, w);
-      issue(ta, v, w);
-      fetch(e0 + 3 * EB2, tb);
-      ready(vb, wb);
-      accumulate(vb, wb);
-    }
-    if (e0 < n2) {
-      issue(tb, vb, wb);
-      ready(v, w);
-      accumulate(v, w);
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(vb[0]), "+v"(vb[1]), "+v"(wb[0]), "+v"(wb[1]));
-    }
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(w[0]), "+v"(w[1]));
-  }
+  tile_rows<NB>(a0, a1, D, E, n, W, Zs, GS, Bp, b0, k0, r, live, l0, l1);
   // per slab maxima m'_b (f32) over its lanes -> fmx[wsid][slab]
 #pragma unroll 1
   for (int sl = 0; sl < nsl; ++sl) {
@@ -2405,6 +2456,272 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   if (lane < nsl && !((failm >> lane) & 1)) {
     const unsigned dn = lane ? doneB : doneA;
     pmask[(long long)g * P + (lane ? pB : pA)] = dn;
+    if (stats) {
+      atomicAdd(&stats[0], 1);
+      atomicAdd(&stats[1], __builtin_popcount(dn));
+      atomicAdd(&stats[2], NT);
+      atomicAdd(&stats[6 + __builtin_popcount(dn)], 1);
+    }
+  }
+}
+
+
+// ------------------------------------------------------------------ gene-block tile bootstrap
+// k_boot_gene: k_boot_tiles' arithmetic with one 4-wave block per (gene, group of up to SG
+// slabs) instead of one wave per (gene, slab) computing a fixed four bound tiles.  At config 3 a
+// slab needs about three of its thirteen 32-point bound tiles (2: 19%, 3: 79%,
+// 4: 2%), so four tiles per slab compute 25% more rows than needed.  Here the block's 16 rows
+// (4 waves x 4 sixteen-lane rows, each one (slab, bound tile)) are shared by the group's slabs:
+//   1. bounds: wave w computes the group's boot window 32 w .. 32 w + 31 (tile_bound_pass;
+//      4 windows = 128 boots >= 5 slabs x 20: one bound pass per 32 boots, not per 20) into LDS;
+//   2. plan: per slab its bound tiles ranked by their largest bound over the live boots; every
+//      slab gets its top K = min(4, 16 / slabs) tiles, the spare rows the next-ranked tiles of the
+//      slabs whose next bound is closest to their top bound (at 5 slabs: 3 each plus one spare);
+//   3. rows (tile_rows: each 16-lane row its own slab's multiplicities by DPP64 broadcast and its
+//      own tile's points), per-row f32 maxima, per-slab maxima m'_b over the slab's rows;
+//   4. post-check per slab exactly as k_boot_tiles (every bound tile not computed must have
+//      UB_bt < m'_b - 51 for every live boot); a slab that fails goes to the four-tile list pass
+//      (k_boot_tiles over `wide`), whose failures go to k_boot2;
+//   5. softmax terms, 16-point tile partials (pair8_sum), per (slab, boot) sums over the slab's
+//      computed tiles in tile order, 1 / (S nboot), the partial jp rows.
+// Every value is formed exactly as in k_boot_tiles and k_boot2 (same fma chains, maxima, terms,
+// tile partials added in tile order), so the outputs are bit-identical to theirs.
+constexpr int kGeneRows = 16;    // 4 waves x 4 rows
+constexpr int kGeneSlabs = 8;    // slabs per group at most (K >= 2 rows each)
+template <int NB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_gene(
+    const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
+    const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
+    int G, int GS, int P, int SG, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
+    long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8g, int Bq,
+    const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
+    int kcap, int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order,
+    unsigned* __restrict__ pmask, int* __restrict__ wide) {
+  static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
+  constexpr int WB = 4;
+  // bound staging of the four waves; once the bounds are in gub: row maxima | tile sums | 1 / (S nboot)
+  __shared__ unsigned bstage[WB][1024 + 512];
+  __shared__ float gub[kBTileMax * 128];          // [bound tile][group boot] bounds
+  __shared__ float sc[kGeneSlabs][16];            // [slab][bound tile] score
+  __shared__ signed char rk[kGeneSlabs][16];      // [slab][rank] bound tile
+  __shared__ signed char rowof[kGeneSlabs][16];   // [slab][bound tile] the row computing it, or -1
+  __shared__ int rowS[kGeneRows], rowT[kGeneRows];  // [row] slab in the group (-1: no work), bound tile
+  __shared__ float fmx[kGeneSlabs][32];           // [slab][boot] maxima m'_b
+  __shared__ unsigned bd[kGeneSlabs];             // [slab] bound tiles computed
+  __shared__ unsigned failm;                      // slabs whose post-check failed
+  __shared__ double etab[64];
+  static_assert(kGeneRows * 32 + 2 * (2 * kGeneRows * NB) + 2 * kGeneSlabs * 32 <= WB * (1024 + 512),
+                "the staging area must hold the row maxima, tile sums and normalisers");
+  float* const rowmax = reinterpret_cast<float*>(&bstage[0][0]);                  // [row][32]
+  double* const tsum = reinterpret_cast<double*>(&bstage[0][0] + kGeneRows * 32);  // [sum slot][NB]
+  double* const finv = tsum + 2 * kGeneRows * NB;                                 // [slab][32]
+  const int lane = threadIdx.x & 63;
+  const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int NGR = (P + SG - 1) / SG;
+  const int blk = xcd_block(blockIdx.x, gridDim.x);
+  if (blk >= ngenes * NGR) return;  // uniform over the block
+  const int gi = blk / NGR, gr = blk - gi * NGR;
+  const int g = order ? order[gi] : gi;
+  const int s0 = gr * SG, ns = min(SG, P - s0);
+  if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
+    if ((int)threadIdx.x < ns) {
+      const int q = g * P + s0 + threadIdx.x;
+      redo[q] = 1;
+      redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = q;
+      pmask[q] = ~0u;
+    }
+    return;
+  }
+  if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
+  if (threadIdx.x == 0) failm = 0u;
+  const int n = nnz[g];
+  const int NT = (G + 15) >> 4, NTB = (G + 31) >> 5;  // 16-point sum tiles, 32-point bound tiles
+  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  const int set = wset ? wset[g] : 0;
+  const int gb0 = s0 * NB, gnb = ns * NB;  // the group's boots (gnb <= 128)
+  // ---- 1. bounds of the group's boot window 32 wsid .. 32 wsid + 31
+  if (32 * wsid < gnb) {
+    const unsigned gstride = (unsigned)NGR * 128u;
+    const unsigned char* __restrict__ W8 = W8g + (long long)set * ncells * gstride + gr * 128 + 32 * wsid;
+    const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq + gb0 + 32 * wsid;
+    tile_bound_pass(E, n, UQ, W8, gstride, ZU, Bq, &bstage[wsid][0], gub + 32 * wsid, 128, min(32, gnb - 32 * wsid),
+                    NTB, lane);
+  }
+  __syncthreads();
+  // ---- 2. the plan: per slab the score of each bound tile (its largest bound over the live boots)
+  {
+    const int s = threadIdx.x >> 4, t = threadIdx.x & 15;
+    if (s < kGeneSlabs) {
+      float v = -INFINITY;
+      if (s < ns && t < NTB) {
+        const int nl = min(NB, nboot - (gb0 + s * NB));
+        for (int b = 0; b < nl; ++b) v = fmaxf(v, gub[t * 128 + s * NB + b]);
+      }
+      sc[s][t] = v;
+      rowof[s][t] = -1;
+    } else if (s < kGeneSlabs + 1) {
+      rowS[t] = -1;
+      rowT[t] = 0;
+    }
+  }
+  __syncthreads();
+  {  // ranks (ties by tile index)
+    const int s = threadIdx.x >> 4, t = threadIdx.x & 15;
+    if (s < ns && t < NTB) {
+      const float v = sc[s][t];
+      int rnk = 0;
+      for (int u = 0; u < NTB; ++u) {
+        const float w = sc[s][u];
+        rnk += (w > v) || (w == v && u < t);
+      }
+      rk[s][rnk] = (signed char)t;
+    }
+  }
+  __syncthreads();
+  // rows per slab (kcap, maxgroups: tests force the list pass / k_boot2 fallback with fewer)
+  const int K = min(min(4, kGeneRows / ns), min(NTB, max(1, min(maxgroups, kcap))));
+  {
+    const int x = threadIdx.x;
+    if (x < K * ns) {  // regular rows: slab x / K, rank x % K
+      const int s = x / K;
+      rowS[x] = s;
+      rowT[x] = rk[s][x - s * K];
+    } else if (x >= 64 && x < 64 + 2 * ns && maxgroups >= 4 && kcap >= 4) {
+      // spare rows: candidates (slab s, rank K + j), j < 2, by how close their bound is to the
+      // slab's top bound (ranks of one slab in order: their keys only decrease)
+      const int c = x - 64, s = c >> 1, k = K + (c & 1);
+      const int nsp = kGeneRows - K * ns;
+      if (k < NTB && nsp > 0) {
+        const float key = sc[s][rk[s][k]] - sc[s][rk[s][0]];
+        int o = 0;
+        for (int c2 = 0; c2 < 2 * ns; ++c2) {
+          const int s2 = c2 >> 1, k2 = K + (c2 & 1);
+          if (k2 >= NTB) continue;
+          const float key2 = sc[s2][rk[s2][k2]] - sc[s2][rk[s2][0]];
+          o += (key2 > key) || (key2 == key && c2 < c);
+        }
+        if (o < nsp) {
+          rowS[K * ns + o] = s;
+          rowT[K * ns + o] = rk[s][k];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // ---- 3. rows: this lane's row q (one bound tile of one slab), two points per lane
+  const int row = lane >> 4, q = 4 * wsid + row;
+  const int sq = rowS[q];
+  const bool live = sq >= 0;
+  const int tq = live ? rowT[q] : 0;
+  const int slot = lane >> 3, m2 = lane & 7, r = lane & 15;
+  const int k0 = 16 * (2 * tq + (slot & 1)) + 2 * m2;
+  const bool l0 = live && k0 < G, l1 = live && k0 + 1 < G;
+  const int b0 = gb0 + (live ? sq : 0) * NB;
+  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
+  const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
+  double a0[NB], a1[NB];
+  tile_rows<NB>(a0, a1, D, E, n, W, Zs, GS, Bp, b0, k0, r, live, l0, l1);
+  // per-row f32 maxima (max is exact: the same m'_b as any other reduction order)
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    float m = (float)gt_max(a0[i], a1[i]);
+    m = gt_maxf(m, dpp_f<kDppXor1>(m));
+    m = gt_maxf(m, dpp_f<kDppXor2>(m));
+    m = gt_maxf(m, dpp_f<kDppHalfMirror>(m));
+    m = gt_maxf(m, dpp_f<kDppMirror>(m));
+    if (r == 0) rowmax[q * 32 + i] = m;
+  }
+  __syncthreads();
+  {
+    const int s = threadIdx.x >> 5, i = threadIdx.x & 31;
+    if (s < ns && i < NB) {
+      float m = -INFINITY;
+      for (int q2 = 0; q2 < kGeneRows; ++q2)
+        if (rowS[q2] == s) m = gt_maxf(m, rowmax[q2 * 32 + i]);
+      fmx[s][i] = m;
+    }
+    if ((int)threadIdx.x < ns) {  // the slab's computed bound tiles and the rows holding them
+      unsigned b = 0;
+      for (int q2 = 0; q2 < kGeneRows; ++q2)
+        if (rowS[q2] == (int)threadIdx.x) {
+          b |= 1u << rowT[q2];
+          rowof[threadIdx.x][rowT[q2]] = (signed char)q2;
+        }
+      bd[threadIdx.x] = b;
+    }
+  }
+  __syncthreads();
+  // ---- 4. post-check per slab (wave w: slabs w, w + 4)
+  for (int s = wsid; s < ns; s += WB) {
+    const int nl = min(NB, nboot - (gb0 + s * NB));
+    bool need = false;
+    if (lane < NTB && !((bd[s] >> lane) & 1))
+      for (int b = 0; b < nl; ++b) need |= (double)gub[lane * 128 + s * NB + b] >= (double)fmx[s][b] - 51.0;
+    if (__ballot(need)) {
+      if (lane == 0) {
+        atomicOr(&failm, 1u << s);
+        wide[1 + atomicAdd(&wide[0], 1)] = g * P + s0 + s;
+        if (stats) atomicAdd(&stats[35], 1);
+      }
+    } else if (lane < nl && !(fabs((double)fmx[s][lane]) <= degen_thresh)) {
+      degen[g] = 1;
+    }
+  }
+  if (stats && threadIdx.x == 0) atomicAdd(&stats[4], WB * 2 * ((n + 1) & ~1));
+  __syncthreads();
+  const unsigned fm = failm;
+  const bool mine = live && !((fm >> sq) & 1);
+  // ---- 5. softmax terms, tile partial sums, jp partial rows
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const double m = live ? (double)fmx[sq][i] : 0.0;
+    const double d0 = a0[i] - m, d1 = a1[i] - m;
+    const bool n0 = mine && l0 && d0 >= kBootExpCut, n1 = mine && l1 && d1 >= kBootExpCut;
+    if (__builtin_amdgcn_ballot_w64(n0 || n1)) {
+      a0[i] = n0 ? exp_tab(d0, etab) : 0.0;
+      a1[i] = n1 ? exp_tab(d1, etab) : 0.0;
+    } else {
+      a0[i] = 0.0;
+      a1[i] = 0.0;
+    }
+    const double ps = pair8_sum(a0[i], a1[i]);
+    if (m2 == 0 && live) tsum[(2 * q + (slot & 1)) * NB + i] = ps;
+  }
+  __syncthreads();
+  {
+    const int s = threadIdx.x >> 5, b = threadIdx.x & 31;
+    if (s < ns && b < NB && !((fm >> s) & 1)) {
+      double S = 0.0;
+      for (unsigned mm = bd[s]; mm; mm &= mm - 1) {  // bound tiles in order, their two sum tiles
+        const int t = __builtin_ffs((int)mm) - 1;
+        const int q2 = rowof[s][t];
+        if (2 * t < NT) S += tsum[(2 * q2) * NB + b];
+        if (2 * t + 1 < NT) S += tsum[(2 * q2 + 1) * NB + b];
+      }
+      finv[s * 32 + b] = (gb0 + s * NB + b < nboot) ? 1.0 / (S * norm_mult) : 0.0;
+    }
+  }
+  __syncthreads();
+  if (mine) {
+    double* prow = part + (long long)(s0 + sq) * part_stride + (long long)g * GS;
+    double j0 = 0.0, j1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      j0 = fma(a0[i], finv[sq * 32 + i], j0);
+      j1 = fma(a1[i], finv[sq * 32 + i], j1);
+    }
+    if (l1)
+      *reinterpret_cast<d2_t*>(prow + k0) = d2_t{j0, j1};
+    else if (l0)
+      prow[k0] = j0;
+  }
+  // tiles not computed stay unwritten: k_sum_partials reads only the tiles in pmask
+  if ((int)threadIdx.x < ns && !((fm >> threadIdx.x) & 1)) {
+    const unsigned ntmask = (NT >= 32) ? ~0u : ((1u << NT) - 1);
+    unsigned dn = 0;
+    for (unsigned mm = bd[threadIdx.x]; mm; mm &= mm - 1) dn |= 3u << (2 * (__builtin_ffs((int)mm) - 1));
+    dn &= ntmask;
+    pmask[(long long)g * P + s0 + threadIdx.x] = dn;
     if (stats) {
       atomicAdd(&stats[0], 1);
       atomicAdd(&stats[1], __builtin_popcount(dn));
@@ -3443,21 +3760,37 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   // pair mode: a wave per two slabs of a gene, two bound tiles each; the slabs that need more
   // go to a four-tile pass over the compacted list `wide` ([0] length, then g * P + p)
   const bool pairs = tb.pairs && P >= 2 && tb.wide;
-  if (pairs) {
+  // gene blocks: one 4-wave block per (gene, group of SG slabs) shares 16 rows among the group's
+  // slabs; the slabs whose post-check fails take the four-tile pass over `wide`
+  const bool gene = !pairs && tb.gene && tb.W8g && tb.wide && tb.SG >= 1 && tb.SG <= kGeneSlabs &&
+                    tb.SG * a.nb <= 128;
+  if (gene) {
+    const int NGR = (P + tb.SG - 1) / tb.SG;
+    if ((long long)a.ncells * NGR * 128 >= (1LL << 31) || tb.Bq < (NGR - 1) * tb.SG * a.nb + 128) return hipErrorInvalidValue;
+  }
+  if (pairs || gene) {
     e = hipMemsetAsync(tb.wide, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
   }
   constexpr int WB = 4;
   const long long items1 = pairs ? (long long)a.ngenes * ((P + 1) / 2) : items;
-  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : 0;  // slabs a pair pass may leave
+  // slabs a pair pass (or a gene block) may leave to the four-tile list pass
+  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? items : 0;
+  const long long gblocks = gene ? (long long)a.ngenes * ((P + tb.SG - 1) / tb.SG) : 0;
 #define SCDE_BT(NBV)                                                                                              \
   case NBV:                                                                                                        \
+    if (gene)                                                                                                      \
+      hipLaunchKernelGGL(k_boot_gene<NBV>, dim3((unsigned)gblocks), dim3(256), 0, s, a.D, a.ent, a.nnz,           \
+                         a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
+                         a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
+                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide); \
+    else                                                                                                           \
     hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
                        a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,      \
                        a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq,      \
                        tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask, pairs ? 1 : 0, \
                        nullptr, tb.wide);                                                                        \
-    if (pairs)                                                                                                     \
+    if (pairs || gene)                                                                                             \
       hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items2, WB)), dim3(64 * WB), 0, s, a.D,   \
                          a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,    \
                          a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq,    \

@@ -43,6 +43,8 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("boot_tiles_cells", opts.get("boot_tiles_cells", 0))
     ctx.set_option("tile_order", opts.get("tile_order", 1))
     ctx.set_option("pair_cells", opts.get("pair_cells", 1000))
+    ctx.set_option("gene_blocks", opts.get("gene_blocks", 1))
+    ctx.set_option("gene_rows", opts.get("gene_rows", 4))
     ctx.set_option("unique_fixed", opts.get("unique_fixed", 1))
     ctx.set_option("lanes", opts.get("lanes", 2))
     ctx.set_option("pipeline_mb", opts.get("pipeline_mb", 32))
@@ -65,6 +67,8 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("boot_tiles_cells", 200)
         ctx.set_option("tile_order", 1)
         ctx.set_option("pair_cells", 1000)
+        ctx.set_option("gene_blocks", 1)
+        ctx.set_option("gene_rows", 4)
         ctx.set_option("unique_fixed", 1)
         ctx.set_option("lanes", 2)
         ctx.set_option("pipeline_mb", 32)
@@ -86,6 +90,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles": {},
         "noskip": {"boot_skip": 0},
         "tiles-forced-redo": {"tile_groups": 2},
+        "tiles-slab-waves": {"gene_blocks": 0},
+        "tiles-slab-waves-redo": {"gene_blocks": 0, "tile_groups": 2},
+        "gene-forced-list": {"gene_rows": 1},
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
         "one-lane": {"lanes": 1},
@@ -105,8 +112,12 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
             assert stats["skip_slabs"] == 0 and stats["boot_path"] == 0, stats
         elif name == "tiles-mult-fallback":  # plain k_boot2 on the tile path's columns, no skipping
             assert stats["boot_path"] == 0 and stats["skip_slabs"] == 0, stats
-        elif name == "tiles-forced-redo":  # 2 bound tiles (64 points): slabs needing more go to k_boot2
+        elif name in ("tiles-forced-redo", "tiles-slab-waves-redo"):
+            # 2 bound tiles (64 points): slabs needing more go to k_boot2 (gene blocks: through the
+            # four-tile list pass, itself limited to 2)
             assert stats["boot_path"] == 1 and stats["skip_redo"] > 0, stats
+        elif name == "gene-forced-list":  # gene blocks with one row per slab: the list pass finishes the rest
+            assert stats["boot_path"] == 1 and stats["pair_redo"] > 0 and stats["skip_slabs"] > 0, stats
         elif name == "tiles-pairs":
             # two slabs per wave, two bound tiles each: at these cell counts many slabs need more and
             # take the four-tile list pass
@@ -129,7 +140,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         assert_cz_close(res["cZ"].to_numpy(), ref["results"]["cZ"], res["Z"].to_numpy(), ref["results"]["Z"],
                         what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
-    for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
+    for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
+                                    "gene-forced-list", "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "tiles-pairs",
                                     "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
         for name in others:
