@@ -137,6 +137,13 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "pair_cells"    the cell count from which k_boot_tiles runs two slabs per wave with two
  *                   bound tiles each (default 1000: wide calls, narrow posteriors); slabs that need
  *                   more take a four-tile pass (results are the same)
+ *   "gene_blocks"   1/0  the tile bootstrap as one 4-wave block per (gene, group of slabs) sharing 16
+ *                   bound-tile rows among the group's slabs (k_boot_gene; default 1, not with pair mode),
+ *                   or one wave per slab with four tiles (k_boot_tiles); results are the same
+ *   "gene_rows"     1..4 rows per slab k_boot_gene gives each slab at most (default 4; tests force
+ *                   its four-tile list pass with fewer)
+ *   "modes_overlap" 1/0  scde.posteriors' posterior-mode read-back overlaps the bootstrap on the
+ *                   copy stream (default 1), or follows it on the main stream (rocprofv3 runs)
  *   "lanes"         2/1  a DE call's second group runs on a peer context (its own streams and
  *                   workspace, same device) beside the first (default 2), or after it (1; bench's
  *                   per-stage timing pass and the rocprof runs use 1); results are the same.

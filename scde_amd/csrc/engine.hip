@@ -280,6 +280,11 @@ struct scde_ctx {
   int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
   int opt_gene_blocks = 1;       // "gene_blocks": k_boot_gene (a 4-wave block per gene's slab group, rows shared
                                  // by its slabs) instead of one k_boot_tiles wave per slab; not with pair mode
+  int opt_upload_staged = 0;     // "upload_staged": host-count uploads through a pinned ring filled by copy threads
+  int opt_upload_threads = 8;    // "upload_threads": threads filling a staging slot (the upload worker included)
+  int opt_modes_overlap = 1;     // "modes_overlap": scde.posteriors' posterior-mode read-back overlaps the bootstrap
+                                 // on the copy stream (0: after it, on the main stream -- rocprofv3 runs, where the
+                                 // pageable read-back becomes blit kernels that would share the CUs)
   int opt_gene_rows = 4;         // "gene_rows": rows per slab k_boot_gene gives each slab at most (tests force its
                                  // four-tile list pass with fewer)
   int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
@@ -316,6 +321,27 @@ struct scde_ctx {
     int nranges = 0, issued = 0, err = 0;
     std::string err_msg;  // the worker thread's error text (its g_err is its own)
   } upl;
+  // Pinned staging for the host-count uploads (option "upload_staged"): the upload worker copies
+  // each chunk of the caller's pageable matrix into a pinned ring slot with T pool threads (it
+  // takes one share itself), then issues the DMA from the slot; a slot is reused once its DMA's
+  // event has fired.  A pageable hipMemcpyAsync is staged by the runtime on the issuing thread.
+  struct Stager {
+    static constexpr int kSlots = 4;
+    static constexpr size_t kSlot = size_t(4) << 20;
+    char* pin = nullptr;
+    hipEvent_t ev[kSlots] = {};
+    bool used[kSlots] = {};
+    long long next = 0;
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, cvd;
+    long long gen = 0;
+    int pending = 0, T = 0;
+    bool stop = false;
+    const char* src = nullptr;
+    char* dst = nullptr;
+    size_t n = 0;
+  } stg;
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // host wall time of scde_expression_difference_{dev,host} phases (ms, summed over calls):
@@ -437,6 +463,14 @@ struct scde_ctx {
     return SCDE_OK;
   }
   ~scde_ctx() {
+    if (!stg.th.empty()) {
+      {
+        std::lock_guard<std::mutex> lk(stg.m);
+        stg.stop = true;
+      }
+      stg.cv.notify_all();
+      for (auto& t : stg.th) t.join();
+    }
     if (upl.th.joinable()) {
       {
         std::lock_guard<std::mutex> lk(upl.m);
@@ -483,6 +517,9 @@ struct scde_ctx {
     if (aux_ev) (void)hipEventDestroy(aux_ev);
     if (aux_stream) (void)hipStreamDestroy(aux_stream);
     if (pin) (void)hipHostFree(pin);
+    if (stg.pin) (void)hipHostFree(stg.pin);
+    for (auto& e : stg.ev)
+      if (e) (void)hipEventDestroy(e);
     for (auto& e : up_ev)
       if (e) (void)hipEventDestroy(e);
   }
@@ -1141,9 +1178,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
                              cx->gorder.as<int>(), cx->gwork.p, &wb, sa));
     }
     // k_boot_gene (not with pair mode): groups of gene_sg slabs per 4-wave block
-    const int gene_sg = (tpath && cx->opt_gene_blocks && !(C >= cx->opt_pair_cells && (s.nboot + nb - 1) / nb >= 2))
-                            ? std::min({(s.nboot + nb - 1) / nb, 8, 128 / nb})
-                            : 0;
+    // k_boot_gene (gene_blocks, the default at every cell count the tile path runs; measured against
+    // pair mode at config 4: bootstrap 11.16 -> 9.94 ms per step) or, without it, k_boot_tiles'
+    // wave per slab (pair mode from pair_cells)
+    const int gene_sg = (tpath && cx->opt_gene_blocks) ? std::min({(s.nboot + nb - 1) / nb, 8, 128 / nb}) : 0;
     if (tpath) {
       // byte multiplicities [set][cell][boot] (baseline bound sums and the tile bounds)
       // and, for the tile bounds' A fragments, per slab the pairs (boot r, boot 16 + r) of its nb
@@ -1261,7 +1299,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
         HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * N)));
         tb.pmask = cx->pmask.as<unsigned>();
-        tb.pairs = (C >= cx->opt_pair_cells && P >= 2) ? 1 : 0;
+        tb.pairs = (gene_sg == 0 && C >= cx->opt_pair_cells && P >= 2) ? 1 : 0;
         if (tb.pairs) {
           HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * N)));
           tb.wide = cx->pwide.as<int>();
@@ -1571,6 +1609,9 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "tile_order") ctx->opt_tile_order = value != 0;
   else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
   else if (n == "gene_blocks") ctx->opt_gene_blocks = value != 0;
+  else if (n == "modes_overlap") ctx->opt_modes_overlap = value != 0;
+  else if (n == "upload_staged") ctx->opt_upload_staged = value != 0;
+  else if (n == "upload_threads") ctx->opt_upload_threads = std::max(1, std::min(32, (int)value));
   else if (n == "gene_rows") ctx->opt_gene_rows = std::max(1, std::min(4, (int)value));
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
@@ -1978,9 +2019,92 @@ struct HostUpload {
   int64_t ld;
   int ngenes, cut, C;
 };
+// the staging pool: share t of [0, n) copied by thread t (share 0 by the caller)
+static void stg_share(const char* src, char* dst, size_t n, int t, int T) {
+  const size_t a = (n * (size_t)t / (size_t)T) & ~size_t(63), b = (t + 1 == T) ? n : ((n * (size_t)(t + 1) / T) & ~size_t(63));
+  if (b > a) std::memcpy(dst + a, src + a, b - a);
+}
+static void stg_copy(scde_ctx* ctx, char* dst, const char* src, size_t n) {
+  auto& g = ctx->stg;
+  const int T = std::max(1, ctx->opt_upload_threads);
+  if (T == 1 || n < (size_t(256) << 10)) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  if ((int)g.th.size() != T - 1) {  // (re)build the pool: T - 1 threads plus the caller
+    if (!g.th.empty()) {
+      {
+        std::lock_guard<std::mutex> lk(g.m);
+        g.stop = true;
+      }
+      g.cv.notify_all();
+      for (auto& t : g.th) t.join();
+      g.th.clear();
+      g.stop = false;
+    }
+    g.T = T;
+    const long long gen0 = g.gen;  // no job is pending while the pool is (re)built
+    for (int t = 1; t < T; ++t)
+      g.th.emplace_back([&g, t, gen0] {
+        long long seen = gen0;
+        std::unique_lock<std::mutex> lk(g.m);
+        for (;;) {
+          g.cv.wait(lk, [&] { return g.stop || g.gen != seen; });
+          if (g.stop) return;
+          seen = g.gen;
+          const char* s = g.src;
+          char* d = g.dst;
+          const size_t nn = g.n;
+          const int TT = g.T;
+          lk.unlock();
+          stg_share(s, d, nn, t, TT);
+          lk.lock();
+          if (--g.pending == 0) g.cvd.notify_all();
+        }
+      });
+  }
+  {
+    std::lock_guard<std::mutex> lk(g.m);
+    g.src = src;
+    g.dst = dst;
+    g.n = n;
+    g.pending = T - 1;
+    ++g.gen;
+  }
+  g.cv.notify_all();
+  stg_share(src, dst, n, 0, T);
+  std::unique_lock<std::mutex> lk(g.m);
+  g.cvd.wait(lk, [&] { return g.pending == 0; });
+}
+
+// columns [lo, hi) of contiguous host counts through the pinned ring, on the copy stream
+static int upload_cols_staged(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
+  auto& g = ctx->stg;
+  if (!g.pin) {
+    HCHK(hipHostMalloc(reinterpret_cast<void**>(&g.pin), scde_ctx::Stager::kSlots * scde_ctx::Stager::kSlot,
+                       hipHostMallocDefault));
+    for (auto& e : g.ev) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const size_t row = sizeof(int) * (size_t)h.ngenes, bytes = row * (size_t)(hi - lo);
+  const char* src = reinterpret_cast<const char*>(h.counts + (size_t)h.ld * lo);
+  char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
+  for (size_t off = 0; off < bytes; off += scde_ctx::Stager::kSlot) {
+    const int k = (int)(g.next++ % scde_ctx::Stager::kSlots);
+    if (g.used[k]) HCHK(hipEventSynchronize(g.ev[k]));
+    const size_t n = std::min(scde_ctx::Stager::kSlot, bytes - off);
+    char* slot = g.pin + (size_t)k * scde_ctx::Stager::kSlot;
+    stg_copy(ctx, slot, src + off, n);
+    HCHK(hipMemcpyAsync(dst + off, slot, n, hipMemcpyHostToDevice, ctx->copy_stream));
+    HCHK(hipEventRecord(g.ev[k], ctx->copy_stream));
+    g.used[k] = true;
+  }
+  return SCDE_OK;
+}
+
 // columns [lo, hi) of the host counts into counts_in, on the copy stream
 static int upload_cols(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   const size_t row = sizeof(int) * (size_t)h.ngenes;
+  if (hi > lo && ctx->opt_upload_staged && h.ld == h.ngenes) return upload_cols_staged(ctx, h, lo, hi);
   if (hi > lo) {
     char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
     const int* src = h.counts + (size_t)h.ld * lo;
@@ -2175,11 +2299,15 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
     };
   }
   RCHK(run_posterior(ctx, s, ctx->us[0]));
-  if (s.modes_early) RCHK(copy_modes_out(ctx, modes, s.modes, (size_t)ngenes * ncells_sel));
+  const bool modes_async = s.modes_early && ctx->opt_modes_overlap;
+  if (modes_async) RCHK(copy_modes_out(ctx, modes, s.modes, (size_t)ngenes * ncells_sel));
+  else if (s.modes_early)  // after the bootstrap, on the main stream (profiling runs: no blits beside it)
+    HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * (size_t)ngenes * ncells_sel, hipMemcpyDeviceToHost,
+                        ctx->stream));
   if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, ctx->stream));
   if (want_post && NG)
     HCHK(hipMemcpyAsync(post, s.post, sizeof(double) * NG * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
-  if (s.modes_early) HCHK(hipStreamSynchronize(ctx->copy_stream));
+  if (modes_async) HCHK(hipStreamSynchronize(ctx->copy_stream));
   return ctx->sync();
 }
 

@@ -58,6 +58,17 @@ def test_config3_whole_table_vs_oracle(api, oracle):
     res, want = got["results"], g["results"]
     for j, k in enumerate(("lb", "mle", "ub", "ce")):
         np.testing.assert_array_equal(res[k].to_numpy(), want[:, j], err_msg=k)
+    # the host counts through the pinned staging ring (8 copy threads): the same table
+    ctx = api.default_context()
+    try:
+        ctx.set_option("upload_staged", 1)
+        api.set_rand("glibc")
+        st = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=nboot,
+                                            n_cores=ncores)
+    finally:
+        ctx.set_option("upload_staged", 0)
+    for k in ("lb", "mle", "ub", "ce", "Z", "cZ"):
+        np.testing.assert_array_equal(st[k].to_numpy(), res[k].to_numpy(), err_msg=f"staged {k}")
     assert_z_close(res["Z"].to_numpy(), want[:, 4], what="Z")
     assert_cz_close(res["cZ"].to_numpy(), want[:, 5], res["Z"].to_numpy(), want[:, 4], what="cZ")
     # posteriors of a window across the first chunk boundary (two draw lists), live oracle

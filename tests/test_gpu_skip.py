@@ -50,6 +50,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("pipeline_mb", opts.get("pipeline_mb", 32))
     ctx.set_option("pieces", opts.get("pieces", 4))
     ctx.set_option("defer_boot", opts.get("defer_boot", 0))
+    ctx.set_option("upload_staged", opts.get("upload_staged", 0))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -74,6 +75,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("pipeline_mb", 32)
         ctx.set_option("pieces", 4)
         ctx.set_option("defer_boot", 0)
+        ctx.set_option("upload_staged", 0)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -99,8 +101,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "pipelined-pieces": {"pipeline_mb": 0, "pieces": 3},
         "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1},
         "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1},
-        "tiles-pairs": {"pair_cells": 1},
-        "tiles-pairs-redo": {"pair_cells": 1, "tile_groups": 2},
+        "pipelined-staged": {"pipeline_mb": 0, "pieces": 3, "upload_staged": 1},
+        "tiles-pairs": {"pair_cells": 1, "gene_blocks": 0},
+        "tiles-pairs-redo": {"pair_cells": 1, "tile_groups": 2, "gene_blocks": 0},
         "tiles-mult-fallback": {"tile_max_mult": 1},
         "stretch": {"boot_tiles": 0},
         "stretch-forced-redo": {"boot_tiles": 0, "skip_slack": -45.0},
@@ -142,7 +145,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
                                     "gene-forced-list", "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
-                                    "pipelined-one-lane", "pipelined-deferred", "tiles-pairs",
+                                    "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "tiles-pairs",
                                     "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
         for name in others:
             for i in range(2):

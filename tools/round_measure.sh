@@ -14,7 +14,7 @@ if [ -z "$SKIP_TESTS" ]; then
   tail -1 gpurun_out/fin/gputests.log
 fi
 for c in $PROF_CFGS; do
-  PROFILE_PREFIX=profiles/${TAG}_config$c timeout -k 10 1000 bash tools/profile.sh gpurun_out/prof${c}_$TAG --config $c --steps 3 --warmup 1 --cpu-sample 0 --no-profile --opt lanes=1 > gpurun_out/fin/prof$c.log 2>&1 || { tail -5 gpurun_out/fin/prof$c.log; exit 1; }
+  PROFILE_PREFIX=profiles/${TAG}_config$c timeout -k 10 1000 bash tools/profile.sh gpurun_out/prof${c}_$TAG --config $c --steps 3 --warmup 1 --cpu-sample 0 --no-profile --opt lanes=1 --opt modes_overlap=0 > gpurun_out/fin/prof$c.log 2>&1 || { tail -5 gpurun_out/fin/prof$c.log; exit 1; }
   echo "profiled config $c"
 done
 cp profiles/${TAG}_* gpurun_out/fin/ 2>/dev/null
