@@ -285,6 +285,7 @@ struct scde_ctx {
   int opt_modes_overlap = 1;     // "modes_overlap": scde.posteriors' posterior-mode read-back overlaps the bootstrap
                                  // on the copy stream (0: after it, on the main stream -- rocprofv3 runs, where the
                                  // pageable read-back becomes blit kernels that would share the CUs)
+  int opt_gene_list_cap = 0;     // "gene_list_cap": slabs k_boot_gene's list pass takes at most (0: 16384; tests)
   int opt_gene_rows = 4;         // "gene_rows": rows per slab k_boot_gene gives each slab at most (tests force its
                                  // four-tile list pass with fewer)
   int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
@@ -296,6 +297,8 @@ struct scde_ctx {
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
+  int opt_lane_thread = 0;      // "lane_thread": a pipelined two-lane DE call drives the second lane from a host
+                                // thread of its own
   int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
                                 // the second group's tables
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
@@ -1310,6 +1313,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           tb.gene = 1;
           tb.SG = gene_sg;
           tb.kcap = cx->opt_gene_rows;
+          tb.list_cap = cx->opt_gene_list_cap;
           tb.W8g = cx->w8g.as<unsigned char>();
         }
         if (have_order) tb.order = cx->gorder.as<int>();
@@ -1612,12 +1616,14 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "modes_overlap") ctx->opt_modes_overlap = value != 0;
   else if (n == "upload_staged") ctx->opt_upload_staged = value != 0;
   else if (n == "upload_threads") ctx->opt_upload_threads = std::max(1, std::min(32, (int)value));
+  else if (n == "gene_list_cap") ctx->opt_gene_list_cap = std::max(0, (int)value);
   else if (n == "gene_rows") ctx->opt_gene_rows = std::max(1, std::min(4, (int)value));
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
   else if (n == "lane_prio") ctx->opt_lane_prio = value != 0;
   else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
+  else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
     if (ctx->opt_lanes == 1 && ctx->peer) {  // one lane: the peer's workspace goes back to the device
@@ -2352,6 +2358,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_pair_cells = cx->opt_pair_cells;
   p->opt_gene_blocks = cx->opt_gene_blocks;
   p->opt_gene_rows = cx->opt_gene_rows;
+  p->opt_gene_list_cap = cx->opt_gene_list_cap;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;
@@ -2469,6 +2476,34 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     evs.push_back(ctx->up_ev[1]);
     UploadWorker uw;
     RCHK(uw.start(ctx, *up, cols, evs));
+    // two lanes with lane_thread: the second group's unique sets, tables and bootstrap are driven
+    // by a host thread of their own from the moment its range lands, beside this thread's pieces
+    // of the first group (each lane's host syncs then wait only for its own kernels)
+    struct LaneThread {
+      std::thread th;
+      int rc = SCDE_OK;
+      std::string err;
+      ~LaneThread() {
+        if (th.joinable()) th.join();  // an early error return of this thread still waits for it
+      }
+    } t2;
+    const bool threaded = lane != ctx && ctx->opt_lane_thread && !ctx->opt_defer_boot;
+    if (threaded) {
+      const int gi = 1 - first;
+      ctx->us[gi].ready = false;
+      t2.th = std::thread([&, gi] {
+        t2.rc = [&]() -> int {
+          HCHK(hipSetDevice(ctx->device));
+          RCHK(uw.wait(K + 1));
+          HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
+          const PostSpec* sp[1] = {&specs[gi]};
+          UniqueSet* usp[1] = {&ctx->us[gi]};
+          RCHK(build_unique_sets(lane, sp, usp, 1));
+          return run_posterior(lane, specs[gi], ctx->us[gi]);
+        }();
+        if (t2.rc != SCDE_OK) t2.err = g_err;  // g_err is thread-local
+      });
+    }
     // two lanes: the first group's bootstrap is queued only after the second group's tables, so
     // those (and their small set-up kernels) do not wait behind its waves; the first group's
     // tables end about when the second group's range lands anyway
@@ -2491,7 +2526,13 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       RCHK(run_posterior(ctx, sf, ctx->us[gi], defer ? &rest0 : nullptr));
       hlap(2);
     }
-    {
+    if (t2.th.joinable()) {  // the second lane ran on its own host thread
+      t2.th.join();
+      if (t2.rc != SCDE_OK) return fail(t2.rc, "%s", t2.err.c_str());
+      HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
+      HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+      hlap(2);
+    } else {
       // the second group, once its range is in HBM: its unique sets on the peer lane (or on
       // the unique stream with one lane), so their host sync waits for its small kernels only
       const int gi = 1 - first;

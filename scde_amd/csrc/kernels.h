@@ -180,6 +180,7 @@ struct TileBootArgs {
                              // by the group's slabs (not with pairs); failures take the list pass over `wide`
   int SG = 0;                // slabs per group (<= 8, SG x nb <= 128)
   int kcap = 4;              // rows per slab at most (tests force the list pass with fewer)
+  int list_cap = 0;          // slabs the list pass takes at most (0: 16384; tests force the overflow to k_boot2)
   const unsigned char* W8g = nullptr;  // [nsets][ncells][groups][4 windows][32] the group's boots 32 w + j
                                        // as pair slots (boot 32 w + j, 32 w + 16 + j), 0 past its boots
 };

@@ -2214,6 +2214,9 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   __shared__ double etab[64];
   const int lane = threadIdx.x & 63;
   const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // list mode: blocks past the list's end leave before the block barrier (the list pass is
+  // launched for the longest list the first pass may build; most of its blocks find no item)
+  if (ilist && xcd_block(blockIdx.x, gridDim.x) * WB >= ilist[0]) return;
   if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
   __syncthreads();
   // the bound staging area, once the bound loops are done: slab B's bounds | tile partial sums
@@ -2496,7 +2499,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8g, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int kcap, int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order,
-    unsigned* __restrict__ pmask, int* __restrict__ wide) {
+    unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
   constexpr int WB = 4;
   // bound staging of the four waves; once the bounds are in gub: row maxima | tile sums | 1 / (S nboot)
@@ -2660,8 +2663,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     if (__ballot(need)) {
       if (lane == 0) {
         atomicOr(&failm, 1u << s);
-        wide[1 + atomicAdd(&wide[0], 1)] = g * P + s0 + s;
-        if (stats) atomicAdd(&stats[35], 1);
+        const int q = g * P + s0 + s;
+        const int pos = atomicAdd(&wide[0], 1);
+        if (pos < wide_cap) {  // the four-tile list pass
+          wide[1 + pos] = q;
+          if (stats) atomicAdd(&stats[35], 1);
+        } else {  // past the list pass's launch: k_boot2 takes the slab whole
+          redo[q] = 1;
+          redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = q;
+          pmask[q] = ~0u;
+          if (stats) atomicAdd(&stats[3], 1);
+        }
       }
     } else if (lane < nl && !(fabs((double)fmx[s][lane]) <= degen_thresh)) {
       degen[g] = 1;
@@ -3775,7 +3787,9 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   constexpr int WB = 4;
   const long long items1 = pairs ? (long long)a.ngenes * ((P + 1) / 2) : items;
   // slabs a pair pass (or a gene block) may leave to the four-tile list pass
-  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? items : 0;
+  // (gene blocks: at most list_cap slabs, 16384 by default; k_boot_gene sends further failures to k_boot2)
+  const long long gene_cap = tb.list_cap > 0 ? tb.list_cap : 16384;
+  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(items, gene_cap) : 0;
   const long long gblocks = gene ? (long long)a.ngenes * ((P + tb.SG - 1) / tb.SG) : 0;
 #define SCDE_BT(NBV)                                                                                              \
   case NBV:                                                                                                        \
@@ -3783,7 +3797,8 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
       hipLaunchKernelGGL(k_boot_gene<NBV>, dim3((unsigned)gblocks), dim3(256), 0, s, a.D, a.ent, a.nnz,           \
                          a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
                          a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
-                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide); \
+                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide,  \
+                         (int)items2);                                                                     \
     else                                                                                                           \
     hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
                        a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,      \

@@ -45,12 +45,14 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("pair_cells", opts.get("pair_cells", 1000))
     ctx.set_option("gene_blocks", opts.get("gene_blocks", 1))
     ctx.set_option("gene_rows", opts.get("gene_rows", 4))
+    ctx.set_option("gene_list_cap", opts.get("gene_list_cap", 0))
     ctx.set_option("unique_fixed", opts.get("unique_fixed", 1))
     ctx.set_option("lanes", opts.get("lanes", 2))
     ctx.set_option("pipeline_mb", opts.get("pipeline_mb", 32))
     ctx.set_option("pieces", opts.get("pieces", 4))
     ctx.set_option("defer_boot", opts.get("defer_boot", 0))
     ctx.set_option("upload_staged", opts.get("upload_staged", 0))
+    ctx.set_option("lane_thread", opts.get("lane_thread", 0))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -70,12 +72,14 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("pair_cells", 1000)
         ctx.set_option("gene_blocks", 1)
         ctx.set_option("gene_rows", 4)
+        ctx.set_option("gene_list_cap", 0)
         ctx.set_option("unique_fixed", 1)
         ctx.set_option("lanes", 2)
         ctx.set_option("pipeline_mb", 32)
         ctx.set_option("pieces", 4)
         ctx.set_option("defer_boot", 0)
         ctx.set_option("upload_staged", 0)
+        ctx.set_option("lane_thread", 0)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -95,6 +99,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-slab-waves": {"gene_blocks": 0},
         "tiles-slab-waves-redo": {"gene_blocks": 0, "tile_groups": 2},
         "gene-forced-list": {"gene_rows": 1},
+        "gene-list-overflow": {"gene_rows": 1, "gene_list_cap": 40},
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
         "one-lane": {"lanes": 1},
@@ -102,6 +107,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1},
         "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1},
         "pipelined-staged": {"pipeline_mb": 0, "pieces": 3, "upload_staged": 1},
+        "pipelined-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1},
         "tiles-pairs": {"pair_cells": 1, "gene_blocks": 0},
         "tiles-pairs-redo": {"pair_cells": 1, "tile_groups": 2, "gene_blocks": 0},
         "tiles-mult-fallback": {"tile_max_mult": 1},
@@ -121,6 +127,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
             assert stats["boot_path"] == 1 and stats["skip_redo"] > 0, stats
         elif name == "gene-forced-list":  # gene blocks with one row per slab: the list pass finishes the rest
             assert stats["boot_path"] == 1 and stats["pair_redo"] > 0 and stats["skip_slabs"] > 0, stats
+        elif name == "gene-list-overflow":  # ... past its 40 slabs the failures go to k_boot2 directly
+            assert stats["boot_path"] == 1 and 0 < stats["pair_redo"] <= 80 and stats["skip_redo"] > 0, stats  # 40 per lane
         elif name == "tiles-pairs":
             # two slabs per wave, two bound tiles each: at these cell counts many slabs need more and
             # take the four-tile list pass
@@ -144,8 +152,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
                         what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
-                                    "gene-forced-list", "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
-                                    "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "tiles-pairs",
+                                    "gene-forced-list", "gene-list-overflow", "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
+                                    "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
+                                    "tiles-pairs",
                                     "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
         for name in others:
             for i in range(2):
