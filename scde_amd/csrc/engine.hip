@@ -368,6 +368,7 @@ struct scde_ctx {
     // pinned landing area of the phases' device -> host size read-backs: the set's own (not
     // the shared staging arena), so no later staging can recycle it before the host reads it
     int fixed_flags = 0;  // unique_phase12_fixed's flags when no pinned landing area exists
+    int woff_fixed = 0;   // entries of woff holding the fixed offsets c * 1024 (0: other contents)
     int* pin_land = nullptr;
     size_t pin_land_cap = 0;  // ints
     const int* pin_in = nullptr;  // this phase's read-back (pin_land, or null: pageable fallback)
@@ -398,6 +399,7 @@ struct scde_ctx {
     void release() {
       Buf* b[] = {&cellidx, &cmax, &cmin, &woff, &bits, &rank, &nuniq, &ucl, &ucl_off, &uci, &flags, &tasks};
       for (Buf* x : b) x->release();
+      woff_fixed = 0;
       if (pin_land) (void)hipHostFree(pin_land);
       pin_land = nullptr;
       pin_land_cap = 0;
@@ -668,6 +670,7 @@ int unique_phase2(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     u.woff_h[c + 1] = u.woff_h[c] + ((long long)u.cmax_h[c] >> 6) + 1;
   }
   RCHK(upload(cx, u.woff, u.woff_h.data(), sizeof(long long) * (C + 1)));
+  u.woff_fixed = 0;
   HCHK(u.bits.ensure(sizeof(unsigned long long) * u.woff_h[C]));
   HCHK(hipMemsetAsync(u.bits.p, 0, sizeof(unsigned long long) * u.woff_h[C], st));
   HCHK(launch_mark(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.woff.as<long long>(),
@@ -722,23 +725,32 @@ int unique_phase12_fixed(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   RCHK(upload(cx, u.cellidx, s.cellidx_host, sizeof(int) * C));
   u.woff_h.resize(C + 1);
   for (int c = 0; c <= C; ++c) u.woff_h[c] = (long long)c * kUniqueFixedWords;
-  RCHK(upload(cx, u.woff, u.woff_h.data(), sizeof(long long) * (C + 1)));
-  HCHK(u.bits.ensure(sizeof(unsigned long long) * u.woff_h[C]));
-  HCHK(hipMemsetAsync(u.bits.p, 0, sizeof(unsigned long long) * u.woff_h[C], st));
-  HCHK(u.flags.ensure(sizeof(int)));
-  HCHK(hipMemsetAsync(u.flags.p, 0, sizeof(int), st));
+  // the fixed offsets c * 1024 are uploaded once per set (grow-only; exact-width builds reset it)
+  if (u.woff_fixed < C + 1) {
+    RCHK(upload(cx, u.woff, u.woff_h.data(), sizeof(long long) * (C + 1)));
+    u.woff_fixed = C + 1;
+  }
+  // one memset for the bitmaps and k_mark's flag word after them
+  HCHK(u.bits.ensure(sizeof(unsigned long long) * (u.woff_h[C] + 1)));
+  HCHK(hipMemsetAsync(u.bits.p, 0, sizeof(unsigned long long) * (u.woff_h[C] + 1), st));
+  int* flags = reinterpret_cast<int*>(u.bits.as<unsigned long long>() + u.woff_h[C]);
   HCHK(launch_mark(s.counts_dev, s.ld, 0, N, C, u.cellidx.as<int>(), u.woff.as<long long>(),
-                   u.bits.as<unsigned long long>(), st, u.flags.as<int>()));
+                   u.bits.as<unsigned long long>(), st, flags));
   HCHK(u.rank.ensure(sizeof(int) * u.woff_h[C]));
-  HCHK(u.nuniq.ensure(sizeof(int) * C));
+  HCHK(u.nuniq.ensure(sizeof(int) * (C + 1)));
   HCHK(launch_rank(u.bits.as<unsigned long long>(), u.woff.as<long long>(), C, u.rank.as<int>(),
-                   u.nuniq.as<int>(), st));
+                   u.nuniq.as<int>(), st, flags, u.nuniq.as<int>() + C));
   u.nuniq_h.assign(C, 0);
   u.fixed_flags = 0;
   int* h = u.landing(2 * (size_t)C + 1);
   u.pin_in = h;
-  HCHK(hipMemcpyAsync(h ? h : u.nuniq_h.data(), u.nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
-  HCHK(hipMemcpyAsync(h ? h + C : &u.fixed_flags, u.flags.p, sizeof(int), hipMemcpyDeviceToHost, st));
+  // the unique counts and the flags (nuniq[C]) in one read-back
+  if (h) {
+    HCHK(hipMemcpyAsync(h, u.nuniq.p, sizeof(int) * (C + 1), hipMemcpyDeviceToHost, st));
+  } else {
+    HCHK(hipMemcpyAsync(u.nuniq_h.data(), u.nuniq.p, sizeof(int) * C, hipMemcpyDeviceToHost, st));
+    HCHK(hipMemcpyAsync(&u.fixed_flags, u.nuniq.as<int>() + C, sizeof(int), hipMemcpyDeviceToHost, st));
+  }
   return SCDE_OK;
 }
 

@@ -274,7 +274,8 @@ hipError_t launch_mark(const int* counts, long long ld, long long g0, int ngenes
                        const long long* woff, unsigned long long* bits, hipStream_t s,
                        int* flags = nullptr);
 hipError_t launch_rank(const unsigned long long* bits, const long long* woff, int ncells, int* rank, int* nuniq,
-                       hipStream_t s);
+                       hipStream_t s,
+                       const int* flags_in = nullptr, int* flags_out = nullptr);
 hipError_t launch_fill_ucl(const unsigned long long* bits, const long long* woff, int ncells, const int* rank,
                            const long long* ucl_off, int* ucl, hipStream_t s);
 hipError_t launch_uci(const int* counts, long long ld, long long g0, int ngenes, int ncells, const int* cellidx,

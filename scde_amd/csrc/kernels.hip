@@ -3017,7 +3017,8 @@ __global__ __launch_bounds__(256) void k_mark(const int* __restrict__ counts, lo
 // per cell: exclusive popcount prefix of its bitmap words -> rank, and #unique
 __global__ __launch_bounds__(256) void k_rank(const unsigned long long* __restrict__ bits,
                                               const long long* __restrict__ woff, int* __restrict__ rank,
-                                              int* __restrict__ nuniq) {
+                                              int* __restrict__ nuniq, const int* __restrict__ flags_in,
+                                              int* __restrict__ flags_out) {
   __shared__ int wsum[4];
   __shared__ int carry;
   const int c = blockIdx.x;
@@ -3043,6 +3044,8 @@ __global__ __launch_bounds__(256) void k_rank(const unsigned long long* __restri
     __syncthreads();
   }
   if (threadIdx.x == 0) nuniq[c] = carry;
+  // k_mark's flags next to the counts (one read-back for both; k_mark ran before in stream order)
+  if (flags_in && c == 0 && threadIdx.x == 0) *flags_out = *flags_in;
 }
 
 __global__ __launch_bounds__(256) void k_fill_ucl(const unsigned long long* __restrict__ bits,
@@ -3930,9 +3933,9 @@ hipError_t launch_mark(const int* counts, long long ld, long long g0, int ngenes
 }
 
 hipError_t launch_rank(const unsigned long long* bits, const long long* woff, int ncells, int* rank, int* nuniq,
-                       hipStream_t s) {
+                       hipStream_t s, const int* flags_in, int* flags_out) {
   if (ncells <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rank, dim3(ncells), dim3(256), 0, s, bits, woff, rank, nuniq);
+  hipLaunchKernelGGL(k_rank, dim3(ncells), dim3(256), 0, s, bits, woff, rank, nuniq, flags_in, flags_out);
   return hipGetLastError();
 }
 
