@@ -247,7 +247,7 @@ struct scde_ctx {
   char* pin = nullptr;
   size_t pin_off = 0;
   // workspace
-  Buf models, mag, mu, lcfp, lcfpr, theta, cellscal, pq, colc, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
+  Buf models, mag, mu, lcfp, cfp, lcfpr, theta, cellscal, pq, colc, T, E, maxi, has_clamp, base_col, zcol, ent, nnz, Wt, Z, draws,
       ubound, zubound, smask, subuf, sredo,
       degen, wset, prior_y, diffv, jpA, jpB, res, ratio, in1, in2, outbuf, part, bhw;
   // scde.expression.prior
@@ -285,6 +285,8 @@ struct scde_ctx {
   int opt_modes_overlap = 1;     // "modes_overlap": scde.posteriors' posterior-mode read-back overlaps the bootstrap
                                  // on the copy stream (0: after it, on the main stream -- rocprofv3 runs, where the
                                  // pageable read-back becomes blit kernels that would share the CUs)
+  int opt_gene_waves = 0;        // "gene_waves": k_boot_gene's waves per block, 3 or 4 (0: by gene3_cells)
+  int opt_gene3_cells = 1000;    // "gene3_cells": cells per call from which k_boot_gene runs 3-wave blocks
   int opt_gene_list_cap = 0;     // "gene_list_cap": slabs k_boot_gene's list pass takes at most (0: 16384; tests)
   int opt_gene_rows = 4;         // "gene_rows": rows per slab k_boot_gene gives each slab at most (tests force its
                                  // four-tile list pass with fewer)
@@ -495,7 +497,7 @@ struct scde_ctx {
     for (auto& e : piece_up_ev)
       if (e) (void)hipEventDestroy(e);
     if (uq_stream) (void)hipStreamDestroy(uq_stream);
-    Buf* all[] = {&models, &mag, &mu,  &lcfp, &lcfpr, &theta,  &cellscal, &pq, &colc, &T,      &E,      &maxi,
+    Buf* all[] = {&models, &mag, &mu,  &lcfp, &cfp, &lcfpr, &theta,  &cellscal, &pq, &colc, &T,      &E,      &maxi,
                   &has_clamp, &base_col, &zcol, &ent, &nnz, &Wt, &Z, &draws, &degen, &wset, &prior_y, &diffv,
                   &jpA,    &jpB, &res,   &ratio, &in1, &in2, &outbuf, &part, &bhw, &ubound, &zubound, &smask, &subuf, &sredo};
     for (Buf* b : all) b->release();
@@ -851,6 +853,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   const size_t cg = sizeof(double) * (size_t)C * GS;
   HCHK(cx->mu.ensure(cg));
   HCHK(cx->lcfp.ensure(cg));
+  HCHK(cx->cfp.ensure(cg));
   HCHK(cx->lcfpr.ensure(cg));
   HCHK(cx->theta.ensure(cg));
   HCHK(cx->cellscal.ensure(sizeof(double) * 2 * C));
@@ -858,7 +861,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   if (!s.localtheta) HCHK(cx->pq.ensure(4 * cg));
   HCHK(launch_cell_prep(cx->models.as<double>(), C, G, GS, cx->mag.as<double>(), s.localtheta, s.squarelogit,
                         cx->mu.as<double>(), cx->lcfp.as<double>(), cx->lcfpr.as<double>(), cx->theta.as<double>(),
-                        cx->cellscal.as<double>(), s.localtheta ? nullptr : cx->pq.as<double>(), st));
+                        cx->cellscal.as<double>(), s.localtheta ? nullptr : cx->pq.as<double>(), st,
+                        cx->cfp.as<double>()));
   cx->mark_end(SLOT_OTHER, ev);
   // ---- unique counts (prebuilt by build_unique_sets when u.ready; piece by piece with the
   // tables below when the counts arrive in pieces)
@@ -957,6 +961,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     ta.const_theta = s.localtheta ? 0 : 1;
     ta.pq = s.localtheta ? nullptr : cx->pq.as<double>();
     ta.colc = s.localtheta ? nullptr : cx->colc.as<double>();
+    ta.cfp = cx->cfp.as<double>();
     ta.use_baseline = s.use_baseline ? 1 : 0;
     ta.UQ = p.tpath ? cx->ubound.as<unsigned>() : nullptr;
     ta.nanflag = p.tpath ? cx->qflags.as<int>() : nullptr;
@@ -1326,6 +1331,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           tb.SG = gene_sg;
           tb.kcap = cx->opt_gene_rows;
           tb.list_cap = cx->opt_gene_list_cap;
+          // 12 rows per gene block from gene3_cells cells per call (slabs mostly need two tiles there)
+          tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (C >= cx->opt_gene3_cells ? 3 : 4);
           tb.W8g = cx->w8g.as<unsigned char>();
         }
         if (have_order) tb.order = cx->gorder.as<int>();
@@ -1628,6 +1635,8 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "modes_overlap") ctx->opt_modes_overlap = value != 0;
   else if (n == "upload_staged") ctx->opt_upload_staged = value != 0;
   else if (n == "upload_threads") ctx->opt_upload_threads = std::max(1, std::min(32, (int)value));
+  else if (n == "gene_waves") ctx->opt_gene_waves = (value == 3 || value == 4) ? (int)value : 0;
+  else if (n == "gene3_cells") ctx->opt_gene3_cells = (int)value;
   else if (n == "gene_list_cap") ctx->opt_gene_list_cap = std::max(0, (int)value);
   else if (n == "gene_rows") ctx->opt_gene_rows = std::max(1, std::min(4, (int)value));
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
@@ -2371,6 +2380,8 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_gene_blocks = cx->opt_gene_blocks;
   p->opt_gene_rows = cx->opt_gene_rows;
   p->opt_gene_list_cap = cx->opt_gene_list_cap;
+  p->opt_gene_waves = cx->opt_gene_waves;
+  p->opt_gene3_cells = cx->opt_gene3_cells;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;

@@ -7,8 +7,17 @@
 #ifndef SCDE_BOOT_ASMLD
 #define SCDE_BOOT_ASMLD 1  // k_boot2 column look-ahead issued from asm with explicit vmcnt waits
 #endif
+#ifndef SCDE_NB_CLOSED
+#define SCDE_NB_CLOSED 1  // k_tables_reg: the NB log-pmf in closed form (0: nmath's saddle-point form)
+#endif
 #ifndef SCDE_TABREG_WPE
-#define SCDE_TABREG_WPE 3  // k_tables_reg occupancy target (waves per SIMD; 4-wave blocks)
+// k_tables_reg occupancy target (waves per SIMD; 4-wave blocks): the closed form's seven staged
+// rows (36 KB of LDS per block) and 118 VGPRs allow four blocks per CU
+#if SCDE_NB_CLOSED
+#define SCDE_TABREG_WPE 4
+#else
+#define SCDE_TABREG_WPE 3
+#endif
 #endif
 #ifndef SCDE_TABREG_G401
 #define SCDE_TABREG_G401 1  // k_tables_reg specialised for the default 401-point grid
@@ -64,6 +73,7 @@ struct TablesArgs {
   int const_theta;           // theta is the same at every grid point (no local theta fit)
   const double* pq;          // [ncells][4][GS] p, q, log p, log q (const_theta), nullable
   const double* colc;        // [ncols][kColc] k_col_consts output (with pq), nullable
+  const double* cfp = nullptr;  // [ncells][GS] exp(lcfp) from k_cell_prep (nullable: computed when staged)
   // Fused baseline-delta output (bootstrap path; the k_delta pass folded into the tables):
   //   phase 0: every column -> T (no D);
   //   phase 1: one wave per cell, its count-0 column -> D (and T if non-null); writes
@@ -181,6 +191,7 @@ struct TileBootArgs {
   int SG = 0;                // slabs per group (<= 8, SG x nb <= 128)
   int kcap = 4;              // rows per slab at most (tests force the list pass with fewer)
   int list_cap = 0;          // slabs the list pass takes at most (0: 16384; tests force the overflow to k_boot2)
+  int gene_waves = 4;        // k_boot_gene waves per block: 4 (16 rows) or 3 (12 rows; wide calls)
   const unsigned char* W8g = nullptr;  // [nsets][ncells][groups][4 windows][32] the group's boots 32 w + j
                                        // as pair slots (boot 32 w + j, 32 w + 16 + j), 0 past its boots
 };
@@ -241,7 +252,7 @@ struct RatioArgs {
 
 hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,
                             double* mu, double* lcfp, double* lcfpr, double* theta, double* cellscal,
-                            double* pq, hipStream_t s);
+                            double* pq, hipStream_t s, double* cfp = nullptr);
 hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long ncols, int ncells,
                              const double* theta, int GS, const double* cellscal, double* colc, hipStream_t s);
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s);

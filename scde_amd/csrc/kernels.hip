@@ -98,7 +98,7 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
                                                    int squarelogit, double* __restrict__ mu,
                                                    double* __restrict__ lcfp, double* __restrict__ lcfpr,
                                                    double* __restrict__ theta, double* __restrict__ cellscal,
-                                                   double* __restrict__ pq) {
+                                                   double* __restrict__ pq, double* __restrict__ cfpo) {
   const int c = blockIdx.x;
   auto M = [&](int col) { return models[(long long)c + (long long)ncells * col]; };
   const double concb = M(0), conca = M(1), failr = M(2), corrb = M(3), corra = M(4), corrt = M(5);
@@ -114,6 +114,7 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
     const double lc = log(cf);
     lcfpr[(long long)c * GS + k] = log(1.0 - cf);
     lcfp[(long long)c * GS + k] = lc;
+    if (cfpo) cfpo[(long long)c * GS + k] = exp(lc);  // k_tables_reg's staged cfp (exp of the stored log)
     lmax = gt_max(lmax, lc);
     double th = corrt;
     if (localtheta) {
@@ -193,9 +194,6 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
   o[10] = f.ok ? ((f.lp + f.S) - f.hlf) - f.X * f.lXn - f.nx * f.lnxn : 0.0;
 }
 
-#ifndef SCDE_NB_CLOSED
-#define SCDE_NB_CLOSED 1  // k_tables_reg: the NB log-pmf in closed form (0: nmath's saddle-point form)
-#endif
 #ifndef SCDE_KT_DIAG
 #define SCDE_KT_DIAG 0  // timing-only builds: 1 trivial dnbinom, 2 no exp, 4 no log, 8 no stores, 16 loop 1
                         // only, 32 staging and constants only, 64 no tile bounds
@@ -655,7 +653,12 @@ __device__ __forceinline__ float wave_maxf(float v) {
 // LDS read is lane * 8 plus an immediate offset: no per-chunk address registers (the
 // compiler would hoist ~8 per chunk out of the column loop and spill them).
 constexpr int kRS = kTabStagedG;
-enum { kRowMu = 0, kRowP = 1, kRowLcfpr = 5, kRowCfp = 6, kRowLcfp = 7, kRowBase = 8, kTabRegRows = 9 };
+#if SCDE_NB_CLOSED  // the closed form reads log p, log q only: seven staged rows (four blocks of 4 waves per CU)
+enum { kRowMu = 0, kRowLP = 1, kRowLQ = 2, kRowLcfpr = 3, kRowCfp = 4, kRowLcfp = 5, kRowBase = 6, kTabRegRows = 7 };
+#else
+enum { kRowMu = 0, kRowP = 1, kRowLP = 3, kRowLQ = 4, kRowLcfpr = 5, kRowCfp = 6, kRowLcfp = 7, kRowBase = 8,
+       kTabRegRows = 9 };
+#endif
 
 // Per grid point k of a column, in log space relative to maxp: t1 = nb_k + log(1 - cfp_k)
 // - maxp (the NB term) and t2 = log cfp_k + fp - maxp (the Poisson term); the reference's
@@ -711,8 +714,12 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       const int k = lane + 64 * j;
       const bool in = k < G;
       const bool last = (k == G - 1);
+#if SCDE_NB_CLOSED
+      double pr = 0.0, qr = 0.0;  // (the saddle-point form's p, q: not staged)
+#else
       double pr = sl[kRowP * kRS + 64 * j], qr = sl[(kRowP + 1) * kRS + 64 * j];
-      double lpr = sl[(kRowP + 2) * kRS + 64 * j], lqr = sl[(kRowP + 3) * kRS + 64 * j];
+#endif
+      double lpr = sl[kRowLP * kRS + 64 * j], lqr = sl[kRowLQ * kRS + 64 * j];
       const double muv = sl[kRowMu * kRS + 64 * j], mnext = sl[kRowMu * kRS + 64 * j + 1];
       const bool over = in && ((!last && x > muv && x < mnext) || (last && x > muv));
       KT_EVENT(12, over);
@@ -762,8 +769,13 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
         const double muv = sm[kRowMu * kRS + k], mnext = sm[kRowMu * kRS + k + 1];
         const bool last = (k == G - 1);
         const bool over = (!last && x > muv && x < mnext) || (last && x > muv);
+#if SCDE_NB_CLOSED
+        const double pr = po, qr = 1 - po;  // (never reached: the closed form has no exact-path lanes)
+        (void)over;
+#else
         const double pr = over ? po : sm[kRowP * kRS + k];
         const double qr = over ? 1 - po : sm[(kRowP + 1) * kRS + k];
+#endif
         if (qr == 0.0 && pr == 1.0)
           nv = nbq0;
         else
@@ -898,7 +910,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 
 template <int BM, int GC>
 __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TABREG_WPE))) void k_tables_reg(TablesArgs a) {
-  __shared__ double sm[kTabRegRows * kRS];  // mu | p | q | log p | log q | lcfpr | cfp | lcfp | base
+  __shared__ double sm[kTabRegRows * kRS];  // mu | [p | q |] log p | log q | lcfpr | cfp | lcfp | base
   __shared__ double etab[64];
   __shared__ double ltab[3][97];
   __shared__ unsigned suqb[kQTiles];
@@ -933,13 +945,15 @@ __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_
   for (int k = threadIdx.x; k < kRS; k += 64 * kTabRegWaves) {
     const bool in = k < G;
     sm[kRowMu * kRS + k] = in ? a.mu[co + k] : 0.0;
+#if !SCDE_NB_CLOSED
     sm[kRowP * kRS + k] = in ? P[k] : 0.0;
     sm[(kRowP + 1) * kRS + k] = in ? P[GS + k] : 0.0;
-    sm[(kRowP + 2) * kRS + k] = in ? P[2 * GS + k] : 0.0;
-    sm[(kRowP + 3) * kRS + k] = in ? P[3 * GS + k] : 0.0;
+#endif
+    sm[kRowLP * kRS + k] = in ? P[2 * GS + k] : 0.0;
+    sm[kRowLQ * kRS + k] = in ? P[3 * GS + k] : 0.0;
     sm[kRowLcfpr * kRS + k] = in ? a.lcfpr[co + k] : 0.0;
     const double lc = in ? a.lcfp[co + k] : -INFINITY;
-    sm[kRowCfp * kRS + k] = exp(lc);
+    sm[kRowCfp * kRS + k] = in ? (a.cfp ? a.cfp[co + k] : exp(lc)) : 0.0;  // exp(-inf) = 0 past the grid
     sm[kRowLcfp * kRS + k] = lc;
     sm[kRowBase * kRS + k] = (in && bc >= 0) ? a.D[(long long)bc * GS + k] : 0.0;
   }
@@ -2111,6 +2125,87 @@ __device__ __forceinline__ void tile_bound_pass(const int2* __restrict__ E, int 
       }
 }
 
+// tile_bound_pass over the 64-entry chunks c0, c0 + cstep, ... only and without the baseline part:
+// the combined digit sums of each (tile t, boot b < nbout) are added into dsum[t * 32 + b] (int64,
+// exact: the bound is linear in the digit sums, so the waves' partial values add up to the full one)
+__device__ __forceinline__ void tile_bound_partial(const int2* __restrict__ E, int n, const unsigned* __restrict__ UQ,
+                                                const unsigned char* __restrict__ W8, unsigned cstride,
+                                                int c0, int cstep, unsigned* stage, long long* dsum, int nbout,
+                                                int NTB, int lane) {
+  const int r = lane & 15, h = lane >> 4;
+  unsigned* sq = stage;         // [tile t][entry l] tile bounds (64 x 16 words)
+  unsigned* sw = stage + 1024;  // [pair r][entry l / 2] multiplicity pairs (two entries a word)
+  const int KP = (n + 63) & ~63;
+  const int t = r;
+  i32x4 acc[2][4];
+#pragma unroll
+  for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+    for (int l = 0; l < 4; ++l)
+      acc[bt][l] = i32x4{0, 0, 0, 0};
+  for (int e0 = 64 * c0; e0 < KP; e0 += 64 * cstep) {
+    const int2 en = E[e0 + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
+    const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
+    const uint4 q0 = uq[0], q1 = uq[1], q2 = uq[2], q3 = uq[3];
+    const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * cstride));
+    const uint4 w0 = wp[0], w1 = wp[1];
+    wave_sync();  // the previous chunk's fragment reads are done before the area is rewritten
+    const unsigned qv[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                             q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+#pragma unroll
+    for (int tt = 0; tt < 16; ++tt) sq[tt * 64 + lane] = qv[tt];
+    // pairs (boot j, boot 16 + j) as 16-bit words: two entries per 32-bit LDS word
+    const unsigned wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    unsigned short* sw16 = reinterpret_cast<unsigned short*>(sw);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      sw16[(2 * j) * 64 + lane] = (unsigned short)(wv[j] & 0xffffu);
+      sw16[(2 * j + 1) * 64 + lane] = (unsigned short)(wv[j] >> 16);
+    }
+    wave_sync();
+    // B fragment: tile t's words of entries 16 h .. 16 h + 15
+    const uint4* bq = reinterpret_cast<const uint4*>(sq + t * 64 + 16 * h);
+    const uint4 b0v = bq[0], b1v = bq[1], b2v = bq[2], b3v = bq[3];
+    const unsigned u[16] = {b0v.x, b0v.y, b0v.z, b0v.w, b1v.x, b1v.y, b1v.z, b1v.w,
+                            b2v.x, b2v.y, b2v.z, b2v.w, b3v.x, b3v.y, b3v.z, b3v.w};
+    // A fragments: pair r of entries 16 h .. 16 h + 15 (two entries a word)
+    const uint4* aw = reinterpret_cast<const uint4*>(sw + r * 32 + 8 * h);
+    const uint4 a0v = aw[0], a1v = aw[1];
+    const unsigned x2[8] = {a0v.x, a0v.y, a0v.z, a0v.w, a1v.x, a1v.y, a1v.z, a1v.w};
+    i32x4 af[2];
+    unsigned lo4[4], hi4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      lo4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x06040200u);
+      hi4[q] = __builtin_amdgcn_perm(x2[2 * q + 1], x2[2 * q], 0x07050301u);
+    }
+    af[0] = i32x4{(int)lo4[0], (int)lo4[1], (int)lo4[2], (int)lo4[3]};
+    af[1] = i32x4{(int)hi4[0], (int)hi4[1], (int)hi4[2], (int)hi4[3]};
+    unsigned pl[4][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      tr4(u[4 * q], u[4 * q + 1], u[4 * q + 2], u[4 * q + 3], pl[0][q], pl[1][q], pl[2][q], pl[3][q]);
+#pragma unroll
+    for (int l = 0; l < 4; ++l) {
+      const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
+      acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
+      acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
+    }
+  }
+  if (t < NTB)
+#pragma unroll
+    for (int bt = 0; bt < 2; ++bt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int b = 16 * bt + 4 * h + q;
+        if (b < nbout) {
+          const long long v =
+              (((long long)acc[bt][3][q] * 256 + acc[bt][2][q]) * 256 + acc[bt][1][q]) * 256 + acc[bt][0][q];
+          atomicAdd(reinterpret_cast<unsigned long long*>(&dsum[t * 32 + b]), (unsigned long long)v);
+        }
+      }
+}
+
 // The rows of k_boot_tiles / k_boot_gene: a0/a1[i] = Z_b + sum_e W_be D_e at points k0, k0 + 1 of
 // boot b = b0 + i (k0 even: 16-byte aligned pairs; -inf where the point is dead).  Per ELL entry
 // one 16-byte column load (both points) and one 16-byte multiplicity load (boots 2J, 2J + 1 on
@@ -2489,10 +2584,13 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
 //      computed tiles in tile order, 1 / (S nboot), the partial jp rows.
 // Every value is formed exactly as in k_boot_tiles and k_boot2 (same fma chains, maxima, terms,
 // tile partials added in tile order), so the outputs are bit-identical to theirs.
-constexpr int kGeneRows = 16;    // 4 waves x 4 rows
-constexpr int kGeneSlabs = 8;    // slabs per group at most (K >= 2 rows each)
-template <int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_gene(
+constexpr int kGeneRowsMax = 16;  // 4 waves x 4 rows
+constexpr int kGeneSlabs = 8;     // slabs per group at most (K >= 2 rows each)
+// WB waves per block (4, or 3 for wide calls whose slabs mostly need two tiles: 12 rows for 5
+// slabs).  With 3 waves the fourth 32-boot bound window is split by entry chunks over the
+// three waves (tile_bound_partial, exact int64 sums in LDS), so no wave does two passes.
+template <int NB, int WB>
+__global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot_gene(
     const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
     const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
     int G, int GS, int P, int SG, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
@@ -2501,9 +2599,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     int kcap, int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order,
     unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
-  constexpr int WB = 4;
-  // bound staging of the four waves; once the bounds are in gub: row maxima | tile sums | 1 / (S nboot)
+  static_assert(WB == 3 || WB == 4, "3 or 4 waves per gene block");
+  constexpr int kGeneRows = 4 * WB;
+  // bound staging of the waves; once the bounds are in gub: row maxima | tile sums | 1 / (S nboot)
   __shared__ unsigned bstage[WB][1024 + 512];
+  __shared__ long long dsum[WB < 4 ? kBTileMax * 32 : 1];  // the split window's partial bounds
   __shared__ float gub[kBTileMax * 128];          // [bound tile][group boot] bounds
   __shared__ float sc[kGeneSlabs][16];            // [slab][bound tile] score
   __shared__ signed char rk[kGeneSlabs][16];      // [slab][rank] bound tile
@@ -2537,18 +2637,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   }
   if (threadIdx.x < 64) etab[threadIdx.x] = kExp2Frac64[threadIdx.x];
   if (threadIdx.x == 0) failm = 0u;
+  if (WB < 4) {
+    for (int i = threadIdx.x; i < kBTileMax * 32; i += 64 * WB) dsum[i] = 0;
+    __syncthreads();  // zeroed before any wave adds into it
+  }
   const int n = nnz[g];
   const int NT = (G + 15) >> 4, NTB = (G + 31) >> 5;  // 16-point sum tiles, 32-point bound tiles
   const int2* __restrict__ E = ent + (long long)g * ent_stride;
   const int set = wset ? wset[g] : 0;
   const int gb0 = s0 * NB, gnb = ns * NB;  // the group's boots (gnb <= 128)
-  // ---- 1. bounds of the group's boot window 32 wsid .. 32 wsid + 31
-  if (32 * wsid < gnb) {
-    const unsigned gstride = (unsigned)NGR * 128u;
-    const unsigned char* __restrict__ W8 = W8g + (long long)set * ncells * gstride + gr * 128 + 32 * wsid;
-    const int* __restrict__ ZU = ZUq + (long long)set * 4 * kQTiles * Bq + gb0 + 32 * wsid;
-    tile_bound_pass(E, n, UQ, W8, gstride, ZU, Bq, &bstage[wsid][0], gub + 32 * wsid, 128, min(32, gnb - 32 * wsid),
-                    NTB, lane);
+  const int NW = (gnb + 31) >> 5;          // 32-boot bound windows
+  const unsigned gstride = (unsigned)NGR * 128u;
+  const unsigned char* __restrict__ W8grp = W8g + (long long)set * ncells * gstride + gr * 128;
+  const int* __restrict__ ZUset = ZUq + (long long)set * 4 * kQTiles * Bq + gb0;
+  // ---- 1. bounds of the group's boot window 32 wsid .. 32 wsid + 31 (with 3 waves: the fourth
+  // window split by entry chunks)
+  if (wsid < NW)
+    tile_bound_pass(E, n, UQ, W8grp + 32 * wsid, gstride, ZUset + 32 * wsid, Bq, &bstage[wsid][0], gub + 32 * wsid, 128,
+                    min(32, gnb - 32 * wsid), NTB, lane);
+  if (WB < 4 && NW > WB) {  // (each wave stages in its own area: no barrier before the partial pass)
+    tile_bound_partial(E, n, UQ, W8grp + 32 * WB, gstride, wsid, WB, &bstage[wsid][0], dsum, min(32, gnb - 32 * WB),
+                       NTB, lane);
+    __syncthreads();
+    // the split window's bounds: the baseline part (ZU digits) plus the waves' partial sums
+    for (int i = threadIdx.x; i < NTB * 32; i += 64 * WB) {
+      const int t = i >> 5, b = i & 31;
+      if (b < gnb - 32 * WB) {
+        const int* zu = ZUset + 32 * WB + b;
+        const long long vz = (((long long)zu[(3LL * kQTiles + t) * Bq] * 256 + zu[(2LL * kQTiles + t) * Bq]) * 256 +
+                              zu[(1LL * kQTiles + t) * Bq]) * 256 + zu[(long long)t * Bq];
+        const double x = (double)(vz + dsum[t * 32 + b]) * 0x1p-8;
+        float f = (float)x;
+        if ((double)f < x) f = nextafterf(f, INFINITY);
+        gub[t * 128 + 32 * WB + b] = f;
+      }
+    }
   }
   __syncthreads();
   // ---- 2. the plan: per slab the score of each bound tile (its largest bound over the live boots)
@@ -2562,7 +2685,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
       }
       sc[s][t] = v;
       rowof[s][t] = -1;
-    } else if (s < kGeneSlabs + 1) {
+    } else if (s < kGeneSlabs + 1 && t < kGeneRows) {
       rowS[t] = -1;
       rowT[t] = 0;
     }
@@ -2636,12 +2759,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
   }
   __syncthreads();
   {
-    const int s = threadIdx.x >> 5, i = threadIdx.x & 31;
-    if (s < ns && i < NB) {
-      float m = -INFINITY;
-      for (int q2 = 0; q2 < kGeneRows; ++q2)
-        if (rowS[q2] == s) m = gt_maxf(m, rowmax[q2 * 32 + i]);
-      fmx[s][i] = m;
+    for (int x = threadIdx.x; x < ns * 32; x += 64 * WB) {
+      const int s = x >> 5, i = x & 31;
+      if (i < NB) {
+        float m = -INFINITY;
+        for (int q2 = 0; q2 < kGeneRows; ++q2)
+          if (rowS[q2] == s) m = gt_maxf(m, rowmax[q2 * 32 + i]);
+        fmx[s][i] = m;
+      }
     }
     if ((int)threadIdx.x < ns) {  // the slab's computed bound tiles and the rows holding them
       unsigned b = 0;
@@ -2700,9 +2825,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_W
     if (m2 == 0 && live) tsum[(2 * q + (slot & 1)) * NB + i] = ps;
   }
   __syncthreads();
-  {
-    const int s = threadIdx.x >> 5, b = threadIdx.x & 31;
-    if (s < ns && b < NB && !((fm >> s) & 1)) {
+  for (int x = threadIdx.x; x < ns * 32; x += 64 * WB) {
+    const int s = x >> 5, b = x & 31;
+    if (b < NB && !((fm >> s) & 1)) {
       double S = 0.0;
       for (unsigned mm = bd[s]; mm; mm &= mm - 1) {  // bound tiles in order, their two sum tiles
         const int t = __builtin_ffs((int)mm) - 1;
@@ -3502,10 +3627,10 @@ static inline int div_up(long long a, long long b) { return (int)((a + b - 1) / 
 
 hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,
                             double* mu, double* lcfp, double* lcfpr, double* theta, double* cellscal,
-                            double* pq, hipStream_t s) {
+                            double* pq, hipStream_t s, double* cfp) {
   if (ncells <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_cell_prep, dim3(ncells), dim3(256), 0, s, models, ncells, G, GS, mag, lt, sq, mu, lcfp,
-                     lcfpr, theta, cellscal, lt ? nullptr : pq);
+                     lcfpr, theta, cellscal, lt ? nullptr : pq, cfp);
   return hipGetLastError();
 }
 
@@ -3796,8 +3921,14 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   const long long gblocks = gene ? (long long)a.ngenes * ((P + tb.SG - 1) / tb.SG) : 0;
 #define SCDE_BT(NBV)                                                                                              \
   case NBV:                                                                                                        \
-    if (gene)                                                                                                      \
-      hipLaunchKernelGGL(k_boot_gene<NBV>, dim3((unsigned)gblocks), dim3(256), 0, s, a.D, a.ent, a.nnz,           \
+    if (gene && tb.gene_waves == 3)                                                                                \
+      hipLaunchKernelGGL((k_boot_gene<NBV, 3>), dim3((unsigned)gblocks), dim3(192), 0, s, a.D, a.ent, a.nnz,      \
+                         a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
+                         a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
+                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide,  \
+                         (int)items2);                                                                     \
+    else if (gene)                                                                                                 \
+      hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3((unsigned)gblocks), dim3(256), 0, s, a.D, a.ent, a.nnz,      \
                          a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
                          a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
                          tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide,  \

@@ -46,6 +46,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("gene_blocks", opts.get("gene_blocks", 1))
     ctx.set_option("gene_rows", opts.get("gene_rows", 4))
     ctx.set_option("gene_list_cap", opts.get("gene_list_cap", 0))
+    ctx.set_option("gene_waves", opts.get("gene_waves", 0))
     ctx.set_option("unique_fixed", opts.get("unique_fixed", 1))
     ctx.set_option("lanes", opts.get("lanes", 2))
     ctx.set_option("pipeline_mb", opts.get("pipeline_mb", 32))
@@ -73,6 +74,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("gene_blocks", 1)
         ctx.set_option("gene_rows", 4)
         ctx.set_option("gene_list_cap", 0)
+        ctx.set_option("gene_waves", 0)
         ctx.set_option("unique_fixed", 1)
         ctx.set_option("lanes", 2)
         ctx.set_option("pipeline_mb", 32)
@@ -100,6 +102,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-slab-waves-redo": {"gene_blocks": 0, "tile_groups": 2},
         "gene-forced-list": {"gene_rows": 1},
         "gene-list-overflow": {"gene_rows": 1, "gene_list_cap": 40},
+        "gene-3waves": {"gene_waves": 3},
+        "gene-4waves": {"gene_waves": 4},
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
         "one-lane": {"lanes": 1},
@@ -152,7 +156,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
                         what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
-                                    "gene-forced-list", "gene-list-overflow", "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
+                                    "gene-forced-list", "gene-list-overflow", "gene-3waves", "gene-4waves",
+                                    "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
                                     "tiles-pairs",
                                     "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
