@@ -157,6 +157,13 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   upload on a copy stream in column pieces that the kernels follow (default 32)
  *   "pieces"        pieces of that upload (the DE call's first group; the posteriors call's
  *                   selected cells), 1..8 (default 4); results are the same
+ *   "lane_thread"   1/0  a pipelined two-lane DE call drives the second lane (its unique sets,
+ *                   tables and bootstrap) from a host thread of its own (results are the same)
+ *   "upload_staged" 1/0  host counts go up through a pinned ring filled by "upload_threads"
+ *                   copy threads instead of pageable copies (default 0: measured no faster)
+ *   "gene_waves"    3/4  k_boot_gene's waves per block (12 or 16 rows); 0 (default) = 3 from
+ *                   "gene3_cells" cells per call (default: never; slower at config 4), else 4
+ *   "gene_list_cap" slabs k_boot_gene's four-tile list pass takes (0 = 16384; beyond: k_boot2)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
@@ -166,7 +173,10 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  * (k_boot_tiles slabs computing i tiles), "pair_redo" (slabs a pair pass left to the four-tile
  * pass) (with skip_stats); "boot_f64_fma" (FP64 lane FMAs the
  * bootstrap kernels issued), also with skip_stats; "boot_path": the bootstrap kernel of the last
- * posterior (0 k_boot2, 1 k_boot_tiles, 3 the general k_boot). */
+ * posterior (0 k_boot2, 1 k_boot_tiles / k_boot_gene, 3 the general k_boot); "stream_syncs",
+ * "arena_syncs" (this context's and its peer's streams drained by a buffer regrowth / a pinned
+ * arena wrap) and "buf_reallocs" (process-wide workspace reallocations, each a hipFree): 0 in
+ * steady state. */
 int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);
 int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
 int scde_ctx_reset_stats(scde_ctx* ctx);

@@ -286,7 +286,8 @@ struct scde_ctx {
                                  // on the copy stream (0: after it, on the main stream -- rocprofv3 runs, where the
                                  // pageable read-back becomes blit kernels that would share the CUs)
   int opt_gene_waves = 0;        // "gene_waves": k_boot_gene's waves per block, 3 or 4 (0: by gene3_cells)
-  int opt_gene3_cells = 1000;    // "gene3_cells": cells per call from which k_boot_gene runs 3-wave blocks
+  int opt_gene3_cells = 1 << 30;  // "gene3_cells": cells per call from which k_boot_gene runs 3-wave blocks (off:
+                                  // config 4 measured 12.85 ms of bootstrap per step with them vs 10.24 with 4)
   int opt_gene_list_cap = 0;     // "gene_list_cap": slabs k_boot_gene's list pass takes at most (0: 16384; tests)
   int opt_gene_rows = 4;         // "gene_rows": rows per slab k_boot_gene gives each slab at most (tests force its
                                  // four-tile list pass with fewer)
@@ -986,6 +987,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     tc.mu = ta.mu + co;
     tc.lcfp = ta.lcfp + co;
     tc.lcfpr = ta.lcfpr + co;
+    if (tc.cfp) tc.cfp = ta.cfp + co;
     tc.theta = ta.theta + co;
     tc.cellscal = ta.cellscal + 2 * (size_t)c0;
     if (tc.pq) tc.pq = ta.pq + 4 * co;

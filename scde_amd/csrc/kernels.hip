@@ -1966,9 +1966,6 @@ __global__ __launch_bounds__(32 * kQTiles) void k_zuq(const unsigned* __restrict
 // with every point computed.  Per ELL entry one 16-byte column load (points k0, k0 + 1) and one
 // 16-byte multiplicity load (DPP broadcast) feed 2 NB FMAs: these waves are bound by the
 // vector-memory instruction rate (the texture addresser), not by the bytes.
-#ifndef SCDE_BOUND_PREFETCH
-#define SCDE_BOUND_PREFETCH 1  // the bound passes load the next 64-entry chunk while staging this one
-#endif
 constexpr int kTileMax = 28;   // 16-point sum tiles, G <= 448
 constexpr int kBTileMax = 14;  // 32-point bound tiles, G <= 448
 #ifndef SCDE_TILE_DIAG
@@ -2062,27 +2059,12 @@ __device__ __forceinline__ void tile_bound_pass(const int2* __restrict__ E, int 
 #pragma unroll
     for (int l = 0; l < 4; ++l)
       acc[bt][l] = *reinterpret_cast<const i32x4*>(ZU + ((long long)l * kQTiles + t) * Bq + 16 * bt + 4 * h);
-  // chunk loads one chunk ahead: the next chunk's (cell, column), tile words and multiplicities are in
-  // flight while this chunk is staged and multiplied (a chunk is 64 entries of the padded row)
-  uint4 nq0, nq1, nq2, nq3, nw0, nw1;
-  auto fetch_chunk = [&](int e) {
-    const int2 en = E[e + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
-    const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
-    nq0 = uq[0];
-    nq1 = uq[1];
-    nq2 = uq[2];
-    nq3 = uq[3];
-    const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * cstride));
-    nw0 = wp[0];
-    nw1 = wp[1];
-  };
-  if (0 < KP) fetch_chunk(0);
   for (int e0 = 0; e0 < KP; e0 += 64) {
-    const uint4 q0 = nq0, q1 = nq1, q2 = nq2, q3 = nq3, w0 = nw0, w1 = nw1;
-    if (e0 + 64 < KP) fetch_chunk(e0 + 64);
-#if !SCDE_BOUND_PREFETCH
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // study builds: no look-ahead
-#endif
+    const int2 en = E[e0 + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
+    const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
+    const uint4 q0 = uq[0], q1 = uq[1], q2 = uq[2], q3 = uq[3];
+    const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * cstride));
+    const uint4 w0 = wp[0], w1 = wp[1];
     wave_sync();  // the previous chunk's fragment reads are done before the area is rewritten
     const unsigned qv[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                              q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
@@ -2161,27 +2143,12 @@ __device__ __forceinline__ void tile_bound_partial(const int2* __restrict__ E, i
 #pragma unroll
     for (int l = 0; l < 4; ++l)
       acc[bt][l] = i32x4{0, 0, 0, 0};
-  // chunk loads one chunk ahead: the next chunk's (cell, column), tile words and multiplicities are in
-  // flight while this chunk is staged and multiplied (a chunk is 64 entries of the padded row)
-  uint4 nq0, nq1, nq2, nq3, nw0, nw1;
-  auto fetch_chunk = [&](int e) {
-    const int2 en = E[e + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
-    const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
-    nq0 = uq[0];
-    nq1 = uq[1];
-    nq2 = uq[2];
-    nq3 = uq[3];
-    const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * cstride));
-    nw0 = wp[0];
-    nw1 = wp[1];
-  };
-  if (64 * c0 < KP) fetch_chunk(64 * c0);
   for (int e0 = 64 * c0; e0 < KP; e0 += 64 * cstep) {
-    const uint4 q0 = nq0, q1 = nq1, q2 = nq2, q3 = nq3, w0 = nw0, w1 = nw1;
-    if (e0 + 64 * cstep < KP) fetch_chunk(e0 + 64 * cstep);
-#if !SCDE_BOUND_PREFETCH
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
+    const int2 en = E[e0 + lane];  // rows are padded to a multiple of 64 (+ 8): pad entries read column ncols
+    const uint4* uq = reinterpret_cast<const uint4*>(UQ + (unsigned)(en.y * kQTiles));
+    const uint4 q0 = uq[0], q1 = uq[1], q2 = uq[2], q3 = uq[3];
+    const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * cstride));
+    const uint4 w0 = wp[0], w1 = wp[1];
     wave_sync();  // the previous chunk's fragment reads are done before the area is rewritten
     const unsigned qv[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                              q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
