@@ -371,7 +371,12 @@ struct scde_ctx {
     // pinned landing area of the phases' device -> host size read-backs: the set's own (not
     // the shared staging arena), so no later staging can recycle it before the host reads it
     int fixed_flags = 0;  // unique_phase12_fixed's flags when no pinned landing area exists
-    int woff_fixed = 0;   // entries of woff holding the fixed offsets c * 1024 (0: other contents)
+    int woff_fixed = 0;   // entries of woff holding the fixed offsets c * fixed_words (0: other contents)
+    // bitmap words per cell of the fixed-width build: 1024 (counts below 65,536), widened to the
+    // power of two an exact rebuild needed (so a data set with larger counts pays the rebuild's two
+    // extra host syncs once, not on every call), at most kUniqueFixedWordsMax
+    long long fixed_words = 1024;
+    long long woff_fixed_w = 0;  // the width woff_fixed's offsets were uploaded for
     int* pin_land = nullptr;
     size_t pin_land_cap = 0;  // ints
     const int* pin_in = nullptr;  // this phase's read-back (pin_land, or null: pageable fallback)
@@ -643,6 +648,8 @@ int upload(scde_ctx* cx, Buf& b, const void* src, size_t bytes) { return upload_
 // build_unique_pair interleaves two groups' phases so a DE call syncs twice, not four
 // times, and before any heavy kernel is queued.
 using UniqueSet = scde_ctx::UniqueSet;
+constexpr long long kUniqueFixedWordsMax = 1 << 16;           // counts below 2^22
+constexpr double kUniqueFixedBytesMax = double(256 << 20);    // a set's fixed-width bitmaps
 
 int unique_phase1(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, N = s.ngenes;
@@ -668,10 +675,16 @@ int unique_phase2(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
     std::copy(u.pin_in + C, u.pin_in + 2 * (size_t)C, u.cmin_h.begin());
   }
   u.woff_h.assign(C + 1, 0);
+  long long wmax = 1;
   for (int c = 0; c < C; ++c) {
     if (N > 0 && u.cmin_h[c] < 0) return fail(SCDE_EARG, "negative count in cell %d", c);
     u.woff_h[c + 1] = u.woff_h[c] + ((long long)u.cmax_h[c] >> 6) + 1;
+    wmax = std::max(wmax, ((long long)u.cmax_h[c] >> 6) + 1);
   }
+  // the next fixed-width build of this set: wide enough for these counts (bounded bitmap memory)
+  long long fw = u.fixed_words;
+  while (fw < wmax && fw < kUniqueFixedWordsMax) fw *= 2;
+  if (fw >= wmax && fw != u.fixed_words && (double)C * fw * 8.0 <= kUniqueFixedBytesMax) u.fixed_words = fw;
   RCHK(upload(cx, u.woff, u.woff_h.data(), sizeof(long long) * (C + 1)));
   u.woff_fixed = 0;
   HCHK(u.bits.ensure(sizeof(unsigned long long) * u.woff_h[C]));
@@ -719,16 +732,20 @@ int unique_phase3(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
 }
 
 // Phases 1 and 2 in one, without the per-cell maxima: every cell gets a bitmap of
-// kUniqueFixedWords words (counts below 65,536); k_mark flags a negative count or one past the
-// bitmap, and such a set is rebuilt with exact widths (phases 1-2).  One host sync per build.
-constexpr long long kUniqueFixedWords = 1024;
+// u.fixed_words words (1024 at first: counts below 65,536); k_mark flags a negative count or one
+// past the bitmap, and such a set is rebuilt with exact widths (phases 1-2), which also widens
+// the set's later fixed builds.  One host sync per build.
 int unique_phase12_fixed(scde_ctx* cx, const PostSpec& s, UniqueSet& u) {
   const int C = s.ncells, N = s.ngenes;
   hipStream_t st = cx->stream;
   RCHK(upload(cx, u.cellidx, s.cellidx_host, sizeof(int) * C));
+  const long long FW = u.fixed_words;
   u.woff_h.resize(C + 1);
-  for (int c = 0; c <= C; ++c) u.woff_h[c] = (long long)c * kUniqueFixedWords;
-  // the fixed offsets c * 1024 are uploaded once per set (grow-only; exact-width builds reset it)
+  for (int c = 0; c <= C; ++c) u.woff_h[c] = (long long)c * FW;
+  // the fixed offsets c * FW are uploaded once per set and width (grow-only; exact-width builds
+  // and a new width reset it)
+  if (u.woff_fixed_w != FW) u.woff_fixed = 0;
+  u.woff_fixed_w = FW;
   if (u.woff_fixed < C + 1) {
     RCHK(upload(cx, u.woff, u.woff_h.data(), sizeof(long long) * (C + 1)));
     u.woff_fixed = C + 1;

@@ -2584,7 +2584,6 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
 //      computed tiles in tile order, 1 / (S nboot), the partial jp rows.
 // Every value is formed exactly as in k_boot_tiles and k_boot2 (same fma chains, maxima, terms,
 // tile partials added in tile order), so the outputs are bit-identical to theirs.
-constexpr int kGeneRowsMax = 16;  // 4 waves x 4 rows
 constexpr int kGeneSlabs = 8;     // slabs per group at most (K >= 2 rows each)
 // WB waves per block (4, or 3 for wide calls whose slabs mostly need two tiles: 12 rows for 5
 // slabs).  With 3 waves the fourth 32-boot bound window is split by entry chunks over the

@@ -266,6 +266,19 @@ def test_edge_cases(api, oracle):
         ref = oracle.scde_posteriors(sub, c, g["prior_x"], n_randomizations=11, n_cores=1)
         got = api.scde_posteriors(sub, c, prior, n_randomizations=11, n_cores=1)
         assert_posterior_close(got, ref, what=name)
+    # the unique build's fixed-width bitmaps widen after a rebuild for large counts: the same
+    # answers again (now from the wider fixed build), counts past the widest width still take the
+    # exact build, and a negative count is still rejected after widening
+    huge = np.ascontiguousarray(cases["huge counts"], np.int32)
+    first = api.scde_posteriors(sub, huge, prior, n_randomizations=11, n_cores=1)
+    for c in (huge, np.array([[0, 1, 2, 100000, 5000000, 7]] * 2, np.int32)):
+        ref = oracle.scde_posteriors(sub, c, g["prior_x"], n_randomizations=11, n_cores=1)
+        for _ in range(2):
+            got = api.scde_posteriors(sub, c, prior, n_randomizations=11, n_cores=1)
+            assert_posterior_close(got, ref, what="huge counts again")
+    np.testing.assert_array_equal(api.scde_posteriors(sub, huge, prior, n_randomizations=11, n_cores=1), first)
+    with pytest.raises(Exception):
+        api.scde_posteriors(sub, np.array([[0, 1, 2, 3, -4, 7]] * 2, np.int32), prior, n_randomizations=11, n_cores=1)
     empty = api.scde_posteriors(sub, np.zeros((0, 6), np.int32), prior, n_randomizations=11, n_cores=1)
     assert np.asarray(empty).shape == (0, len(g["prior_x"]))
     tab = api.scde_expression_difference(models, np.zeros((0, len(g["groups"])), np.int32), prior,
