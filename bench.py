@@ -650,7 +650,10 @@ def main():
     sync_stats = {"stream_syncs_per_step": ctx.stat("stream_syncs") / args.steps,
                   "arena_syncs_per_step": ctx.stat("arena_syncs") / args.steps,
                   "buf_reallocs_per_step": (ctx.stat("buf_reallocs") - reallocs0[0]) / args.steps,
-                  "device_syncs_per_step": 0.0}
+                  "device_syncs_per_step": 0.0,
+                  # host-count pieces: host ms per step waiting for uploads / building and launching
+                  "piece_wait_ms_per_step": ctx.stat("piece_wait_ms") / args.steps,
+                  "piece_host_ms_per_step": ctx.stat("piece_host_ms") / args.steps}
     # device-resident rate (counts already in HBM), product settings
     dc = api.DeviceCounts(ctx, counts)
     dt_dev = timed(dc.ptr)

@@ -130,7 +130,7 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   operand; a call with a larger one runs plain k_boot2 on the same columns --
  *                   tests force that fallback with a small value)
  *   "tile_order"    1/0  k_boot_tiles takes the genes in order of their count sums, so waves in
- *                   flight share columns and tiles in L2 (default 1; results are the same)
+ *                   flight share columns and tiles in L2 (default 0 while under test; results are the same)
  *   "unique_fixed"  1/0  build each call's unique count tables with one host sync (fixed
  *                   1024-word bitmaps per cell, counts below 65,536; a set with another count is
  *                   rebuilt with exact widths); default 1
@@ -159,10 +159,15 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   selected cells), 1..8 (default 4); results are the same
  *   "lane_thread"   1/0  a pipelined two-lane DE call drives the second lane (its unique sets,
  *                   tables and bootstrap) from a host thread of its own (results are the same)
+ *   "interleave"    1/0  with lane_thread: both groups' ranges go up in alternating pieces, each
+ *                   group's pieces built and tabled as they land (default 1; only when every
+ *                   cell of the second group follows the first group's cells)
  *   "upload_staged" 1/0  host counts go up through a pinned ring filled by "upload_threads"
  *                   copy threads instead of pageable copies (default 0: measured no faster)
  *   "gene_waves"    3/4  k_boot_gene's waves per block (12 or 16 rows); 0 (default) = 3 from
  *                   "gene3_cells" cells per call (default: never; slower at config 4), else 4
+ *   "gene_direct"   1/0  gene blocks holding all of a gene's slabs write its jp row themselves
+ *                   (default 0 while under test; results are the same)
  *   "gene_list_cap" slabs k_boot_gene's four-tile list pass takes (0 = 16384; beyond: k_boot2)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
@@ -177,6 +182,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  * "arena_syncs" (this context's and its peer's streams drained by a buffer regrowth / a pinned
  * arena wrap) and "buf_reallocs" (process-wide workspace reallocations, each a hipFree): 0 in
  * steady state. */
+/* Options can also come from the environment: SCDE_OPTIONS="name=value,..." is applied to every
+ * context as it is created (an unknown name fails the creation). */
 int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);
 int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
 int scde_ctx_reset_stats(scde_ctx* ctx);

@@ -261,7 +261,7 @@ struct scde_ctx {
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, w8g, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
-  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide;
+  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide, gdone;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 30 + 0.4 C); tests force redo slabs
@@ -300,6 +300,10 @@ struct scde_ctx {
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
+  int opt_gene_direct = 0;      // "gene_direct": gene blocks holding all of a gene's slabs write its jp row
+                                // (no partial rows, no k_sum_partials pass for it)
+  int opt_interleave = 1;       // "interleave": with lane_thread, both groups' ranges go up in alternating
+                                // pieces (when the second group's cells all follow the first group's range)
   int opt_lane_thread = 0;      // "lane_thread": a pipelined two-lane DE call drives the second lane from a host
                                 // thread of its own
   int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
@@ -358,6 +362,8 @@ struct scde_ctx {
   double st_boot_f64_fma = 0;
   double st_stream_syncs = 0;  // grow(keep) drains of this context's streams (scoped, never the device)
   double st_arena_syncs = 0;   // pinned-arena wraps (this context's streams drained)
+  // run_posterior's pieces (host ms): waiting for a piece's upload, then its unique build and tables launch
+  double st_piece_wait_ms = 0, st_piece_host_ms = 0;
   double st_pair_redo = 0;  // slabs a pair pass of k_boot_tiles left to the four-tile list pass
   double st_boot_path = -1;  // the bootstrap kernel of the last posterior: 0 k_boot2, 1 k_boot_tiles, 3 general
   static constexpr int kQMaxTilesHost = 28;
@@ -511,7 +517,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide};
+                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide, &gdone};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (auto& u : upc) u.release();
@@ -1068,9 +1074,21 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     int jlast = 0;
     for (int j = 0; j < s.npieces; ++j)
       if (s.piece_c[j + 1] > s.piece_c[j]) jlast = j;
+    using pclock = std::chrono::steady_clock;
+    auto pms = [](pclock::time_point a, pclock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
     for (int j = 0; j < s.npieces; ++j) {
       const int c0 = s.piece_c[j], c1 = s.piece_c[j + 1];
+      const auto tw = pclock::now();
       RCHK(s.piece_ready(j));
+      const auto th = pclock::now();
+      cx->st_piece_wait_ms += pms(tw, th);
+      struct Lap {
+        scde_ctx* cx;
+        pclock::time_point t;
+        ~Lap() { cx->st_piece_host_ms += std::chrono::duration<double, std::milli>(pclock::now() - t).count(); }
+      } lap{cx, th};
       if (c1 == c0) continue;
       UniqueSet& pu = cx->upc[j];
       PostSpec ps;
@@ -1353,6 +1371,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           // 12 rows per gene block from gene3_cells cells per call (slabs mostly need two tiles there)
           tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (C >= cx->opt_gene3_cells ? 3 : 4);
           tb.W8g = cx->w8g.as<unsigned char>();
+          if (cx->opt_gene_direct) {
+            HCHK(cx->gdone.ensure(sizeof(int) * std::max<size_t>(1, (size_t)N)));
+            tb.gdone = cx->gdone.as<int>();
+          }
         }
         if (have_order) tb.order = cx->gorder.as<int>();
         HCHK(launch_boot_tiles(b2, tb, st));
@@ -1583,6 +1605,26 @@ int scde_ctx_create(int device, scde_ctx** out) {
     return fail(SCDE_EHIP, "hipStreamCreate: %s", hipGetErrorString(e));
   }
   c->home_stream = c->stream;
+  // SCDE_OPTIONS="name=value,name=value": context options from the environment (tuning runs)
+  if (const char* env = std::getenv("SCDE_OPTIONS")) {
+    std::string all(env);
+    size_t pos = 0;
+    while (pos < all.size()) {
+      size_t end = all.find(',', pos);
+      if (end == std::string::npos) end = all.size();
+      const std::string item = all.substr(pos, end - pos);
+      pos = end + 1;
+      const size_t eq = item.find('=');
+      if (item.empty()) continue;
+      const int rc = eq == std::string::npos ? fail(SCDE_EARG, "SCDE_OPTIONS item '%s' is not name=value", item.c_str())
+                                             : scde_ctx_set_option(c, item.substr(0, eq).c_str(),
+                                                                   std::atof(item.c_str() + eq + 1));
+      if (rc != SCDE_OK) {
+        scde_ctx_destroy(c);
+        return rc;
+      }
+    }
+  }
   *out = c;
   return SCDE_OK;
 }
@@ -1664,6 +1706,8 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "lane_prio") ctx->opt_lane_prio = value != 0;
   else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
   else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
+  else if (n == "interleave") ctx->opt_interleave = value != 0;
+  else if (n == "gene_direct") ctx->opt_gene_direct = value != 0;
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
     if (ctx->opt_lanes == 1 && ctx->peer) {  // one lane: the peer's workspace goes back to the device
@@ -1691,6 +1735,8 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "degen") *value = ctx->st_degen;
   else if (n == "stream_syncs") *value = ctx->st_stream_syncs + (ctx->peer ? ctx->peer->st_stream_syncs : 0);
   else if (n == "arena_syncs") *value = ctx->st_arena_syncs + (ctx->peer ? ctx->peer->st_arena_syncs : 0);
+  else if (n == "piece_wait_ms") *value = ctx->st_piece_wait_ms + (ctx->peer ? ctx->peer->st_piece_wait_ms : 0);
+  else if (n == "piece_host_ms") *value = ctx->st_piece_host_ms + (ctx->peer ? ctx->peer->st_piece_host_ms : 0);
   else if (n == "buf_reallocs") *value = (double)g_buf_reallocs.load();
   else if (n == "host_setup_ms") *value = ctx->st_host_ms[0];
   else if (n == "host_unique_ms") *value = ctx->st_host_ms[1];
@@ -1708,6 +1754,8 @@ int scde_ctx_reset_stats(scde_ctx* ctx) {
   ctx->st_pair_redo = 0;
   ctx->st_stream_syncs = ctx->st_arena_syncs = 0;
   if (ctx->peer) ctx->peer->st_stream_syncs = ctx->peer->st_arena_syncs = 0;
+  ctx->st_piece_wait_ms = ctx->st_piece_host_ms = 0;
+  if (ctx->peer) ctx->peer->st_piece_wait_ms = ctx->peer->st_piece_host_ms = 0;
   for (double& x : ctx->st_host_ms) x = 0;
   ctx->st_boot_f64_fma = 0;
   for (double& x : ctx->st_tile_hist) x = 0;
@@ -2170,7 +2218,15 @@ static int upload_cols(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
 // each followed by evs[j]; wait(n) returns once the first n are issued (their events recorded).
 struct UploadWorker {
   scde_ctx* ctx = nullptr;
-  int start(scde_ctx* c, const HostUpload& h, std::vector<int> cols, std::vector<hipEvent_t> evs) {
+  int start(scde_ctx* c, const HostUpload& h, const std::vector<int>& cols, std::vector<hipEvent_t> evs) {
+    if (cols.size() != evs.size() + 1)
+      return fail(SCDE_EINTERNAL, "upload ranges: %d bounds for %d events", (int)cols.size(), (int)evs.size());
+    std::vector<std::pair<int, int>> ranges;
+    for (size_t j = 0; j + 1 < cols.size(); ++j) ranges.emplace_back(cols[j], cols[j + 1]);
+    return start(c, h, std::move(ranges), std::move(evs));
+  }
+  // ranges[j] = [lo, hi) in any order (the interleaved two-group upload)
+  int start(scde_ctx* c, const HostUpload& h, std::vector<std::pair<int, int>> ranges, std::vector<hipEvent_t> evs) {
     ctx = c;
     auto& u = c->upl;
     if (!u.th.joinable()) {
@@ -2205,11 +2261,11 @@ struct UploadWorker {
       });
     }
     const int nranges = (int)evs.size();  // (before the vectors move into the closure)
-    if ((int)cols.size() != nranges + 1) return fail(SCDE_EINTERNAL, "upload ranges: %d bounds for %d events",
-                                                     (int)cols.size(), nranges);
+    if ((int)ranges.size() != nranges) return fail(SCDE_EINTERNAL, "upload ranges: %d ranges for %d events",
+                                                   (int)ranges.size(), nranges);
     std::lock_guard<std::mutex> lk(u.m);
-    u.issue = [c, h, cols = std::move(cols), evs = std::move(evs)](int j) -> int {
-      RCHK(upload_cols(c, h, cols[j], cols[j + 1]));
+    u.issue = [c, h, ranges = std::move(ranges), evs = std::move(evs)](int j) -> int {
+      RCHK(upload_cols(c, h, ranges[j].first, ranges[j].second));
       HCHK(hipEventRecord(evs[j], c->copy_stream));
       return SCDE_OK;
     };
@@ -2401,6 +2457,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_gene_list_cap = cx->opt_gene_list_cap;
   p->opt_gene_waves = cx->opt_gene_waves;
   p->opt_gene3_cells = cx->opt_gene3_cells;
+  p->opt_gene_direct = cx->opt_gene_direct;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;
@@ -2505,19 +2562,48 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     // the first group's range in pieces, then the second group's range, uploaded back to back by
     // a worker thread: each piece's unique sets and tables start as it lands
     const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
-    std::vector<int> piece_c, cols;
+    const bool threaded = lane != ctx && ctx->opt_lane_thread && !ctx->opt_defer_boot;
+    // interleaved (second lane on its own host thread, every cell of the second group after the
+    // first group's range): both groups' ranges in K pieces, uploaded alternately, so the second
+    // group's unique sets and tables run beside the first group's instead of after its range
+    const int other = 1 - first;
+    const bool inter = threaded && ctx->opt_interleave && !idx[other].empty() && idx[other].front() >= up->cut;
+    std::vector<int> piece_c, cols, piece_c2;
     const std::vector<int>& ix = idx[first];
     for (int j = 0; j <= K; ++j) {
       const int a = (int)((long long)up->cut * j / K);
       cols.push_back(a);
       piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
     }
-    cols.push_back(up->C);
     RCHK(ensure_piece_streams(ctx));
-    std::vector<hipEvent_t> evs(ctx->piece_up_ev, ctx->piece_up_ev + K);
-    evs.push_back(ctx->up_ev[1]);
     UploadWorker uw;
-    RCHK(uw.start(ctx, *up, cols, evs));
+    if (inter) {
+      RCHK(ensure_piece_streams(lane));
+      const std::vector<int>& iy = idx[other];
+      std::vector<int> cols2;
+      for (int j = 0; j <= K; ++j) {
+        const int a = up->cut + (int)((long long)(up->C - up->cut) * j / K);
+        cols2.push_back(a);
+        piece_c2.push_back((int)(std::lower_bound(iy.begin(), iy.end(), a) - iy.begin()));
+      }
+      // range 2j: the first group's piece j; range 2j + 1: the second group's piece j
+      std::vector<std::pair<int, int>> ranges;
+      std::vector<hipEvent_t> evs;
+      for (int j = 0; j < K; ++j) {
+        ranges.emplace_back(cols[j], cols[j + 1]);
+        evs.push_back(ctx->piece_up_ev[j]);
+        ranges.emplace_back(cols2[j], cols2[j + 1]);
+        evs.push_back(lane->piece_up_ev[j]);
+      }
+      RCHK(uw.start(ctx, *up, std::move(ranges), std::move(evs)));
+    } else {
+      cols.push_back(up->C);
+      std::vector<hipEvent_t> evs(ctx->piece_up_ev, ctx->piece_up_ev + K);
+      evs.push_back(ctx->up_ev[1]);
+      RCHK(uw.start(ctx, *up, cols, evs));
+    }
+    // upload range of the first group's piece j
+    auto range_of = [&](int j) { return inter ? 2 * j : j; };
     // two lanes with lane_thread: the second group's unique sets, tables and bootstrap are driven
     // by a host thread of their own from the moment its range lands, beside this thread's pieces
     // of the first group (each lane's host syncs then wait only for its own kernels)
@@ -2529,13 +2615,25 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         if (th.joinable()) th.join();  // an early error return of this thread still waits for it
       }
     } t2;
-    const bool threaded = lane != ctx && ctx->opt_lane_thread && !ctx->opt_defer_boot;
     if (threaded) {
       const int gi = 1 - first;
       ctx->us[gi].ready = false;
       t2.th = std::thread([&, gi] {
         t2.rc = [&]() -> int {
           HCHK(hipSetDevice(ctx->device));
+          if (inter) {  // the second group's pieces as they land (ranges 1, 3, 5, ...)
+            PostSpec& s2 = specs[gi];
+            s2.npieces = K;
+            s2.piece_c = piece_c2.data();
+            s2.piece_stream = lane->uq_stream;
+            s2.piece_ev = lane->piece_ev;
+            s2.piece_ready = [&](int j) {
+              RCHK(uw.wait(2 * j + 2));
+              HCHK(hipStreamWaitEvent(lane->uq_stream, lane->piece_up_ev[j], 0));
+              return SCDE_OK;
+            };
+            return run_posterior(lane, s2, ctx->us[gi]);
+          }
           RCHK(uw.wait(K + 1));
           HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
           const PostSpec* sp[1] = {&specs[gi]};
@@ -2560,7 +2658,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       sf.piece_stream = ctx->uq_stream;
       sf.piece_ev = ctx->piece_ev;
       sf.piece_ready = [&](int j) {
-        RCHK(uw.wait(j + 1));
+        RCHK(uw.wait(range_of(j) + 1));
         HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
         return SCDE_OK;
       };

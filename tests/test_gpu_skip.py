@@ -54,6 +54,8 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("defer_boot", opts.get("defer_boot", 0))
     ctx.set_option("upload_staged", opts.get("upload_staged", 0))
     ctx.set_option("lane_thread", opts.get("lane_thread", 0))
+    ctx.set_option("interleave", opts.get("interleave", 1))
+    ctx.set_option("gene_direct", opts.get("gene_direct", 0))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -82,6 +84,8 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("defer_boot", 0)
         ctx.set_option("upload_staged", 0)
         ctx.set_option("lane_thread", 0)
+        ctx.set_option("interleave", 1)
+        ctx.set_option("gene_direct", 0)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -104,6 +108,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "gene-list-overflow": {"gene_rows": 1, "gene_list_cap": 40},
         "gene-3waves": {"gene_waves": 3},
         "gene-4waves": {"gene_waves": 4},
+        "gene-direct": {"gene_direct": 1},
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
         "one-lane": {"lanes": 1},
@@ -111,7 +116,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1},
         "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1},
         "pipelined-staged": {"pipeline_mb": 0, "pieces": 3, "upload_staged": 1},
-        "pipelined-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1},
+        "pipelined-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1},  # both groups in alternating pieces
+        "pipelined-thread-seq": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1, "interleave": 0},
         "tiles-pairs": {"pair_cells": 1, "gene_blocks": 0},
         "tiles-pairs-redo": {"pair_cells": 1, "tile_groups": 2, "gene_blocks": 0},
         "tiles-mult-fallback": {"tile_max_mult": 1},
@@ -156,9 +162,10 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
                         what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
-                                    "gene-forced-list", "gene-list-overflow", "gene-3waves", "gene-4waves",
+                                    "gene-forced-list", "gene-list-overflow", "gene-3waves", "gene-4waves", "gene-direct",
                                     "tiles-unordered", "unique-exact", "one-lane", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
+                                    "pipelined-thread-seq",
                                     "tiles-pairs",
                                     "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
         for name in others:

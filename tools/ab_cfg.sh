@@ -17,7 +17,8 @@ d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d["roofline"]
 print("[" + sys.argv[2] + "]", "ms/step", round(d["ms_per_step"], 3), "dev", round(d["device_resident_ms_per_step"], 3),
       "boot launch ms", round(r["avg_launch_ms"], 3), "frac", round(r["frac"], 3),
-      "kms", {k: round(v, 3) for k, v in d["kernel_ms_per_step"].items()})
+      "kms", {k: round(v, 3) for k, v in d["kernel_ms_per_step"].items()},
+      "piece wait/host", round(d["host_syncs"].get("piece_wait_ms_per_step", 0), 3), round(d["host_syncs"].get("piece_host_ms_per_step", 0), 3))
 PY
   done
 done
