@@ -166,8 +166,6 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   copy threads instead of pageable copies (default 0: measured no faster)
  *   "gene_waves"    3/4  k_boot_gene's waves per block (12 or 16 rows); 0 (default) = 3 from
  *                   "gene3_cells" cells per call (default: never; slower at config 4), else 4
- *   "gene_direct"   1/0  gene blocks holding all of a gene's slabs write its jp row themselves
- *                   (default 0 while under test; results are the same)
  *   "gene_list_cap" slabs k_boot_gene's four-tile list pass takes (0 = 16384; beyond: k_boot2)
  *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])

@@ -261,7 +261,7 @@ struct scde_ctx {
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, w8g, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
-  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide, gdone;
+  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 30 + 0.4 C); tests force redo slabs
@@ -300,8 +300,6 @@ struct scde_ctx {
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
-  int opt_gene_direct = 0;      // "gene_direct": gene blocks holding all of a gene's slabs write its jp row
-                                // (no partial rows, no k_sum_partials pass for it)
   int opt_interleave = 1;       // "interleave": with lane_thread, both groups' ranges go up in alternating
                                 // pieces (when the second group's cells all follow the first group's range)
   int opt_lane_thread = 0;      // "lane_thread": a pipelined two-lane DE call drives the second lane from a host
@@ -517,7 +515,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide, &gdone};
+                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (auto& u : upc) u.release();
@@ -1371,10 +1369,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           // 12 rows per gene block from gene3_cells cells per call (slabs mostly need two tiles there)
           tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (C >= cx->opt_gene3_cells ? 3 : 4);
           tb.W8g = cx->w8g.as<unsigned char>();
-          if (cx->opt_gene_direct) {
-            HCHK(cx->gdone.ensure(sizeof(int) * std::max<size_t>(1, (size_t)N)));
-            tb.gdone = cx->gdone.as<int>();
-          }
         }
         if (have_order) tb.order = cx->gorder.as<int>();
         HCHK(launch_boot_tiles(b2, tb, st));
@@ -1707,7 +1701,6 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
   else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
   else if (n == "interleave") ctx->opt_interleave = value != 0;
-  else if (n == "gene_direct") ctx->opt_gene_direct = value != 0;
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
     if (ctx->opt_lanes == 1 && ctx->peer) {  // one lane: the peer's workspace goes back to the device
@@ -2457,7 +2450,6 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_gene_list_cap = cx->opt_gene_list_cap;
   p->opt_gene_waves = cx->opt_gene_waves;
   p->opt_gene3_cells = cx->opt_gene3_cells;
-  p->opt_gene_direct = cx->opt_gene_direct;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;

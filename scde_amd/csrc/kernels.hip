@@ -2596,8 +2596,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8g, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int kcap, int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order,
-    unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap, double* __restrict__ out, long long out_g,
-    long long out_k, int* __restrict__ gdone) {
+    unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
   static_assert(WB == 3 || WB == 4, "3 or 4 waves per gene block");
   constexpr int kGeneRows = 4 * WB;
@@ -2626,11 +2625,6 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   const int gi = blk / NGR, gr = blk - gi * NGR;
   const int g = order ? order[gi] : gi;
   const int s0 = gr * SG, ns = min(SG, P - s0);
-  // direct rows (gdone, one group per gene, the slabs' rows fit the staging area): a gene whose
-  // slabs all pass their post-checks writes its jp row itself, summed over the slabs in slab order
-  // exactly as k_sum_partials would, and flags gdone[g] so k_sum_partials leaves it alone
-  const bool direct = gdone && NGR == 1 && ns * ((G + 31) & ~31) * 8 <= (int)sizeof(bstage);
-  if (gdone && threadIdx.x == 0) gdone[g] = 0;  // (gdone only with one group per gene: one block per gene)
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
     if ((int)threadIdx.x < ns) {
       const int q = g * P + s0 + threadIdx.x;
@@ -2844,49 +2838,14 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     }
   }
   __syncthreads();
-  double j0 = 0.0, j1 = 0.0;
   if (mine) {
+    double* prow = part + (long long)(s0 + sq) * part_stride + (long long)g * GS;
+    double j0 = 0.0, j1 = 0.0;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       j0 = fma(a0[i], finv[sq * 32 + i], j0);
       j1 = fma(a1[i], finv[sq * 32 + i], j1);
     }
-  }
-  if (direct && fm == 0u) {
-    // the slabs' rows in LDS ([slab][point], zeros where a slab computed no tile), then per point
-    // the sum over slabs in order: the partial rows k_sum_partials would add, added the same way
-    const int GP = (G + 31) & ~31;
-    double* rows = reinterpret_cast<double*>(&bstage[0][0]);
-    __syncthreads();  // every lane's finv reads are done: the staging area is free
-    for (int x = threadIdx.x; x < ns * GP; x += 64 * WB) rows[x] = 0.0;
-    __syncthreads();
-    if (mine) {
-      if (l1)
-        *reinterpret_cast<d2_t*>(rows + sq * GP + k0) = d2_t{j0, j1};
-      else if (l0)
-        rows[sq * GP + k0] = j0;
-    }
-    __syncthreads();
-    double* orow = out + (long long)g * out_g;
-    for (int k = threadIdx.x; k < G; k += 64 * WB) {
-      double v = rows[k];
-      for (int p = 1; p < ns; ++p) v += rows[p * GP + k];
-      orow[(long long)k * out_k] = v;
-    }
-    if (threadIdx.x == 0) gdone[g] = 1;
-    if (stats && (int)threadIdx.x < ns) {
-      unsigned dn = 0;
-      for (unsigned mm = bd[threadIdx.x]; mm; mm &= mm - 1) dn |= 3u << (2 * (__builtin_ffs((int)mm) - 1));
-      dn &= (NT >= 32) ? ~0u : ((1u << NT) - 1);
-      atomicAdd(&stats[0], 1);
-      atomicAdd(&stats[1], __builtin_popcount(dn));
-      atomicAdd(&stats[2], NT);
-      atomicAdd(&stats[6 + __builtin_popcount(dn)], 1);
-    }
-    return;
-  }
-  if (mine) {
-    double* prow = part + (long long)(s0 + sq) * part_stride + (long long)g * GS;
     if (l1)
       *reinterpret_cast<d2_t*>(prow + k0) = d2_t{j0, j1};
     else if (l0)
@@ -2927,11 +2886,10 @@ template __global__ void k_boot_tiles<20, 1>(const double* __restrict__, const i
 // are zeros, read as +0.0, so the sums are those of full rows.
 __global__ void k_sum_partials(const double* __restrict__ part, long long part_stride, int P, int ngenes, int G,
                                int GS, double* __restrict__ out, long long out_g, long long out_k,
-                               const unsigned* __restrict__ pmask, const int* __restrict__ gdone) {
+                               const unsigned* __restrict__ pmask) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)ngenes * G) return;
   const int g = (int)(i / G), k = (int)(i % G);
-  if (gdone && gdone[g]) return;  // k_boot_gene wrote the row itself
   const unsigned bit = 1u << (k >> 4);
   double s = (!pmask || (pmask[(long long)g * P] & bit)) ? part[(long long)g * GS + k] : 0.0;
   for (int p = 1; p < P; ++p)
@@ -3894,7 +3852,7 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (e != hipSuccess) return e;
   const long long n = (long long)a.ngenes * a.G;
   hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                     a.G, a.GS, a.out, a.out_g, a.out_k, nullptr, nullptr);
+                     a.G, a.GS, a.out, a.out_g, a.out_k, nullptr);
   return hipGetLastError();
 }
 
@@ -3960,8 +3918,6 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   const long long gene_cap = tb.list_cap > 0 ? tb.list_cap : 16384;
   const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(items, gene_cap) : 0;
   const long long gblocks = gene ? (long long)a.ngenes * ((P + tb.SG - 1) / tb.SG) : 0;
-  // gene blocks holding all of a gene's slabs write the finished jp rows of their genes themselves
-  int* const gdone = (gene && tb.gdone && tb.SG >= P) ? tb.gdone : nullptr;
 #define SCDE_BT(NBV)                                                                                              \
   case NBV:                                                                                                        \
     if (gene && tb.gene_waves == 3)                                                                                \
@@ -3969,13 +3925,13 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
                          a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
                          a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
                          tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide,  \
-                         (int)items2, a.out, a.out_g, a.out_k, gdone);                                     \
+                         (int)items2);                                     \
     else if (gene)                                                                                                 \
       hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3((unsigned)gblocks), dim3(256), 0, s, a.D, a.ent, a.nnz,      \
                          a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
                          a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
                          tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide,  \
-                         (int)items2, a.out, a.out_g, a.out_k, gdone);                                     \
+                         (int)items2);                                     \
     else                                                                                                           \
     hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
                        a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,      \
@@ -4035,7 +3991,7 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if (e != hipSuccess) return e;
   const long long nn = (long long)a.ngenes * a.G;
   hipLaunchKernelGGL(k_sum_partials, dim3(div_up(nn, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                     a.G, a.GS, a.out, a.out_g, a.out_k, tb.pmask, gdone);
+                     a.G, a.GS, a.out, a.out_g, a.out_k, tb.pmask);
   return hipGetLastError();
 }
 
