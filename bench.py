@@ -115,7 +115,8 @@ def dominant_kernel_bytes(ngenes, cells_per_group):
 
 
 BOOT_STAGES = {0: "bootstrap stage (k_stretch_mask + k_boot2 + redo pass + k_sum_partials)",
-               1: "bootstrap stage (k_boot_tiles + k_boot2_list fallback + k_sum_partials)",
+               1: "bootstrap stage (k_boot_gene gene blocks + k_boot_tiles list pass + k_boot2_list fallback + "
+                  "k_sum_partials)",
                3: "bootstrap stage (general k_boot)"}
 
 
