@@ -118,12 +118,13 @@ int scde_ctx_set_profiling(scde_ctx* ctx, int on);
  * 6 prior_bin, 7 prior_tail; ms totals and launch counts */
 int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslots);
 int scde_ctx_reset_kernel_times(scde_ctx* ctx);
-/* Tuning and test options of a context (defaults are the product settings; nothing is read
- * from the environment on the compute path):
+/* Tuning and test options of a context (defaults are the product settings; the environment is
+ * read once, at context creation, for SCDE_OPTIONS -- see scde_ctx_set_option):
  *   "boot_skip"     1/0  grid-stretch skipping in the bootstrap (output unchanged either way)
  *   "boot_tiles"    1/0  the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles; default 1)
- *   "boot_tiles_cells"  the cell count from which it is used (default 200; below: k_boot2's
- *                   64-point stretch mask)
+ *   "boot_tiles_cells"  the cell count from which it is used (default 400; below: k_boot2's
+ *                   64-point stretch mask -- config 2b's 200-cell batch posteriors: 8.2 ms of
+ *                   bootstrap per step with it against 12.0 with gene blocks)
  *   "tile_groups"   32-point grid tiles k_boot_tiles computes per slab, 1..4 (default 4; slabs
  *                   needing more go to k_boot2 whole -- tests force that with 2)
  *   "tile_max_mult" the largest draw multiplicity the tile path takes (default 127, the int8 bound

@@ -271,7 +271,7 @@ struct scde_ctx {
   int opt_ratio_block = 128;     // "ratio_block": k_ratio_summary block size (64, 128, 256)
   int opt_wpca_ms = 1;           // "wpca_ms": the multi-start npcs = 1 kernel (k_wpca_ms1)
   int opt_boot_tiles = 1;        // "boot_tiles": the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles)
-  int opt_boot_tiles_cells = 200;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
+  int opt_boot_tiles_cells = 400;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
                                    // rows are wide, most slabs need > 8 tiles, k_boot2's stretches win)
   int opt_tile_groups = 4;       // "tile_groups": 32-point bound tiles k_boot_tiles computes per slab (1..4)
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it

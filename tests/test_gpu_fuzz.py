@@ -8,7 +8,7 @@ counts from a zero-inflated negative binomial with occasional huge counts, model
 resampled from the es.mef (6-column) or knn (12-column: local theta, squared-logit
 concentration) fixtures, n.randomizations in {1, 2, 7, 20, 33}, n.cores in {1, 2, 5},
 prior length.out in {60, 401}.  Every case runs through the bootstrap kernels: k_boot2 (or
-k_boot_tiles from 200 cells), and k_boot_tiles at every size (boot_tiles_cells 0).
+the tile path from 400 cells), and the tile path at every size (boot_tiles_cells 0).
 """
 import numpy as np
 import pytest
@@ -60,7 +60,7 @@ def test_expression_difference_fuzz(seed, opts):
                                              n_randomizations=kw["n_randomizations"], n_cores=kw["n_cores"],
                                              return_posteriors=True)
     finally:
-        ctx.set_option("boot_tiles_cells", 200)
+        ctx.set_option("boot_tiles_cells", 400)
     # the oracle takes factor codes (level order a < b, NA = -1), the api R-style labels
     codes = np.array([{"a": 0, "b": 1, None: -1}[v] for v in glist])
     ref = O.scde_expression_difference(models, counts, prior["x"], prior["y"], codes,

@@ -69,7 +69,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("skip_slack", math.nan)
         ctx.set_option("boot_tiles", 1)
         ctx.set_option("tile_groups", 4)
-        ctx.set_option("boot_tiles_cells", 200)
+        ctx.set_option("boot_tiles_cells", 400)
         ctx.set_option("tile_order", 1)
         ctx.set_option("pair_cells", 1000)
         ctx.set_option("gene_blocks", 1)
