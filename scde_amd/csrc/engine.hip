@@ -300,6 +300,8 @@ struct scde_ctx {
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
+  int opt_rest_thread = 0;      // "rest_thread": a two-lane DE call on counts in HBM runs the second group's
+                                // draws, set-up and bootstrap launch from a host thread of its own
   int opt_interleave = 1;       // "interleave": with lane_thread, both groups' ranges go up in alternating
                                 // pieces (when the second group's cells all follow the first group's range)
   int opt_lane_thread = 0;      // "lane_thread": a pipelined two-lane DE call drives the second lane from a host
@@ -1701,6 +1703,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
   else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
   else if (n == "interleave") ctx->opt_interleave = value != 0;
+  else if (n == "rest_thread") ctx->opt_rest_thread = value != 0;
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
     if (ctx->opt_lanes == 1 && ctx->peer) {  // one lane: the peer's workspace goes back to the device
@@ -2715,8 +2718,24 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       std::function<int()> rest0, rest1;
       RCHK(run_posterior(ctx, specs[0], ctx->us[0], &rest0));
       RCHK(run_posterior(lane, specs[1], ctx->us[1], &rest1));
-      RCHK(rest0());
-      RCHK(rest1());
+      if (ctx->opt_rest_thread) {
+        // the second group's draws, set-up kernels and bootstrap from a host thread of its own:
+        // its set-up no longer queues behind the first group's host-side set-up and bootstrap
+        // launch, so the two bootstraps can overlap
+        int rc1 = SCDE_OK;
+        std::string err1;
+        std::thread t1([&] {
+          rc1 = hipSetDevice(ctx->device) == hipSuccess ? rest1() : fail(SCDE_EHIP, "hipSetDevice");
+          if (rc1 != SCDE_OK) err1 = g_err;  // g_err is thread-local
+        });
+        const int rc0 = rest0();
+        t1.join();
+        RCHK(rc0);
+        if (rc1 != SCDE_OK) return fail(rc1, "%s", err1.c_str());
+      } else {
+        RCHK(rest0());
+        RCHK(rest1());
+      }
     } else {
       RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
       RCHK(run_posterior(ctx, specs[1], ctx->us[1]));
