@@ -160,6 +160,10 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   selected cells), 1..8 (default 4); results are the same
  *   "lane_thread"   1/0  a pipelined two-lane DE call drives the second lane (its unique sets,
  *                   tables and bootstrap) from a host thread of its own (results are the same)
+ *   "rest_thread"   1/0  a two-lane DE call on counts in HBM (or host counts under the pipelining
+ *                   threshold) drives the second group's draws, set-up and bootstrap launch from a
+ *                   host thread of its own (default 1; shard of 8: 1.72-1.81 -> 1.67-1.68 ms per
+ *                   step; results are the same)
  *   "interleave"    1/0  with lane_thread: both groups' ranges go up in alternating pieces, each
  *                   group's pieces built and tabled as they land (default 1; only when every
  *                   cell of the second group follows the first group's cells)

@@ -300,7 +300,7 @@ struct scde_ctx {
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
-  int opt_rest_thread = 0;      // "rest_thread": a two-lane DE call on counts in HBM runs the second group's
+  int opt_rest_thread = 1;      // "rest_thread": a two-lane DE call on counts in HBM runs the second group's
                                 // draws, set-up and bootstrap launch from a host thread of its own
   int opt_interleave = 1;       // "interleave": with lane_thread, both groups' ranges go up in alternating
                                 // pieces (when the second group's cells all follow the first group's range)

@@ -55,7 +55,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("upload_staged", opts.get("upload_staged", 0))
     ctx.set_option("lane_thread", opts.get("lane_thread", 0))
     ctx.set_option("interleave", opts.get("interleave", 1))
-    ctx.set_option("rest_thread", opts.get("rest_thread", 0))
+    ctx.set_option("rest_thread", opts.get("rest_thread", 1))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -85,7 +85,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("upload_staged", 0)
         ctx.set_option("lane_thread", 0)
         ctx.set_option("interleave", 1)
-        ctx.set_option("rest_thread", 0)
+        ctx.set_option("rest_thread", 1)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -111,7 +111,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
         "one-lane": {"lanes": 1},
-        "rest-thread": {"rest_thread": 1},
+        "rest-inline": {"rest_thread": 0},
         "pipelined-pieces": {"pipeline_mb": 0, "pieces": 3},
         "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1},
         "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1},
@@ -163,7 +163,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
                                     "gene-forced-list", "gene-list-overflow", "gene-3waves", "gene-4waves",
-                                    "tiles-unordered", "unique-exact", "one-lane", "rest-thread", "pipelined-pieces",
+                                    "tiles-unordered", "unique-exact", "one-lane", "rest-inline", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
                                     "pipelined-thread-seq",
                                     "tiles-pairs",
