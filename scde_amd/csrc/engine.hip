@@ -2413,6 +2413,30 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
 // posterior on its own streams and workspace, concurrently with the first group's on this
 // context's stream.  Both groups' launches then share the CUs: the second group's small set-up
 // kernels and its tables fill the first group's tails instead of waiting behind them.
+// The continuations of two lanes' posteriors (draws, set-up kernels, bootstrap launch): with
+// option rest_thread the second runs on a host thread of its own beside the first, so its set-up
+// does not queue behind the first lane's host-side set-up and bootstrap launch and the two
+// bootstraps can overlap; else one after the other.  (Each continuation touches only its own
+// context's buffers and streams; a shared unique set is read-only there.)
+static int run_rests(scde_ctx* ctx, const std::function<int()>& rest0, const std::function<int()>& rest1) {
+  if (!ctx->opt_rest_thread) {
+    RCHK(rest0());
+    return rest1();
+  }
+  int rc1 = SCDE_OK;
+  std::string err1;
+  std::thread t1([&] {
+    rc1 = hipSetDevice(ctx->device) == hipSuccess ? rest1() : fail(SCDE_EHIP, "hipSetDevice failed");
+    if (rc1 != SCDE_OK) err1 = g_err;  // g_err is thread-local
+  });
+  const int rc0 = rest0();
+  const std::string err0 = g_err;
+  t1.join();
+  if (rc0 != SCDE_OK) return fail(rc0, "%s", err0.c_str());
+  if (rc1 != SCDE_OK) return fail(rc1, "%s", err1.c_str());
+  return SCDE_OK;
+}
+
 static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   if (!cx->peer) {
     scde_ctx* p = nullptr;
@@ -2680,10 +2704,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         RCHK(build_unique_sets(lane, sp, usp, 1));
         hlap(1);
         RCHK(run_posterior(lane, specs[gi], ctx->us[gi], defer ? &rest1 : nullptr));
-        if (defer) {
-          RCHK(rest0());
-          RCHK(rest1());
-        }
+        if (defer) RCHK(run_rests(ctx, rest0, rest1));
         HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
         HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
       } else {
@@ -2718,24 +2739,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       std::function<int()> rest0, rest1;
       RCHK(run_posterior(ctx, specs[0], ctx->us[0], &rest0));
       RCHK(run_posterior(lane, specs[1], ctx->us[1], &rest1));
-      if (ctx->opt_rest_thread) {
-        // the second group's draws, set-up kernels and bootstrap from a host thread of its own:
-        // its set-up no longer queues behind the first group's host-side set-up and bootstrap
-        // launch, so the two bootstraps can overlap
-        int rc1 = SCDE_OK;
-        std::string err1;
-        std::thread t1([&] {
-          rc1 = hipSetDevice(ctx->device) == hipSuccess ? rest1() : fail(SCDE_EHIP, "hipSetDevice");
-          if (rc1 != SCDE_OK) err1 = g_err;  // g_err is thread-local
-        });
-        const int rc0 = rest0();
-        t1.join();
-        RCHK(rc0);
-        if (rc1 != SCDE_OK) return fail(rc1, "%s", err1.c_str());
-      } else {
-        RCHK(rest0());
-        RCHK(rest1());
-      }
+      RCHK(run_rests(ctx, rest0, rest1));
     } else {
       RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
       RCHK(run_posterior(ctx, specs[1], ctx->us[1]));
@@ -2912,12 +2916,10 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     RCHK(run_posterior(ctx, sb[0], ctx->us[2], &rest0));
     ctx->us[2].ready = true;  // same cells, same counts: reuse for the second batch run
     RCHK(run_posterior(lane, sb[1], ctx->us[2], &rest1));
-    RCHK(rest0());
-    RCHK(rest1());
+    RCHK(run_rests(ctx, rest0, rest1));
     RCHK(run_posterior(ctx, sg[0], ctx->us[0], &rest0));
     RCHK(run_posterior(lane, sg[1], ctx->us[1], &rest1));
-    RCHK(rest0());
-    RCHK(rest1());
+    RCHK(run_rests(ctx, rest0, rest1));
     HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
     HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
   } else {
