@@ -160,6 +160,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   selected cells), 1..8 (default 4); results are the same
  *   "lane_thread"   1/0  a pipelined two-lane DE call drives the second lane (its unique sets,
  *                   tables and bootstrap) from a host thread of its own (results are the same)
+ *   "boot_chunks"   k_boot_gene's grid in this many launches (default 1; 4 and 8 measured slower:
+ *                   config 3 6.85 -> 6.94-6.99 ms per step; results are the same)
  *   "rest_thread"   1/0  a two-lane DE call on counts in HBM (or host counts under the pipelining
  *                   threshold) drives the second group's draws, set-up and bootstrap launch from a
  *                   host thread of its own (default 1; shard of 8: 1.72-1.81 -> 1.67-1.68 ms per

@@ -300,6 +300,7 @@ struct scde_ctx {
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
+  int opt_boot_chunks = 1;      // "boot_chunks": k_boot_gene's grid in this many launches
   int opt_rest_thread = 1;      // "rest_thread": a two-lane DE call on counts in HBM runs the second group's
                                 // draws, set-up and bootstrap launch from a host thread of its own
   int opt_interleave = 1;       // "interleave": with lane_thread, both groups' ranges go up in alternating
@@ -1371,6 +1372,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           // 12 rows per gene block from gene3_cells cells per call (slabs mostly need two tiles there)
           tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (C >= cx->opt_gene3_cells ? 3 : 4);
           tb.W8g = cx->w8g.as<unsigned char>();
+          tb.chunks = std::max(1, cx->opt_boot_chunks);
         }
         if (have_order) tb.order = cx->gorder.as<int>();
         HCHK(launch_boot_tiles(b2, tb, st));
@@ -1704,6 +1706,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
   else if (n == "interleave") ctx->opt_interleave = value != 0;
   else if (n == "rest_thread") ctx->opt_rest_thread = value != 0;
+  else if (n == "boot_chunks") ctx->opt_boot_chunks = std::max(1, std::min((int)value, 64));
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
     if (ctx->opt_lanes == 1 && ctx->peer) {  // one lane: the peer's workspace goes back to the device
@@ -2477,6 +2480,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_gene_list_cap = cx->opt_gene_list_cap;
   p->opt_gene_waves = cx->opt_gene_waves;
   p->opt_gene3_cells = cx->opt_gene3_cells;
+  p->opt_boot_chunks = cx->opt_boot_chunks;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;

@@ -194,6 +194,7 @@ struct TileBootArgs {
   int gene_waves = 4;        // k_boot_gene waves per block: 4 (16 rows) or 3 (12 rows; wide calls)
   const unsigned char* W8g = nullptr;  // [nsets][ncells][groups][4 windows][32] the group's boots 32 w + j
                                        // as pair slots (boot 32 w + j, 32 w + 16 + j), 0 past its boots
+  int chunks = 1;  // k_boot_gene launches the gene blocks are split into (same blocks, same results)
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending

@@ -2596,7 +2596,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8g, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int kcap, int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order,
-    unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap) {
+    unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap, int blk0) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
   static_assert(WB == 3 || WB == 4, "3 or 4 waves per gene block");
   constexpr int kGeneRows = 4 * WB;
@@ -2620,7 +2620,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   const int lane = threadIdx.x & 63;
   const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NGR = (P + SG - 1) / SG;
-  const int blk = xcd_block(blockIdx.x, gridDim.x);
+  const int blk = blk0 + xcd_block(blockIdx.x, gridDim.x);  // blk0: this launch's first block (chunked grids)
   if (blk >= ngenes * NGR) return;  // uniform over the block
   const int gi = blk / NGR, gr = blk - gi * NGR;
   const int g = order ? order[gi] : gi;
@@ -3918,20 +3918,27 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   const long long gene_cap = tb.list_cap > 0 ? tb.list_cap : 16384;
   const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(items, gene_cap) : 0;
   const long long gblocks = gene ? (long long)a.ngenes * ((P + tb.SG - 1) / tb.SG) : 0;
+  // gene blocks in tb.chunks launches (>= 1): between launches the other lane's queued kernels
+  // get CU slots that one long grid would hold until its last block is dispatched
+  const long long chunk = std::max<long long>(1, (gblocks + std::max(1, tb.chunks) - 1) / std::max(1, tb.chunks));
 #define SCDE_BT(NBV)                                                                                              \
   case NBV:                                                                                                        \
-    if (gene && tb.gene_waves == 3)                                                                                \
-      hipLaunchKernelGGL((k_boot_gene<NBV, 3>), dim3((unsigned)gblocks), dim3(192), 0, s, a.D, a.ent, a.nnz,      \
-                         a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
-                         a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
-                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide,  \
-                         (int)items2);                                     \
-    else if (gene)                                                                                                 \
-      hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3((unsigned)gblocks), dim3(256), 0, s, a.D, a.ent, a.nnz,      \
-                         a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
-                         a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,    \
-                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, tb.wide,  \
-                         (int)items2);                                     \
+    if (gene)                                                                                                      \
+      for (long long c0 = 0; c0 < gblocks; c0 += chunk) {                                                          \
+        const unsigned nblk = (unsigned)std::min<long long>(chunk, gblocks - c0);                                  \
+        if (tb.gene_waves == 3)                                                                                    \
+          hipLaunchKernelGGL((k_boot_gene<NBV, 3>), dim3(nblk), dim3(192), 0, s, a.D, a.ent, a.nnz,               \
+                             a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
+                             a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
+                             tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
+                             tb.order, tb.pmask, tb.wide, (int)items2, (int)c0);                                 \
+        else                                                                                                       \
+          hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3(nblk), dim3(256), 0, s, a.D, a.ent, a.nnz,               \
+                             a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
+                             a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
+                             tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
+                             tb.order, tb.pmask, tb.wide, (int)items2, (int)c0);                                 \
+      }                                                                                                            \
     else                                                                                                           \
     hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
                        a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,      \

@@ -56,6 +56,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("lane_thread", opts.get("lane_thread", 0))
     ctx.set_option("interleave", opts.get("interleave", 1))
     ctx.set_option("rest_thread", opts.get("rest_thread", 1))
+    ctx.set_option("boot_chunks", opts.get("boot_chunks", 1))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -86,6 +87,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("lane_thread", 0)
         ctx.set_option("interleave", 1)
         ctx.set_option("rest_thread", 1)
+        ctx.set_option("boot_chunks", 1)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -108,6 +110,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "gene-list-overflow": {"gene_rows": 1, "gene_list_cap": 40},
         "gene-3waves": {"gene_waves": 3},
         "gene-4waves": {"gene_waves": 4},
+        "gene-chunks": {"boot_chunks": 3},
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
         "one-lane": {"lanes": 1},
@@ -162,7 +165,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
                         what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
-                                    "gene-forced-list", "gene-list-overflow", "gene-3waves", "gene-4waves",
+                                    "gene-forced-list", "gene-list-overflow", "gene-3waves", "gene-4waves", "gene-chunks",
                                     "tiles-unordered", "unique-exact", "one-lane", "rest-inline", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
                                     "pipelined-thread-seq",
