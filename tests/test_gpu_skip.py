@@ -178,3 +178,26 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
                                           got[base]["difference.posterior"].values)
             for k in ("Z", "cZ"):
                 np.testing.assert_array_equal(got[name]["results"][k].to_numpy(), got[base]["results"][k].to_numpy())
+
+
+@pytest.mark.parametrize("layout", ["reversed", "mixed"])
+def test_threaded_lane_group_layouts(api, layout):
+    """The host-count pipeline with the second lane on its own thread (options lane_thread,
+    interleave): with the groups' cells reversed (the second group's range first: both groups go up
+    in alternating pieces) and with the groups' cells mixed (no separable ranges: the sequential
+    upload), the table equals the unpipelined one bit for bit."""
+    import bench
+    from scde_amd.prior import expression_prior
+    models, counts, groups = bench.synthetic(8004, 150, 400)
+    groups = np.asarray(groups)
+    if layout == "reversed":
+        groups = 1 - groups
+    else:
+        groups = np.random.default_rng(5).permutation(groups)
+    prior = expression_prior(models, counts, length_out=400)
+    base, _ = _run(api, {}, models, counts, prior, groups, 30, 1)
+    got, _ = _run(api, {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1}, models, counts, prior, groups, 30, 1)
+    for i in range(2):
+        np.testing.assert_array_equal(got["joint.posteriors"][i], base["joint.posteriors"][i])
+    for k in ("lb", "mle", "ub", "ce", "Z", "cZ"):
+        np.testing.assert_array_equal(got["results"][k].to_numpy(), base["results"][k].to_numpy(), err_msg=k)
