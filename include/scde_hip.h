@@ -174,7 +174,7 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "gene_waves"    3/4  k_boot_gene's waves per block (12 or 16 rows); 0 (default) = 3 from
  *                   "gene3_cells" cells per call (default: never; slower at config 4), else 4
  *   "gene_list_cap" slabs k_boot_gene's four-tile list pass takes (0 = 16384; beyond: k_boot2)
- *   "skip_slack"    mask heuristic slack (NaN = default 30 + 0.4 C; tests force redo slabs)
+ *   "skip_slack"    mask heuristic slack (NaN = default 20 + 0.15 C; tests force redo slabs)
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
  *   "ratio_window"  k_ratio_summary register window 4, 5, 7 or 8;  "ratio_block" 64, 128, 256

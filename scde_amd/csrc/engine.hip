@@ -264,7 +264,7 @@ struct scde_ctx {
   Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
-  double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 30 + 0.4 C); tests force redo slabs
+  double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 20 + 0.15 C); tests force redo slabs
   int opt_boot_nb = 0;           // "boot_nb": boots per slab (0 = automatic; a multiple of 4 in [4, 32])
   int opt_skip_stats = 0;        // "skip_stats": count kept stretches / redo slabs (a host sync per launch)
   int opt_ratio_window = 4;      // "ratio_window": k_ratio_summary register window (4, 5, 7, 8)

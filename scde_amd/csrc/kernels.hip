@@ -3810,7 +3810,9 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (a.U && a.ZU && a.mask && a.ubuf && a.redo && block <= 64 * kStretchSlots &&
       sizeof(int2) * (size_t)a.ent_stride <= 60 * 1024) {
     // slack of the heuristic: UB's looseness grows with the draws per boot (~0.1 per cell)
-    const double slack = std::isnan(a.slack) ? 30.0 + 0.4 * a.ncells : a.slack;  // tests force post-check failures
+    // default 20 + 0.15 C (round 4 A/B: config 2 bootstrap 3.23 -> 3.14 ms per step, 2b 8.25 -> 7.9;
+    // was 30 + 0.4 C); the post-check keeps the output exact whatever the slack
+    const double slack = std::isnan(a.slack) ? 20.0 + 0.15 * a.ncells : a.slack;  // tests force post-check failures
     const size_t eshm = sizeof(int2) * (size_t)a.ent_stride;
 #define SCDE_SM(NBV)                                                                                              \
   case NBV:                                                                                                        \
