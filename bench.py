@@ -147,6 +147,10 @@ def profiled_traffic(config: str, member=None, last=None):
     out = {"file": "profiles/" + cands[-1], "kernel": " + ".join(sorted(stage)),
            "avg_ms": sum(v["avg_ms"] * v["calls"] for v in stage.values()) / n,
            "traffic_bytes": sum(v["traffic_bytes"] * v["calls"] for v in stage.values()) / n}
+    if all(v.get("fp64_flops") is not None for v in stage.values()):
+        # FP64 VALU flops per stage from the gfx950 instruction counters (tools/pmc_summary.py)
+        out["fp64_flops"] = sum(v["fp64_flops"] * v["calls"] for v in stage.values()) / n
+        out["fma_f64_insts"] = sum(v["SQ_INSTS_VALU_FMA_F64"] * v["calls"] for v in stage.values()) / n
     cyc = sum(v.get("SQ_WAVE_CYCLES", 0) * v["calls"] for v in stage.values())
     if cyc > 0:  # share of the stage's wave cycles spent waiting (SQ_WAIT_ANY / SQ_WAVE_CYCLES)
         out["wait_frac"] = sum(v.get("SQ_WAIT_ANY", 0) * v["calls"] for v in stage.values()) / cyc
@@ -154,19 +158,19 @@ def profiled_traffic(config: str, member=None, last=None):
 
 
 def add_profile_fields(roof: dict, prof, stage_s=None):
-    """traffic / counter-bytes fraction / wait share from a profiled_traffic() record.  Every
-    fraction in a roofline is on ONE time base: the stage's live HIP-event time in this run
-    (stage_s, seconds per stage) when given, else the profile's own rocprof time (stated in
-    `time_base`); the rocprof average stays beside it as a cross-check."""
+    """traffic / counter-bytes fraction / wait share from a profiled_traffic() record, on the
+    profile's own rocprofv3 stage time (the time base of `frac` too, so every fraction in the line
+    can be recomputed from the committed profile); stage_s (seconds per stage, HIP events in this
+    run), when given, adds the same bytes over that live time beside it."""
     if not prof:
         return
     roof["traffic"] = prof["traffic_bytes"]
     roof["traffic_source"] = f"{prof['file']} ({prof['kernel']}, rocprofv3 avg {prof['avg_ms']:.3f} ms per stage)"
     roof["rocprof_stage_ms"] = prof["avg_ms"]
-    t = stage_s if stage_s else prof["avg_ms"] / 1e3
-    roof["counter_bytes_frac"] = prof["traffic_bytes"] / t / 1e9 / HBM_PEAK_GBS
-    roof["time_base"] = ("HIP events around the stage in this run (its lanes = 1 pass)" if stage_s else
-                         "rocprofv3 kernel durations of the committed profile")
+    roof["counter_bytes_frac"] = prof["traffic_bytes"] / (prof["avg_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
+    roof["time_base"] = "rocprofv3 kernel durations of the committed profile (stage = its kernels per stage)"
+    if stage_s:
+        roof["counter_bytes_frac_live"] = prof["traffic_bytes"] / stage_s / 1e9 / HBM_PEAK_GBS
     if prof.get("wait_frac") is not None:
         roof["wait_frac"] = prof["wait_frac"]
 
@@ -695,37 +699,53 @@ def main():
     boot_ms, boot_n = kt["boot"]
     boot_avg_s = (boot_ms / max(boot_n, 1)) / 1e3
     boot_step_s = boot_ms / 1e3 / args.steps
+    launches_per_step = boot_n / args.steps if boot_n else 0
     cpg = NC // 2 if de else NC
     # bootstrap launches of one step and their cells: (per group) + (all cells, per group) if batched
     launch_cells = ([cpg, cpg] if de else [NC]) + ([NC, NC] if batched else [])
     step_bytes = sum(dominant_kernel_bytes(NG, c) for c in launch_cells)
     per_launch_bytes = step_bytes / len(launch_cells)
-    hbm_alg = step_bytes * args.steps / (boot_ms / 1e3) / 1e9 if boot_n else None
-    prof = profiled_traffic(args.config)
-    # reference-formulation FP64 adds per launch: B x C x G x N
-    ref_adds = NBOOT * sum(launch_cells) / len(launch_cells) * G * NG
-    f64_tf = 2 * step_fma / boot_step_s / 1e12 if boot_n and step_fma else 0.0
-    # FP64 bootstrap: the FMAs its computed tiles / kept stretches issue, against the FP64 VALU peak
-    roof = {"bound": "fp64-valu", "kernel": stage_name, "achieved": f64_tf, "peak": FP64_VALU_PEAK_TF,
-            "unit": "TFLOP/s", "frac": f64_tf / FP64_VALU_PEAK_TF,
-            "frac_of_measured_fma_rate": f64_tf / FP64_FMA_MEASURED_TF,
-            "achieved_basis": "lane FMAs the FP64 bootstrap kernels issue (computed grid points x slab boots x "
-                              "entries, x2 flops) per step / stage time per step (HIP events)"}
-    roof.update({
-        "traffic": None,
-        "avg_launch_ms": boot_avg_s * 1e3, "launches": boot_n,
-        # SURVEY.md §8(d)'s algorithmic bytes of the reference formulation over the stage time:
-        # the work avoided (sparse deltas, skipped stretches) counts as if it were read
-        "algorithmic_bytes_per_launch": per_launch_bytes,
-        "hbm_algorithmic_gbs": hbm_alg,
-        "hbm_algorithmic_frac": (hbm_alg / HBM_PEAK_GBS) if hbm_alg else None,
-        "ref_fp64_adds_per_s": ref_adds / boot_avg_s if boot_n else None,
-        "f64_fma_per_step": step_fma})
-    # what the stage really moves: counter bytes per stage (committed profile of this config at
-    # N = 1), over this run's stage time; a shard's stage moves other bytes, so --shard-of lines
-    # carry no traffic
-    if args.shard_of <= 1 and world == 1:
-        add_profile_fields(roof, prof, boot_avg_s if boot_n else None)
+    # the committed rocprofv3 profile of this config (N = 1 only: a shard's stage is another workload)
+    prof = profiled_traffic(args.config) if args.shard_of <= 1 and world == 1 else None
+    # live: the FMAs the FP64 bootstrap kernels issue (self-counted in one extra step) over the stage's
+    # HIP-event time in this run's lanes = 1 pass
+    live_tf = 2 * step_fma / boot_step_s / 1e12 if boot_n and step_fma else None
+    live = {"stage_ms": boot_avg_s * 1e3 if boot_n else None, "launches_per_step": launches_per_step,
+            "achieved": live_tf, "frac": live_tf / FP64_VALU_PEAK_TF if live_tf else None,
+            "f64_fma_per_step": step_fma,
+            "basis": "lane FMAs the FP64 bootstrap kernels issue (self-counted: computed grid points x slab boots x "
+                     "entries, x2 flops) / the stage's HIP-event time in this run (lanes = 1 pass)"}
+    if prof and prof.get("fp64_flops"):
+        # One time base, the committed profile's: FP64 flops per stage from the gfx950 instruction
+        # counters (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F64 x 64 lanes, FMA x2) over its rocprofv3 stage time
+        achieved = prof["fp64_flops"] / (prof["avg_ms"] / 1e3) / 1e12
+        basis = (f"FP64 VALU flops per stage from {prof['file']} (SQ_INSTS_VALU_{{FMA,ADD,MUL,TRANS}}_F64 x 64, "
+                 f"FMA x2) / its rocprofv3 stage time (sum of the stage's kernel durations per stage)")
+    else:
+        achieved = live_tf or 0.0
+        basis = live["basis"]
+    roof = {"bound": "fp64-valu", "kernel": stage_name, "achieved": achieved, "peak": FP64_VALU_PEAK_TF,
+            "unit": "TFLOP/s", "frac": achieved / FP64_VALU_PEAK_TF,
+            "frac_of_measured_fma_rate": achieved / FP64_FMA_MEASURED_TF, "achieved_basis": basis,
+            "traffic": None, "live": live}
+    if prof:
+        add_profile_fields(roof, prof)
+        if prof.get("fp64_flops"):
+            roof["fp64_flops_per_stage"] = prof["fp64_flops"]
+            roof["fma_f64_wave_insts_per_stage"] = prof["fma_f64_insts"]
+            if step_fma and launches_per_step:
+                # the self-counted row FMAs against the counter's FMA lanes (rows are most of them)
+                roof["self_counted_over_counter_fma"] = (step_fma / launches_per_step) / (64.0 * prof["fma_f64_insts"])
+    # SURVEY.md §8(d)'s byte model describes the reference formulation (every cell's column read per
+    # gene and boot); the kernels skip the baseline cells and the tiles the post-check proves
+    # irrelevant, so this is work avoided, not a roofline (its "fraction" can exceed 1): reported
+    # outside `roofline`
+    ref_model = {"algorithmic_bytes_per_launch": per_launch_bytes,
+                 "bytes_per_s_over_live_stage": step_bytes * args.steps / (boot_ms / 1e3) if boot_n else None,
+                 "reference_fp64_adds_per_launch": NBOOT * sum(launch_cells) / len(launch_cells) * G * NG,
+                 "note": "SURVEY.md 8(d)'s reference-formulation work per bootstrap launch; the kernels do not "
+                         "perform it (sparse deltas over a shared baseline, post-checked tile skipping), so it "
+                         "bounds nothing and is not a roofline fraction"}
     out = {
         "metric": (METRIC_BATCH if batched else METRIC) if de else "genes/sec for scde.posteriors with posterior modes "
                                                                    "(400-pt grid, 100 randomizations)",
@@ -751,6 +771,7 @@ def main():
         "device_resident_genes_per_s": NTOT * args.steps / dt_dev,
         "device_resident_ms_per_step": dt_dev / args.steps * 1e3,
         "roofline": roof,
+        "reference_formulation": ref_model,
         "kernel_ms_per_step": {k: v[0] / args.steps for k, v in kt.items() if v[1]},
         # in-library synchronisation over the timed steps: context-scoped
         # stream drains by grow-only buffer regrowth and pinned-arena wraps, and reallocations

@@ -131,7 +131,7 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   operand; a call with a larger one runs plain k_boot2 on the same columns --
  *                   tests force that fallback with a small value)
  *   "tile_order"    1/0  k_boot_tiles takes the genes in order of their count sums, so waves in
- *                   flight share columns and tiles in L2 (default 0 while under test; results are the same)
+ *                   flight share columns and tiles in L2 (default 1; results are the same)
  *   "unique_fixed"  1/0  build each call's unique count tables with one host sync (fixed
  *                   1024-word bitmaps per cell, counts below 65,536; a set with another count is
  *                   rebuilt with exact widths); default 1

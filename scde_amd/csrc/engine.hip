@@ -9,6 +9,7 @@
 #include <chrono>
 #include <cfloat>
 #include <cmath>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1614,9 +1615,20 @@ int scde_ctx_create(int device, scde_ctx** out) {
       pos = end + 1;
       const size_t eq = item.find('=');
       if (item.empty()) continue;
-      const int rc = eq == std::string::npos ? fail(SCDE_EARG, "SCDE_OPTIONS item '%s' is not name=value", item.c_str())
-                                             : scde_ctx_set_option(c, item.substr(0, eq).c_str(),
-                                                                   std::atof(item.c_str() + eq + 1));
+      int rc = SCDE_OK;
+      if (eq == std::string::npos) {
+        rc = fail(SCDE_EARG, "SCDE_OPTIONS item '%s' is not name=value", item.c_str());
+      } else {
+        // the whole value must be a number ("lanes=abc" or "lanes=" fail instead of becoming 0)
+        const char* vs = item.c_str() + eq + 1;
+        char* vend = nullptr;
+        errno = 0;
+        const double v = std::strtod(vs, &vend);
+        if (*vs == '\0' || vend == vs || *vend != '\0' || errno == ERANGE)
+          rc = fail(SCDE_EARG, "SCDE_OPTIONS item '%s': value is not a number", item.c_str());
+        else
+          rc = scde_ctx_set_option(c, item.substr(0, eq).c_str(), v);
+      }
       if (rc != SCDE_OK) {
         scde_ctx_destroy(c);
         return rc;

@@ -3917,7 +3917,11 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   const long long items1 = pairs ? (long long)a.ngenes * ((P + 1) / 2) : items;
   // slabs a pair pass (or a gene block) may leave to the four-tile list pass
   // (gene blocks: at most list_cap slabs, 16384 by default; k_boot_gene sends further failures to k_boot2)
-  const long long gene_cap = tb.list_cap > 0 ? tb.list_cap : 16384;
+  // The cap is rounded down to a multiple of the list pass's WB waves per block: k_boot_gene writes
+  // list entries only below it (wide[0] keeps counting past it), and the list pass's grid of
+  // items2 / WB blocks must then hold no wave whose index lies in [cap, grid * WB) -- such a wave
+  // would read an entry this call never wrote.
+  const long long gene_cap = std::max<long long>(WB, ((tb.list_cap > 0 ? tb.list_cap : 16384) / WB) * WB);
   const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(items, gene_cap) : 0;
   const long long gblocks = gene ? (long long)a.ngenes * ((P + tb.SG - 1) / tb.SG) : 0;
   // gene blocks in tb.chunks launches (>= 1): between launches the other lane's queued kernels

@@ -10,7 +10,7 @@ import socket
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import assert_cz_close, assert_z_close, golden
 
 NRAND = 12
 NCORES = 7
@@ -124,11 +124,11 @@ def test_device_shards_match_unsharded():
              for lo, hi in ((0, 31), (31, 32), (32, NGENES))]
     sh = np.vstack(parts)
     np.testing.assert_array_equal(sh[:, :4], full[:, :4])
-    np.testing.assert_allclose(sh[:, 4], full[:, 4], rtol=1e-6, atol=1e-9)
+    assert_z_close(sh[:, 4], full[:, 4], what="shards Z vs unsharded")
     want = oracle_shard(models, counts, prior, codes, NRAND, NCORES, 0.0, 0, NGENES)
     for j in range(4):
         np.testing.assert_array_equal(full[:, j], want[:, j])
-    np.testing.assert_allclose(full[:, 4], want[:, 4], rtol=1e-6, atol=1e-9)
+    assert_z_close(full[:, 4], want[:, 4], what="device shard Z vs oracle")
 
 
 @pytest.mark.gpu
@@ -146,4 +146,5 @@ def test_gloo_hip_shards_match_single_process(tmp_path):
                                          n_cores=NCORES)
     want = ref[["lb", "mle", "ub", "ce", "Z", "cZ"]].to_numpy()
     np.testing.assert_array_equal(got[:, :4], want[:, :4])
-    np.testing.assert_allclose(got[:, 4:], want[:, 4:], rtol=1e-6, atol=1e-9)
+    assert_z_close(got[:, 4], want[:, 4], what="gloo HIP shards Z")
+    assert_cz_close(got[:, 5], want[:, 5], got[:, 4], want[:, 4], what="gloo HIP shards cZ")

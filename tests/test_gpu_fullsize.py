@@ -145,3 +145,79 @@ def test_config2b_slice_b100(api, oracle):
             np.testing.assert_array_equal(got[k].to_numpy(), want[k], err_msg=f"{table}.{k}")
         assert_z_close(got["Z"].to_numpy(), want["Z"], what=f"{table}.Z")
         assert_cz_close(got["cZ"].to_numpy(), want["cZ"], got["Z"].to_numpy(), want["Z"], what=f"{table}.cZ")
+
+
+def test_config3_host_pipeline_after_call_history(api):
+    """a full-size wrong table once appeared only after other calls in the same
+    process (the dropped direct-row experiment).  The per-call state kept in grow-only buffers (the
+    list pass's `wide` count and entries, the `redo` flags and list, `pmask`, partial rows, the
+    unique sets' fixed-width offsets and bitmaps, the peer lane's workspace) must not leak from one
+    call into the next.  So: the device-resident config-3 table on a fresh context (one lane, no
+    pipelining) is the reference; then, on another fresh context, a varied history -- a batch DE,
+    scde.posteriors with modes (postflag 1), a smaller DE (fewer genes: every per-gene buffer holds
+    longer stale contents), a DE with the list pass forced and capped (gene_rows = 1,
+    gene_list_cap = 41: stale list entries past the cap), a DE with NaN-free but wider counts --
+    and then the full host pipeline twice (4 and 3 pieces, two lanes): both equal the reference bit
+    for bit."""
+    import ctypes
+    import bench
+    from scde_amd._lib import DEParams, check, lib
+    from scde_amd.models import model_matrix
+    from scde_amd.prior import expression_prior
+    cfg = bench.CONFIGS["3"]
+    models, counts, groups = bench.synthetic(cfg["seed"], cfg["genes"], cfg["cells"], two_groups=True)
+    prior = expression_prior(models, counts, length_out=bench.LENGTH_OUT)
+    mat = np.asfortranarray(counts, dtype=np.int32)
+    N, C = mat.shape
+    codes = np.ascontiguousarray(np.asarray(groups), np.int32)
+    mm, lt, sq = model_matrix(models)
+    px = np.ascontiguousarray(prior["x"], np.float64)
+    py = np.ascontiguousarray(prior["y"], np.float64)
+    params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, len(px), 100, 1,
+                      0, N, 0.0, api.get_rand_kind(), 1)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    api.set_rand("glibc")
+    ref_ctx = api.Context(0)
+    try:
+        ref_ctx.set_option("lanes", 1)
+        dc = api.DeviceCounts(ref_ctx, mat)
+        ref = np.zeros((N, 6), order="F")
+        check(lib().scde_expression_difference_dev(ref_ctx.handle, dc.ptr, N, N, ctypes.byref(params), vp(ref), None,
+                                                   None, None))
+        dc.free()
+    finally:
+        ref_ctx.close()
+    ctx = api.Context(0)
+    try:
+        # history: batch DE (four posteriors, 1601-column second level) on a slice
+        sub = np.asfortranarray(mat[:700])
+        batch = np.array(["b%d" % (c % 2) for c in range(C)], dtype=object)
+        api.scde_expression_difference(models, sub, prior, groups=list(groups), batch=batch, n_randomizations=30,
+                                       n_cores=3, ctx=ctx)
+        # scde.posteriors with posterior modes (one group, all cells)
+        api.scde_posteriors(models, np.asfortranarray(mat[:1500]), prior, n_randomizations=40,
+                            return_individual_posterior_modes=True, n_cores=2, ctx=ctx)
+        # a smaller DE, then one with the list pass forced and capped off a multiple of 4
+        api.scde_expression_difference(models, np.asfortranarray(mat[5000:9000]), prior, groups=list(groups),
+                                       n_randomizations=100, n_cores=1, ctx=ctx)
+        ctx.set_option("gene_rows", 1)
+        ctx.set_option("gene_list_cap", 41)
+        api.scde_expression_difference(models, np.asfortranarray(mat[:3000]), prior, groups=list(groups),
+                                       n_randomizations=100, n_cores=5, ctx=ctx)
+        ctx.set_option("gene_rows", 4)
+        ctx.set_option("gene_list_cap", 0)
+        # counts past the fixed bitmaps' 65,535 in a slice of the matrix (the exact unique rebuild)
+        wide = np.asfortranarray(mat[:800].copy())
+        wide[::97, ::13] += 70000
+        api.scde_expression_difference(models, wide, prior, groups=list(groups), n_randomizations=20, n_cores=1,
+                                       ctx=ctx)
+        for pieces in (4, 3):
+            ctx.set_option("pieces", pieces)
+            host = np.zeros((N, 6), order="F")
+            check(lib().scde_expression_difference_host(ctx.handle, vp(mat), N, N, ctypes.byref(params), vp(host),
+                                                        None, None, None))
+            bad = np.nonzero(np.any(host != ref, axis=1))[0]
+            assert bad.size == 0, (f"pieces {pieces}: {bad.size} of {N} genes differ after the call history; "
+                                   f"first gene {bad[0]}: {host[bad[0]]} vs {ref[bad[0]]}")
+    finally:
+        ctx.close()

@@ -45,3 +45,9 @@ def test_unknown_option_fails_creation_with_its_name():
 def test_malformed_item_fails_creation():
     out = _run("lanes")
     assert "CREATE-FAILED" in out and "name=value" in out, out
+
+
+@pytest.mark.parametrize("bad", ["lanes=abc", "boot_tiles_cells=", "lanes=2x"])
+def test_non_numeric_value_fails_creation(bad):
+    out = _run(bad)
+    assert "CREATE-FAILED" in out and "not a number" in out, out

@@ -108,6 +108,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-slab-waves-redo": {"gene_blocks": 0, "tile_groups": 2},
         "gene-forced-list": {"gene_rows": 1},
         "gene-list-overflow": {"gene_rows": 1, "gene_list_cap": 40},
+        # a cap that is not a multiple of the list pass's 4 waves per block (rounded down to 40)
+        "gene-list-overflow-odd": {"gene_rows": 1, "gene_list_cap": 41},
         "gene-3waves": {"gene_waves": 3},
         "gene-4waves": {"gene_waves": 4},
         "gene-chunks": {"boot_chunks": 3},
@@ -140,7 +142,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
             assert stats["boot_path"] == 1 and stats["skip_redo"] > 0, stats
         elif name == "gene-forced-list":  # gene blocks with one row per slab: the list pass finishes the rest
             assert stats["boot_path"] == 1 and stats["pair_redo"] > 0 and stats["skip_slabs"] > 0, stats
-        elif name == "gene-list-overflow":  # ... past its 40 slabs the failures go to k_boot2 directly
+        elif name in ("gene-list-overflow", "gene-list-overflow-odd"):  # past 40 slabs: k_boot2 directly
             assert stats["boot_path"] == 1 and 0 < stats["pair_redo"] <= 80 and stats["skip_redo"] > 0, stats  # 40 per lane
         elif name == "tiles-pairs":
             # two slabs per wave, two bound tiles each: at these cell counts many slabs need more and
@@ -165,7 +167,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
                         what=f"{name} cZ")
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
-                                    "gene-forced-list", "gene-list-overflow", "gene-3waves", "gene-4waves", "gene-chunks",
+                                    "gene-forced-list", "gene-list-overflow", "gene-list-overflow-odd", "gene-3waves", "gene-4waves", "gene-chunks",
                                     "tiles-unordered", "unique-exact", "one-lane", "rest-inline", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
                                     "pipelined-thread-seq",

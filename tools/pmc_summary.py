@@ -20,6 +20,9 @@ import sys
 import pandas as pd
 
 
+F64_COUNTERS = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_TRANS_F64")
+
+
 def short_name(name: str) -> str:
     """'void scde::k_boot2<20>(double const*, ...)' -> 'k_boot2<20>';
     'scde::(anonymous namespace)::k_prior_bin(int const*, ...)' -> 'k_prior_bin'."""
@@ -72,9 +75,14 @@ def main(src: str, prefix: str) -> None:
             if pd.notna(hit) and pd.notna(miss) and hit + miss > 0:
                 e["l2_hit"] = float(hit / (hit + miss))
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAVE_CYCLES", "SQ_INSTS_VALU",
-                      "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD"):
+                      "SQ_INSTS_SMEM", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD") + F64_COUNTERS:
                 if c in row.index and pd.notna(row[c]):
                     e[c] = float(row[c])
+            # FP64 VALU flops per launch from the gfx950 per-class instruction counters (wave
+            # instructions x 64 lanes; an FMA counts 2), omniperf's formula
+            if all(c in e for c in F64_COUNTERS):
+                e["fp64_flops"] = 64.0 * (2.0 * e["SQ_INSTS_VALU_FMA_F64"] + e["SQ_INSTS_VALU_ADD_F64"] +
+                                          e["SQ_INSTS_VALU_MUL_F64"] + e["SQ_INSTS_VALU_TRANS_F64"])
         summary["kernels"][k] = e
     with open(prefix + "_summary.json", "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
