@@ -310,6 +310,8 @@ struct scde_ctx {
                                 // thread of its own
   int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
                                 // the second group's tables
+  int opt_fuse_groups = 1;       // "fuse_groups": a DE call's two group posteriors run as one (PostSpec::ngroups:
+                                 // concatenated cells, doubled genes, one launch per stage); 0: two posteriors
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                  // group on `peer`, its own streams and workspace) or one after the other (1)
   // the second lane of a DE call: a context on the same device, created on first use; its
@@ -604,6 +606,15 @@ struct PostSpec {
   std::function<int(int)> piece_ready;
   hipStream_t piece_stream = nullptr;
   hipEvent_t* piece_ev = nullptr;
+  // A DE call's two group posteriors fused into one (de_run, option fuse_groups): the spec's cells
+  // are group A's (cells [0, gsplit)) then group B's, its seed sets A's then B's (B's set s is
+  // nsets_g + s; `seeds` lists both, `wset` is [2 ngenes], B's genes offset by nsets_g), and the
+  // bootstrap runs over 2 ngenes genes: gene g + ngenes is gene g of group B.  Every value is formed
+  // as in the group's own call (its cells' order in the baseline sums, its clamp constant, its
+  // draws), so the fused call is bit-identical to two calls.  jp holds 2 ngenes gene-major rows.
+  int ngroups = 1;
+  int gsplit = 0;
+  int nsets_g = 0;
 };
 
 constexpr size_t kPinCap = size_t(16) << 20;  // the arena
@@ -813,6 +824,28 @@ int build_unique_sets(scde_ctx* cx, const PostSpec* const* s, UniqueSet* const* 
 // Draw lists and per-cell multiplicities for each seed set.
 void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<double>& W, int& ndraw) {
   const int C = s.ncells, B = s.nboot, nsets = (int)s.seeds.size();
+  if (s.ngroups == 2 && !s.batch_call) {
+    // fused groups: set `set` belongs to group B from nsets_g on; each draws from its own group's
+    // cells (the group's own call, cell indices offset into the fused list); the shorter group's
+    // draw lists are padded with -1
+    const int Cg[2] = {s.gsplit, C - s.gsplit};
+    ndraw = std::max(Cg[0], Cg[1]);
+    draws.assign((size_t)nsets * B * std::max(ndraw, 1), -1);
+    W.assign((size_t)nsets * C * Bp, 0.0);
+    for (int set = 0; set < nsets; ++set) {
+      const int gi = set >= s.nsets_g ? 1 : 0, c0 = gi ? s.gsplit : 0, n = Cg[gi];
+      PlatformRand rng((unsigned int)s.seeds[set], s.rand_kind);
+      int* dr = draws.data() + (size_t)set * B * std::max(ndraw, 1);
+      double* w = W.data() + (size_t)set * C * Bp;
+      for (int b = 0; b < B; ++b)
+        for (int j = 0; j < n; ++j) {
+          const int cell = c0 + rng.draw(n);
+          dr[(size_t)b * ndraw + j] = cell;
+          w[(size_t)cell * Bp + b] += 1.0;
+        }
+    }
+    return;
+  }
   if (s.batch_call) {
     ndraw = 0;
     for (int k = 0; k < s.nbatch; ++k) ndraw += std::max(0, s.comp[k]);
@@ -854,8 +887,21 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
 // rest (nullable): return once the tables are queued, with the remaining work (modes, draws,
 // bootstrap, outputs) in *rest, to be run later on the same stream -- de_run queues both groups'
 // tables before either bootstrap, so the second lane's tables start at once
+// status of run_posterior for a fused two-group spec whose fused column count leaves the fast
+// bootstrap path (columns past 2^31 / GS): de_run runs the two groups separately instead
+constexpr int kRetryUnfused = 1001;
+
 int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<int()>* rest = nullptr) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
+  const bool two = s.ngroups == 2;
+  if (two && (s.gsplit <= 0 || s.gsplit >= C || s.batch_call || s.ensemble || s.nboot <= 0 || s.modes || s.post ||
+              s.ucl_host || (int)s.wset.size() != 2 * N || (int)s.seeds.size() != 2 * s.nsets_g))
+    return fail(SCDE_EINTERNAL, "fused groups: bad spec");
+  // cells per call of the kernel choices (a fused call's groups choose alike, de_run checks) and
+  // the widest group (ELL rows); the bootstrap's genes (both groups' when fused)
+  const int Ccall = two ? std::min(s.gsplit, C - s.gsplit) : C;
+  const int Cmax = two ? std::max(s.gsplit, C - s.gsplit) : C;
+  const int NBg = two ? 2 * N : N;
   // column stride: >= the k_boot2 block (lanes never read past a column); 512 keeps
   // columns 4 KiB-aligned
   const int GS = G <= 448 ? 512 : (int)round_up(G, 64);
@@ -946,7 +992,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // tables are set up for it before the draws exist; should a multiplicity exceed 127 (a
     // cell drawn 128 times in one boot), plain k_boot2 runs on the same D columns instead.
     p.tpath = p.fused && s.nboot > 0 && G <= 448 && cx->opt_boot_skip && cx->opt_boot_tiles &&
-              C >= cx->opt_boot_tiles_cells && nbp <= 20 && C < 100000 && (nc + 1) * (long long)GS < (1LL << 31);
+              Ccall >= cx->opt_boot_tiles_cells && nbp <= 20 && C < 100000 && (nc + 1) * (long long)GS < (1LL << 31);
     // k_boot2 grid-stretch skipping (G <= 448: at most 7 stretches of 64 points); the
     // tables kernel emits the per-column stretch maxima
     p.stretch_skip = p.fused && !p.tpath && G <= 448 && cx->opt_boot_skip;
@@ -954,6 +1000,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   };
   // pieces: planned for the smallest column count (every condition holds for fewer columns)
   const Plan plan0 = make_plan(pieces ? 0 : ucl_off_h[C]);
+  if (two && !plan0.fused) return kRetryUnfused;
   const bool want_maxi = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
   TablesArgs ta{};
   // buffers for `cap` columns (pieces: grown keeping what earlier pieces wrote) and the
@@ -980,7 +1027,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     ta.lcfpr = cx->lcfpr.as<double>();
     ta.theta = cx->theta.as<double>();
     ta.cellscal = cx->cellscal.as<double>();
-    ta.minlogprob = -1 * DBL_MAX / C / 1.1;
+    // the reference's clamp, -DBL_MAX / (cells in the call) / 1.1: per group when two are fused
+    ta.minlogprob = -1 * DBL_MAX / (s.ngroups == 2 ? s.gsplit : C) / 1.1;
+    ta.minlogprob2 = -1 * DBL_MAX / (s.ngroups == 2 ? C - s.gsplit : C) / 1.1;
+    ta.mlp_split = s.ngroups == 2 ? s.gsplit : C;
     ta.T = p.keep_T ? cx->T.as<double>() : nullptr;
     ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
     ta.has_clamp = cx->has_clamp.as<unsigned char>();
@@ -1026,6 +1076,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     if (tc.zcol) tc.zcol = ta.zcol + c0;
     if (tc.base_col) tc.base_col = ta.base_col + c0;
     tc.col_base = (int)col0;
+    tc.mlp_split = ta.mlp_split - c0;  // relative to the launch's first cell
     // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
     if (G <= 448 && nc > 0) {
       constexpr long long kTaskCols = kTabTaskCols;
@@ -1127,6 +1178,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   }
   const long long ncols = ucl_off_h[C];
   const Plan plan = make_plan(ncols);
+  if (two && !plan.fused) return kRetryUnfused;
   const bool fast = plan.fast, fused = plan.fused, stretch_skip = plan.stretch_skip;
   bool tpath = plan.tpath;
   ta.ncols = ncols;
@@ -1147,8 +1199,11 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   std::vector<double> W;
   int ndraw = 0, maxw = 0;
   const int nsets = (int)s.seeds.size();
+  // the cells a seed set draws from (fused groups: its own group's)
+  auto set_c0 = [&](int set) { return two && set >= s.nsets_g ? s.gsplit : 0; };
+  auto set_c1 = [&](int set) { return two && set < s.nsets_g ? s.gsplit : C; };
   // tile path ELL rows: a multiple of 64 entries (the bound MFMAs' K steps) plus 64
-  const int qstride = (int)round_up(std::max(C, 1), 64) + 64;
+  const int qstride = (int)round_up(std::max(Cmax, 1), 64) + 64;
   // FP64 path: boots per slab; the draws come after the tables launch (the host's RNG work
   // then overlaps the tables kernel instead of leaving the GPU idle in front of it)
   int nb = fast ? boot2_nb(s.nboot) : 16;
@@ -1208,9 +1263,9 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
                             s.use_baseline ? 1 : 0, cx->base_col.as<int>(), st));
     }
     // + one look-ahead batch (k_boot2); the tile path's bounds read whole 64-entry steps
-    const int stride = tpath ? qstride : (int)round_up(C, 8) + 8;
-    HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)N * stride)));
-    HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, N)));
+    const int stride = tpath ? qstride : (int)round_up(Cmax, 8) + 8;
+    HCHK(cx->ent.ensure(sizeof(int2) * std::max<long long>(1, (long long)NBg * stride)));
+    HCHK(cx->nnz.ensure(sizeof(int) * std::max(1, NBg)));
     ev = cx->mark_begin(SLOT_OTHER);
     if (!fused) {
       HCHK(cx->E.ensure(sizeof(double) * (size_t)(ncols + 1) * GS));
@@ -1219,21 +1274,26 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     }
     // the baseline columns: T (slow path) or the fused D buffer, which holds T there
     const double* Tbase = fused ? cx->E.as<double>() : cx->T.as<double>();
-    HCHK(launch_ell(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->base_col.as<int>(), stride,
-                    (int)ncols, tpath ? 64 : 8, cx->ent.as<int2>(), cx->nnz.as<int>(), sa));
+    // ELL rows (fused groups: group B's genes after group A's, over B's cells, cells offset by gsplit)
+    for (int gi = 0; gi < (two ? 2 : 1); ++gi) {
+      const int c0 = gi ? s.gsplit : 0, nc = two ? (gi ? C - s.gsplit : s.gsplit) : C;
+      HCHK(launch_ell(u.uci.as<int>() + (size_t)N * c0, N, N, nc, u.ucl_off.as<long long>() + c0,
+                      cx->base_col.as<int>() + c0, stride, (int)ncols, tpath ? 64 : 8,
+                      cx->ent.as<int2>() + (size_t)gi * N * stride, cx->nnz.as<int>() + (size_t)gi * N, sa, c0));
+    }
     // tile path: genes in order of their count sums (waves in flight share columns in L2)
-    const bool have_order = tpath && fast && cx->opt_tile_order && N > 1;
+    const bool have_order = tpath && fast && cx->opt_tile_order && NBg > 1;
     if (have_order) {
-      HCHK(cx->gkey.ensure(sizeof(unsigned) * N));
-      HCHK(cx->gkey2.ensure(sizeof(unsigned) * N));
-      HCHK(cx->gidx.ensure(sizeof(int) * N));
-      HCHK(cx->gorder.ensure(sizeof(int) * N));
+      HCHK(cx->gkey.ensure(sizeof(unsigned) * NBg));
+      HCHK(cx->gkey2.ensure(sizeof(unsigned) * NBg));
+      HCHK(cx->gidx.ensure(sizeof(int) * NBg));
+      HCHK(cx->gorder.ensure(sizeof(int) * NBg));
       size_t wb = 0;
-      HCHK(launch_gene_order(nullptr, nullptr, N, nullptr, nullptr, nullptr, &wb, sa));
+      HCHK(launch_gene_order(nullptr, nullptr, NBg, nullptr, nullptr, nullptr, &wb, sa));
       HCHK(cx->gwork.ensure(std::max<size_t>(wb, 1)));
-      HCHK(launch_gene_key(cx->ent.as<int2>(), cx->nnz.as<int>(), stride, u.ucl.as<int>(), N, cx->gkey.as<unsigned>(),
-                           cx->gidx.as<int>(), sa));
-      HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), N, cx->gkey2.as<unsigned>(),
+      HCHK(launch_gene_key(cx->ent.as<int2>(), cx->nnz.as<int>(), stride, u.ucl.as<int>(), NBg,
+                           cx->gkey.as<unsigned>(), cx->gidx.as<int>(), sa));
+      HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), NBg, cx->gkey2.as<unsigned>(),
                              cx->gorder.as<int>(), cx->gwork.p, &wb, sa));
     }
     // k_boot_gene (not with pair mode): groups of gene_sg slabs per 4-wave block
@@ -1248,7 +1308,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       const int P = (s.nboot + nb - 1) / nb;
       std::vector<unsigned char> w8((size_t)nsets * C * Bt, 0), w8p((size_t)nsets * C * P * 32, 0);
       for (int set = 0; set < nsets; ++set)
-        for (int c = 0; c < C; ++c) {
+        for (int c = set_c0(set); c < set_c1(set); ++c) {
           const double* wr = W.data() + ((size_t)set * C + c) * Bp;
           for (int b = 0; b < Bp; ++b) w8[((size_t)set * C + c) * Bt + b] = (unsigned char)wr[b];
           for (int p = 0; p < P; ++p)
@@ -1265,7 +1325,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         const int NGR = (P + gene_sg - 1) / gene_sg;
         std::vector<unsigned char> w8g((size_t)nsets * C * NGR * 128, 0);
         for (int set = 0; set < nsets; ++set)
-          for (int c = 0; c < C; ++c) {
+          for (int c = set_c0(set); c < set_c1(set); ++c) {
             const double* wr = W.data() + ((size_t)set * C + c) * Bp;
             for (int gr = 0; gr < NGR; ++gr) {
               const int gb0 = gr * gene_sg * nb, gnb = std::min(gene_sg, P - gr * gene_sg) * nb;
@@ -1286,19 +1346,19 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     }
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
     HCHK(launch_baseline_z(Tbase, G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
-                           cx->Z.as<double>(), sa));
+                           cx->Z.as<double>(), sa, two ? s.nsets_g : 0, two ? s.gsplit : 0));
     if (stretch_skip) {
       HCHK(cx->zubound.ensure(sizeof(double) * 8 * (size_t)nsets * Bp));
       HCHK(launch_stretch_zu(cx->ubound.as<double>(), cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
-                             cx->zubound.as<double>(), sa));
+                             cx->zubound.as<double>(), sa, two ? s.nsets_g : 0, two ? s.gsplit : 0));
     }
     cx->mark_end(SLOT_OTHER, ev);
     if (nsets > 1) {
-      if ((int)s.wset.size() != N) return fail(SCDE_EINTERNAL, "wset size mismatch");
-      RCHK(upload_on(cx, cx->wset, s.wset.data(), sizeof(int) * N, sa));
+      if ((int)s.wset.size() != NBg) return fail(SCDE_EINTERNAL, "wset size mismatch");
+      RCHK(upload_on(cx, cx->wset, s.wset.data(), sizeof(int) * NBg, sa));
     }
-    HCHK(cx->degen.ensure(sizeof(int) * std::max(1, N)));
-    HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, N), sa));
+    HCHK(cx->degen.ensure(sizeof(int) * std::max(1, NBg)));
+    HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, NBg), sa));
     if (sa != st) {  // the bootstrap waits for the set-up and for phase 2
       HCHK(hipEventRecord(cx->aux_ev, sa));
       HCHK(hipStreamWaitEvent(st, cx->aux_ev, 0));
@@ -1323,8 +1383,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       b2.nboot = s.nboot;
       b2.nb = nb;
       const int P = (s.nboot + nb - 1) / nb;
-      b2.part_stride = (long long)N * GS;
-      HCHK(cx->part.ensure(sizeof(double) * std::max<size_t>(1, (size_t)P * N * GS)));
+      b2.part_stride = (long long)NBg * GS;
+      HCHK(cx->part.ensure(sizeof(double) * std::max<size_t>(1, (size_t)P * NBg * GS)));
       b2.part = cx->part.as<double>();
       b2.norm_mult = (double)s.nboot;
       b2.degen_thresh = thresh;
@@ -1332,21 +1392,23 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       b2.out_g = s.jp_g;
       b2.out_k = s.jp_k;
       b2.degen = cx->degen.as<int>();
-      b2.ngenes = N;
-      b2.slack = cx->opt_skip_slack;
+      b2.ngenes = NBg;
+      // the stretch mask's heuristic slack grows with the cells per call (the kernel's default reads
+      // ncells, which counts both groups when fused): set here from the cells of one call
+      b2.slack = std::isnan(cx->opt_skip_slack) ? 20.0 + 0.15 * Ccall : cx->opt_skip_slack;
       b2.U = stretch_skip ? cx->ubound.as<double>() : nullptr;
       b2.ZU = stretch_skip ? cx->zubound.as<double>() : nullptr;
       if (stretch_skip) {
-        HCHK(cx->smask.ensure(sizeof(int) * std::max<size_t>(1, (size_t)P * N)));
-        HCHK(cx->subuf.ensure(sizeof(double) * 8 * nb * std::max<size_t>(1, (size_t)P * N)));
-        HCHK(cx->sredo.ensure(sizeof(int) * ((size_t)P * N + 1)));
+        HCHK(cx->smask.ensure(sizeof(int) * std::max<size_t>(1, (size_t)P * NBg)));
+        HCHK(cx->subuf.ensure(sizeof(double) * 8 * nb * std::max<size_t>(1, (size_t)P * NBg)));
+        HCHK(cx->sredo.ensure(sizeof(int) * ((size_t)P * NBg + 1)));
         b2.mask = cx->smask.as<int>();
         b2.ubuf = cx->subuf.as<double>();
         b2.redo = cx->sredo.as<int>();
       }
       cx->st_boot_path = tpath ? 1 : 0;
       if (tpath) {
-        HCHK(cx->sredo.ensure(sizeof(int) * (2 * (size_t)P * N + 1)));  // flags, list length, list
+        HCHK(cx->sredo.ensure(sizeof(int) * (2 * (size_t)P * NBg + 1)));  // flags, list length, list
         b2.redo = cx->sredo.as<int>();
         TileBootArgs tb{};
         tb.W8p = cx->w8t.as<unsigned char>();
@@ -1356,22 +1418,22 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         tb.nanflag = cx->qflags.as<int>();
         tb.maxgroups = cx->opt_tile_groups;
         tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
-        HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * N)));
+        HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * NBg)));
         tb.pmask = cx->pmask.as<unsigned>();
-        tb.pairs = (gene_sg == 0 && C >= cx->opt_pair_cells && P >= 2) ? 1 : 0;
+        tb.pairs = (gene_sg == 0 && Ccall >= cx->opt_pair_cells && P >= 2) ? 1 : 0;
         if (tb.pairs) {
-          HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * N)));
+          HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * NBg)));
           tb.wide = cx->pwide.as<int>();
         }
         if (gene_sg > 0) {
-          HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * N)));
+          HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * NBg)));
           tb.wide = cx->pwide.as<int>();
           tb.gene = 1;
           tb.SG = gene_sg;
           tb.kcap = cx->opt_gene_rows;
           tb.list_cap = cx->opt_gene_list_cap;
           // 12 rows per gene block from gene3_cells cells per call (slabs mostly need two tiles there)
-          tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (C >= cx->opt_gene3_cells ? 3 : 4);
+          tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (Ccall >= cx->opt_gene3_cells ? 3 : 4);
           tb.W8g = cx->w8g.as<unsigned char>();
           tb.chunks = std::max(1, cx->opt_boot_chunks);
         }
@@ -1393,7 +1455,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         HCHK(launch_boot2(b2, st));
       }
       if (stretch_skip && cx->opt_skip_stats) {  // diagnostics: kept stretches, redo slabs
-        std::vector<int> m((size_t)P * N), r((size_t)P * N), nz(N);
+        std::vector<int> m((size_t)P * NBg), r((size_t)P * NBg), nz(NBg);
         HCHK(hipMemcpyAsync(m.data(), cx->smask.p, sizeof(int) * m.size(), hipMemcpyDeviceToHost, st));
         HCHK(hipMemcpyAsync(r.data(), cx->sredo.p, sizeof(int) * r.size(), hipMemcpyDeviceToHost, st));
         HCHK(hipMemcpyAsync(nz.data(), cx->nnz.p, sizeof(int) * nz.size(), hipMemcpyDeviceToHost, st));
@@ -1456,7 +1518,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     xa.out = s.jp;
     xa.out_g = s.jp_g;
     xa.out_k = s.jp_k;
-    xa.ngenes = N;
+    xa.ngenes = NBg;
+    xa.gene_mod = two ? N : 0;
     HCHK(launch_boot_exact(xa, st));
   }
   // ---- individual outputs (src/jpmatLogBoot.cpp:277-328)
@@ -1718,6 +1781,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
   else if (n == "interleave") ctx->opt_interleave = value != 0;
   else if (n == "rest_thread") ctx->opt_rest_thread = value != 0;
+  else if (n == "fuse_groups") ctx->opt_fuse_groups = value != 0;
   else if (n == "boot_chunks") ctx->opt_boot_chunks = std::max(1, std::min((int)value, 64));
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
@@ -2585,186 +2649,284 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     s.jp_k = 1;
   }
   hlap(0);
-  scde_ctx* lane = ctx;  // the context that runs the second group's posterior
-  if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
-  if (up) {
-    // group by group, each after its columns have arrived (the first range ends with the
-    // last cell of the group whose cells end first)
-    int max0 = 0, max1 = 0;
-    for (int c : idx[0]) max0 = std::max(max0, c);
-    for (int c : idx[1]) max1 = std::max(max1, c);
-    const int first = max0 <= max1 ? 0 : 1;
-    // the first group's range in pieces, then the second group's range, uploaded back to back by
-    // a worker thread: each piece's unique sets and tables start as it lands
-    const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
-    const bool threaded = lane != ctx && ctx->opt_lane_thread && !ctx->opt_defer_boot;
-    // interleaved (second lane on its own host thread, every cell of the second group after the
-    // first group's range): both groups' ranges in K pieces, uploaded alternately, so the second
-    // group's unique sets and tables run beside the first group's instead of after its range
-    const int other = 1 - first;
-    const bool inter = threaded && ctx->opt_interleave && !idx[other].empty() && idx[other].front() >= up->cut;
-    std::vector<int> piece_c, cols, piece_c2;
-    const std::vector<int>& ix = idx[first];
-    for (int j = 0; j <= K; ++j) {
-      const int a = (int)((long long)up->cut * j / K);
-      cols.push_back(a);
-      piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
-    }
-    RCHK(ensure_piece_streams(ctx));
-    UploadWorker uw;
-    if (inter) {
-      RCHK(ensure_piece_streams(lane));
-      const std::vector<int>& iy = idx[other];
-      std::vector<int> cols2;
-      for (int j = 0; j <= K; ++j) {
-        const int a = up->cut + (int)((long long)(up->C - up->cut) * j / K);
-        cols2.push_back(a);
-        piece_c2.push_back((int)(std::lower_bound(iy.begin(), iy.end(), a) - iy.begin()));
+  // Fused groups (option fuse_groups): both group posteriors as ONE posterior over the concatenated
+  // cells and doubled genes (PostSpec::ngroups), one launch per stage on this context's stream --
+  // no peer lane, no second chain of small set-up kernels queued behind a running bootstrap, one
+  // bootstrap grid for both groups.  Bit-identical to the two separate posteriors (run_posterior).
+  const double* jp_dev[2] = {ctx->jpA.as<double>(), ctx->jpB.as<double>()};
+  bool fused_done = false;
+  {
+    const int C0 = (int)idx[0].size(), C1 = (int)idx[1].size();
+    auto same = [&](int th) { return (C0 >= th) == (C1 >= th); };
+    const bool fuse = ctx->opt_fuse_groups && p->nboot > 0 && same(ctx->opt_boot_tiles_cells) &&
+                      same(ctx->opt_pair_cells) && same(ctx->opt_gene3_cells);
+    if (fuse) {
+      // group a's cells first: the group whose cells end first in the matrix (the host upload's order)
+      const int a = (idx[0].back() <= idx[1].back()) ? 0 : 1, b = 1 - a;
+      const int Ca = (int)idx[a].size(), Cb = (int)idx[b].size(), Cf = Ca + Cb;
+      std::vector<int> cells(idx[a]);
+      cells.insert(cells.end(), idx[b].begin(), idx[b].end());
+      std::vector<double> mmf((size_t)Cf * 12);
+      for (int j = 0; j < 12; ++j) {
+        std::copy(mm[a].begin() + (size_t)Ca * j, mm[a].begin() + (size_t)Ca * (j + 1), mmf.begin() + (size_t)Cf * j);
+        std::copy(mm[b].begin() + (size_t)Cb * j, mm[b].begin() + (size_t)Cb * (j + 1),
+                  mmf.begin() + (size_t)Cf * j + Ca);
       }
-      // range 2j: the first group's piece j; range 2j + 1: the second group's piece j
-      std::vector<std::pair<int, int>> ranges;
-      std::vector<hipEvent_t> evs;
-      for (int j = 0; j < K; ++j) {
-        ranges.emplace_back(cols[j], cols[j + 1]);
-        evs.push_back(ctx->piece_up_ev[j]);
-        ranges.emplace_back(cols2[j], cols2[j + 1]);
-        evs.push_back(lane->piece_up_ev[j]);
+      HCHK(ctx->jpA.ensure(sizeof(double) * std::max<size_t>(1, 2 * NG)));
+      PostSpec sf = specs[a];
+      sf.ncells = Cf;
+      sf.models = mmf.data();
+      sf.cellidx_host = cells.data();
+      sf.ngroups = 2;
+      sf.gsplit = Ca;
+      sf.nsets_g = (int)seeds.size();
+      sf.seeds = seeds;
+      sf.seeds.insert(sf.seeds.end(), seeds.begin(), seeds.end());
+      sf.wset.assign(2 * (size_t)ngenes, 0);
+      for (int g = 0; g < ngenes; ++g) {
+        const int w = wset.empty() ? 0 : wset[g];
+        sf.wset[g] = w;
+        sf.wset[(size_t)ngenes + g] = w + sf.nsets_g;
       }
-      RCHK(uw.start(ctx, *up, std::move(ranges), std::move(evs)));
-    } else {
-      cols.push_back(up->C);
-      std::vector<hipEvent_t> evs(ctx->piece_up_ev, ctx->piece_up_ev + K);
-      evs.push_back(ctx->up_ev[1]);
-      RCHK(uw.start(ctx, *up, cols, evs));
-    }
-    // upload range of the first group's piece j
-    auto range_of = [&](int j) { return inter ? 2 * j : j; };
-    // two lanes with lane_thread: the second group's unique sets, tables and bootstrap are driven
-    // by a host thread of their own from the moment its range lands, beside this thread's pieces
-    // of the first group (each lane's host syncs then wait only for its own kernels)
-    struct LaneThread {
-      std::thread th;
-      int rc = SCDE_OK;
-      std::string err;
-      ~LaneThread() {
-        if (th.joinable()) th.join();  // an early error return of this thread still waits for it
+      sf.jp = ctx->jpA.as<double>();
+      sf.jp_g = G;
+      sf.jp_k = 1;
+      UniqueSet& uf = ctx->us[0];
+      uf.ready = false;
+      std::vector<int> piece_c, cols;
+      UploadWorker uw;
+      if (up) {
+        // the count columns in pieces over the fused cell list when it runs in matrix order (the
+        // groups' cells separable: each piece a column range; its unique sets and tables start as it
+        // lands), else in one range before the unique sets
+        const bool sep = idx[a].back() < idx[b].front();
+        const int K = sep ? std::max(1, std::min(2 * ctx->opt_pieces, scde_ctx::kMaxPieces)) : 1;
+        for (int j = 0; j <= K; ++j) piece_c.push_back((int)((long long)Cf * j / K));
+        cols.push_back(0);
+        for (int j = 1; j < K; ++j) cols.push_back(std::max(cols.back(), cells[piece_c[j]]));
+        cols.push_back(up->C);
+        RCHK(ensure_piece_streams(ctx));
+        RCHK(uw.start(ctx, *up, cols, std::vector<hipEvent_t>(ctx->piece_up_ev, ctx->piece_up_ev + K)));
+        if (sep) {
+          sf.npieces = K;
+          sf.piece_c = piece_c.data();
+          sf.piece_stream = ctx->uq_stream;
+          sf.piece_ev = ctx->piece_ev;
+          sf.piece_ready = [&](int j) {
+            RCHK(uw.wait(j + 1));
+            HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
+            return SCDE_OK;
+          };
+        } else {
+          RCHK(uw.wait(1));
+          HCHK(hipStreamWaitEvent(ctx->stream, ctx->piece_up_ev[0], 0));
+        }
       }
-    } t2;
-    if (threaded) {
-      const int gi = 1 - first;
-      ctx->us[gi].ready = false;
-      t2.th = std::thread([&, gi] {
-        t2.rc = [&]() -> int {
-          HCHK(hipSetDevice(ctx->device));
-          if (inter) {  // the second group's pieces as they land (ranges 1, 3, 5, ...)
-            PostSpec& s2 = specs[gi];
-            s2.npieces = K;
-            s2.piece_c = piece_c2.data();
-            s2.piece_stream = lane->uq_stream;
-            s2.piece_ev = lane->piece_ev;
-            s2.piece_ready = [&](int j) {
-              RCHK(uw.wait(2 * j + 2));
-              HCHK(hipStreamWaitEvent(lane->uq_stream, lane->piece_up_ev[j], 0));
-              return SCDE_OK;
-            };
-            return run_posterior(lane, s2, ctx->us[gi]);
-          }
-          RCHK(uw.wait(K + 1));
-          HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
-          const PostSpec* sp[1] = {&specs[gi]};
-          UniqueSet* usp[1] = {&ctx->us[gi]};
-          RCHK(build_unique_sets(lane, sp, usp, 1));
-          return run_posterior(lane, specs[gi], ctx->us[gi]);
-        }();
-        if (t2.rc != SCDE_OK) t2.err = g_err;  // g_err is thread-local
-      });
-    }
-    // two lanes: the first group's bootstrap is queued only after the second group's tables, so
-    // those (and their small set-up kernels) do not wait behind its waves; the first group's
-    // tables end about when the second group's range lands anyway
-    const bool defer = lane != ctx && ctx->opt_defer_boot;
-    std::function<int()> rest0, rest1;
-    {
-      const int gi = first;
-      ctx->us[gi].ready = false;
-      PostSpec& sf = specs[gi];
-      sf.npieces = K;
-      sf.piece_c = piece_c.data();
-      sf.piece_stream = ctx->uq_stream;
-      sf.piece_ev = ctx->piece_ev;
-      sf.piece_ready = [&](int j) {
-        RCHK(uw.wait(range_of(j) + 1));
-        HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
-        return SCDE_OK;
-      };
       hlap(1);
-      RCHK(run_posterior(ctx, sf, ctx->us[gi], defer ? &rest0 : nullptr));
+      if (!up || sf.npieces == 0) {
+        const PostSpec* sp[1] = {&sf};
+        UniqueSet* usp[1] = {&uf};
+        RCHK(build_unique_sets(ctx, sp, usp, 1));
+      }
+      const int rc = run_posterior(ctx, sf, uf);
       hlap(2);
+      if (rc == SCDE_OK) {
+        jp_dev[a] = ctx->jpA.as<double>();
+        jp_dev[b] = ctx->jpA.as<double>() + NG;
+        fused_done = true;
+      } else if (rc == kRetryUnfused) {
+        // the fused column count leaves the fast path: every count is in HBM by now (the pieces were
+        // all awaited); the two groups run separately on the resident counts
+        HCHK(hipStreamSynchronize(ctx->copy_stream ? ctx->copy_stream : ctx->stream));
+        HCHK(hipStreamSynchronize(ctx->stream));
+        up = nullptr;
+      } else {
+        return rc;
+      }
     }
-    if (t2.th.joinable()) {  // the second lane ran on its own host thread
-      t2.th.join();
-      if (t2.rc != SCDE_OK) return fail(t2.rc, "%s", t2.err.c_str());
-      HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
-      HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
-      hlap(2);
-    } else {
-      // the second group, once its range is in HBM: its unique sets on the peer lane (or on
-      // the unique stream with one lane), so their host sync waits for its small kernels only
-      const int gi = 1 - first;
-      ctx->us[gi].ready = false;
-      RCHK(uw.wait(K + 1));
-      const PostSpec* sp[1] = {&specs[gi]};
-      UniqueSet* usp[1] = {&ctx->us[gi]};
-      if (lane != ctx) {
-        HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
-        RCHK(build_unique_sets(lane, sp, usp, 1));
+  }
+  if (!fused_done) {
+    scde_ctx* lane = ctx;  // the context that runs the second group's posterior
+    if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
+    if (up) {
+      // group by group, each after its columns have arrived (the first range ends with the
+      // last cell of the group whose cells end first)
+      int max0 = 0, max1 = 0;
+      for (int c : idx[0]) max0 = std::max(max0, c);
+      for (int c : idx[1]) max1 = std::max(max1, c);
+      const int first = max0 <= max1 ? 0 : 1;
+      // the first group's range in pieces, then the second group's range, uploaded back to back by
+      // a worker thread: each piece's unique sets and tables start as it lands
+      const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
+      const bool threaded = lane != ctx && ctx->opt_lane_thread && !ctx->opt_defer_boot;
+      // interleaved (second lane on its own host thread, every cell of the second group after the
+      // first group's range): both groups' ranges in K pieces, uploaded alternately, so the second
+      // group's unique sets and tables run beside the first group's instead of after its range
+      const int other = 1 - first;
+      const bool inter = threaded && ctx->opt_interleave && !idx[other].empty() && idx[other].front() >= up->cut;
+      std::vector<int> piece_c, cols, piece_c2;
+      const std::vector<int>& ix = idx[first];
+      for (int j = 0; j <= K; ++j) {
+        const int a = (int)((long long)up->cut * j / K);
+        cols.push_back(a);
+        piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
+      }
+      RCHK(ensure_piece_streams(ctx));
+      UploadWorker uw;
+      if (inter) {
+        RCHK(ensure_piece_streams(lane));
+        const std::vector<int>& iy = idx[other];
+        std::vector<int> cols2;
+        for (int j = 0; j <= K; ++j) {
+          const int a = up->cut + (int)((long long)(up->C - up->cut) * j / K);
+          cols2.push_back(a);
+          piece_c2.push_back((int)(std::lower_bound(iy.begin(), iy.end(), a) - iy.begin()));
+        }
+        // range 2j: the first group's piece j; range 2j + 1: the second group's piece j
+        std::vector<std::pair<int, int>> ranges;
+        std::vector<hipEvent_t> evs;
+        for (int j = 0; j < K; ++j) {
+          ranges.emplace_back(cols[j], cols[j + 1]);
+          evs.push_back(ctx->piece_up_ev[j]);
+          ranges.emplace_back(cols2[j], cols2[j + 1]);
+          evs.push_back(lane->piece_up_ev[j]);
+        }
+        RCHK(uw.start(ctx, *up, std::move(ranges), std::move(evs)));
+      } else {
+        cols.push_back(up->C);
+        std::vector<hipEvent_t> evs(ctx->piece_up_ev, ctx->piece_up_ev + K);
+        evs.push_back(ctx->up_ev[1]);
+        RCHK(uw.start(ctx, *up, cols, evs));
+      }
+      // upload range of the first group's piece j
+      auto range_of = [&](int j) { return inter ? 2 * j : j; };
+      // two lanes with lane_thread: the second group's unique sets, tables and bootstrap are driven
+      // by a host thread of their own from the moment its range lands, beside this thread's pieces
+      // of the first group (each lane's host syncs then wait only for its own kernels)
+      struct LaneThread {
+        std::thread th;
+        int rc = SCDE_OK;
+        std::string err;
+        ~LaneThread() {
+          if (th.joinable()) th.join();  // an early error return of this thread still waits for it
+        }
+      } t2;
+      if (threaded) {
+        const int gi = 1 - first;
+        ctx->us[gi].ready = false;
+        t2.th = std::thread([&, gi] {
+          t2.rc = [&]() -> int {
+            HCHK(hipSetDevice(ctx->device));
+            if (inter) {  // the second group's pieces as they land (ranges 1, 3, 5, ...)
+              PostSpec& s2 = specs[gi];
+              s2.npieces = K;
+              s2.piece_c = piece_c2.data();
+              s2.piece_stream = lane->uq_stream;
+              s2.piece_ev = lane->piece_ev;
+              s2.piece_ready = [&](int j) {
+                RCHK(uw.wait(2 * j + 2));
+                HCHK(hipStreamWaitEvent(lane->uq_stream, lane->piece_up_ev[j], 0));
+                return SCDE_OK;
+              };
+              return run_posterior(lane, s2, ctx->us[gi]);
+            }
+            RCHK(uw.wait(K + 1));
+            HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
+            const PostSpec* sp[1] = {&specs[gi]};
+            UniqueSet* usp[1] = {&ctx->us[gi]};
+            RCHK(build_unique_sets(lane, sp, usp, 1));
+            return run_posterior(lane, specs[gi], ctx->us[gi]);
+          }();
+          if (t2.rc != SCDE_OK) t2.err = g_err;  // g_err is thread-local
+        });
+      }
+      // two lanes: the first group's bootstrap is queued only after the second group's tables, so
+      // those (and their small set-up kernels) do not wait behind its waves; the first group's
+      // tables end about when the second group's range lands anyway
+      const bool defer = lane != ctx && ctx->opt_defer_boot;
+      std::function<int()> rest0, rest1;
+      {
+        const int gi = first;
+        ctx->us[gi].ready = false;
+        PostSpec& sf = specs[gi];
+        sf.npieces = K;
+        sf.piece_c = piece_c.data();
+        sf.piece_stream = ctx->uq_stream;
+        sf.piece_ev = ctx->piece_ev;
+        sf.piece_ready = [&](int j) {
+          RCHK(uw.wait(range_of(j) + 1));
+          HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
+          return SCDE_OK;
+        };
         hlap(1);
-        RCHK(run_posterior(lane, specs[gi], ctx->us[gi], defer ? &rest1 : nullptr));
-        if (defer) RCHK(run_rests(ctx, rest0, rest1));
+        RCHK(run_posterior(ctx, sf, ctx->us[gi], defer ? &rest0 : nullptr));
+        hlap(2);
+      }
+      if (t2.th.joinable()) {  // the second lane ran on its own host thread
+        t2.th.join();
+        if (t2.rc != SCDE_OK) return fail(t2.rc, "%s", t2.err.c_str());
         HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
         HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+        hlap(2);
       } else {
-        if (!ctx->uq_ev) HCHK(hipEventCreateWithFlags(&ctx->uq_ev, hipEventDisableTiming));
-        HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->up_ev[1], 0));
-        const hipStream_t main = ctx->stream;
-        ctx->stream = ctx->uq_stream;
-        const int rc = build_unique_sets(ctx, sp, usp, 1);
-        ctx->stream = main;
-        RCHK(rc);
-        HCHK(hipEventRecord(ctx->uq_ev, ctx->uq_stream));
-        HCHK(hipStreamWaitEvent(ctx->stream, ctx->uq_ev, 0));
-        hlap(1);
-        RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
+        // the second group, once its range is in HBM: its unique sets on the peer lane (or on
+        // the unique stream with one lane), so their host sync waits for its small kernels only
+        const int gi = 1 - first;
+        ctx->us[gi].ready = false;
+        RCHK(uw.wait(K + 1));
+        const PostSpec* sp[1] = {&specs[gi]};
+        UniqueSet* usp[1] = {&ctx->us[gi]};
+        if (lane != ctx) {
+          HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
+          RCHK(build_unique_sets(lane, sp, usp, 1));
+          hlap(1);
+          RCHK(run_posterior(lane, specs[gi], ctx->us[gi], defer ? &rest1 : nullptr));
+          if (defer) RCHK(run_rests(ctx, rest0, rest1));
+          HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
+          HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+        } else {
+          if (!ctx->uq_ev) HCHK(hipEventCreateWithFlags(&ctx->uq_ev, hipEventDisableTiming));
+          HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->up_ev[1], 0));
+          const hipStream_t main = ctx->stream;
+          ctx->stream = ctx->uq_stream;
+          const int rc = build_unique_sets(ctx, sp, usp, 1);
+          ctx->stream = main;
+          RCHK(rc);
+          HCHK(hipEventRecord(ctx->uq_ev, ctx->uq_stream));
+          HCHK(hipStreamWaitEvent(ctx->stream, ctx->uq_ev, 0));
+          hlap(1);
+          RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
+        }
+        hlap(2);
+      }
+    } else {
+      // both groups' unique tables first (two host syncs, GPU otherwise idle), then the
+      // heavy per-group kernels back to back on the stream
+      ctx->us[0].ready = ctx->us[1].ready = false;
+      const PostSpec* sp[2] = {&specs[0], &specs[1]};
+      UniqueSet* up[2] = {&ctx->us[0], &ctx->us[1]};
+      RCHK(build_unique_sets(ctx, sp, up, 2));
+      hlap(1);
+      if (lane != ctx) {
+        HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
+        HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
+      }
+      if (lane != ctx) {
+        // both groups' tables first, then both bootstraps
+        std::function<int()> rest0, rest1;
+        RCHK(run_posterior(ctx, specs[0], ctx->us[0], &rest0));
+        RCHK(run_posterior(lane, specs[1], ctx->us[1], &rest1));
+        RCHK(run_rests(ctx, rest0, rest1));
+      } else {
+        RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
+        RCHK(run_posterior(ctx, specs[1], ctx->us[1]));
+      }
+      if (lane != ctx) {
+        HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
+        HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
       }
       hlap(2);
     }
-  } else {
-    // both groups' unique tables first (two host syncs, GPU otherwise idle), then the
-    // heavy per-group kernels back to back on the stream
-    ctx->us[0].ready = ctx->us[1].ready = false;
-    const PostSpec* sp[2] = {&specs[0], &specs[1]};
-    UniqueSet* up[2] = {&ctx->us[0], &ctx->us[1]};
-    RCHK(build_unique_sets(ctx, sp, up, 2));
-    hlap(1);
-    if (lane != ctx) {
-      HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
-      HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
-    }
-    if (lane != ctx) {
-      // both groups' tables first, then both bootstraps
-      std::function<int()> rest0, rest1;
-      RCHK(run_posterior(ctx, specs[0], ctx->us[0], &rest0));
-      RCHK(run_posterior(lane, specs[1], ctx->us[1], &rest1));
-      RCHK(run_rests(ctx, rest0, rest1));
-    } else {
-      RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
-      RCHK(run_posterior(ctx, specs[1], ctx->us[1]));
-    }
-    if (lane != ctx) {
-      HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
-      HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
-    }
-    hlap(2);
   }
   // ratio posterior + summary
   const std::vector<double> diffv = ratio_diffv(p->prior_x, G);
@@ -2776,10 +2938,10 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
   HCHK(ctx->res.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * ncol)));
   if (ratio) HCHK(ctx->ratio.ensure(sizeof(double) * std::max<size_t>(1, (size_t)ngenes * m)));
   RatioArgs ra{};
-  ra.jp1 = ctx->jpA.as<double>();
+  ra.jp1 = jp_dev[0];
   ra.j1g = G;
   ra.j1k = 1;
-  ra.jp2 = ctx->jpB.as<double>();
+  ra.jp2 = jp_dev[1];
   ra.j2g = G;
   ra.j2k = 1;
   ra.prior_y = ctx->prior_y.as<double>();
@@ -2810,12 +2972,12 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
   std::vector<double> tmp;
   if ((jp1 || jp2) && NG) tmp.resize(NG);
   if (jp1 && NG) {
-    HCHK(hipMemcpyAsync(tmp.data(), ctx->jpA.p, sizeof(double) * NG, hipMemcpyDeviceToHost, st));
+    HCHK(hipMemcpyAsync(tmp.data(), jp_dev[0], sizeof(double) * NG, hipMemcpyDeviceToHost, st));
     RCHK(ctx->sync());
     transpose_rows_to_colmajor(tmp.data(), ngenes, G, jp1);
   }
   if (jp2 && NG) {
-    HCHK(hipMemcpyAsync(tmp.data(), ctx->jpB.p, sizeof(double) * NG, hipMemcpyDeviceToHost, st));
+    HCHK(hipMemcpyAsync(tmp.data(), jp_dev[1], sizeof(double) * NG, hipMemcpyDeviceToHost, st));
     RCHK(ctx->sync());
     transpose_rows_to_colmajor(tmp.data(), ngenes, G, jp2);
   }

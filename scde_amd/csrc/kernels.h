@@ -67,6 +67,11 @@ struct TablesArgs {
   const double* theta;       // [ncells][GS]
   const double* cellscal;    // [ncells][2] = {max log cfp, exp(fail.r)}
   double minlogprob;         // -DBL_MAX / ncells / 1.1
+  // a DE call's two groups fused into one set of tables (engine.hip run_posterior, ngroups 2):
+  // cells from mlp_split on (the second group's, relative to this launch's first cell) clamp at
+  // minlogprob2 = -DBL_MAX / (its group's cells) / 1.1; one group: mlp_split >= ncells
+  double minlogprob2;
+  int mlp_split;
   double* T;                 // [ncols][GS] log-posterior columns
   int* maxi;                 // [ncols] argmax (nullable)
   unsigned char* has_clamp;  // [ncols]
@@ -207,8 +212,10 @@ struct ExactArgs {
   const double* T;  // log tables; or fused D columns when base_col is set (T = D + D[base])
   const int* base_col;
   int G, GS;
-  const int* draws;  // [nsets][nboot][ndraw] cell index per draw, reference order
+  const int* draws;  // [nsets][nboot][ndraw] cell index per draw, reference order (-1: no draw, the
+                     // shorter group's padding when two groups are fused)
   int ndraw, nboot;
+  long long gene_mod;  // fused groups: gene g reads uci row g % gene_mod (0: g)
   const int* wset;
   const long long* ucl_off;
   const int* uci;  // [ld_uci x ncells] or null for jpmat (column = cell*ngenes + g)
@@ -257,16 +264,20 @@ hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, con
 hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long ncols, int ncells,
                              const double* theta, int GS, const double* cellscal, double* colc, hipStream_t s);
 hipError_t launch_tables(const TablesArgs& a, hipStream_t s);
+// gsets > 0 (two fused groups): sets from gsets on sum the cells from gsplit on, the others the
+// cells before it, each in its group's own order
 hipError_t launch_stretch_zu(const double* U, const int* base_col, int ncells, const double* Wt, int Bp, int nsets,
-                             double* ZU, hipStream_t s);
+                             double* ZU, hipStream_t s, int gsets = 0, int gsplit = 0);
 hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells, const unsigned char* has_clamp,
                             int use_baseline, int* base_col, hipStream_t s);
 // padto 8: rows padded to a multiple of 8 plus one batch of 8 (k_boot2's look-ahead); 64: to a
 // multiple of 64 plus 8 (k_boot_tiles' bound MFMAs take 64-entry steps)
+// cell_off: added to the cell of every entry (a fused second group's cells follow the first's)
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
-                      const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s);
+                      const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s,
+                      int cell_off = 0);
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
-                             int Bp, int nsets, double* Z, hipStream_t s);
+                             int Bp, int nsets, double* Z, hipStream_t s, int gsets = 0, int gsplit = 0);
 hipError_t launch_boot(const BootArgs& a, hipStream_t s);
 hipError_t launch_boot_exact(const ExactArgs& a, hipStream_t s);
 int boot2_nb(int nboot);

@@ -366,8 +366,9 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         bv = r;
         bi = k;
       }
-      if (r < a.minlogprob) {
-        r = a.minlogprob;
+      const double mlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
+      if (r < mlp) {
+        r = mlp;
         clamp = true;
       }
       if (SCDE_KT_DIAG & 8) {
@@ -820,7 +821,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
   KT_STAMP(4);
   double* out = a.T ? a.T + col * a.GS : nullptr;
   double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
-  const double minlp = a.minlogprob;
+  const double minlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
   unsigned uqv = 0;  // lane t < kQTiles: bound tile t's value (BM == kBoundTiles)
 #pragma unroll
   for (int j = 0; j < kTabChunks; ++j) {
@@ -1006,7 +1007,7 @@ constexpr int kEllWaves = 16;
 __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
                                              int ncells, const long long* __restrict__ ucl_off,
                                              const int* __restrict__ base_col, int stride, int pad_col,
-                                             int padto, int2* __restrict__ ent, int* __restrict__ nnz) {
+                                             int padto, int2* __restrict__ ent, int* __restrict__ nnz, int cell_off) {
   __shared__ int tile[64][65];  // [cell][gene]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g0 = blockIdx.x * 64;
@@ -1040,7 +1041,7 @@ __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ 
       }
       const unsigned long long m = __ballot(keep);
       const int pos = n[i] + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
-      if (keep) ent[(long long)g * stride + pos] = make_int2(c, col);
+      if (keep) ent[(long long)g * stride + pos] = make_int2(c + cell_off, col);
       n[i] += __popcll(m);
     }
   }
@@ -1092,14 +1093,17 @@ constexpr int kZWaves = 16;
 __global__ __launch_bounds__(64 * kZWaves) void k_baseline_z(const double* __restrict__ T, int G, int GS,
                                                             const int* __restrict__ base_col, int ncells,
                                                             const double* __restrict__ Wt, int Bp,
-                                                            double* __restrict__ Z) {
+                                                            double* __restrict__ Z, int gsets, int gsplit) {
   __shared__ double part[kZWaves][4][64];  // [wave][boot][lane]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int b0 = blockIdx.x * 4, k = blockIdx.y * 64 + lane, set = blockIdx.z;
   const double* W = Wt + (long long)set * ncells * Bp + b0;
+  // fused groups: the set's own group's cells, in that group's order (the same sums as its own call)
+  const bool g2 = gsets > 0 && set >= gsets;
+  const int clo = g2 ? gsplit : 0, chi = (gsets > 0 && !g2) ? gsplit : ncells;
   double z[4] = {0.0, 0.0, 0.0, 0.0};
   if (k < G) {
-    for (int c = wid; c < ncells; c += kZWaves) {
+    for (int c = clo + wid; c < chi; c += kZWaves) {
       const int bc = base_col[c];
       if (bc < 0) continue;
       const double t = T[(long long)bc * GS + k];
@@ -1125,14 +1129,16 @@ __global__ __launch_bounds__(64 * kZWaves) void k_baseline_z(const double* __res
 // fixed-order tree over the block.
 __global__ __launch_bounds__(256) void k_stretch_zu(const double* __restrict__ U, const int* __restrict__ base_col,
                                                     int ncells, const double* __restrict__ Wt, int Bp,
-                                                    double* __restrict__ ZU) {
+                                                    double* __restrict__ ZU, int gsets, int gsplit) {
   __shared__ double part[256][kStretchSlots + 1];
   const int b = blockIdx.x, set = blockIdx.y, t = threadIdx.x;
   const double* W = Wt + (long long)set * ncells * Bp + b;
+  const bool g2 = gsets > 0 && set >= gsets;  // fused groups: the set's own group's cells
+  const int clo = g2 ? gsplit : 0, chi = (gsets > 0 && !g2) ? gsplit : ncells;
   double z[kStretchSlots];
 #pragma unroll
   for (int j = 0; j < kStretchSlots; ++j) z[j] = 0.0;
-  for (int c = t; c < ncells; c += 256) {
+  for (int c = clo + t; c < chi; c += 256) {
     const int bc = base_col[c];
     if (bc < 0) continue;
     const double w = W[(long long)c * Bp];
@@ -2935,11 +2941,13 @@ __global__ __launch_bounds__(1024) void k_boot_exact(ExactArgs a) {
   for (int b = 0; b < a.nboot; ++b) {
     double t[KPT];
     for (int j = 0; j < KPT; ++j) t[j] = 0.0;
+    const long long gu = a.gene_mod > 0 ? g % a.gene_mod : g;  // fused groups: the gene's uci row
     for (int d = 0; d < a.ndraw; ++d) {
       const int cell = dr[(long long)b * a.ndraw + d];
+      if (cell < 0) continue;  // the shorter fused group's padding (uniform over the block)
       long long col;
       if (a.uci)
-        col = a.ucl_off[cell] + a.uci[(long long)g + a.ld_uci * cell];
+        col = a.ucl_off[cell] + a.uci[gu + a.ld_uci * cell];
       else
         col = (long long)cell * a.ngenes + g;  // jpmat layout: matrix-major rows
       // fused tables: T = D + D[baseline column] (<= 1 ulp of T; clamped values exact)
@@ -3727,12 +3735,14 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 }
 
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
-                      const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s) {
+                      const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s,
+                      int cell_off) {
   if (ngenes <= 0) return hipSuccess;
   if (padto == 64 ? stride < ((ncells + 63) & ~63) + 8 || stride < 72 : stride < ((ncells + 7) & ~7) + 8)
     return hipErrorInvalidValue;
+  if (cell_off < 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 64)), dim3(64 * kEllWaves), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
-                     base_col, stride, pad_col, padto, ent, nnz);
+                     base_col, stride, pad_col, padto, ent, nnz, cell_off);
   return hipGetLastError();
 }
 
@@ -3744,16 +3754,18 @@ hipError_t launch_delta(const double* T, const long long* ucl_off, int ncells, l
 }
 
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
-                             int Bp, int nsets, double* Z, hipStream_t s) {
+                             int Bp, int nsets, double* Z, hipStream_t s, int gsets, int gsplit) {
+  if (gsets < 0 || gsets > nsets || gsplit < 0 || gsplit > ncells) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_baseline_z, dim3(Bp / 4, (GS + 63) / 64, nsets), dim3(64 * kZWaves), 0, s, T, G, GS, base_col, ncells, Wt,
-                     Bp, Z);
+                     Bp, Z, gsets, gsplit);
   return hipGetLastError();
 }
 
 hipError_t launch_stretch_zu(const double* U, const int* base_col, int ncells, const double* Wt, int Bp, int nsets,
-                             double* ZU, hipStream_t s) {
+                             double* ZU, hipStream_t s, int gsets, int gsplit) {
   if (nsets <= 0 || Bp <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_stretch_zu, dim3(Bp, nsets), dim3(256), 0, s, U, base_col, ncells, Wt, Bp, ZU);
+  if (gsets < 0 || gsets > nsets || gsplit < 0 || gsplit > ncells) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_stretch_zu, dim3(Bp, nsets), dim3(256), 0, s, U, base_col, ncells, Wt, Bp, ZU, gsets, gsplit);
   return hipGetLastError();
 }
 

@@ -103,7 +103,9 @@ def test_config3_host_pipeline_equals_device_resident(api):
     whose unique sets and tables start as each lands (option pieces), and builds the second
     group's unique sets and posterior on the peer lane beside the first group's
     (engine.hip de_run, lanes = 2); the table must equal, bit for bit, the device-resident entry
-    on the same counts with the groups one after the other (lanes = 1, no pipelining)."""
+    on the same counts with the groups one after the other (lanes = 1, no pipelining, fuse_groups 0).
+    The host calls run the default fused path (both groups as one posterior over concatenated cells,
+    the count columns in pieces over the fused cell list)."""
     import ctypes
     import bench
     from scde_amd._lib import DEParams, check, lib
@@ -139,10 +141,12 @@ def test_config3_host_pipeline_equals_device_resident(api):
     try:
         dev = np.zeros((N, 6), order="F")
         ctx.set_option("lanes", 1)
+        ctx.set_option("fuse_groups", 0)  # the two group posteriors one after the other
         check(lib().scde_expression_difference_dev(ctx.handle, dc.ptr, N, N, ctypes.byref(params), vp(dev), None,
                                                    None, None))
     finally:
         ctx.set_option("lanes", 2)
+        ctx.set_option("fuse_groups", 1)
         dc.free()
     for host in hosts:
         assert np.isfinite(host[:, :4]).all()

@@ -180,6 +180,7 @@ def test_config3_host_pipeline_after_call_history(api):
     ref_ctx = api.Context(0)
     try:
         ref_ctx.set_option("lanes", 1)
+        ref_ctx.set_option("fuse_groups", 0)
         dc = api.DeviceCounts(ref_ctx, mat)
         ref = np.zeros((N, 6), order="F")
         check(lib().scde_expression_difference_dev(ref_ctx.handle, dc.ptr, N, N, ctypes.byref(params), vp(ref), None,

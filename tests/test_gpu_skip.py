@@ -57,6 +57,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("interleave", opts.get("interleave", 1))
     ctx.set_option("rest_thread", opts.get("rest_thread", 1))
     ctx.set_option("boot_chunks", opts.get("boot_chunks", 1))
+    ctx.set_option("fuse_groups", opts.get("fuse_groups", 1))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -88,6 +89,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("interleave", 1)
         ctx.set_option("rest_thread", 1)
         ctx.set_option("boot_chunks", 1)
+        ctx.set_option("fuse_groups", 1)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -115,14 +117,19 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "gene-chunks": {"boot_chunks": 3},
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
-        "one-lane": {"lanes": 1},
-        "rest-inline": {"rest_thread": 0},
-        "pipelined-pieces": {"pipeline_mb": 0, "pieces": 3},
-        "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1},
-        "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1},
-        "pipelined-staged": {"pipeline_mb": 0, "pieces": 3, "upload_staged": 1},
-        "pipelined-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1},  # both groups in alternating pieces
-        "pipelined-thread-seq": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1, "interleave": 0},
+        # the two group posteriors fused into one (default) against the two-posterior paths (fuse_groups 0)
+        "unfused": {"fuse_groups": 0},
+        "one-lane": {"lanes": 1, "fuse_groups": 0},
+        "rest-inline": {"rest_thread": 0, "fuse_groups": 0},
+        "fused-pipelined": {"pipeline_mb": 0, "pieces": 3},
+        "fused-pipelined-staged": {"pipeline_mb": 0, "pieces": 2, "upload_staged": 1},
+        "pipelined-pieces": {"pipeline_mb": 0, "pieces": 3, "fuse_groups": 0},
+        "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1, "fuse_groups": 0},
+        "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1, "fuse_groups": 0},
+        "pipelined-staged": {"pipeline_mb": 0, "pieces": 3, "upload_staged": 1, "fuse_groups": 0},
+        # both groups in alternating pieces
+        "pipelined-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1, "fuse_groups": 0},
+        "pipelined-thread-seq": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1, "interleave": 0, "fuse_groups": 0},
         "tiles-pairs": {"pair_cells": 1, "gene_blocks": 0},
         "tiles-pairs-redo": {"pair_cells": 1, "tile_groups": 2, "gene_blocks": 0},
         "tiles-mult-fallback": {"tile_max_mult": 1},
@@ -168,7 +175,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
                                     "gene-forced-list", "gene-list-overflow", "gene-list-overflow-odd", "gene-3waves", "gene-4waves", "gene-chunks",
-                                    "tiles-unordered", "unique-exact", "one-lane", "rest-inline", "pipelined-pieces",
+                                    "tiles-unordered", "unique-exact", "unfused", "one-lane", "rest-inline",
+                                    "fused-pipelined", "fused-pipelined-staged", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
                                     "pipelined-thread-seq",
                                     "tiles-pairs",
@@ -197,9 +205,16 @@ def test_threaded_lane_group_layouts(api, layout):
     else:
         groups = np.random.default_rng(5).permutation(groups)
     prior = expression_prior(models, counts, length_out=400)
-    base, _ = _run(api, {}, models, counts, prior, groups, 30, 1)
-    got, _ = _run(api, {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1}, models, counts, prior, groups, 30, 1)
-    for i in range(2):
-        np.testing.assert_array_equal(got["joint.posteriors"][i], base["joint.posteriors"][i])
-    for k in ("lb", "mle", "ub", "ce", "Z", "cZ"):
-        np.testing.assert_array_equal(got["results"][k].to_numpy(), base["results"][k].to_numpy(), err_msg=k)
+    base, _ = _run(api, {"fuse_groups": 0}, models, counts, prior, groups, 30, 1)
+    runs = {"lane-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1, "fuse_groups": 0},
+            # fused groups: reversed = the second group's cells first (its rows lead the fused list);
+            # mixed = no separable ranges (one upload range before the unique sets)
+            "fused-pipelined": {"pipeline_mb": 0, "pieces": 3},
+            "fused": {}}
+    for name, opts in runs.items():
+        got, _ = _run(api, opts, models, counts, prior, groups, 30, 1)
+        for i in range(2):
+            np.testing.assert_array_equal(got["joint.posteriors"][i], base["joint.posteriors"][i], err_msg=name)
+        for k in ("lb", "mle", "ub", "ce", "Z", "cZ"):
+            np.testing.assert_array_equal(got["results"][k].to_numpy(), base["results"][k].to_numpy(),
+                                          err_msg=f"{name} {k}")
