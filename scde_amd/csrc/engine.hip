@@ -310,6 +310,8 @@ struct scde_ctx {
                                 // thread of its own
   int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
                                 // the second group's tables
+  int opt_boot2_rows = 1;        // "boot2_rows": the stretch-mask bootstrap (below boot_tiles_cells) on tile rows
+                                 // (k_boot2t: two kept stretches per wave, DPP64 multiplicities); 0: k_boot2
   int opt_fuse_groups = 1;       // "fuse_groups": a DE call's two group posteriors run as one (PostSpec::ngroups:
                                  // concatenated cells, doubled genes, one launch per stage); 0: two posteriors
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
@@ -1405,6 +1407,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         b2.mask = cx->smask.as<int>();
         b2.ubuf = cx->subuf.as<double>();
         b2.redo = cx->sredo.as<int>();
+        if (cx->opt_boot2_rows) {  // k_boot2t: the kept stretches on tile rows, pmask for the slab sums
+          HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * NBg)));
+          b2.pmask = cx->pmask.as<unsigned>();
+        }
       }
       cx->st_boot_path = tpath ? 1 : 0;
       if (tpath) {
@@ -1782,6 +1788,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "interleave") ctx->opt_interleave = value != 0;
   else if (n == "rest_thread") ctx->opt_rest_thread = value != 0;
   else if (n == "fuse_groups") ctx->opt_fuse_groups = value != 0;
+  else if (n == "boot2_rows") ctx->opt_boot2_rows = value != 0;
   else if (n == "boot_chunks") ctx->opt_boot_chunks = std::max(1, std::min((int)value, 64));
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
@@ -2557,6 +2564,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_gene_waves = cx->opt_gene_waves;
   p->opt_gene3_cells = cx->opt_gene3_cells;
   p->opt_boot_chunks = cx->opt_boot_chunks;
+  p->opt_boot2_rows = cx->opt_boot2_rows;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;

@@ -170,7 +170,10 @@ struct Boot2Args {
   double* ubuf;  // [ngenes][P][8][nb] stretch upper bounds (k_stretch_mask output)
   int* redo;     // [ngenes][P] slabs whose skipped stretches failed the post-check (tile path:
                  // fallback flags, then the fallback list length and [ngenes * P] list)
-  double slack;  // heuristic slack of the mask (NaN: the default 30 + 0.4 C)
+  double slack;  // heuristic slack of the mask (NaN: the default 20 + 0.15 C)
+  // k_boot2t (the stretch path on tile rows, with the mask): the 16-point tiles each slab's partial
+  // row holds ([ngenes][P]; k_sum_partials reads the rest as zeros); null: k_boot2
+  unsigned* pmask = nullptr;
 };
 
 // k_boot_tiles (with Boot2Args; needs G <= 448): multiplicities as bytes and the tables'

@@ -2873,6 +2873,141 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   }
 }
 
+// k_boot2's grid-stretch bootstrap on the tile rows (round 5; the default below 400 cells per
+// call, option boot2_rows): one 4-wave block per (gene, slab of NB boots), as k_boot2, but the
+// stretches k_stretch_mask keeps are packed two to a wave -- 16-lane row r of wave w computes the
+// 32-point bound tile 2 s + (r & 1) of the stretch s = (2 w + (r >> 1))-th kept stretch, two
+// points per lane, every multiplicity by DPP64 broadcast from a 16-byte load (tile_rows: no scalar
+// loads), so a wave covers 128 points and a block only as many waves as half its kept stretches.
+// Maxima, post-check, softmax terms, 16-point tile sums (pair8_sum = row16_sum's operand pairs)
+// added in tile order, normalisers and partial rows are formed exactly as in k_boot2, so the
+// outputs are bit-identical to it.  Only the computed tiles are written (pmask, as the tile path;
+// k_sum_partials reads the rest as zeros).  redo_pass 1: the slabs the post-check flagged, every
+// stretch (up to 8 in 4 waves).
+template <int NB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot2t(
+    const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
+    const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
+    int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
+    long long part_stride, int* __restrict__ degen, int ngenes, const int* __restrict__ smask,
+    const double* __restrict__ sub, int* __restrict__ redo, int redo_pass, unsigned* __restrict__ pmask) {
+  static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
+  __shared__ float rowmax[16 * 32];  // [row][boot] row maxima
+  __shared__ double tsum[32 * NB];   // [16-point tile][boot] tile partial sums (G <= 512)
+  __shared__ double fin[32];         // [boot] maxima, then 1 / (S nboot)
+  __shared__ double etab[64];
+  const int within = blockIdx.x % (8 * P);
+  const int p = within >> 3;
+  const int g = (blockIdx.x / (8 * P)) * 8 + (within & 7);
+  if (g >= ngenes) return;
+  if (redo_pass == 1 && !redo[(long long)g * P + p]) return;
+  const int lane = threadIdx.x & 63;
+  const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nst = (G + 63) >> 6;
+  const unsigned wmask = (smask ? (unsigned)__builtin_amdgcn_readfirstlane(smask[(long long)g * P + p]) : ~0u) &
+                         ((1u << nst) - 1);
+  const int nlive = __builtin_popcount(wmask);  // >= 1: the mask keeps the stretch of the largest bound
+  if (2 * wsid >= nlive) return;                 // no stretch for this wave (barriers wait for the others)
+  const int nwl = (nlive + 1) >> 1;              // waves with stretches: 0 .. nwl - 1
+  if (wsid == 0) etab[lane] = kExp2Frac64[lane];
+  // this wave's stretches: the (2 wsid)-th and (2 wsid + 1)-th kept ones
+  unsigned mm = wmask;
+  for (int i = 0; i < 2 * wsid; ++i) mm &= mm - 1;
+  const int sA = __builtin_ffs((int)mm) - 1;
+  mm &= mm - 1;
+  const int sB = mm ? __builtin_ffs((int)mm) - 1 : -1;
+  const int r4 = lane >> 4, r = lane & 15;
+  const int st = (r4 < 2) ? sA : sB;
+  const bool live = st >= 0;
+  const int T = 2 * (live ? st : 0) + (r4 & 1);  // the row's 32-point bound tile
+  const int t16 = 2 * T + ((lane >> 3) & 1);      // the lane's 16-point sum tile
+  const int k0 = 16 * t16 + 2 * (lane & 7);
+  const bool l0 = live && k0 < G, l1 = live && k0 + 1 < G;
+  const int b0 = p * NB;
+  const int n = nnz[g];
+  const int2* __restrict__ E = ent + (long long)g * ent_stride;
+  const int set = wset ? wset[g] : 0;
+  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
+  const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
+  double a0[NB], a1[NB];
+  tile_rows<NB>(a0, a1, D, E, n, W, Zs, GS, Bp, b0, k0, r, live, l0, l1);
+  // per-row f32 maxima (dead points are -inf), combined over the block's rows by the lead wave
+  const int q = 4 * wsid + r4;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    float m = (float)gt_max(a0[i], a1[i]);
+    m = gt_maxf(m, dpp_f<kDppXor1>(m));
+    m = gt_maxf(m, dpp_f<kDppXor2>(m));
+    m = gt_maxf(m, dpp_f<kDppHalfMirror>(m));
+    m = gt_maxf(m, dpp_f<kDppMirror>(m));
+    if (r == 0) rowmax[q * 32 + i] = m;
+  }
+  __syncthreads();
+  if (wsid == 0) {
+    const bool lb = lane < NB && b0 + lane < nboot;
+    if (lane < NB) {
+      float m = -INFINITY;
+      for (int q2 = 0; q2 < 4 * nwl; ++q2) m = gt_maxf(m, rowmax[q2 * 32 + lane]);
+      fin[lane] = (double)m;
+    }
+    // post-check of the left-out stretches against the exact row maxima (as k_boot2)
+    bool fails = false;
+    if (smask && lb)
+      for (int w = 0; w < nst; ++w)
+        if (!((wmask >> w) & 1) && !(sub[((long long)(g * P + p) * kStretchSlots + w) * NB + lane] < fin[lane] - 51.0))
+          fails = true;
+    const bool flagged = __builtin_amdgcn_ballot_w64(fails) != 0;
+    if (flagged && lane == 0) redo[(long long)g * P + p] = 1;
+    if (!flagged && lb && !(fabs(fin[lane]) <= degen_thresh)) degen[g] = 1;
+    if (lane == 0) {  // the 16-point tiles this slab's partial row holds
+      const int NT = (G + 15) >> 4;
+      unsigned dn = 0;
+      for (int w = 0; w < nst; ++w)
+        if ((wmask >> w) & 1) dn |= 15u << (4 * w);
+      pmask[(long long)g * P + p] = dn & ((NT >= 32) ? ~0u : ((1u << NT) - 1));
+    }
+  }
+  __syncthreads();
+  // softmax terms (below e^-50 zeroed, as k_boot2), 16-point tile partial sums
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const double m = fin[i];
+    const double d0 = a0[i] - m, d1 = a1[i] - m;
+    const bool n0 = l0 && d0 >= kBootExpCut, n1 = l1 && d1 >= kBootExpCut;
+    if (__builtin_amdgcn_ballot_w64(n0 || n1)) {
+      a0[i] = n0 ? exp_tab(d0, etab) : 0.0;
+      a1[i] = n1 ? exp_tab(d1, etab) : 0.0;
+    } else {
+      a0[i] = 0.0;
+      a1[i] = 0.0;
+    }
+    const double ps = pair8_sum(a0[i], a1[i]);
+    if ((lane & 7) == 0 && live) tsum[t16 * NB + i] = ps;
+  }
+  __syncthreads();
+  if (wsid == 0 && lane < NB) {
+    const int nt = (G + 15) >> 4;
+    double S = 0.0;
+    for (int t = 0; t < nt; ++t)
+      if ((wmask >> (t >> 2)) & 1) S += tsum[t * NB + lane];
+    fin[lane] = (b0 + lane < nboot) ? 1.0 / (S * norm_mult) : 0.0;
+  }
+  __syncthreads();
+  if (l0) {
+    double j0 = 0.0, j1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      j0 = fma(a0[i], fin[i], j0);
+      j1 = fma(a1[i], fin[i], j1);
+    }
+    double* prow = part + (long long)p * part_stride + (long long)g * GS;
+    if (l1)
+      *reinterpret_cast<d2_t*>(prow + k0) = d2_t{j0, j1};
+    else
+      prow[k0] = j0;
+  }
+}
+
 #ifdef SCDE_TILE_TEST_WB1
 // hazard-test builds only (tests/test_kernel_resources.py), never run: one-wave blocks with a
 // token bound-staging area, whose LDS no longer caps occupancy at 4 waves per SIMD, so
@@ -3844,6 +3979,30 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
     sub = a.ubuf;
   }
   const int grid = (a.ngenes + 7) / 8 * 8 * P;
+  // the tile-row kernel (k_boot2t): with the mask, nb <= 20, 16-byte aligned multiplicity rows and
+  // at most 8 stretches of a 512-point column stride
+  const bool rows = smask && a.pmask && a.nb <= 20 && a.Bp % 2 == 0 && a.GS % 2 == 0 && a.G <= 512;
+  if (rows) {
+#define SCDE_B2T(NBV)                                                                                             \
+  case NBV:                                                                                                        \
+    hipLaunchKernelGGL(k_boot2t<NBV>, dim3(grid), dim3(256), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,    \
+                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
+                       a.part_stride, a.degen, a.ngenes, RP ? nullptr : smask, sub, a.redo, RP, a.pmask);      \
+    break;
+    for (int RP = 0; RP < 2; ++RP) {
+      switch (a.nb) {
+        SCDE_B2T(4) SCDE_B2T(8) SCDE_B2T(12) SCDE_B2T(16) SCDE_B2T(20)
+        default: return hipErrorInvalidValue;
+      }
+    }
+#undef SCDE_B2T
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const long long n = (long long)a.ngenes * a.G;
+    hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
+                       a.G, a.GS, a.out, a.out_g, a.out_k, a.pmask);
+    return hipGetLastError();
+  }
 #define SCDE_B2(NBV)                                                                                              \
   case NBV:                                                                                                        \
     hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid), dim3(block), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
