@@ -310,6 +310,8 @@ struct scde_ctx {
                                 // thread of its own
   int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
                                 // the second group's tables
+  int opt_task_cols = 0;         // "task_cols": columns per tables task (0: 32 for launches under 4096
+                                 // 64-column tasks, else 64; at most kTabTaskCols)
   int opt_boot2_rows = 1;        // "boot2_rows": the stretch-mask bootstrap (below boot_tiles_cells) on tile rows
                                  // (k_boot2t: two kept stretches per wave, DPP64 multiplicities); 0: k_boot2
   int opt_fuse_groups = 1;       // "fuse_groups": a DE call's two group posteriors run as one (PostSpec::ngroups:
@@ -1081,7 +1083,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     tc.mlp_split = ta.mlp_split - c0;  // relative to the launch's first cell
     // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
     if (G <= 448 && nc > 0) {
-      constexpr long long kTaskCols = kTabTaskCols;
+      // tasks of up to 64 columns of one cell (the kernel stages at most kTabTaskCols); a launch
+      // that would fill fewer than 4 rounds of the chip's block slots (~1,000 four-wave blocks
+      // per round) takes 32-column tasks, so its last round is shorter (small shards, pieces)
+      const long long kTaskCols =
+          (cx->opt_task_cols > 0) ? std::min<long long>(cx->opt_task_cols, kTabTaskCols)
+                                  : ((nc / kTabTaskCols < 4096) ? std::min(32, kTabTaskCols) : kTabTaskCols);
       tu.tasks_h.clear();
       for (int c = 0; c < Cc; ++c)
         for (long long b = off_h[c]; b < off_h[c + 1]; b += kTaskCols)
@@ -1789,6 +1796,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "rest_thread") ctx->opt_rest_thread = value != 0;
   else if (n == "fuse_groups") ctx->opt_fuse_groups = value != 0;
   else if (n == "boot2_rows") ctx->opt_boot2_rows = value != 0;
+  else if (n == "task_cols") ctx->opt_task_cols = std::max(0, (int)value);
   else if (n == "boot_chunks") ctx->opt_boot_chunks = std::max(1, std::min((int)value, 64));
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
@@ -2565,6 +2573,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_gene3_cells = cx->opt_gene3_cells;
   p->opt_boot_chunks = cx->opt_boot_chunks;
   p->opt_boot2_rows = cx->opt_boot2_rows;
+  p->opt_task_cols = cx->opt_task_cols;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;
