@@ -1976,7 +1976,8 @@ constexpr int kTileMax = 28;   // 16-point sum tiles, G <= 448
 constexpr int kBTileMax = 14;  // 32-point bound tiles, G <= 448
 #ifndef SCDE_TILE_DIAG
 #define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only, 2 = rows without bounds, 4 = no multiplicity loads,
-                          // 8 = every column load from the entry-0 column (cache-resident)
+                          // 8 = every column load from the entry-0 column (cache-resident); k_boot_gene:
+                          // 16 = no bound pass, 32 = no row loop, 64 = rows only (no softmax / sums / rows out)
 #endif
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2657,9 +2658,12 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   const int* __restrict__ ZUset = ZUq + (long long)set * 4 * kQTiles * Bq + gb0;
   // ---- 1. bounds of the group's boot window 32 wsid .. 32 wsid + 31 (with 3 waves: the fourth
   // window split by entry chunks)
-  if (wsid < NW)
+  if (SCDE_TILE_DIAG & 16) {  // timing build: no bound pass (results wrong)
+    for (int i = threadIdx.x; i < kBTileMax * 128; i += 64 * WB) gub[i] = -INFINITY;
+  } else if (wsid < NW) {
     tile_bound_pass(E, n, UQ, W8grp + 32 * wsid, gstride, ZUset + 32 * wsid, Bq, &bstage[wsid][0], gub + 32 * wsid, 128,
                     min(32, gnb - 32 * wsid), NTB, lane);
+  }
   if (WB < 4 && NW > WB) {  // (each wave stages in its own area: no barrier before the partial pass)
     tile_bound_partial(E, n, UQ, W8grp + 32 * WB, gstride, wsid, WB, &bstage[wsid][0], dsum, min(32, gnb - 32 * WB),
                        NTB, lane);
@@ -2751,7 +2755,22 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
   const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
   double a0[NB], a1[NB];
-  tile_rows<NB>(a0, a1, D, E, n, W, Zs, GS, Bp, b0, k0, r, live, l0, l1);
+  if (SCDE_TILE_DIAG & 32) {  // timing build: no row loop (results wrong)
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      a0[i] = l0 ? (double)(k0 + i) : -INFINITY;
+      a1[i] = l1 ? (double)(k0 + i) : -INFINITY;
+    }
+  } else {
+    tile_rows<NB>(a0, a1, D, E, n, W, Zs, GS, Bp, b0, k0, r, live, l0, l1);
+  }
+  if (SCDE_TILE_DIAG & 64) {  // timing build: rows only (results wrong)
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) v += a0[i] + a1[i];
+    if (v == 12345.0) part[0] = v;
+    return;
+  }
   // per-row f32 maxima (max is exact: the same m'_b as any other reduction order)
 #pragma unroll
   for (int i = 0; i < NB; ++i) {

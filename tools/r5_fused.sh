@@ -21,4 +21,9 @@ run c2_f1_r0 --config 2 --opt boot2_rows=0
 run c2_f0_r0 --config 2 --opt fuse_groups=0 --opt boot2_rows=0
 run c2b_r1 --config 2b
 run c2b_r0 --config 2b --opt boot2_rows=0
-echo done
+echo main done
+# k_boot_gene timing builds (results wrong by construction): 16 no bound pass, 32 no row loop, 64 rows only
+for d in 16 32 64; do
+  SCDE_LIB=diag/libt$d.so run c3_diag$d --config 3 --opt lanes=1
+done
+echo diag done
