@@ -310,6 +310,7 @@ struct scde_ctx {
                                 // thread of its own
   int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
                                 // the second group's tables
+  int opt_tables_pair = 1;       // "tables_pair": k_tables_reg computes a wave's columns two at a time (0: one)
   int opt_task_cols = 0;         // "task_cols": columns per tables task (0: 32 for launches under 4096
                                  // 64-column tasks, else 64; at most kTabTaskCols)
   int opt_boot2_rows = 1;        // "boot2_rows": the stretch-mask bootstrap (below boot_tiles_cells) on tile rows
@@ -1035,6 +1036,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     ta.minlogprob = -1 * DBL_MAX / (s.ngroups == 2 ? s.gsplit : C) / 1.1;
     ta.minlogprob2 = -1 * DBL_MAX / (s.ngroups == 2 ? C - s.gsplit : C) / 1.1;
     ta.mlp_split = s.ngroups == 2 ? s.gsplit : C;
+    ta.pair_cols = cx->opt_tables_pair;
     ta.T = p.keep_T ? cx->T.as<double>() : nullptr;
     ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
     ta.has_clamp = cx->has_clamp.as<unsigned char>();
@@ -1797,6 +1799,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "fuse_groups") ctx->opt_fuse_groups = value != 0;
   else if (n == "boot2_rows") ctx->opt_boot2_rows = value != 0;
   else if (n == "task_cols") ctx->opt_task_cols = std::max(0, (int)value);
+  else if (n == "tables_pair") ctx->opt_tables_pair = value != 0;
   else if (n == "boot_chunks") ctx->opt_boot_chunks = std::max(1, std::min((int)value, 64));
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
@@ -2574,6 +2577,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_boot_chunks = cx->opt_boot_chunks;
   p->opt_boot2_rows = cx->opt_boot2_rows;
   p->opt_task_cols = cx->opt_task_cols;
+  p->opt_tables_pair = cx->opt_tables_pair;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;

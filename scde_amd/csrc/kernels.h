@@ -13,7 +13,9 @@
 #ifndef SCDE_TABREG_WPE
 // k_tables_reg occupancy target (waves per SIMD; 4-wave blocks): the closed form's seven staged
 // rows (36 KB of LDS per block) and 118 VGPRs allow four blocks per CU
-#if SCDE_NB_CLOSED
+#if SCDE_NB_CLOSED && (!defined(SCDE_TABREG_PAIR) || SCDE_TABREG_PAIR)
+#define SCDE_TABREG_WPE 3  // two columns per wave (k_tables_reg's paired columns) need the registers of 3 waves/SIMD
+#elif SCDE_NB_CLOSED
 #define SCDE_TABREG_WPE 4
 #else
 #define SCDE_TABREG_WPE 3
@@ -72,6 +74,8 @@ struct TablesArgs {
   // minlogprob2 = -DBL_MAX / (its group's cells) / 1.1; one group: mlp_split >= ncells
   double minlogprob2;
   int mlp_split;
+  // k_tables_reg takes a wave's columns two at a time (0: one at a time; the same bits either way)
+  int pair_cols;
   double* T;                 // [ncols][GS] log-posterior columns
   int* maxi;                 // [ncols] argmax (nullable)
   unsigned char* has_clamp;  // [ncols]

@@ -909,6 +909,194 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 #endif
 }
 
+#ifndef SCDE_TABREG_PAIR
+#define SCDE_TABREG_PAIR 1  // k_tables_reg takes a wave's columns two at a time (closed form only)
+#endif
+#if SCDE_NB_CLOSED
+// Two columns of one cell per wave, interleaved (round 5).  A column is a dependency chain -- the
+// NB row, a wave max, the exps, a wave sum, a table log, the final row -- and at four waves per
+// SIMD the chain's latencies were exposed (the VALU was ~40% busy).  Two independent columns per
+// pass give the scheduler a second chain, and the cell's staged rows are read once for both.
+// Every value of a column is formed exactly as tables_column_reg forms it (closed form), so the
+// outputs are the same bits; a column whose constants fall outside the fast form (ok false: the
+// gated k_tables pass takes it) writes nothing.
+template <int BM, int GC>
+__device__ __forceinline__ void tables_column_reg2(const TablesArgs& a, long long colA, long long colB, int c,
+                                                   int phase, const double* __restrict__ sm, bool have_base,
+                                                   const unsigned* __restrict__ uqb, const double* etab,
+                                                   const LogTab& lt, int lane, double theta, const double* ccA,
+                                                   const double* ccB, double xA, double xB, double maxcfp, int bc_u) {
+  constexpr int Q = 2;
+  const int G = GC ? GC : a.G;
+  const long long col[Q] = {colA, colB};
+  const double* const cc[Q] = {ccA, ccB};
+  const double x[Q] = {xA, xB};
+  bool ok[Q];
+  double fp[Q], lpo[Q], lqo[Q], c10[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    ok[q] = cc[q][0] > 0.0;  // k_col_consts stores n = -1 where the fast form does not apply
+    fp[q] = cc[q][7];
+    lpo[q] = cc[q][8];
+    lqo[q] = cc[q][9];
+    c10[q] = cc[q][10];
+  }
+  const double* sl = sm + lane;
+  double v[Q][kTabChunks];
+  double lmax[Q] = {-INFINITY, -INFINITY};
+#pragma unroll
+  for (int j = 0; j < kTabChunks; ++j) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q][j] = -INFINITY;
+    if (64 * j < G) {
+      const int k = lane + 64 * j;
+      const bool in = k < G;
+      const bool last = (k == G - 1);
+      const double lp0 = sl[kRowLP * kRS + 64 * j], lq0 = sl[kRowLQ * kRS + 64 * j];
+      const double muv = sl[kRowMu * kRS + 64 * j], mnext = sl[kRowMu * kRS + 64 * j + 1];
+      const double lcfpr = sl[kRowLcfpr * kRS + 64 * j];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const bool over = in && ((!last && x[q] > muv && x[q] < mnext) || (last && x[q] > muv));
+        double lpr = lp0, lqr = lq0;
+        if (__builtin_amdgcn_ballot_w64(over)) {
+          lpr = over ? lpo[q] : lpr;
+          lqr = over ? lqo[q] : lqr;
+        }
+        double nb = (x[q] == 0.0) ? theta * lpr : fma(x[q], lqr, fma(theta, lpr, c10[q]));
+        nb += lcfpr;
+        v[q][j] = in ? nb : -INFINITY;
+        lmax[q] = gt_max(lmax[q], v[q][j]);
+      }
+    }
+  }
+  double maxp[Q], d0[Q], E[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) maxp[q] = wave_allreduce<true>(lmax[q]);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    if (maxp[q] < (maxcfp + fp[q])) maxp[q] = maxcfp + fp[q];
+    d0[q] = fp[q] - maxp[q];
+    E[q] = exp_tab(fmax(d0[q], -746.0), etab);  // exp(fp - maxp); 0 below -746 (and for NaN)
+  }
+  double ls[Q] = {0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < kTabChunks; ++j) {
+    if (64 * j < G) {
+      const int k = lane + 64 * j;
+      const bool in = k < G;
+      const double cfp = sl[kRowCfp * kRS + 64 * j];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        v[q][j] -= maxp[q];  // t1
+        double e = cfp * E[q];
+        if (__builtin_amdgcn_ballot_w64(in && v[q][j] > -60.0)) e += exp_tab(fmax(v[q][j], -746.0), etab);
+        ls[q] += in ? e : 0.0;
+      }
+    }
+  }
+  double sq[Q], lsum[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) sq[q] = wave_allreduce<false>(ls[q]);
+#pragma unroll
+  for (int q = 0; q < Q; ++q) lsum[q] = log_tab(sq[q], lt);  // s >= 1 (the maximum term is exp(0))
+  const bool want_maxi = a.maxi != nullptr;
+  double bv[Q] = {-INFINITY, -INFINITY};
+  int bi[Q] = {0x7fffffff, 0x7fffffff};
+  bool clamp[Q] = {false, false}, nanq[Q] = {false, false};
+  double* out[Q];
+  double* dout[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    out[q] = (a.T && ok[q]) ? a.T + col[q] * a.GS : nullptr;
+    dout[q] = (phase && a.D && ok[q]) ? a.D + col[q] * a.GS : nullptr;
+  }
+  const double minlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
+  unsigned uqv[Q] = {0u, 0u};  // lane t < kQTiles: bound tile t's value (BM == kBoundTiles)
+#pragma unroll
+  for (int j = 0; j < kTabChunks; ++j) {
+    if (64 * j < G) {
+      const int k = lane + 64 * j;
+      const bool in = k < G;
+      const double lcfp = sl[kRowLcfp * kRS + 64 * j], cfp = sl[kRowCfp * kRS + 64 * j];
+      const double base = sl[kRowBase * kRS + 64 * j];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const double t1 = v[q][j], t2 = lcfp + d0[q];
+        const double hi = gt_max(t2, t1), lo = (t1 > t2) ? t2 : t1;
+        const bool tiny = !(hi >= -665.0);
+        const bool mixed = !tiny && !(hi - lo > 37.5);
+        double r = hi - lsum[q];
+        if (__builtin_amdgcn_ballot_w64(in && (tiny || mixed))) {
+          const double e = fma(cfp, E[q], exp_tab(fmax(t1, -746.0), etab));
+          const double rm = log_tab(tiny ? e / sq[q] : e, lt) - (tiny ? 0.0 : lsum[q]);
+          r = (tiny || mixed) ? rm : r;
+        }
+        if (want_maxi && r > bv[q] && in) {
+          bv[q] = r;
+          bi[q] = k;
+        }
+        const bool cl = r < minlp;
+        r = cl ? minlp : r;
+        clamp[q] = clamp[q] || (cl && in);
+        nanq[q] = nanq[q] || (in && r != r);
+        // unconditional stores: lanes past the grid write the pad zeros (k < GS always)
+        if (out[q]) out[q][k] = in ? r : 0.0;
+        if (dout[q]) dout[q][k] = in ? (have_base ? r - base : r) : 0.0;
+        r = in ? r : -INFINITY;
+        if (BM == kBoundTiles) {
+          int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
+          const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
+          u = max((int)sw[0], (int)sw[1]);
+          const int g = __builtin_amdgcn_ds_bpermute(((lane - 2 * j) & 1) << 7, u);
+          uqv[q] = ((lane >> 1) == j) ? (unsigned)g : uqv[q];
+        }
+        if (BM == kBoundStretch) {  // the stretch maximum (64 points = this chunk), f32 widened
+          const float mf = wave_maxf((float)r);
+          if (lane == 0 && ok[q]) {
+            const double m = (double)mf + 0x1p-23 * fabs((double)mf);
+            a.U[col[q] * kStretchSlots + j] = (bc_u >= 0) ? m - a.U[(long long)bc_u * kStretchSlots + j] : m;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    if (!ok[q]) continue;  // wave-uniform
+    if (BM == kBoundTiles) {
+      if (__ballot(nanq[q]) && lane == 0) *a.nanflag = 1;
+      if (lane < kQTiles) {
+        int u = (int)uqv[q];
+        if (kBTile * lane >= G)
+          u = 0;
+        else if (bc_u >= 0)
+          u -= unpacku(uqb[lane]);
+        a.UQ[col[q] * kQTiles + lane] = packu(u);
+      }
+    }
+    if (dout[q])
+      for (int k = 64 * ((G + 63) / 64) + lane; k < a.GS; k += 64) dout[q][k] = 0.0;
+    if (want_maxi) {
+      double b = bv[q];
+      int bix = bi[q];
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        const double ov = __shfl_xor(b, m, 64);
+        const int oi = __shfl_xor(bix, m, 64);
+        if (ov > b || (ov == b && oi < bix)) {
+          b = ov;
+          bix = oi;
+        }
+      }
+      if (lane == 0) a.maxi[col[q]] = (bix == 0x7fffffff) ? 0 : bix;
+    }
+    const unsigned long long anyc = __ballot(clamp[q]);
+    if (lane == 0) a.has_clamp[col[q]] = anyc ? 1 : 0;
+  }
+}
+#endif
+
 template <int BM, int GC>
 __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TABREG_WPE))) void k_tables_reg(TablesArgs a) {
   __shared__ double sm[kTabRegRows * kRS];  // mu | [p | q |] log p | log q | lcfpr | cfp | lcfp | base
@@ -963,12 +1151,35 @@ __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_
   const int zc = (phase == 2) ? tab_zcol(a, c) : -1;
   const double theta = a.theta[co];
   const double maxcfp = a.cellscal[2 * c];
+#if SCDE_NB_CLOSED && SCDE_TABREG_PAIR
+  // the wave's columns two at a time (the count-0 column zc was done in phase 1), a last odd one alone
+  int col = task.y + wid;
+  if (col == zc) col += kTabRegWaves;
+  while (col < task.z) {
+    int col2 = col + kTabRegWaves;
+    if (col2 == zc) col2 += kTabRegWaves;
+    const int i = col - task.y;
+    if (col2 < task.z && a.pair_cols) {
+      const int i2 = col2 - task.y;
+      tables_column_reg2<BM, GC>(a, col, col2, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta, scc + i * kColc,
+                                 scc + i2 * kColc, (double)sx[i], (double)sx[i2], maxcfp, bc);
+      col = col2 + kTabRegWaves;
+      if (col == zc) col += kTabRegWaves;
+    } else {
+      tables_column_reg<BM, GC>(a, col, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta, scc + i * kColc,
+                                (double)sx[i], maxcfp, bc);
+      col += kTabRegWaves;
+      if (col == zc) col += kTabRegWaves;
+    }
+  }
+#else
   for (int col = task.y + wid; col < task.z; col += kTabRegWaves) {
     if (col == zc) continue;  // done in phase 1
     const int i = col - task.y;
     tables_column_reg<BM, GC>(a, col, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta,
                       scc + i * kColc, (double)sx[i], maxcfp, bc);
   }
+#endif
 }
 
 // ------------------------------------------------------------------ baseline / ELL

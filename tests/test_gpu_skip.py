@@ -58,6 +58,9 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("rest_thread", opts.get("rest_thread", 1))
     ctx.set_option("boot_chunks", opts.get("boot_chunks", 1))
     ctx.set_option("fuse_groups", opts.get("fuse_groups", 1))
+    ctx.set_option("tables_pair", opts.get("tables_pair", 1))
+    ctx.set_option("task_cols", opts.get("task_cols", 0))
+    ctx.set_option("boot2_rows", opts.get("boot2_rows", 1))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -90,6 +93,9 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("rest_thread", 1)
         ctx.set_option("boot_chunks", 1)
         ctx.set_option("fuse_groups", 1)
+        ctx.set_option("tables_pair", 1)
+        ctx.set_option("task_cols", 0)
+        ctx.set_option("boot2_rows", 1)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -135,6 +141,13 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-mult-fallback": {"tile_max_mult": 1},
         "stretch": {"boot_tiles": 0},
         "stretch-forced-redo": {"boot_tiles": 0, "skip_slack": -45.0},
+        # k_boot2 itself (the stretch path before its tile-row kernel), with forced redo slabs too
+        "stretch-k_boot2": {"boot_tiles": 0, "boot2_rows": 0},
+        "stretch-k_boot2-redo": {"boot_tiles": 0, "boot2_rows": 0, "skip_slack": -45.0},
+        # the tables one column per wave, and in 64- and 16-column tasks
+        "tables-single": {"tables_pair": 0},
+        "tables-tasks64": {"task_cols": 64},
+        "tables-tasks16": {"task_cols": 16},
     }
     got = {}
     for name, opts in runs.items():
@@ -160,7 +173,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         else:
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
             assert stats["boot_path"] == (0 if name.startswith("stretch") else 1), (name, stats)
-        if name.endswith("forced-redo"):
+        if name.endswith("forced-redo") or name == "stretch-k_boot2-redo":
             assert stats["skip_redo"] > 0, stats  # the second-chance path really adds work
         g = got[name]
         for i in range(2):
@@ -180,7 +193,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
                                     "pipelined-thread-seq",
                                     "tiles-pairs",
-                                    "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo")),):
+                                    "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo",
+                                    "stretch-k_boot2", "stretch-k_boot2-redo", "tables-single", "tables-tasks64",
+                                    "tables-tasks16")),):
         for name in others:
             for i in range(2):
                 np.testing.assert_array_equal(got[name]["joint.posteriors"][i], got[base]["joint.posteriors"][i])

@@ -16,6 +16,7 @@ run s8_f0 --config 3 --shard-of 8 --opt fuse_groups=0
 run s8_t64 --config 3 --shard-of 8 --opt task_cols=64
 run s8_p2 --config 3 --shard-of 8 --opt pipeline_mb=0 --opt pieces=1
 run c3_t64 --config 3 --opt task_cols=64
+run c3_single --config 3 --opt tables_pair=0
 run c2_f1_r1 --config 2
 run c2_f1_r0 --config 2 --opt boot2_rows=0
 run c2_f0_r0 --config 2 --opt fuse_groups=0 --opt boot2_rows=0
