@@ -1211,8 +1211,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   int ndraw = 0, maxw = 0;
   const int nsets = (int)s.seeds.size();
   // the cells a seed set draws from (fused groups: its own group's)
-  auto set_c0 = [&](int set) { return two && set >= s.nsets_g ? s.gsplit : 0; };
-  auto set_c1 = [&](int set) { return two && set < s.nsets_g ? s.gsplit : C; };
+  // (by value: rest_fn, which uses them, may run after this function has returned)
+  const int nsets_g = s.nsets_g, gsplit = s.gsplit;
+  auto set_c0 = [two, nsets_g, gsplit](int set) { return two && set >= nsets_g ? gsplit : 0; };
+  auto set_c1 = [two, nsets_g, gsplit, C](int set) { return two && set < nsets_g ? gsplit : C; };
   // tile path ELL rows: a multiple of 64 entries (the bound MFMAs' K steps) plus 64
   const int qstride = (int)round_up(std::max(Cmax, 1), 64) + 64;
   // FP64 path: boots per slab; the draws come after the tables launch (the host's RNG work
