@@ -1177,13 +1177,18 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       HCHK(hipStreamWaitEvent(st, s.piece_ev[j], 0));
       for (int c = c0; c < c1; ++c) ucl_off_h[c + 1] = col0 + pu.ucl_off_h[c - c0 + 1];
       const long long nc = pu.ucl_off_h[c1 - c0];
+      // The whole set's column offsets go up on this stream BEFORE the last piece's tables: the
+      // bootstrap set-up (ELL rows) reads them on the aux stream, which waits only for p1_ev, the
+      // event after the last piece's phase-1 tables.  Uploaded after the loop (rounds 3-4), the ELL
+      // builder could read the previous call's offsets -- identical when the same data is run again,
+      // garbage after a call on other data (the r04 full-size failure).
+      if (j == jlast) RCHK(upload(cx, u.ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
       // capacity for this piece plus an estimate of the rest (grown keeping the columns so far)
       const long long est = std::max<long long>(col0 + nc, (long long)((double)(col0 + nc) / c1 * C * 1.1));
       RCHK(setup_tables(plan0, est, j > 0));
       RCHK(launch_tables_range(plan0, c0, c1, col0, pu.ucl_off.as<long long>(), pu.ucl_off_h, j == jlast, pu));
       col0 += nc;
     }
-    RCHK(upload(cx, u.ucl_off, ucl_off_h.data(), sizeof(long long) * (C + 1)));
     ta.ucl_off = u.ucl_off.as<long long>();
     tables_done = make_plan(col0) == plan0;  // else: the whole tables again, planned for col0 columns
   }
