@@ -658,7 +658,11 @@ def main():
                   "device_syncs_per_step": 0.0,
                   # host-count pieces: host ms per step waiting for uploads / building and launching
                   "piece_wait_ms_per_step": ctx.stat("piece_wait_ms") / args.steps,
-                  "piece_host_ms_per_step": ctx.stat("piece_host_ms") / args.steps}
+                  "piece_host_ms_per_step": ctx.stat("piece_host_ms") / args.steps,
+                  # host wall time of the call's phases (set-up, unique sets, posteriors enqueued,
+                  # ratio + read-back incl. the final wait), ms per step
+                  "host_phase_ms_per_step": {k: ctx.stat(f"host_{k}_ms") / args.steps
+                                             for k in ("setup", "unique", "post", "tail")}}
     # device-resident rate (counts already in HBM), product settings
     dc = api.DeviceCounts(ctx, counts)
     dt_dev = timed(dc.ptr)

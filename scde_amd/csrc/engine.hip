@@ -826,9 +826,57 @@ int build_unique_sets(scde_ctx* cx, const PostSpec* const* s, UniqueSet* const* 
   return SCDE_OK;
 }
 
-// Draw lists and per-cell multiplicities for each seed set.
-void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<double>& W, int& ndraw) {
+// The draw lists alone (cell per draw; -1 pads a fused shorter group's lists) and the largest
+// multiplicity of a cell in one boot.
+void make_draws_lists(const PostSpec& s, std::vector<int>& draws, int& ndraw, int* maxw) {
   const int C = s.ncells, B = s.nboot, nsets = (int)s.seeds.size();
+  const bool two = s.ngroups == 2 && !s.batch_call;
+  if (two) {
+    ndraw = std::max(s.gsplit, C - s.gsplit);
+  } else if (s.batch_call) {
+    ndraw = 0;
+    for (int k = 0; k < s.nbatch; ++k) ndraw += std::max(0, s.comp[k]);
+  } else {
+    ndraw = C;
+  }
+  const size_t per = (size_t)B * std::max(ndraw, 1);
+  draws.assign((size_t)nsets * per, -1);
+  std::vector<int> hist((size_t)std::max(C, 1), 0);
+  int mx = 0;
+  for (int set = 0; set < nsets; ++set) {
+    PlatformRand rng((unsigned int)s.seeds[set], s.rand_kind);
+    int* dr = draws.data() + (size_t)set * per;
+    const int gi = (two && set >= s.nsets_g) ? 1 : 0, c0 = gi ? s.gsplit : 0;
+    const int n = two ? (gi ? C - s.gsplit : s.gsplit) : C;
+    for (int b = 0; b < B; ++b) {
+      int* row = dr + (size_t)b * ndraw;
+      int d = 0;
+      if (!s.batch_call) {
+        for (int j = 0; j < n; ++j) row[d++] = c0 + rng.draw(n);
+      } else {
+        for (int k = 0; k < s.nbatch; ++k) {
+          const int* bi = s.batch_vals + s.batch_off[k];
+          const int nbk = (int)(s.batch_off[k + 1] - s.batch_off[k]);
+          for (int j = 0; j < s.comp[k]; ++j) row[d++] = bi[rng.draw(nbk)];
+        }
+      }
+      for (int j = 0; j < d; ++j) mx = std::max(mx, ++hist[row[j]]);
+      for (int j = 0; j < d; ++j) hist[row[j]] = 0;
+    }
+  }
+  if (maxw) *maxw = mx;
+}
+
+// Draw lists and per-cell multiplicities for each seed set.  want_W false: the multiplicities are
+// left to the device (launch_mult); only their maximum is formed here (*maxw), from a per-boot
+// count of the cells drawn.
+void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<double>& W, int& ndraw,
+                int* maxw = nullptr, bool want_W = true) {
+  const int C = s.ncells, B = s.nboot, nsets = (int)s.seeds.size();
+  if (!want_W) {
+    make_draws_lists(s, draws, ndraw, maxw);
+    return;
+  }
   if (s.ngroups == 2 && !s.batch_call) {
     // fused groups: set `set` belongs to group B from nsets_g on; each draws from its own group's
     // cells (the group's own call, cell indices offset into the fused list); the shorter group's
@@ -1242,10 +1290,16 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     if (!cx->modes_ev) HCHK(hipEventCreateWithFlags(&cx->modes_ev, hipEventDisableTiming));
     HCHK(hipEventRecord(cx->modes_ev, st));
   }
+  // fused (fast) path: the draw lists here, the multiplicity arrays on the device (launch_mult)
+  const bool dev_mult = fused && C <= kMultMaxCells;
   if (fused && s.nboot > 0) {
-    make_draws(s, Bp, draws, W, ndraw);
-    maxw = 0;
-    for (double w : W) maxw = std::max(maxw, (int)w);
+    if (dev_mult) {
+      make_draws(s, Bp, draws, W, ndraw, &maxw, false);
+    } else {
+      make_draws(s, Bp, draws, W, ndraw);
+      maxw = 0;
+      for (double w : W) maxw = std::max(maxw, (int)w);
+    }
     tpath = tpath && maxw <= std::min(127, cx->opt_tile_max_mult);
   }
   // ---- joint posterior
@@ -1273,7 +1327,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       sa = cx->aux_stream;
       HCHK(hipStreamWaitEvent(sa, cx->p1_ev, 0));
     }
-    RCHK(upload_on(cx, cx->Wt, W.data(), sizeof(double) * W.size(), sa));
+    if (!dev_mult) RCHK(upload_on(cx, cx->Wt, W.data(), sizeof(double) * W.size(), sa));
     RCHK(upload_on(cx, cx->draws, draws.data(), sizeof(int) * draws.size(), sa));
     if (!fused) {
       HCHK(cx->base_col.ensure(sizeof(int) * C));
@@ -1319,7 +1373,24 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // pair mode at config 4: bootstrap 11.16 -> 9.94 ms per step) or, without it, k_boot_tiles'
     // wave per slab (pair mode from pair_cells)
     const int gene_sg = (tpath && cx->opt_gene_blocks) ? std::min({(s.nboot + nb - 1) / nb, 8, 128 / nb}) : 0;
-    if (tpath) {
+    if (dev_mult) {
+      // the multiplicity arrays from the uploaded draw lists, on the device (host loops over
+      // sets x cells x boots and their uploads cost ~0.1-0.4 ms of host time per posterior)
+      const int P = (s.nboot + nb - 1) / nb;
+      const int NGR = gene_sg > 0 ? (P + gene_sg - 1) / gene_sg : 0;
+      const size_t sc = (size_t)nsets * C;
+      HCHK(cx->Wt.ensure(sizeof(double) * std::max<size_t>(1, sc * Bp)));
+      if (tpath) {
+        HCHK(cx->w8.ensure(std::max<size_t>(1, sc * Bt)));
+        HCHK(cx->w8t.ensure(std::max<size_t>(1, sc * P * 32)));
+        if (gene_sg > 0) HCHK(cx->w8g.ensure(std::max<size_t>(1, sc * NGR * 128)));
+      }
+      HCHK(launch_mult(cx->draws.as<int>(), nsets, s.nboot, ndraw, C, Bp, cx->Wt.as<double>(), Bt,
+                       tpath ? cx->w8.as<unsigned char>() : nullptr, nb, P,
+                       tpath ? cx->w8t.as<unsigned char>() : nullptr, gene_sg, NGR,
+                       (tpath && gene_sg > 0) ? cx->w8g.as<unsigned char>() : nullptr, sa));
+    }
+    if (tpath && !dev_mult) {
       // byte multiplicities [set][cell][boot] (baseline bound sums and the tile bounds)
       // and, for the tile bounds' A fragments, per slab the pairs (boot r, boot 16 + r) of its nb
       // boots, so one 16-bit load serves both 16-boot MFMA tiles
@@ -1358,6 +1429,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           }
         RCHK(upload_on(cx, cx->w8g, w8g.data(), w8g.size(), sa));
       }
+    }
+    if (tpath) {
       HCHK(cx->zubound.ensure(sizeof(int) * (size_t)nsets * 4 * kQTiles * Bt));
       HCHK(launch_zuq(cx->ubound.as<unsigned>(), cx->base_col.as<int>(), C, cx->w8.as<unsigned char>(), Bt, nsets,
                       cx->zubound.as<int>(), sa));

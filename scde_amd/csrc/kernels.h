@@ -285,6 +285,15 @@ hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, 
                       int cell_off = 0);
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
                              int Bp, int nsets, double* Z, hipStream_t s, int gsets = 0, int gsplit = 0);
+// Draw multiplicities on the device from the draw lists draws[nsets][nboot][ndraw] (cell index, -1
+// = no draw): Wt[set][c][Bp] (doubles), and for the tile path (nullable) W8[set][c][Bt],
+// W8p[set][c][P][32] (per slab of nb boots the pairs (j, 16 + j) in slots 2j, 2j + 1) and
+// W8g[set][c][NGR][128] (per group of SG slabs four 32-boot windows as pair slots).  The arrays are
+// zeroed here first.  ncells <= kMultMaxCells.
+constexpr int kMultMaxCells = 16384;
+hipError_t launch_mult(const int* draws, int nsets, int nboot, int ndraw, int ncells, int Bp, double* Wt, int Bt,
+                       unsigned char* W8, int nb, int P, unsigned char* W8p, int SG, int NGR, unsigned char* W8g,
+                       hipStream_t s);
 hipError_t launch_boot(const BootArgs& a, hipStream_t s);
 hipError_t launch_boot_exact(const ExactArgs& a, hipStream_t s);
 int boot2_nb(int nboot);

@@ -4259,6 +4259,55 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// One block per (boot, seed set): the boot's draws counted per cell in LDS, then the cell column
+// of every multiplicity array written (strided, small: cells x boots per set).
+__global__ __launch_bounds__(256) void k_mult(const int* __restrict__ draws, int nboot, int ndraw, int ncells, int Bp,
+                                              double* __restrict__ Wt, int Bt, unsigned char* __restrict__ W8,
+                                              int nb, int P, unsigned char* __restrict__ W8p, int SG, int NGR,
+                                              unsigned char* __restrict__ W8g) {
+  __shared__ int hist[kMultMaxCells];
+  const int b = blockIdx.x, set = blockIdx.y;
+  for (int c = threadIdx.x; c < ncells; c += blockDim.x) hist[c] = 0;
+  __syncthreads();
+  const int* dr = draws + ((long long)set * nboot + b) * ndraw;
+  for (int d = threadIdx.x; d < ndraw; d += blockDim.x) {
+    const int cell = dr[d];
+    if (cell >= 0) atomicAdd(&hist[cell], 1);
+  }
+  __syncthreads();
+  const int p = b / nb, j = b - p * nb;
+  const int gr = SG > 0 ? b / (SG * nb) : 0, jg = b - gr * SG * nb, wg = jg >> 5, jj = jg & 31;
+  const int slotp = (j < 16) ? 2 * j : 2 * (j - 16) + 1;
+  const int slotg = (jj < 16) ? 2 * jj : 2 * (jj - 16) + 1;
+  for (int c = threadIdx.x; c < ncells; c += blockDim.x) {
+    const int w = hist[c];
+    if (!w) continue;  // (the arrays were zeroed)
+    const long long sc = (long long)set * ncells + c;
+    Wt[sc * Bp + b] = (double)w;
+    if (W8) W8[sc * Bt + b] = (unsigned char)w;
+    if (W8p && j < 32) W8p[(sc * P + p) * 32 + slotp] = (unsigned char)w;
+    if (W8g && jg < 128) W8g[(sc * NGR + gr) * 128 + 32 * wg + slotg] = (unsigned char)w;
+  }
+}
+
+hipError_t launch_mult(const int* draws, int nsets, int nboot, int ndraw, int ncells, int Bp, double* Wt, int Bt,
+                       unsigned char* W8, int nb, int P, unsigned char* W8p, int SG, int NGR, unsigned char* W8g,
+                       hipStream_t s) {
+  if (ncells <= 0 || ncells > kMultMaxCells || nsets <= 0 || nb <= 0 || Bp < nboot || (W8 && Bt < nboot) ||
+      (W8p && P * nb < nboot) || (W8g && (SG <= 0 || NGR * SG * nb < nboot)))
+    return hipErrorInvalidValue;
+  const size_t sc = (size_t)nsets * ncells;
+  hipError_t e = hipMemsetAsync(Wt, 0, sizeof(double) * sc * Bp, s);
+  if (e == hipSuccess && W8) e = hipMemsetAsync(W8, 0, sc * Bt, s);
+  if (e == hipSuccess && W8p) e = hipMemsetAsync(W8p, 0, sc * P * 32, s);
+  if (e == hipSuccess && W8g) e = hipMemsetAsync(W8g, 0, sc * NGR * 128, s);
+  if (e != hipSuccess) return e;
+  if (nboot <= 0 || ndraw <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mult, dim3(nboot, nsets), dim3(256), 0, s, draws, nboot, ndraw, ncells, Bp, Wt, Bt, W8, nb, P,
+                     W8p, SG, NGR, W8g);
+  return hipGetLastError();
+}
+
 // Per gene the sum of its counts over the call's cells (from the ELL entries: each entry's
 // column is a unique count), the key of the tile bootstrap's gene order.
 __global__ __launch_bounds__(256) void k_gene_key(const int2* __restrict__ ent, const int* __restrict__ nnz,

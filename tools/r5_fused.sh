@@ -7,16 +7,19 @@ tail -3 gpurun_out/r5b/gputests.log; [ $rc -eq 0 ] || exit $rc
 run() {  # tag, bench args...
   local tag=$1; shift
   timeout -k 10 300 python bench.py "$@" --steps 20 --warmup 3 --cpu-sample 0 --cpu-workers 0 > gpurun_out/r5b/b_$tag.json 2> gpurun_out/r5b/b_$tag.err || { tail -5 gpurun_out/r5b/b_$tag.err; exit 1; }
-  echo "$tag $(grep -o '"ms_per_step": [0-9.e+]*\|device_resident_ms_per_step": [0-9.e+]*' gpurun_out/r5b/b_$tag.json | tr '\n' ' ') $(grep -o '"kernel_ms_per_step": {[^}]*}' gpurun_out/r5b/b_$tag.json)"
+  python3 -c "
+import json,sys; d=json.load(open('gpurun_out/r5b/b_$tag.json'))
+k=d['kernel_ms_per_step']; h=d['host_syncs']['host_phase_ms_per_step']
+print('$tag', 'host %.3f dev %.3f' % (d['ms_per_step'], d['device_resident_ms_per_step']), 'kern', {a: round(b,3) for a,b in k.items()}, 'hostph', {a: round(b,3) for a,b in h.items()})"
 }
 run c3_f1 --config 3
 run c3_f0 --config 3 --opt fuse_groups=0
 run s8_f1 --config 3 --shard-of 8
 run s8_f0 --config 3 --shard-of 8 --opt fuse_groups=0
-run s8_t64 --config 3 --shard-of 8 --opt task_cols=64
+
 run s8_p2 --config 3 --shard-of 8 --opt pipeline_mb=0 --opt pieces=1
-run c3_t64 --config 3 --opt task_cols=64
-run c3_single --config 3 --opt tables_pair=0
+
+
 run c2_f1_r1 --config 2
 run c2_f1_r0 --config 2 --opt boot2_rows=0
 run c2_f0_r0 --config 2 --opt fuse_groups=0 --opt boot2_rows=0
