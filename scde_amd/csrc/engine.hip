@@ -313,10 +313,14 @@ struct scde_ctx {
   int opt_tables_pair = 1;       // "tables_pair": k_tables_reg computes a wave's columns two at a time (0: one)
   int opt_task_cols = 0;         // "task_cols": columns per tables task (0: 32 for launches under 4096
                                  // 64-column tasks, else 64; at most kTabTaskCols)
-  int opt_boot2_rows = 1;        // "boot2_rows": the stretch-mask bootstrap (below boot_tiles_cells) on tile rows
-                                 // (k_boot2t: two kept stretches per wave, DPP64 multiplicities); 0: k_boot2
-  int opt_fuse_groups = 1;       // "fuse_groups": a DE call's two group posteriors run as one (PostSpec::ngroups:
-                                 // concatenated cells, doubled genes, one launch per stage); 0: two posteriors
+  int opt_boot2_rows = 0;        // "boot2_rows": the stretch-mask bootstrap (below boot_tiles_cells) on tile rows
+                                 // (k_boot2t: two kept stretches per wave, DPP64 multiplicities; same bits).  Off:
+                                 // measured slower than k_boot2 (config 2 bootstrap 3.51 vs 3.19 ms per step, 2b
+                                 // 8.72 vs 7.93)
+  int opt_fuse_groups = 0;       // "fuse_groups": a DE call's two group posteriors run as one (PostSpec::ngroups:
+                                 // concatenated cells, doubled genes, one launch per stage; same bits).  Off:
+                                 // measured no faster than the two lanes (config 3 host -> host 7.20 vs 6.80 ms,
+                                 // shard of 8 1.69 vs 1.66)
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                  // group on `peer`, its own streams and workspace) or one after the other (1)
   // the second lane of a DE call: a context on the same device, created on first use; its

@@ -57,10 +57,10 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("interleave", opts.get("interleave", 1))
     ctx.set_option("rest_thread", opts.get("rest_thread", 1))
     ctx.set_option("boot_chunks", opts.get("boot_chunks", 1))
-    ctx.set_option("fuse_groups", opts.get("fuse_groups", 1))
+    ctx.set_option("fuse_groups", opts.get("fuse_groups", 0))
     ctx.set_option("tables_pair", opts.get("tables_pair", 1))
     ctx.set_option("task_cols", opts.get("task_cols", 0))
-    ctx.set_option("boot2_rows", opts.get("boot2_rows", 1))
+    ctx.set_option("boot2_rows", opts.get("boot2_rows", 0))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -92,10 +92,10 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("interleave", 1)
         ctx.set_option("rest_thread", 1)
         ctx.set_option("boot_chunks", 1)
-        ctx.set_option("fuse_groups", 1)
+        ctx.set_option("fuse_groups", 0)
         ctx.set_option("tables_pair", 1)
         ctx.set_option("task_cols", 0)
-        ctx.set_option("boot2_rows", 1)
+        ctx.set_option("boot2_rows", 0)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -123,12 +123,12 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "gene-chunks": {"boot_chunks": 3},
         "tiles-unordered": {"tile_order": 0},
         "unique-exact": {"unique_fixed": 0},
-        # the two group posteriors fused into one (default) against the two-posterior paths (fuse_groups 0)
-        "unfused": {"fuse_groups": 0},
+        # the two group posteriors fused into one (option fuse_groups) against the two-posterior paths
+        "fused": {"fuse_groups": 1},
         "one-lane": {"lanes": 1, "fuse_groups": 0},
         "rest-inline": {"rest_thread": 0, "fuse_groups": 0},
-        "fused-pipelined": {"pipeline_mb": 0, "pieces": 3},
-        "fused-pipelined-staged": {"pipeline_mb": 0, "pieces": 2, "upload_staged": 1},
+        "fused-pipelined": {"pipeline_mb": 0, "pieces": 3, "fuse_groups": 1},
+        "fused-pipelined-staged": {"pipeline_mb": 0, "pieces": 2, "upload_staged": 1, "fuse_groups": 1},
         "pipelined-pieces": {"pipeline_mb": 0, "pieces": 3, "fuse_groups": 0},
         "pipelined-one-lane": {"pipeline_mb": 0, "pieces": 1, "lanes": 1, "fuse_groups": 0},
         "pipelined-deferred": {"pipeline_mb": 0, "pieces": 3, "defer_boot": 1, "fuse_groups": 0},
@@ -141,9 +141,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-mult-fallback": {"tile_max_mult": 1},
         "stretch": {"boot_tiles": 0},
         "stretch-forced-redo": {"boot_tiles": 0, "skip_slack": -45.0},
-        # k_boot2 itself (the stretch path before its tile-row kernel), with forced redo slabs too
-        "stretch-k_boot2": {"boot_tiles": 0, "boot2_rows": 0},
-        "stretch-k_boot2-redo": {"boot_tiles": 0, "boot2_rows": 0, "skip_slack": -45.0},
+        # the stretch path on tile rows (k_boot2t, option boot2_rows), with forced redo slabs too
+        "stretch-k_boot2t": {"boot_tiles": 0, "boot2_rows": 1},
+        "stretch-k_boot2t-redo": {"boot_tiles": 0, "boot2_rows": 1, "skip_slack": -45.0},
         # the tables one column per wave, and in 64- and 16-column tasks
         "tables-single": {"tables_pair": 0},
         "tables-tasks64": {"task_cols": 64},
@@ -173,7 +173,7 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         else:
             assert stats["skip_slabs"] > 0 and stats["skip_kept"] < stats["skip_stretches"], (name, stats)
             assert stats["boot_path"] == (0 if name.startswith("stretch") else 1), (name, stats)
-        if name.endswith("forced-redo") or name == "stretch-k_boot2-redo":
+        if name.endswith("forced-redo") or name == "stretch-k_boot2t-redo":
             assert stats["skip_redo"] > 0, stats  # the second-chance path really adds work
         g = got[name]
         for i in range(2):
@@ -188,13 +188,13 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
     # skipping leaves out only terms the e^-50 cut zeroes anyway: the outputs are identical
     for base, others in (("tiles", ("noskip", "tiles-forced-redo", "tiles-slab-waves", "tiles-slab-waves-redo",
                                     "gene-forced-list", "gene-list-overflow", "gene-list-overflow-odd", "gene-3waves", "gene-4waves", "gene-chunks",
-                                    "tiles-unordered", "unique-exact", "unfused", "one-lane", "rest-inline",
+                                    "tiles-unordered", "unique-exact", "fused", "one-lane", "rest-inline",
                                     "fused-pipelined", "fused-pipelined-staged", "pipelined-pieces",
                                     "pipelined-one-lane", "pipelined-deferred", "pipelined-staged", "pipelined-thread",
                                     "pipelined-thread-seq",
                                     "tiles-pairs",
                                     "tiles-pairs-redo", "tiles-mult-fallback", "stretch", "stretch-forced-redo",
-                                    "stretch-k_boot2", "stretch-k_boot2-redo", "tables-single", "tables-tasks64",
+                                    "stretch-k_boot2t", "stretch-k_boot2t-redo", "tables-single", "tables-tasks64",
                                     "tables-tasks16")),):
         for name in others:
             for i in range(2):
@@ -220,12 +220,12 @@ def test_threaded_lane_group_layouts(api, layout):
     else:
         groups = np.random.default_rng(5).permutation(groups)
     prior = expression_prior(models, counts, length_out=400)
-    base, _ = _run(api, {"fuse_groups": 0}, models, counts, prior, groups, 30, 1)
-    runs = {"lane-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1, "fuse_groups": 0},
+    base, _ = _run(api, {}, models, counts, prior, groups, 30, 1)
+    runs = {"lane-thread": {"pipeline_mb": 0, "pieces": 3, "lane_thread": 1},
             # fused groups: reversed = the second group's cells first (its rows lead the fused list);
             # mixed = no separable ranges (one upload range before the unique sets)
-            "fused-pipelined": {"pipeline_mb": 0, "pieces": 3},
-            "fused": {}}
+            "fused-pipelined": {"pipeline_mb": 0, "pieces": 3, "fuse_groups": 1},
+            "fused": {"fuse_groups": 1}}
     bad = []
     for name, opts in runs.items():
         got, _ = _run(api, opts, models, counts, prior, groups, 30, 1)
