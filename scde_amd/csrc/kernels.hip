@@ -2283,6 +2283,10 @@ __device__ __forceinline__ void tile_bound_pass(const int2* __restrict__ E, int 
     const uint4 q0 = uq[0], q1 = uq[1], q2 = uq[2], q3 = uq[3];
     const uint4* wp = reinterpret_cast<const uint4*>(W8 + (unsigned)(en.x * cstride));
     const uint4 w0 = wp[0], w1 = wp[1];
+    if (SCDE_TILE_DIAG & 128) {  // timing build: the chunk's loads only (results wrong)
+      acc[0][0][0] += (int)(q0.x ^ q1.y ^ q2.z ^ q3.w ^ w0.x ^ w1.w);
+      continue;
+    }
     wave_sync();  // the previous chunk's fragment reads are done before the area is rewritten
     const unsigned qv[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
                              q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
@@ -2322,8 +2326,13 @@ __device__ __forceinline__ void tile_bound_pass(const int2* __restrict__ E, int 
 #pragma unroll
     for (int l = 0; l < 4; ++l) {
       const i32x4 bf = {(int)pl[l][0], (int)pl[l][1], (int)pl[l][2], (int)pl[l][3]};
-      acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
-      acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
+      if (SCDE_TILE_DIAG & 256) {  // timing build: loads and LDS staging, no MFMA (results wrong)
+        acc[0][l][0] += bf[0] ^ af[0][1];
+        acc[1][l][1] += bf[2] ^ af[1][3];
+      } else {
+        acc[0][l] = mfma_i8(af[0], bf, acc[0][l]);
+        acc[1][l] = mfma_i8(af[1], bf, acc[1][l]);
+      }
     }
   }
   if (t < NTB)
