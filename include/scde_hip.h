@@ -130,8 +130,10 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "tile_max_mult" the largest draw multiplicity the tile path takes (default 127, the int8 bound
  *                   operand; a call with a larger one runs plain k_boot2 on the same columns --
  *                   tests force that fallback with a small value)
- *   "tile_order"    1/0  k_boot_tiles takes the genes in order of their count sums, so waves in
- *                   flight share columns and tiles in L2 (default 1; results are the same)
+ *   "tile_order"    0..3  the tile bootstrap takes the genes in order of their count-rank sums,
+ *                   so waves in flight share columns and tiles in L2: 1 ascending, 2 descending
+ *                   (heaviest genes first: a shorter tail), 3 (default) descending for launches
+ *                   of at most 8,192 genes and ascending above, 0 gene order; results are the same
  *   "unique_fixed"  1/0  build each call's unique count tables with one host sync (fixed
  *                   1024-word bitmaps per cell, counts below 65,536; a set with another count is
  *                   rebuilt with exact widths); default 1
@@ -143,8 +145,13 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   or one wave per slab with four tiles (k_boot_tiles); results are the same
  *   "gene_rows"     1..4 rows per slab k_boot_gene gives each slab at most (default 4; tests force
  *                   its four-tile list pass with fewer)
- *   "modes_overlap" 1/0  scde.posteriors' posterior-mode read-back overlaps the bootstrap on the
- *                   copy stream (default 1), or follows it on the main stream (rocprofv3 runs)
+ *   "modes_overlap" 1/0  scde.posteriors' read-backs run on a read-back thread beside the device
+ *                   work (default 1): the modes piece by piece as each piece's tables finish, the
+ *                   joint posterior in gene chunks of the bootstrap; 0: both after the bootstrap on
+ *                   the main stream (rocprofv3 runs); results are the same
+ *   "jp_chunks"     1..64 gene chunks of scde.posteriors' gene-block bootstrap (default 4, at most
+ *                   one per 256 genes): each chunk finishes before the next starts and its joint
+ *                   posterior rows are read back while the next runs; results are the same
  *   "lanes"         2/1  a DE call's second group runs on a peer context (its own streams and
  *                   workspace, same device) beside the first (default 2), or after it (1; bench's
  *                   per-stage timing pass and the rocprof runs use 1); results are the same.
@@ -171,6 +178,10 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   cell of the second group follows the first group's cells)
  *   "upload_staged" 1/0  host counts go up through a pinned ring filled by "upload_threads"
  *                   copy threads instead of pageable copies (default 0: measured no faster)
+ *   "upload_u16"    1/0  host-count ranges of 8 MB or more go up as 16-bit counts: narrowed by
+ *                   "upload_threads" threads (default 4) into a pinned ring, widened on the device
+ *                   (default 1; half the PCIe bytes); a range holding a count outside [0, 65535]
+ *                   goes up as int32; results are the same
  *   "gene_waves"    3/4  k_boot_gene's waves per block (12 or 16 rows); 0 (default) = 3 from
  *                   "gene3_cells" cells per call (default: never; slower at config 4), else 4
  *   "gene_list_cap" slabs k_boot_gene's four-tile list pass takes (0 = 16384; beyond: k_boot2)

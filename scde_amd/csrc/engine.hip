@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <thread>
 #include <atomic>
@@ -262,7 +263,7 @@ struct scde_ctx {
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, w8g, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
-  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide;
+  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide, ellw, excd;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 20 + 0.15 C); tests force redo slabs
@@ -277,15 +278,24 @@ struct scde_ctx {
   int opt_tile_groups = 4;       // "tile_groups": 32-point bound tiles k_boot_tiles computes per slab (1..4)
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
-  int opt_tile_order = 1;        // "tile_order": k_boot_tiles takes genes by count sum (cache sharing)
+  int opt_tile_order = 3;        // "tile_order": the tile bootstrap takes genes by count-rank sum (cache sharing):
+                                 // 1 ascending, 2 descending (heaviest first), 3 by size (default: descending for
+                                 // launches of at most kDescGenes genes, where the last, heaviest blocks would
+                                 // set the launch's tail), 0 in gene order
   int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
   int opt_gene_blocks = 1;       // "gene_blocks": k_boot_gene (a 4-wave block per gene's slab group, rows shared
                                  // by its slabs) instead of one k_boot_tiles wave per slab; not with pair mode
   int opt_upload_staged = 0;     // "upload_staged": host-count uploads through a pinned ring filled by copy threads
-  int opt_upload_threads = 8;    // "upload_threads": threads filling a staging slot (the upload worker included)
-  int opt_modes_overlap = 1;     // "modes_overlap": scde.posteriors' posterior-mode read-back overlaps the bootstrap
-                                 // on the copy stream (0: after it, on the main stream -- rocprofv3 runs, where the
-                                 // pageable read-back becomes blit kernels that would share the CUs)
+  int opt_upload_threads = 4;     // "upload_threads": threads filling a staging slot (staged: the upload worker
+                                 // included; 16-bit: the narrowing pool)
+  int opt_upload_u16 = 1;        // "upload_u16": host-count ranges of >= 8 MB go up as 16-bit counts (U16Ring)
+  int opt_modes_overlap = 1;     // "modes_overlap": scde.posteriors' read-backs (modes piece by piece, jp in gene
+                                 // chunks) overlap the tables and the bootstrap from a read-back thread (0: after
+                                 // the bootstrap, on the main stream -- rocprofv3 runs, where the pageable
+                                 // read-back becomes blit kernels that would share the CUs)
+  int opt_ell_chunks = 0;        // "ell_chunks": at most this many cell chunks in the ELL build (0: by size)
+  int opt_jp_chunks = 4;         // "jp_chunks": gene chunks of scde.posteriors' gene-block bootstrap, each chunk's
+                                 // jp rows read back while the next runs (1: one launch, jp after it)
   int opt_gene_waves = 0;        // "gene_waves": k_boot_gene's waves per block, 3 or 4 (0: by gene3_cells)
   int opt_gene3_cells = 1 << 30;  // "gene3_cells": cells per call from which k_boot_gene runs 3-wave blocks (off:
                                   // config 4 measured 12.85 ms of bootstrap per step with them vs 10.24 with 4)
@@ -344,6 +354,28 @@ struct scde_ctx {
     int nranges = 0, issued = 0, err = 0;
     std::string err_msg;  // the worker thread's error text (its g_err is its own)
   } upl;
+  // Device -> host read-backs from a worker thread (a pageable hipMemcpy blocks its calling thread
+  // for the whole transfer): scde.posteriors' modes columns piece by piece and its jp rows chunk by
+  // chunk, each after the event recorded when its kernels were queued, so the read-back streams
+  // out while later pieces' tables and chunks' bootstraps run.  Jobs of one call; dnl_wait drains.
+  struct Downloader {
+    struct Job {
+      int ev;  // index into evs
+      void* dst;
+      const void* src;
+      size_t dpitch, spitch, width, height;
+    };
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv, cvd;
+    std::deque<Job> q;
+    std::vector<hipEvent_t> evs;
+    hipStream_t stream = nullptr;
+    int pending = 0, err = 0, nev = 0;
+    std::string err_msg;
+    bool stop = false;
+    bool hold = false;  // jobs queue but wait (dnl_hold): pageable read-backs slow the host-count uploads
+  } dnl;
   // Pinned staging for the host-count uploads (option "upload_staged"): the upload worker copies
   // each chunk of the caller's pageable matrix into a pinned ring slot with T pool threads (it
   // takes one share itself), then issues the DMA from the slot; a slot is reused once its DMA's
@@ -365,6 +397,41 @@ struct scde_ctx {
     char* dst = nullptr;
     size_t n = 0;
   } stg;
+  // 16-bit host-count uploads (option "upload_u16"): a pool of T threads narrows each 4M-count
+  // slot of the caller's int32 matrix to uint16 into a pinned ring slot, listing the counts
+  // outside [0, 65535] (index, value) as they go; the upload worker sends the slot up, a widening
+  // kernel writes the int32 counts behind it on the copy stream and a patch kernel the listed
+  // ones (real matrices hold a few: config 4's synthetic 60M counts hold 10) -- half the PCIe bytes (tools/micro/h2d_u16.hip, 240 MB of counts: 2.9 ms
+  // against 4.5 ms pageable).  Slots carry a global sequence number q (ring slot q % kRing); the
+  // threads may write slot q once q < free_upto, i.e. once slot q - kRing's DMA has completed.
+  // Every wait blocks (condition variables, blocking-sync events): spinning threads would eat the
+  // process's CPU share that the caller's thread and the lanes' threads need.
+  struct U16Ring {
+    static constexpr int kRing = 4;
+    static constexpr size_t kSlotCounts = size_t(4) << 20;
+    unsigned short* pin = nullptr;  // kRing slots
+    unsigned short* dev = nullptr;  // kRing device slots (widened from)
+    hipEvent_t ev[kRing] = {};
+    long long seq = 0;     // next sequence number
+    long long issued = 0;  // slots whose DMA is queued
+    long long free_upto = kRing;  // (under m, as fin and abort)
+    int fin[kRing] = {};
+    static constexpr int kMaxT = 32;
+    std::vector<int2> exc[kRing][kMaxT];  // per ring slot and thread: (index in the slot, count)
+    std::vector<int2> exc_all;            // one slot's list, uploaded
+    bool abort = false;
+    std::vector<std::thread> th;
+    int T = 0;
+    std::mutex m;
+    std::condition_variable cv, cvd, cvf;  // job / job done, slot freed / slot narrowed
+    long long job = 0;
+    int busy = 0;
+    bool stop = false;
+    const int* src = nullptr;
+    size_t n = 0;
+    long long q0 = 0;
+    int nslots = 0;
+  } u16;
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
   // host wall time of scde_expression_difference_{dev,host} phases (ms, summed over calls):
@@ -503,6 +570,16 @@ struct scde_ctx {
       stg.cv.notify_all();
       for (auto& t : stg.th) t.join();
     }
+    if (dnl.th.joinable()) {
+      {
+        std::lock_guard<std::mutex> lk(dnl.m);
+        dnl.stop = true;
+      }
+      dnl.cv.notify_all();
+      dnl.th.join();
+    }
+    for (auto e : dnl.evs) (void)hipEventDestroy(e);
+    if (dnl.stream) (void)hipStreamDestroy(dnl.stream);
     if (upl.th.joinable()) {
       {
         std::lock_guard<std::mutex> lk(upl.m);
@@ -511,6 +588,18 @@ struct scde_ctx {
       upl.cv.notify_all();
       upl.th.join();
     }
+    if (!u16.th.empty()) {  // (after the upload worker, its only user)
+      {
+        std::lock_guard<std::mutex> lk(u16.m);
+        u16.stop = true;
+      }
+      u16.cv.notify_all();
+      for (auto& t : u16.th) t.join();
+    }
+    if (u16.pin) (void)hipHostFree(u16.pin);
+    if (u16.dev) (void)hipFree(u16.dev);
+    for (auto& e : u16.ev)
+      if (e) (void)hipEventDestroy(e);
     if (peer) {
       (void)hipStreamSynchronize(peer->stream);
       delete peer;
@@ -530,7 +619,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide};
+                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide,  &ellw,  &excd};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (auto& u : upc) u.release();
@@ -556,6 +645,75 @@ struct scde_ctx {
       if (e) (void)hipEventDestroy(e);
   }
 };
+
+// Downloader: queue a read-back of `height` rows of `width` bytes (pitches in bytes) after the work
+// queued so far on `after`; dnl_wait returns once every queued read-back has landed (or failed).
+int dnl_push(scde_ctx* cx, hipStream_t after, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
+             size_t height) {
+  auto& d = cx->dnl;
+  if (!d.th.joinable()) {
+    HCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    d.th = std::thread([cx] {
+      auto& q = cx->dnl;
+      (void)hipSetDevice(cx->device);
+      std::unique_lock<std::mutex> lk(q.m);
+      for (;;) {
+        q.cv.wait(lk, [&] { return q.stop || (!q.q.empty() && !q.hold); });
+        if (q.stop) return;
+        const scde_ctx::Downloader::Job j = q.q.front();
+        q.q.pop_front();
+        const hipEvent_t ev = q.evs[j.ev];
+        lk.unlock();
+        hipError_t e = hipEventSynchronize(ev);
+        if (e == hipSuccess)
+          e = hipMemcpy2DAsync(j.dst, j.dpitch, j.src, j.spitch, j.width, j.height, hipMemcpyDeviceToHost, q.stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(q.stream);
+        lk.lock();
+        if (e != hipSuccess && !q.err) {
+          q.err = SCDE_EHIP;
+          q.err_msg = hipGetErrorString(e);
+        }
+        if (--q.pending == 0) q.cvd.notify_all();
+      }
+    });
+  }
+  std::lock_guard<std::mutex> lk(d.m);
+  if (d.nev == (int)d.evs.size()) {  // one event per job of a call (reused once dnl_wait drained them)
+    hipEvent_t e = nullptr;
+    HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    d.evs.push_back(e);
+  }
+  const int ei = d.nev++;
+  HCHK(hipEventRecord(d.evs[ei], after));
+  d.q.push_back({ei, dst, src, dpitch, spitch, width, height});
+  ++d.pending;
+  d.cv.notify_all();
+  return SCDE_OK;
+}
+
+// hold queued read-backs back (on) or let them run (off)
+void dnl_hold(scde_ctx* cx, bool on) {
+  auto& d = cx->dnl;
+  {
+    std::lock_guard<std::mutex> lk(d.m);
+    d.hold = on;
+  }
+  d.cv.notify_all();
+}
+
+int dnl_wait(scde_ctx* cx) {
+  auto& d = cx->dnl;
+  dnl_hold(cx, false);
+  std::unique_lock<std::mutex> lk(d.m);
+  d.cvd.wait(lk, [&] { return d.pending == 0; });
+  d.nev = 0;
+  const int err = d.err;
+  const std::string msg = d.err_msg;
+  d.err = 0;
+  d.err_msg.clear();
+  lk.unlock();
+  return err ? fail(err, "read-back failed: %s", msg.c_str()) : SCDE_OK;
+}
 
 // every stream of the context that touches its workspace (grow(keep) drains these, not the device)
 hipError_t ctx_streams_sync(scde_ctx* cx) {
@@ -624,6 +782,14 @@ struct PostSpec {
   int ngroups = 1;
   int gsplit = 0;
   int nsets_g = 0;
+  // host destinations read back by the context's Downloader while later work runs (the caller then
+  // copies neither and drains the Downloader before returning): modes_host, the modes matrix
+  // (pieces: each piece's columns once its tables are done); jp_host, the joint posterior in R's
+  // layout (jp_g = 1, jp_k = ngenes) -- with the gene-block bootstrap in jp_chunks gene chunks, each
+  // chunk's rows read back while the next chunk's bootstrap runs
+  double* modes_host = nullptr;
+  double* jp_host = nullptr;
+  int jp_chunks = 1;
 };
 
 constexpr size_t kPinCap = size_t(16) << 20;  // the arena
@@ -1180,6 +1346,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     HCHK(cx->zcol.ensure(sizeof(int) * std::max(1, C)));
   }
   bool tables_done = false;
+  const bool want_modes = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
+  const bool modes_pieces = pieces && want_modes && s.modes && s.modes_host && N > 0;
   if (pieces) {
     // piece j: cells [piece_c[j], piece_c[j+1]) of this spec; its unique sets are built (on
     // the copy stream, beside the previous piece's tables) into u's arrays at the running
@@ -1190,6 +1358,9 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     int jlast = 0;
     for (int j = 0; j < s.npieces; ++j)
       if (s.piece_c[j + 1] > s.piece_c[j]) jlast = j;
+    // the pieces' modes read-backs start once every piece's counts are up: run beside the uploads,
+    // the pageable read-backs held them back (config 4: ~1 ms per 120 MB read-back)
+    if (modes_pieces) dnl_hold(cx, true);
     using pclock = std::chrono::steady_clock;
     auto pms = [](pclock::time_point a, pclock::time_point b) {
       return std::chrono::duration<double, std::milli>(b - a).count();
@@ -1198,6 +1369,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       const int c0 = s.piece_c[j], c1 = s.piece_c[j + 1];
       const auto tw = pclock::now();
       RCHK(s.piece_ready(j));
+      if (j == jlast && modes_pieces) dnl_hold(cx, false);  // (every piece's counts are up)
       const auto th = pclock::now();
       cx->st_piece_wait_ms += pms(tw, th);
       struct Lap {
@@ -1239,6 +1411,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       const long long est = std::max<long long>(col0 + nc, (long long)((double)(col0 + nc) / c1 * C * 1.1));
       RCHK(setup_tables(plan0, est, j > 0));
       RCHK(launch_tables_range(plan0, c0, c1, col0, pu.ucl_off.as<long long>(), pu.ucl_off_h, j == jlast, pu));
+      if (modes_pieces) {  // the piece's posterior modes, read back while the next pieces' tables run
+        HCHK(launch_modes(u.uci.as<int>() + (size_t)N * c0, N, N, c1 - c0, pu.ucl_off.as<long long>(),
+                          cx->maxi.as<int>() + col0, cx->mag.as<double>(), s.modes + (size_t)N * c0, 1, N, st));
+        const size_t bytes = sizeof(double) * (size_t)N * (c1 - c0);
+        RCHK(dnl_push(cx, st, s.modes_host + (size_t)N * c0, bytes, s.modes + (size_t)N * c0, bytes, bytes, 1));
+      }
       col0 += nc;
     }
     ta.ucl_off = u.ucl_off.as<long long>();
@@ -1286,14 +1464,20 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   auto rest_fn = [=, &s, &u]() mutable -> int {
   // ---- individual posterior modes (src/jpmatLogBoot.cpp:277-296): argmax of each cell's table
   // column, known as soon as the tables are; computed here so the caller's read-back of the
-  // (ngenes x ncells) matrix overlaps the bootstrap
-  const bool want_modes = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
-  if (want_modes && s.modes && s.modes_early) {
+  // (ngenes x ncells) matrix overlaps the bootstrap (pieces with modes_host: done piece by piece)
+  if (want_modes && s.modes && s.modes_early && !modes_pieces) {
     HCHK(launch_modes(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->maxi.as<int>(),
                       cx->mag.as<double>(), s.modes, 1, N, st));
-    if (!cx->modes_ev) HCHK(hipEventCreateWithFlags(&cx->modes_ev, hipEventDisableTiming));
-    HCHK(hipEventRecord(cx->modes_ev, st));
+    if (s.modes_host) {
+      const size_t bytes = sizeof(double) * (size_t)N * C;
+      RCHK(dnl_push(cx, st, s.modes_host, bytes, s.modes, bytes, bytes, 1));
+    } else {
+      if (!cx->modes_ev) HCHK(hipEventCreateWithFlags(&cx->modes_ev, hipEventDisableTiming));
+      HCHK(hipEventRecord(cx->modes_ev, st));
+    }
   }
+  // jp read back in gene chunks (the gene-block bootstrap below), else once at the end
+  bool jp_sent = false;
   // fused (fast) path: the draw lists here, the multiplicity arrays on the device (launch_mult)
   const bool dev_mult = fused && C <= kMultMaxCells;
   if (fused && s.nboot > 0) {
@@ -1350,33 +1534,52 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     }
     // the baseline columns: T (slow path) or the fused D buffer, which holds T there
     const double* Tbase = fused ? cx->E.as<double>() : cx->T.as<double>();
-    // ELL rows (fused groups: group B's genes after group A's, over B's cells, cells offset by gsplit)
-    for (int gi = 0; gi < (two ? 2 : 1); ++gi) {
-      const int c0 = gi ? s.gsplit : 0, nc = two ? (gi ? C - s.gsplit : s.gsplit) : C;
-      HCHK(launch_ell(u.uci.as<int>() + (size_t)N * c0, N, N, nc, u.ucl_off.as<long long>() + c0,
-                      cx->base_col.as<int>() + c0, stride, (int)ncols, tpath ? 64 : 8,
-                      cx->ent.as<int2>() + (size_t)gi * N * stride, cx->nnz.as<int>() + (size_t)gi * N, sa, c0));
-    }
-    // tile path: genes in order of their count sums (waves in flight share columns in L2)
-    const bool have_order = tpath && fast && cx->opt_tile_order && NBg > 1;
-    if (have_order) {
-      HCHK(cx->gkey.ensure(sizeof(unsigned) * NBg));
-      HCHK(cx->gkey2.ensure(sizeof(unsigned) * NBg));
-      HCHK(cx->gidx.ensure(sizeof(int) * NBg));
-      HCHK(cx->gorder.ensure(sizeof(int) * NBg));
-      size_t wb = 0;
-      HCHK(launch_gene_order(nullptr, nullptr, NBg, nullptr, nullptr, nullptr, &wb, sa));
-      HCHK(cx->gwork.ensure(std::max<size_t>(wb, 1)));
-      HCHK(launch_gene_key(cx->ent.as<int2>(), cx->nnz.as<int>(), stride, u.ucl.as<int>(), NBg,
-                           cx->gkey.as<unsigned>(), cx->gidx.as<int>(), sa));
-      HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), NBg, cx->gkey2.as<unsigned>(),
-                             cx->gorder.as<int>(), cx->gwork.p, &wb, sa));
-    }
     // k_boot_gene (not with pair mode): groups of gene_sg slabs per 4-wave block
     // k_boot_gene (gene_blocks, the default at every cell count the tile path runs; measured against
     // pair mode at config 4: bootstrap 11.16 -> 9.94 ms per step) or, without it, k_boot_tiles'
     // wave per slab (pair mode from pair_cells)
     const int gene_sg = (tpath && cx->opt_gene_blocks) ? std::min({(s.nboot + nb - 1) / nb, 8, 128 / nb}) : 0;
+    // gene chunks (jp_host): the bootstrap over genes [gch(k), gch(k + 1)) finishes (list pass,
+    // fallback, slab sums, exact rows) before chunk k + 1 starts, and chunk k's jp rows go back to
+    // the host while it runs -- the read-back of the last chunk only is left after the bootstrap
+    const int nchunks = (s.jp_host && !two && gene_sg > 0 && s.jp_g == 1 && s.jp_k == N)
+                            ? std::max(1, std::min(cx->opt_jp_chunks, NBg / 256 + 1)) : 1;
+    auto gch = [NBg, nchunks](int k) { return (int)((long long)NBg * k / nchunks); };
+    // tile path: genes in order of their count-rank sums (waves in flight share columns in L2), keyed by
+    // the ELL builder; with gene chunks each chunk's genes in order among themselves (the chunk
+    // index in the keys' top bits: one sort)
+    const bool have_order = tpath && fast && cx->opt_tile_order && NBg > 1;
+    // descending (heaviest genes first, shorter tail) for small launches; ascending for large ones.
+    // Measured (bootstrap ms per step, ascending -> descending): config 4's 7,500-gene chunks 10.59
+    // -> 9.77, config 3's shard of 8 (2,500 genes per lane) 0.70 -> 0.63, config 3 (20,000 genes
+    // per lane) 3.95 -> 4.09
+    constexpr int kDescGenes = 8192;
+    const int order_desc =
+        cx->opt_tile_order == 2 || (cx->opt_tile_order == 3 && (NBg + nchunks - 1) / nchunks <= kDescGenes);
+    if (have_order) {
+      HCHK(cx->gkey.ensure(sizeof(unsigned) * NBg));
+      HCHK(cx->gkey2.ensure(sizeof(unsigned) * NBg));
+      HCHK(cx->gidx.ensure(sizeof(int) * NBg));
+      HCHK(cx->gorder.ensure(sizeof(int) * NBg));
+    }
+    // ELL rows (fused groups: group B's genes after group A's, over B's cells, cells offset by gsplit)
+    for (int gi = 0; gi < (two ? 2 : 1); ++gi) {
+      const int c0 = gi ? s.gsplit : 0, nc = two ? (gi ? C - s.gsplit : s.gsplit) : C;
+      HCHK(cx->ellw.ensure(std::max<size_t>(1, ell_work_bytes(N, nc, cx->opt_ell_chunks))));
+      HCHK(launch_ell(u.uci.as<int>() + (size_t)N * c0, N, N, nc, u.ucl_off.as<long long>() + c0,
+                      cx->base_col.as<int>() + c0, stride, (int)ncols, tpath ? 64 : 8,
+                      cx->ent.as<int2>() + (size_t)gi * N * stride, cx->nnz.as<int>() + (size_t)gi * N, sa, c0,
+                      cx->ellw.p, have_order ? cx->gkey.as<unsigned>() + (size_t)gi * N : nullptr,
+                      have_order ? cx->gidx.as<int>() + (size_t)gi * N : nullptr, gi * N, NBg, nchunks,
+                      order_desc, cx->opt_ell_chunks));
+    }
+    if (have_order) {
+      size_t wb = 0;
+      HCHK(launch_gene_order(nullptr, nullptr, NBg, nullptr, nullptr, nullptr, &wb, sa));
+      HCHK(cx->gwork.ensure(std::max<size_t>(wb, 1)));
+      HCHK(launch_gene_order(cx->gkey.as<unsigned>(), cx->gidx.as<int>(), NBg, cx->gkey2.as<unsigned>(),
+                             cx->gorder.as<int>(), cx->gwork.p, &wb, sa));
+    }
     if (dev_mult) {
       // the multiplicity arrays from the uploaded draw lists, on the device (host loops over
       // sets x cells x boots and their uploads cost ~0.1-0.4 ms of host time per posterior)
@@ -1460,6 +1663,34 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     }
     const int* wset_d = nsets > 1 ? cx->wset.as<int>() : nullptr;
     const double thresh = 16777216.0;  // 2^24: beyond this the sums' rounding order matters
+    // rows whose sums left the exact range, in the reference's order (genes [g_lo, g_hi))
+    bool exact_done = false;
+    auto boot_exact = [&](int g_lo, int g_hi) -> int {
+      ExactArgs xa{};
+      xa.T = fused ? cx->E.as<double>() : cx->T.as<double>();
+      xa.base_col = fused ? cx->base_col.as<int>() : nullptr;
+      xa.G = G;
+      xa.GS = GS;
+      xa.draws = cx->draws.as<int>();
+      xa.ndraw = ndraw;
+      xa.nboot = s.nboot;
+      xa.wset = wset_d;
+      xa.ucl_off = u.ucl_off.as<long long>();
+      xa.uci = u.uci.as<int>();
+      xa.ld_uci = N;
+      xa.norm_mult = (double)s.nboot;
+      xa.degen = cx->degen.as<int>();
+      xa.out = s.jp;
+      xa.out_g = s.jp_g;
+      xa.out_k = s.jp_k;
+      xa.ngenes = NBg;
+      xa.gene_mod = two ? N : 0;
+      xa.g_lo = g_lo;
+      xa.g_hi = g_hi;
+      HCHK(launch_boot_exact(xa, st));
+      exact_done = true;
+      return SCDE_OK;
+    };
     ev = cx->mark_begin(SLOT_BOOT);
     if (fast) {
       Boot2Args b2{};
@@ -1537,7 +1768,21 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           tb.chunks = std::max(1, cx->opt_boot_chunks);
         }
         if (have_order) tb.order = cx->gorder.as<int>();
-        HCHK(launch_boot_tiles(b2, tb, st));
+        if (nchunks > 1) {
+          for (int k = 0; k < nchunks; ++k) {
+            tb.g_lo = gch(k);
+            tb.g_hi = gch(k + 1);
+            HCHK(launch_boot_tiles(b2, tb, st));
+            RCHK(boot_exact(tb.g_lo, tb.g_hi));
+            // chunk k's rows of the ngenes x ngrid column-major jp
+            const size_t pitch = sizeof(double) * N;
+            RCHK(dnl_push(cx, st, s.jp_host + tb.g_lo, pitch, s.jp + tb.g_lo, pitch,
+                          sizeof(double) * (tb.g_hi - tb.g_lo), G));
+          }
+          jp_sent = true;
+        } else {
+          HCHK(launch_boot_tiles(b2, tb, st));
+        }
         if (cx->opt_skip_stats) {
           int h[40];
           HCHK(hipMemcpyAsync(h, cx->qflags.p, sizeof(int) * 40, hipMemcpyDeviceToHost, st));
@@ -1600,31 +1845,22 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       HCHK(launch_boot(ba, st));
     }
     cx->mark_end(SLOT_BOOT, ev);
-    ExactArgs xa{};
-    xa.T = Tbase;
-    xa.base_col = fused ? cx->base_col.as<int>() : nullptr;
-    xa.G = G;
-    xa.GS = GS;
-    xa.draws = cx->draws.as<int>();
-    xa.ndraw = ndraw;
-    xa.nboot = s.nboot;
-    xa.wset = wset_d;
-    xa.ucl_off = u.ucl_off.as<long long>();
-    xa.uci = u.uci.as<int>();
-    xa.ld_uci = N;
-    xa.norm_mult = (double)s.nboot;
-    xa.degen = cx->degen.as<int>();
-    xa.out = s.jp;
-    xa.out_g = s.jp_g;
-    xa.out_k = s.jp_k;
-    xa.ngenes = NBg;
-    xa.gene_mod = two ? N : 0;
-    HCHK(launch_boot_exact(xa, st));
+    if (!exact_done) RCHK(boot_exact(0, NBg));
+  }
+  if (s.jp_host && !jp_sent) {
+    if (s.jp_g != 1 || s.jp_k != N) return fail(SCDE_EINTERNAL, "jp_host: jp not in R layout");
+    const size_t bytes = sizeof(double) * (size_t)N * G;
+    if (bytes) RCHK(dnl_push(cx, st, s.jp_host, bytes, s.jp, bytes, bytes, 1));
   }
   // ---- individual outputs (src/jpmatLogBoot.cpp:277-328)
-  if (want_modes && s.modes && !s.modes_early)
+  if (want_modes && s.modes && !s.modes_early) {
     HCHK(launch_modes(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->maxi.as<int>(),
                       cx->mag.as<double>(), s.modes, 1, N, st));
+    if (s.modes_host) {
+      const size_t bytes = sizeof(double) * (size_t)N * C;
+      RCHK(dnl_push(cx, st, s.modes_host, bytes, s.modes, bytes, bytes, 1));
+    }
+  }
   if (want_post && s.post)
     for (int c = 0; c < C; ++c)
       HCHK(launch_post(u.uci.as<int>(), N, N, c, u.ucl_off.as<long long>(), cx->T.as<double>(), G, GS,
@@ -1862,11 +2098,14 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "boot_tiles_cells") ctx->opt_boot_tiles_cells = (int)value;
   else if (n == "tile_groups") ctx->opt_tile_groups = (int)value;
   else if (n == "tile_max_mult") ctx->opt_tile_max_mult = (int)value;
-  else if (n == "tile_order") ctx->opt_tile_order = value != 0;
+  else if (n == "tile_order") ctx->opt_tile_order = (value >= 1 && value <= 3) ? (int)value : 0;
   else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
   else if (n == "gene_blocks") ctx->opt_gene_blocks = value != 0;
   else if (n == "modes_overlap") ctx->opt_modes_overlap = value != 0;
+  else if (n == "ell_chunks") ctx->opt_ell_chunks = std::max(0, std::min(64, (int)value));
+  else if (n == "jp_chunks") ctx->opt_jp_chunks = std::max(1, std::min(64, (int)value));
   else if (n == "upload_staged") ctx->opt_upload_staged = value != 0;
+  else if (n == "upload_u16") ctx->opt_upload_u16 = value != 0;
   else if (n == "upload_threads") ctx->opt_upload_threads = std::max(1, std::min(32, (int)value));
   else if (n == "gene_waves") ctx->opt_gene_waves = (value == 3 || value == 4) ? (int)value : 0;
   else if (n == "gene3_cells") ctx->opt_gene3_cells = (int)value;
@@ -2372,9 +2611,157 @@ static int upload_cols_staged(scde_ctx* ctx, const HostUpload& h, int lo, int hi
   return SCDE_OK;
 }
 
+// narrow n int32 counts to uint16, appending the counts outside [0, 65535] (negative ones
+// included) to `exc` as (i0 + index, count): blocks of 256 narrowed by a vectorisable loop, a
+// block whose high halves are not all zero scanned again
+static void narrow16(const int* s, unsigned short* d, size_t n, int i0, std::vector<int2>& exc) {
+  for (size_t b0 = 0; b0 < n; b0 += 256) {
+    const size_t e = std::min(n, b0 + 256);
+    unsigned b = 0;
+    for (size_t i = b0; i < e; ++i) {
+      const unsigned v = (unsigned)s[i];
+      b |= v >> 16;
+      d[i] = (unsigned short)v;
+    }
+    if (b)
+      for (size_t i = b0; i < e; ++i)
+        if ((unsigned)s[i] >> 16) exc.push_back(make_int2(i0 + (int)i, s[i]));
+  }
+}
+
+// the narrowing pool's thread t: per job, its share of every slot, in sequence order
+static void u16_thread(scde_ctx* ctx, int t) {
+  auto& r = ctx->u16;
+  using R = scde_ctx::U16Ring;
+  long long seen = 0;
+  std::unique_lock<std::mutex> lk(r.m);
+  for (;;) {
+    r.cv.wait(lk, [&] { return r.stop || r.job != seen; });
+    if (r.stop) return;
+    seen = r.job;
+    const int* src = r.src;
+    const size_t n = r.n;
+    const long long q0 = r.q0;
+    const int nslots = r.nslots, T = r.T;
+    for (int sl = 0; sl < nslots; ++sl) {
+      const long long q = q0 + sl;
+      r.cv.wait(lk, [&] { return r.free_upto > q || r.abort; });
+      if (r.abort) break;
+      lk.unlock();
+      const int k = (int)(q % R::kRing);
+      const size_t off = (size_t)sl * R::kSlotCounts;
+      const size_t m = std::min(R::kSlotCounts, n - off);
+      const size_t a = (m * t / T) & ~size_t(15), e = (t + 1 == T) ? m : ((m * (t + 1) / T) & ~size_t(15));
+      r.exc[k][t].clear();
+      if (e > a) narrow16(src + off + a, r.pin + (size_t)k * R::kSlotCounts + a, e - a, (int)a, r.exc[k][t]);
+      lk.lock();
+      if (++r.fin[k] == T) r.cvf.notify_all();
+    }
+    if (--r.busy == 0) r.cvd.notify_all();
+  }
+}
+
+// columns [lo, hi) of contiguous host counts as 16-bit counts through U16Ring, widened (and the
+// counts outside [0, 65535] patched in) on the copy stream
+static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
+  auto& r = ctx->u16;
+  using R = scde_ctx::U16Ring;
+  if (!r.pin) {
+    HCHK(hipHostMalloc(reinterpret_cast<void**>(&r.pin), sizeof(unsigned short) * R::kRing * R::kSlotCounts,
+                       hipHostMallocDefault));
+    HCHK(hipMalloc(reinterpret_cast<void**>(&r.dev), sizeof(unsigned short) * R::kRing * R::kSlotCounts));
+    for (auto& e : r.ev) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
+  }
+  const int T = std::max(1, std::min(R::kMaxT, ctx->opt_upload_threads));
+  if ((int)r.th.size() != T) {  // (re)build the pool (no job is running: the upload worker is its only user)
+    if (!r.th.empty()) {
+      {
+        std::lock_guard<std::mutex> lk(r.m);
+        r.stop = true;
+      }
+      r.cv.notify_all();
+      for (auto& t : r.th) t.join();
+      r.th.clear();
+      r.stop = false;
+    }
+    {
+      std::lock_guard<std::mutex> lk(r.m);
+      r.T = T;
+    }
+    for (int t = 0; t < T; ++t) r.th.emplace_back(u16_thread, ctx, t);
+  }
+  const size_t n = (size_t)h.ngenes * (size_t)(hi - lo);
+  const int* src = h.counts + (size_t)h.ld * lo;
+  int* dst = static_cast<int*>(ctx->counts_in.p) + (size_t)h.ngenes * lo;
+  const int nslots = (int)((n + R::kSlotCounts - 1) / R::kSlotCounts);
+  const long long q0 = r.seq;
+  std::unique_lock<std::mutex> lk(r.m);
+  r.src = src;
+  r.n = n;
+  r.q0 = q0;
+  r.nslots = nslots;
+  r.abort = false;
+  r.busy = T;
+  ++r.job;
+  r.cv.notify_all();
+  int rc = SCDE_OK;
+  for (int sl = 0; sl < nslots; ++sl) {
+    const long long q = q0 + sl;
+    const int k = (int)(q % R::kRing);
+    r.cvf.wait(lk, [&] { return r.fin[k] == T; });
+    r.fin[k] = 0;
+    lk.unlock();
+    const size_t off = (size_t)sl * R::kSlotCounts;
+    const size_t m = std::min(R::kSlotCounts, n - off);
+    unsigned short* dslot = r.dev + (size_t)k * R::kSlotCounts;
+    hipError_t e = hipMemcpyAsync(dslot, r.pin + (size_t)k * R::kSlotCounts, sizeof(unsigned short) * m,
+                                  hipMemcpyHostToDevice, ctx->copy_stream);
+    if (e == hipSuccess) e = hipEventRecord(r.ev[k], ctx->copy_stream);
+    if (e == hipSuccess) e = launch_widen16(dslot, dst + off, m, ctx->copy_stream);
+    // the slot's counts outside 16 bits (the threads' lists of ring slot k are complete and
+    // untouched until the slot is freed again below)
+    r.exc_all.clear();
+    for (int t = 0; t < T; ++t) r.exc_all.insert(r.exc_all.end(), r.exc[k][t].begin(), r.exc[k][t].end());
+    if (e == hipSuccess && !r.exc_all.empty()) {
+      // (a pageable copy has read the host list when it returns; the patch follows it in stream order)
+      e = ctx->excd.ensure(sizeof(int2) * std::max<size_t>(r.exc_all.size(), 65536));
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->excd.p, r.exc_all.data(), sizeof(int2) * r.exc_all.size(), hipMemcpyHostToDevice,
+                           ctx->copy_stream);
+      if (e == hipSuccess) e = launch_patch32(ctx->excd.as<int2>(), r.exc_all.size(), dst + off, ctx->copy_stream);
+    }
+    r.issued = q + 1;
+    // free the ring slot the threads need next (slot q + 1 reuses slot q + 1 - kRing's): wait for
+    // that DMA, then let them write (only this thread writes free_upto)
+    const long long f = q + 1 - R::kRing;
+    const bool advance = e == hipSuccess && r.free_upto <= q + 1;
+    if (advance && f >= 0) e = hipEventSynchronize(r.ev[f % R::kRing]);
+    lk.lock();
+    if (e != hipSuccess) {
+      rc = fail(SCDE_EHIP, "%s", hipGetErrorString(e));
+      break;
+    }
+    if (advance) {
+      r.free_upto = q + 2;
+      r.cv.notify_all();
+    }
+  }
+  if (rc != SCDE_OK) {
+    r.abort = true;
+    r.cv.notify_all();
+  }
+  r.cvd.wait(lk, [&] { return r.busy == 0; });
+  for (auto& f : r.fin) f = 0;  // (an aborted job leaves partial counts)
+  r.seq = r.issued;             // sequence numbers of slots never issued are reused
+  lk.unlock();
+  return rc;
+}
+
 // columns [lo, hi) of the host counts into counts_in, on the copy stream
 static int upload_cols(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   const size_t row = sizeof(int) * (size_t)h.ngenes;
+  if (hi > lo && ctx->opt_upload_u16 && h.ld == h.ngenes && row * (size_t)(hi - lo) >= (size_t(8) << 20))
+    return upload_cols_u16(ctx, h, lo, hi);
   if (hi > lo && ctx->opt_upload_staged && h.ld == h.ngenes) return upload_cols_staged(ctx, h, lo, hi);
   if (hi > lo) {
     char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
@@ -2577,16 +2964,32 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
       return SCDE_OK;
     };
   }
+  // read-backs from the Downloader thread while the tables and the bootstrap run (modes piece by
+  // piece, jp in gene chunks); every queued read-back has landed before this call returns, on
+  // every return path (they write into the caller's buffers)
+  struct DrainDownloads {
+    scde_ctx* cx;
+    bool on;
+    ~DrainDownloads() {
+      if (on) (void)dnl_wait(cx);
+    }
+  } drain{ctx, ctx->opt_modes_overlap != 0};
+  if (drain.on) {
+    if (s.modes_early) s.modes_host = modes;
+    s.jp_host = jp;
+    s.jp_chunks = ctx->opt_jp_chunks;
+  }
   RCHK(run_posterior(ctx, s, ctx->us[0]));
-  const bool modes_async = s.modes_early && ctx->opt_modes_overlap;
-  if (modes_async) RCHK(copy_modes_out(ctx, modes, s.modes, (size_t)ngenes * ncells_sel));
-  else if (s.modes_early)  // after the bootstrap, on the main stream (profiling runs: no blits beside it)
+  if (s.modes_early && !drain.on)  // after the bootstrap, on the main stream (profiling runs: no blits beside it)
     HCHK(hipMemcpyAsync(modes, s.modes, sizeof(double) * (size_t)ngenes * ncells_sel, hipMemcpyDeviceToHost,
                         ctx->stream));
-  if (NG) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, ctx->stream));
+  if (NG && !drain.on) HCHK(hipMemcpyAsync(jp, s.jp, sizeof(double) * NG, hipMemcpyDeviceToHost, ctx->stream));
   if (want_post && NG)
     HCHK(hipMemcpyAsync(post, s.post, sizeof(double) * NG * ncells_sel, hipMemcpyDeviceToHost, ctx->stream));
-  if (modes_async) HCHK(hipStreamSynchronize(ctx->copy_stream));
+  if (drain.on) {
+    drain.on = false;
+    RCHK(dnl_wait(ctx));
+  }
   return ctx->sync();
 }
 
@@ -2651,6 +3054,8 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_tile_groups = cx->opt_tile_groups;
   p->opt_tile_max_mult = cx->opt_tile_max_mult;
   p->opt_tile_order = cx->opt_tile_order;
+  p->opt_ell_chunks = cx->opt_ell_chunks;
+  p->opt_jp_chunks = cx->opt_jp_chunks;
   p->opt_unique_fixed = cx->opt_unique_fixed;
   p->opt_pair_cells = cx->opt_pair_cells;
   p->opt_gene_blocks = cx->opt_gene_blocks;

@@ -207,11 +207,13 @@ struct TileBootArgs {
   const unsigned char* W8g = nullptr;  // [nsets][ncells][groups][4 windows][32] the group's boots 32 w + j
                                        // as pair slots (boot 32 w + j, 32 w + 16 + j), 0 past its boots
   int chunks = 1;  // k_boot_gene launches the gene blocks are split into (same blocks, same results)
+  // gene blocks only: this launch takes genes [g_lo, g_hi) (g_hi < 0: all) -- a posterior's bootstrap in
+  // gene chunks, each finished (list pass, fallback, slab sums) before the next, so its jp rows can
+  // be read back while the next chunk runs; `order` then holds each chunk's genes sorted within it
+  int g_lo = 0, g_hi = -1;
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
-// gene order for the tile bootstrap: per-gene count sums from the ELL rows, sorted ascending
-hipError_t launch_gene_key(const int2* ent, const int* nnz, int ent_stride, const int* ucl, int ngenes, unsigned* key,
-                           int* idx, hipStream_t s);
+// gene order for the tile bootstrap: the keys launch_ell formed (per-gene count-rank sums), sorted
 hipError_t launch_gene_order(const unsigned* key, const int* idx, int n, unsigned* key_out, int* order, void* work,
                              size_t* work_bytes, hipStream_t s);
 
@@ -232,6 +234,7 @@ struct ExactArgs {
   double* out;
   long long out_g, out_k;
   int ngenes;
+  int g_lo = 0, g_hi = -1;  // the launch's genes [g_lo, g_hi) (g_hi < 0: all): a gene chunk
 };
 
 struct NoBootArgs {
@@ -280,9 +283,21 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 // padto 8: rows padded to a multiple of 8 plus one batch of 8 (k_boot2's look-ahead); 64: to a
 // multiple of 64 plus 8 (k_boot_tiles' bound MFMAs take 64-entry steps)
 // cell_off: added to the cell of every entry (a fused second group's cells follow the first's)
+// work: ell_work_bytes(ngenes, ncells) bytes (null allowed when that is 0) -- the per cell-chunk
+// entry counts and rank sums of the two-pass build.  key (nullable, with idx): the tile
+// bootstrap's gene-order keys (sums of the entries' count ranks) and gene indices, the launch's
+// genes being genes kg0 .. of kgn split into kch gene chunks (the chunk index in the key's top
+// bits; desc: descending within a chunk)
+// out[i] = in[i] for n 16-bit counts
+hipError_t launch_widen16(const unsigned short* in, int* out, size_t n, hipStream_t s);
+// out[exc[i].x] = exc[i].y for n listed counts (indices relative to out)
+hipError_t launch_patch32(const int2* exc, size_t n, int* out, hipStream_t s);
+// max_chunks: at most this many cell chunks (0: as many as fill the chip twice, at most 64)
+size_t ell_work_bytes(int ngenes, int ncells, int max_chunks = 0);
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
                       const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s,
-                      int cell_off = 0);
+                      int cell_off, void* work, unsigned* key = nullptr, int* idx = nullptr,
+                      int kg0 = 0, int kgn = 0, int kch = 1, int desc = 0, int max_chunks = 0);
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
                              int Bp, int nsets, double* Z, hipStream_t s, int gsets = 0, int gsplit = 0);
 // Draw multiplicities on the device from the draw lists draws[nsets][nboot][ndraw] (cell index, -1

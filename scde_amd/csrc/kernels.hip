@@ -1202,68 +1202,137 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
   base_col[c] = bc;
 }
 
-// Per-gene ELL list of explicit (cell, column) entries, cell order ascending; rows
-// have `stride` slots and are padded up to a multiple of 8 with (0, pad_col).
-// One wavefront per gene, lanes over cells: each 64-cell step ballots the cells whose
-// count is not the baseline and writes their (cell, column) pairs contiguously (mbcnt
-// prefix), keeping the cell order.  The row is padded with zero-column entries to a
-// multiple of 8 plus one more batch of 8 (the k_boot2 look-ahead).
 // ELL rows: per gene the (cell, column) pairs of the cells whose column is not the cell's
-// baseline, in cell order, then pad entries (cell 0, the zero column).  A block takes 64
-// genes: each 64-cell chunk of uci (genes fastest, as R lays out the count matrix) is read
-// coalesced into an LDS tile (stride 65 against bank conflicts), then each wave compacts 16
-// genes' rows from it with ballots.
-// 16 waves per 64-gene block (4 genes each): the grid has only ngenes / 64 blocks
+// baseline, in cell order, then pad entries (cell 0, the zero column) to a multiple of 8 plus
+// one look-ahead batch of 8 (k_boot2), or with padto 64 to whole 64-entry steps plus 8 (the tile
+// bootstrap's bounds).  A block takes 64 genes x one chunk of `ccells` cells: each 64-cell step
+// of uci (genes fastest, as R lays out the count matrix) is read coalesced into an LDS tile
+// (stride 65 against bank conflicts), then each wave compacts its 4 genes' entries with ballots
+// (mbcnt prefix, cell order kept).  With nchk > 1 cell chunks a first pass (WRITE = false)
+// counts each (gene, chunk)'s entries and rank sum, and the second writes each chunk's entries
+// after the earlier chunks' (a grid of ngenes / 64 blocks alone left most CUs idle: config 4's
+// 30k x 2000 took 330-420 us in one pass over 32 serial cell steps per block).  The last chunk's
+// block writes the row length, the pad entries and, with `key`, the gene's tile-order key: the
+// sum of its entries' count ranks (uci, the count's index in its cell's ascending unique list;
+// saturated) -- genes of like expression next to each other, so that waves in flight share
+// columns -- under its gene chunk's index in the top bits (kch chunks of the kgn genes, this
+// launch's genes from kg0), descending when `desc` (heaviest genes first within each chunk).
 constexpr int kEllWaves = 16;
+constexpr int kEllMaxChunks = 64;
+template <bool WRITE>
 __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
                                              int ncells, const long long* __restrict__ ucl_off,
                                              const int* __restrict__ base_col, int stride, int pad_col,
-                                             int padto, int2* __restrict__ ent, int* __restrict__ nnz, int cell_off) {
+                                             int padto, int2* __restrict__ ent, int* __restrict__ nnz, int cell_off,
+                                             int ccells, int nchk, unsigned* __restrict__ cnt,
+                                             unsigned* __restrict__ ksum, unsigned* __restrict__ key, int* __restrict__ idx, int kg0, int kgn,
+                                             int kch, int desc) {
   __shared__ int tile[64][65];  // [cell][gene]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int g0 = blockIdx.x * 64;
+  const int g0 = blockIdx.x * 64, cy = blockIdx.y;
+  const int cbeg = cy * ccells, cend = min(ncells, cbeg + ccells);
   constexpr int GPW = 64 / kEllWaves;  // genes per wave
+  const bool want_key = key != nullptr;
   int n[GPW];
+  unsigned long long ks[GPW];  // per lane: its cells' kept count ranks (the key)
 #pragma unroll
-  for (int i = 0; i < GPW; ++i) n[i] = 0;
-  for (int c0 = 0; c0 < ncells; c0 += 64) {
-    __syncthreads();
-    for (int j = wid; j < 64; j += kEllWaves) {  // row j of the tile: cell c0 + j, lanes over genes
-      const int c = c0 + j, g = g0 + lane;
-      tile[j][lane] = (c < ncells && g < ngenes) ? uci[(long long)g + ld_uci * c] : 0;
+  for (int i = 0; i < GPW; ++i) {
+    n[i] = 0;
+    ks[i] = 0;
+    if (WRITE && cy > 0) {  // the earlier chunks' entries come first
+      const int g = g0 + wid * GPW + i;
+      if (g < ngenes)
+        for (int k = 0; k < cy; ++k) n[i] += (int)cnt[(long long)k * ngenes + g];
     }
-    __syncthreads();
+  }
+  // software pipeline: the next 64-cell step's uci rows (this wave's 4 rows of the tile) and
+  // its lane cell's column offset and baseline column are loaded before the current step is
+  // compacted, so each step's loads wait behind the previous step's work, not in front of it
+  constexpr int RPW = 64 / kEllWaves;  // tile rows per wave
+  int pu[RPW];
+  long long poff = 0;
+  int pbc = -1;
+  auto prefetch = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+      const int c = c0 + wid + r * kEllWaves, g = g0 + lane;
+      pu[r] = (c < cend && g < ngenes) ? uci[(long long)g + ld_uci * c] : 0;
+    }
     const int c = c0 + lane;
-    long long off = 0;
-    int bc = -1;
-    if (c < ncells) {
-      off = ucl_off[c];
-      bc = base_col[c];
+    poff = 0;
+    pbc = -1;
+    if (c < cend) {
+      poff = ucl_off[c];
+      pbc = base_col[c];
     }
+  };
+  if (cbeg < cend) prefetch(cbeg);
+  for (int c0 = cbeg; c0 < cend; c0 += 64) {
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) tile[wid + r * kEllWaves][lane] = pu[r];
+    const long long off = poff;
+    const int bc = pbc;
+    __syncthreads();
+    if (c0 + 64 < cend) prefetch(c0 + 64);
+    const int c = c0 + lane;
 #pragma unroll
     for (int i = 0; i < GPW; ++i) {
       const int gl = wid * GPW + i, g = g0 + gl;
       if (g >= ngenes) break;
       int col = -1;
       bool keep = false;
-      if (c < ncells) {
-        col = (int)(off + tile[lane][gl]);
+      int rank = 0;
+      if (c < cend) {
+        rank = tile[lane][gl];
+        col = (int)(off + rank);
         keep = col != bc;
       }
       const unsigned long long m = __ballot(keep);
-      const int pos = n[i] + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
-      if (keep) ent[(long long)g * stride + pos] = make_int2(c + cell_off, col);
+      if (WRITE) {
+        const int pos = n[i] + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+        if (keep) ent[(long long)g * stride + pos] = make_int2(c + cell_off, col);
+      }
+      if (want_key && keep) ks[i] += (unsigned)max(rank, 0);
       n[i] += __popcll(m);
     }
   }
-  // padto 64: k_boot_tiles' bounds read whole 64-entry steps; its FP64 loop also looks one
-  // 4-entry batch past its last batch, hence the extra 8
 #pragma unroll
   for (int i = 0; i < GPW; ++i) {
     const int g = g0 + wid * GPW + i;
     if (g >= ngenes) break;
+    unsigned long long kv = ks[i];
+    if (want_key) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) kv += __shfl_xor(kv, o, 64);
+    }
+    if (!WRITE) {  // this chunk's entries (n counts only this chunk here) and rank sum
+      if (lane == 0) {
+        cnt[(long long)cy * ngenes + g] = (unsigned)n[i];
+        if (want_key) ksum[(long long)cy * ngenes + g] = kv > 0xffffffffull ? 0xffffffffu : (unsigned)kv;
+      }
+      continue;
+    }
+    if (cy != nchk - 1) continue;
     const int nn = n[i];
-    if (lane == 0) nnz[g] = nn;
+    if (lane == 0) {
+      nnz[g] = nn;
+      if (want_key) {
+        for (int k = 0; k < cy; ++k) kv += ksum[(long long)k * ngenes + g];
+        // the gene chunk of gene kg0 + g: chunk k holds [kgn k / kch, kgn (k + 1) / kch)
+        const long long gg = (long long)kg0 + g;
+        int k = (int)(gg * kch / kgn);
+        while (k + 1 < kch && (long long)kgn * (k + 1) / kch <= gg) ++k;
+        while (k > 0 && (long long)kgn * k / kch > gg) --k;
+        int hb = 0;  // bits of the chunk index
+        while ((1 << hb) < kch) ++hb;
+        const unsigned vmax = hb ? (0xffffffffu >> hb) : 0xffffffffu;
+        unsigned v = kv > vmax ? vmax : (unsigned)kv;
+        if (desc) v = vmax - v;
+        key[g] = (hb ? ((unsigned)k << (32 - hb)) : 0u) | v;
+        idx[g] = kg0 + g;
+      }
+    }
     const int end = padto == 64 ? (nn > 0 ? (nn + 63) & ~63 : 64) + 8 : ((nn + 7) & ~7) + 8;
     int2* E = ent + (long long)g * stride;
     for (int q = nn + lane; q < end && q < stride; q += 64) E[q] = make_int2(0, pad_col);
@@ -2188,7 +2257,8 @@ constexpr int kBTileMax = 14;  // 32-point bound tiles, G <= 448
 #ifndef SCDE_TILE_DIAG
 #define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only, 2 = rows without bounds, 4 = no multiplicity loads,
                           // 8 = every column load from the entry-0 column (cache-resident); k_boot_gene:
-                          // 16 = no bound pass, 32 = no row loop, 64 = rows only (no softmax / sums / rows out)
+                          // 16 = bounds replaced by -inf, 512 = no bound pass, 32 = no row loop, 64 = rows only (no
+                          // softmax / sums / rows out), 128 = bound pass loads only, 256 = bound pass without MFMA
 #endif
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -2878,11 +2948,12 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   const int* __restrict__ ZUset = ZUq + (long long)set * 4 * kQTiles * Bq + gb0;
   // ---- 1. bounds of the group's boot window 32 wsid .. 32 wsid + 31 (with 3 waves: the fourth
   // window split by entry chunks)
-  if (SCDE_TILE_DIAG & 16) {  // timing build: no bound pass (results wrong)
-    for (int i = threadIdx.x; i < kBTileMax * 128; i += 64 * WB) gub[i] = -INFINITY;
-  } else if (wsid < NW) {
+  if (!(SCDE_TILE_DIAG & 512) && wsid < NW)  // (512: timing build without the bound pass)
     tile_bound_pass(E, n, UQ, W8grp + 32 * wsid, gstride, ZUset + 32 * wsid, Bq, &bstage[wsid][0], gub + 32 * wsid, 128,
                     min(32, gnb - 32 * wsid), NTB, lane);
+  if (SCDE_TILE_DIAG & 16) {  // timing build: the bounds replaced by -inf (no post-check failures; results wrong)
+    __syncthreads();
+    for (int i = threadIdx.x; i < kBTileMax * 128; i += 64 * WB) gub[i] = -INFINITY;
   }
   if (WB < 4 && NW > WB) {  // (each wave stages in its own area: no barrier before the partial pass)
     tile_bound_partial(E, n, UQ, W8grp + 32 * WB, gstride, wsid, WB, &bstage[wsid][0], dsum, min(32, gnb - 32 * WB),
@@ -3305,7 +3376,7 @@ __device__ inline double block_sum(double v, double* sh) {
 template <int KPT>
 __global__ __launch_bounds__(1024) void k_boot_exact(ExactArgs a) {
   __shared__ double sh[16];
-  const int g = blockIdx.x;
+  const int g = blockIdx.x + a.g_lo;
   if (!a.degen[g]) return;
   const int tid = threadIdx.x;
   const int set = a.wset ? a.wset[g] : 0;
@@ -4108,15 +4179,73 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
   return hipGetLastError();
 }
 
+// 16-bit host counts widened to the int32 counts the unique-set build reads (U16Ring uploads)
+__global__ __launch_bounds__(256) void k_widen16(const unsigned short* __restrict__ in, int* __restrict__ out,
+                                                 long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = in[i];
+}
+
+// out[idx] = count for each listed (idx, count): the counts the 16-bit upload could not carry
+__global__ __launch_bounds__(256) void k_patch32(const int2* __restrict__ exc, long long n, int* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[exc[i].x] = exc[i].y;
+}
+
+hipError_t launch_patch32(const int2* exc, size_t n, int* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_patch32, dim3((unsigned)div_up((long long)n, 256)), dim3(256), 0, s, exc, (long long)n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_widen16(const unsigned short* in, int* out, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_widen16, dim3((unsigned)div_up((long long)n, 256)), dim3(256), 0, s, in, out, (long long)n);
+  return hipGetLastError();
+}
+
+// cell chunks of launch_ell: enough (gene tile, chunk) blocks to fill the chip twice, whole
+// 64-cell steps, at most kEllMaxChunks
+static void ell_chunks(int ngenes, int ncells, int max_chunks, int* ccells, int* nchk) {
+  const long long gt = std::max<long long>(1, div_up(ngenes, 64)), steps = std::max<long long>(1, div_up(ncells, 64));
+  long long k = std::min<long long>({div_up(1024, gt), steps, kEllMaxChunks});
+  if (max_chunks > 0) k = std::min<long long>(k, max_chunks);
+  k = std::max<long long>(1, k);
+  const long long cc = div_up(steps, k) * 64;
+  *ccells = (int)cc;
+  *nchk = (int)std::max<long long>(1, div_up(ncells, cc));
+}
+
+size_t ell_work_bytes(int ngenes, int ncells, int max_chunks) {
+  int cc, k;
+  ell_chunks(ngenes, ncells, max_chunks, &cc, &k);
+  return k > 1 ? sizeof(unsigned) * 2 * (size_t)k * std::max(ngenes, 1) : 0;
+}
+
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
                       const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s,
-                      int cell_off) {
+                      int cell_off, void* work, unsigned* key, int* idx, int kg0, int kgn, int kch, int desc,
+                      int max_chunks) {
   if (ngenes <= 0) return hipSuccess;
   if (padto == 64 ? stride < ((ncells + 63) & ~63) + 8 || stride < 72 : stride < ((ncells + 7) & ~7) + 8)
     return hipErrorInvalidValue;
   if (cell_off < 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_ell, dim3(div_up(ngenes, 64)), dim3(64 * kEllWaves), 0, s, uci, ld_uci, ngenes, ncells, ucl_off,
-                     base_col, stride, pad_col, padto, ent, nnz, cell_off);
+  if (key && (!idx || kch < 1 || kgn < kg0 + ngenes || kch > kgn)) return hipErrorInvalidValue;
+  int cc, k;
+  ell_chunks(ngenes, ncells, max_chunks, &cc, &k);
+  unsigned* cnt = nullptr;
+  unsigned* ksum = nullptr;
+  if (k > 1) {
+    if (!work) return hipErrorInvalidValue;
+    cnt = static_cast<unsigned*>(work);
+    ksum = cnt + (size_t)k * ngenes;
+    hipLaunchKernelGGL(k_ell<false>, dim3(div_up(ngenes, 64), k), dim3(64 * kEllWaves), 0, s, uci, ld_uci, ngenes,
+                       ncells, ucl_off, base_col, stride, pad_col, padto, ent, nnz, cell_off, cc, k, cnt, ksum, key,
+                       idx, kg0, kgn, kch, desc);
+  }
+  hipLaunchKernelGGL(k_ell<true>, dim3(div_up(ngenes, 64), k), dim3(64 * kEllWaves), 0, s, uci, ld_uci, ngenes, ncells,
+                     ucl_off, base_col, stride, pad_col, padto, ent, nnz, cell_off, cc, k, cnt, ksum, key, idx, kg0,
+                     kgn, kch, desc);
   return hipGetLastError();
 }
 
@@ -4317,33 +4446,6 @@ hipError_t launch_mult(const int* draws, int nsets, int nboot, int ndraw, int nc
   return hipGetLastError();
 }
 
-// Per gene the sum of its counts over the call's cells (from the ELL entries: each entry's
-// column is a unique count), the key of the tile bootstrap's gene order.
-__global__ __launch_bounds__(256) void k_gene_key(const int2* __restrict__ ent, const int* __restrict__ nnz,
-                                                 int ent_stride, const int* __restrict__ ucl, int ngenes,
-                                                 unsigned* __restrict__ key, int* __restrict__ idx) {
-  const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (g >= ngenes) return;
-  const int2* E = ent + (long long)g * ent_stride;
-  const int n = nnz[g];
-  unsigned long long sum = 0;
-  for (int e = lane; e < n; e += 64) sum += (unsigned)max(ucl[E[e].y], 0);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 64);
-  if (lane == 0) {
-    key[g] = sum > 0xffffffffull ? 0xffffffffu : (unsigned)sum;
-    idx[g] = g;
-  }
-}
-
-hipError_t launch_gene_key(const int2* ent, const int* nnz, int ent_stride, const int* ucl, int ngenes, unsigned* key,
-                           int* idx, hipStream_t s) {
-  if (ngenes <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gene_key, dim3(div_up(ngenes, 4)), dim3(256), 0, s, ent, nnz, ent_stride, ucl, ngenes, key, idx);
-  return hipGetLastError();
-}
-
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s) {
   if (a.ngenes <= 0) return hipSuccess;
   const int P = (a.nboot + a.nb - 1) / a.nb;
@@ -4368,6 +4470,11 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
     const int NGR = (P + tb.SG - 1) / tb.SG;
     if ((long long)a.ncells * NGR * 128 >= (1LL << 31) || tb.Bq < (NGR - 1) * tb.SG * a.nb + 128) return hipErrorInvalidValue;
   }
+  // the launch's genes (a gene chunk with gene blocks; every gene otherwise)
+  const int g_lo = tb.g_hi >= 0 ? tb.g_lo : 0, g_hi = tb.g_hi >= 0 ? tb.g_hi : a.ngenes;
+  if (g_lo < 0 || g_hi > a.ngenes || g_lo > g_hi || ((g_lo != 0 || g_hi != a.ngenes) && !gene))
+    return hipErrorInvalidValue;
+  const long long gspan = g_hi - g_lo;
   if (pairs || gene) {
     e = hipMemsetAsync(tb.wide, 0, sizeof(int), s);
     if (e != hipSuccess) return e;
@@ -4381,8 +4488,9 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   // items2 / WB blocks must then hold no wave whose index lies in [cap, grid * WB) -- such a wave
   // would read an entry this call never wrote.
   const long long gene_cap = std::max<long long>(WB, ((tb.list_cap > 0 ? tb.list_cap : 16384) / WB) * WB);
-  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(items, gene_cap) : 0;
-  const long long gblocks = gene ? (long long)a.ngenes * ((P + tb.SG - 1) / tb.SG) : 0;
+  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(gspan * P, gene_cap) : 0;
+  const long long gblocks = gene ? gspan * ((P + tb.SG - 1) / tb.SG) : 0;
+  const long long gblk0 = gene ? (long long)g_lo * ((P + tb.SG - 1) / tb.SG) : 0;
   // gene blocks in tb.chunks launches (>= 1): between launches the other lane's queued kernels
   // get CU slots that one long grid would hold until its last block is dispatched
   const long long chunk = std::max<long long>(1, (gblocks + std::max(1, tb.chunks) - 1) / std::max(1, tb.chunks));
@@ -4396,13 +4504,13 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
                              a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
                              a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
                              tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
-                             tb.order, tb.pmask, tb.wide, (int)items2, (int)c0);                                 \
+                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0));                       \
         else                                                                                                       \
           hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3(nblk), dim3(256), 0, s, a.D, a.ent, a.nnz,               \
                              a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
                              a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
                              tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
-                             tb.order, tb.pmask, tb.wide, (int)items2, (int)c0);                                 \
+                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0));                       \
       }                                                                                                            \
     else                                                                                                           \
     hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
@@ -4461,20 +4569,28 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const long long nn = (long long)a.ngenes * a.G;
-  hipLaunchKernelGGL(k_sum_partials, dim3(div_up(nn, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                     a.G, a.GS, a.out, a.out_g, a.out_k, tb.pmask);
+  // the launch's genes' jp rows (a chunk: its rows, offset pointers)
+  const long long nn = gspan * a.G;
+  if (nn > 0)
+    hipLaunchKernelGGL(k_sum_partials, dim3(div_up(nn, 256)), dim3(256), 0, s, a.part + (long long)g_lo * a.GS,
+                       a.part_stride, P, (int)gspan, a.G, a.GS, a.out + (long long)g_lo * a.out_g, a.out_g, a.out_k,
+                       tb.pmask + (long long)g_lo * P);
   return hipGetLastError();
 }
 
 hipError_t launch_boot_exact(const ExactArgs& a, hipStream_t s) {
-  if (a.ngenes <= 0) return hipSuccess;
+  const int g_lo = a.g_hi >= 0 ? a.g_lo : 0, g_hi = a.g_hi >= 0 ? a.g_hi : a.ngenes;
+  if (g_lo < 0 || g_hi > a.ngenes || g_lo > g_hi) return hipErrorInvalidValue;
+  if (g_hi == g_lo) return hipSuccess;
+  ExactArgs b = a;
+  b.g_lo = g_lo;  // blockIdx.x + g_lo
   int kpt;
   const int block = block_for_grid(a.G, &kpt);
+  const dim3 grid(g_hi - g_lo);
   switch (kpt) {
-    case 1: hipLaunchKernelGGL(k_boot_exact<1>, dim3(a.ngenes), dim3(block), 0, s, a); break;
-    case 2: hipLaunchKernelGGL(k_boot_exact<2>, dim3(a.ngenes), dim3(block), 0, s, a); break;
-    case 4: hipLaunchKernelGGL(k_boot_exact<4>, dim3(a.ngenes), dim3(block), 0, s, a); break;
+    case 1: hipLaunchKernelGGL(k_boot_exact<1>, grid, dim3(block), 0, s, b); break;
+    case 2: hipLaunchKernelGGL(k_boot_exact<2>, grid, dim3(block), 0, s, b); break;
+    case 4: hipLaunchKernelGGL(k_boot_exact<4>, grid, dim3(block), 0, s, b); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -97,17 +97,23 @@ def test_config4_1000_gene_slice_modes(api):
     # the host entry's piece pipeline (forced below its 32 MB threshold): the same bits
     ctx = api.default_context()
     try:
-        for pieces in (3, 8):
+        # and the read-backs: modes piece by piece / jp in gene chunks from the read-back thread
+        # (jp_chunks 1 = one bootstrap launch; modes_overlap 0 = plain copies after the bootstrap)
+        for pieces, chunks, overlap in ((3, 4, 1), (8, 3, 1), (8, 1, 1), (3, 7, 1), (3, 4, 0)):
             ctx.set_option("pipeline_mb", 0)
             ctx.set_option("pieces", pieces)
+            ctx.set_option("jp_chunks", chunks)
+            ctx.set_option("modes_overlap", overlap)
             api.set_rand("glibc")
             pip = api.scde_posteriors(models, sub, prior, n_randomizations=100,
                                       return_individual_posterior_modes=True, n_cores=1)
-            np.testing.assert_array_equal(pip["jp"], got["jp"])
-            np.testing.assert_array_equal(pip["modes"], got["modes"])
+            np.testing.assert_array_equal(pip["jp"], got["jp"], err_msg=f"pieces {pieces} chunks {chunks}")
+            np.testing.assert_array_equal(pip["modes"], got["modes"], err_msg=f"pieces {pieces} chunks {chunks}")
     finally:
         ctx.set_option("pipeline_mb", 32)
         ctx.set_option("pieces", 4)
+        ctx.set_option("jp_chunks", 4)
+        ctx.set_option("modes_overlap", 1)
     px = np.asarray(prior["x"])
     w = _workers()
     bounds = np.linspace(0, n, w + 1).astype(int)
@@ -220,5 +226,72 @@ def test_config3_host_pipeline_after_call_history(api):
             bad = np.nonzero(np.any(host != ref, axis=1))[0]
             assert bad.size == 0, (f"pieces {pieces}: {bad.size} of {N} genes differ after the call history; "
                                    f"first gene {bad[0]}: {host[bad[0]]} vs {ref[bad[0]]}")
+    finally:
+        ctx.close()
+
+
+def test_host_upload_16bit_counts(api):
+    """Host-count ranges of 8 MB and more go up as 16-bit counts (option upload_u16: narrowed on the
+    host in pinned ring slots, widened on the device, the counts outside [0, 65535] listed and
+    patched in).  Config 3's full host DE (whose synthetic matrix holds 3 counts past 65,535) and
+    the same matrix with a count past 16 bits every 997 genes x 7 cells equal the int32 upload bit
+    for bit, as does a config-4 posteriors slice with such counts; a negative count still fails the
+    call as it does on the int32 path."""
+    import ctypes
+    import bench
+    from scde_amd._lib import DEParams, check, lib
+    from scde_amd.models import model_matrix
+    from scde_amd.prior import expression_prior
+    cfg = bench.CONFIGS["3"]
+    models, counts, groups = bench.synthetic(cfg["seed"], cfg["genes"], cfg["cells"], two_groups=True)
+    prior = expression_prior(models, counts, length_out=bench.LENGTH_OUT)
+    N, C = counts.shape
+    codes = np.ascontiguousarray(np.asarray(groups), np.int32)
+    mm, lt, sq = model_matrix(models)
+    px = np.ascontiguousarray(prior["x"], np.float64)
+    py = np.ascontiguousarray(prior["y"], np.float64)
+    params = DEParams(C, mm.ctypes.data, lt, sq, codes.ctypes.data, px.ctypes.data, py.ctypes.data, len(px), 100, 1,
+                      0, N, 0.0, api.get_rand_kind(), 1)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    mat = np.asfortranarray(counts, dtype=np.int32)
+    wide = mat.copy(order="F")
+    wide[::997, ::7] += 70000  # past 16 bits in every range
+    ctx = api.Context(0)
+    try:
+        def de(m, u16):
+            ctx.set_option("upload_u16", u16)
+            out = np.zeros((N, 6), order="F")
+            api.set_rand("glibc")
+            check(lib().scde_expression_difference_host(ctx.handle, vp(m), N, N, ctypes.byref(params), vp(out), None,
+                                                        None, None))
+            return out
+        for m, what in ((mat, "config 3"), (wide, "counts past 65535")):
+            ref = de(m, 0)
+            got = de(m, 1)
+            bad = np.nonzero(np.any(got != ref, axis=1))[0]
+            assert bad.size == 0, f"{what}: {bad.size} genes differ, first {bad[:3]}"
+        neg = mat.copy(order="F")
+        neg[123, 456] = -3
+        for u16 in (0, 1):
+            ctx.set_option("upload_u16", u16)
+            with pytest.raises(Exception) as e:
+                out = np.zeros((N, 6), order="F")
+                check(lib().scde_expression_difference_host(ctx.handle, vp(neg), N, N, ctypes.byref(params), vp(out),
+                                                            None, None, None))
+            assert "negative" in str(e.value).lower() or "count" in str(e.value).lower(), str(e.value)
+        # scde.posteriors host entry (one range in pieces), modes included
+        c4 = bench.CONFIGS["4"]
+        m4, k4, _ = bench.synthetic(c4["seed"], 4000, c4["cells"], two_groups=False)
+        p4 = expression_prior(m4, k4, length_out=bench.LENGTH_OUT)
+        sub = np.asfortranarray(k4)
+        sub[::31, ::5] += 66000
+        res = {}
+        for u16 in (0, 1):
+            ctx.set_option("upload_u16", u16)
+            api.set_rand("glibc")
+            res[u16] = api.scde_posteriors(m4, sub, p4, n_randomizations=100, return_individual_posterior_modes=True,
+                                           n_cores=1, ctx=ctx)
+        np.testing.assert_array_equal(res[1]["jp"], res[0]["jp"])
+        np.testing.assert_array_equal(res[1]["modes"], res[0]["modes"])
     finally:
         ctx.close()

@@ -41,7 +41,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("boot_tiles", opts.get("boot_tiles", 1))
     ctx.set_option("tile_groups", opts.get("tile_groups", 4))
     ctx.set_option("boot_tiles_cells", opts.get("boot_tiles_cells", 0))
-    ctx.set_option("tile_order", opts.get("tile_order", 1))
+    ctx.set_option("tile_order", opts.get("tile_order", 3))
     ctx.set_option("pair_cells", opts.get("pair_cells", 1000))
     ctx.set_option("gene_blocks", opts.get("gene_blocks", 1))
     ctx.set_option("gene_rows", opts.get("gene_rows", 4))
@@ -76,7 +76,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("boot_tiles", 1)
         ctx.set_option("tile_groups", 4)
         ctx.set_option("boot_tiles_cells", 400)
-        ctx.set_option("tile_order", 1)
+        ctx.set_option("tile_order", 3)
         ctx.set_option("pair_cells", 1000)
         ctx.set_option("gene_blocks", 1)
         ctx.set_option("gene_rows", 4)
@@ -122,6 +122,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "gene-4waves": {"gene_waves": 4},
         "gene-chunks": {"boot_chunks": 3},
         "tiles-unordered": {"tile_order": 0},
+        "tiles-ascending": {"tile_order": 1},
+        "tiles-descending": {"tile_order": 2},
         "unique-exact": {"unique_fixed": 0},
         # the two group posteriors fused into one (option fuse_groups) against the two-posterior paths
         "fused": {"fuse_groups": 1},

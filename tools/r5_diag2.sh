@@ -10,4 +10,4 @@ k=d['kernel_ms_per_step']
 print('$tag', 'host %.3f dev %.3f' % (d['ms_per_step'], d['device_resident_ms_per_step']), 'kern', {a: round(b,3) for a,b in k.items()})"
 }
 run base --config 3
-for d in 16 128 256; do SCDE_LIB=diag/libt$d.so run diag$d --config 3; done
+for d in 528 16 144 272; do SCDE_LIB=diag/libt$d.so run diag$d --config 3; done
