@@ -178,10 +178,12 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   cell of the second group follows the first group's cells)
  *   "upload_staged" 1/0  host counts go up through a pinned ring filled by "upload_threads"
  *                   copy threads instead of pageable copies (default 0: measured no faster)
- *   "upload_u16"    1/0  host-count ranges of 8 MB or more go up as 16-bit counts: narrowed by
- *                   "upload_threads" threads (default 4) into a pinned ring, widened on the device
- *                   (default 1; half the PCIe bytes); a range holding a count outside [0, 65535]
- *                   goes up as int32; results are the same
+ *   "upload_u16"    0..2  host-count ranges of 8 MB or more go up as 16-bit counts: narrowed by
+ *                   "upload_threads" threads (default 4) into a pinned ring, widened on the device,
+ *                   counts outside [0, 65535] listed and patched in (half the PCIe bytes): 1
+ *                   (default) in scde_posteriors_host calls, 2 in every host entry (a DE call's
+ *                   upload overlaps its first group's work: measured slower), 0 none; results
+ *                   are the same
  *   "gene_waves"    3/4  k_boot_gene's waves per block (12 or 16 rows); 0 (default) = 3 from
  *                   "gene3_cells" cells per call (default: never; slower at config 4), else 4
  *   "gene_list_cap" slabs k_boot_gene's four-tile list pass takes (0 = 16384; beyond: k_boot2)

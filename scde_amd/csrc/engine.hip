@@ -288,7 +288,8 @@ struct scde_ctx {
   int opt_upload_staged = 0;     // "upload_staged": host-count uploads through a pinned ring filled by copy threads
   int opt_upload_threads = 4;     // "upload_threads": threads filling a staging slot (staged: the upload worker
                                  // included; 16-bit: the narrowing pool)
-  int opt_upload_u16 = 1;        // "upload_u16": host-count ranges of >= 8 MB go up as 16-bit counts (U16Ring)
+  int opt_upload_u16 = 1;        // "upload_u16": host-count ranges of >= 8 MB go up as 16-bit counts (U16Ring): 1
+                                 // scde.posteriors' host entry, 2 every host entry, 0 none
   int opt_modes_overlap = 1;     // "modes_overlap": scde.posteriors' read-backs (modes piece by piece, jp in gene
                                  // chunks) overlap the tables and the bootstrap from a read-back thread (0: after
                                  // the bootstrap, on the main stream -- rocprofv3 runs, where the pageable
@@ -2105,7 +2106,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "ell_chunks") ctx->opt_ell_chunks = std::max(0, std::min(64, (int)value));
   else if (n == "jp_chunks") ctx->opt_jp_chunks = std::max(1, std::min(64, (int)value));
   else if (n == "upload_staged") ctx->opt_upload_staged = value != 0;
-  else if (n == "upload_u16") ctx->opt_upload_u16 = value != 0;
+  else if (n == "upload_u16") ctx->opt_upload_u16 = (value >= 0 && value <= 2) ? (int)value : 1;
   else if (n == "upload_threads") ctx->opt_upload_threads = std::max(1, std::min(32, (int)value));
   else if (n == "gene_waves") ctx->opt_gene_waves = (value == 3 || value == 4) ? (int)value : 0;
   else if (n == "gene3_cells") ctx->opt_gene3_cells = (int)value;
@@ -2528,6 +2529,7 @@ struct HostUpload {
   const int* counts;
   int64_t ld;
   int ngenes, cut, C;
+  bool u16 = false;  // ranges of >= 8 MB as 16-bit counts (upload_cols_u16)
 };
 // the staging pool: share t of [0, n) copied by thread t (share 0 by the caller)
 static void stg_share(const char* src, char* dst, size_t n, int t, int T) {
@@ -2760,7 +2762,7 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
 // columns [lo, hi) of the host counts into counts_in, on the copy stream
 static int upload_cols(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   const size_t row = sizeof(int) * (size_t)h.ngenes;
-  if (hi > lo && ctx->opt_upload_u16 && h.ld == h.ngenes && row * (size_t)(hi - lo) >= (size_t(8) << 20))
+  if (hi > lo && h.u16 && h.ld == h.ngenes && row * (size_t)(hi - lo) >= (size_t(8) << 20))
     return upload_cols_u16(ctx, h, lo, hi);
   if (hi > lo && ctx->opt_upload_staged && h.ld == h.ngenes) return upload_cols_staged(ctx, h, lo, hi);
   if (hi > lo) {
@@ -3756,7 +3758,10 @@ int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld
   // the previous call's kernels may still read counts_in: the copies wait for them
   HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
   HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
-  const HostUpload h{counts, ld, ngenes, cut, C};
+  // (a DE call's upload hides behind the first group's unique sets and tables: as int32, unless
+  // upload_u16 = 2 -- config 3 measured 6.78 ms per step with int32 against 7.22 with 16-bit counts,
+  // whose narrowing threads then share the CPU with the lanes' threads)
+  const HostUpload h{counts, ld, ngenes, cut, C, ctx->opt_upload_u16 == 2};
   return de_run(ctx, ctx->counts_in.as<int>(), ngenes, ngenes, p, results, jp1, jp2, ratio, &h);
 }
 
@@ -3797,7 +3802,7 @@ int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngene
     // the previous call's kernels may still read counts_in: the copies wait for them
     HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
     HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
-    const HostUpload h{counts, ld, ngenes, 0, ncells_total};
+    const HostUpload h{counts, ld, ngenes, 0, ncells_total, ctx->opt_upload_u16 != 0};
     return posteriors_run(ctx, ctx->counts_in.as<int>(), ngenes, ngenes, cellidx, ncells_sel, models_sel, local_theta,
                           square_logit_conc, prior_x, ngrid, nboot, n_cores, gene_offset, ngenes_total, return_post,
                           ensemble, batch_vals, batch_off, composition, nbatch, jp, modes, post, &h);

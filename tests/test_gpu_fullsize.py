@@ -259,7 +259,7 @@ def test_host_upload_16bit_counts(api):
     ctx = api.Context(0)
     try:
         def de(m, u16):
-            ctx.set_option("upload_u16", u16)
+            ctx.set_option("upload_u16", 2 * u16)  # (2: DE host calls too)
             out = np.zeros((N, 6), order="F")
             api.set_rand("glibc")
             check(lib().scde_expression_difference_host(ctx.handle, vp(m), N, N, ctypes.byref(params), vp(out), None,
@@ -273,7 +273,7 @@ def test_host_upload_16bit_counts(api):
         neg = mat.copy(order="F")
         neg[123, 456] = -3
         for u16 in (0, 1):
-            ctx.set_option("upload_u16", u16)
+            ctx.set_option("upload_u16", 2 * u16)
             with pytest.raises(Exception) as e:
                 out = np.zeros((N, 6), order="F")
                 check(lib().scde_expression_difference_host(ctx.handle, vp(neg), N, N, ctypes.byref(params), vp(out),
