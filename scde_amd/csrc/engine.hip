@@ -294,7 +294,9 @@ struct scde_ctx {
                                  // chunks) overlap the tables and the bootstrap from a read-back thread (0: after
                                  // the bootstrap, on the main stream -- rocprofv3 runs, where the pageable
                                  // read-back becomes blit kernels that would share the CUs)
-  int opt_ell_chunks = 0;        // "ell_chunks": at most this many cell chunks in the ELL build (0: by size)
+  int opt_ell_chunks = 1;        // "ell_chunks": at most this many cell chunks in the ELL build (0: by size, two
+                                 // passes; measured no faster: config 3 6.75-6.90 ms host -> host with one pass vs
+                                 // 6.90 chunked, shard of 8 1.68 vs 1.72, configs 2 / 2b / 4 within noise)
   int opt_jp_chunks = 4;         // "jp_chunks": gene chunks of scde.posteriors' gene-block bootstrap, each chunk's
                                  // jp rows read back while the next runs (1: one launch, jp after it)
   int opt_gene_waves = 0;        // "gene_waves": k_boot_gene's waves per block, 3 or 4 (0: by gene3_cells)

@@ -61,6 +61,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("tables_pair", opts.get("tables_pair", 1))
     ctx.set_option("task_cols", opts.get("task_cols", 0))
     ctx.set_option("boot2_rows", opts.get("boot2_rows", 0))
+    ctx.set_option("ell_chunks", opts.get("ell_chunks", 1))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -96,6 +97,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("tables_pair", 1)
         ctx.set_option("task_cols", 0)
         ctx.set_option("boot2_rows", 0)
+        ctx.set_option("ell_chunks", 1)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -124,6 +126,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "tiles-unordered": {"tile_order": 0},
         "tiles-ascending": {"tile_order": 1},
         "tiles-descending": {"tile_order": 2},
+        # the ELL rows built in cell chunks (two passes) and in chunks of at most 2
+        "ell-chunked": {"ell_chunks": 0},
+        "ell-chunks2": {"ell_chunks": 2},
         "unique-exact": {"unique_fixed": 0},
         # the two group posteriors fused into one (option fuse_groups) against the two-posterior paths
         "fused": {"fuse_groups": 1},
