@@ -130,7 +130,7 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "tile_max_mult" the largest draw multiplicity the tile path takes (default 127, the int8 bound
  *                   operand; a call with a larger one runs plain k_boot2 on the same columns --
  *                   tests force that fallback with a small value)
- *   "tile_order"    0..3  the tile bootstrap takes the genes in order of their count-rank sums,
+ *   "tile_order"    0..3  the tile bootstrap takes the genes in order of their count sums,
  *                   so waves in flight share columns and tiles in L2: 1 ascending, 2 descending
  *                   (heaviest genes first: a shorter tail), 3 (default) descending for launches
  *                   of at most 8,192 genes and ascending above, 0 gene order; results are the same

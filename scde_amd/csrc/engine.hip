@@ -278,7 +278,7 @@ struct scde_ctx {
   int opt_tile_groups = 4;       // "tile_groups": 32-point bound tiles k_boot_tiles computes per slab (1..4)
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
-  int opt_tile_order = 3;        // "tile_order": the tile bootstrap takes genes by count-rank sum (cache sharing):
+  int opt_tile_order = 3;        // "tile_order": the tile bootstrap takes genes by count sum (cache sharing):
                                  // 1 ascending, 2 descending (heaviest first), 3 by size (default: descending for
                                  // launches of at most kDescGenes genes, where the last, heaviest blocks would
                                  // set the launch's tail), 0 in gene order
@@ -1548,7 +1548,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     const int nchunks = (s.jp_host && !two && gene_sg > 0 && s.jp_g == 1 && s.jp_k == N)
                             ? std::max(1, std::min(cx->opt_jp_chunks, NBg / 256 + 1)) : 1;
     auto gch = [NBg, nchunks](int k) { return (int)((long long)NBg * k / nchunks); };
-    // tile path: genes in order of their count-rank sums (waves in flight share columns in L2), keyed by
+    // tile path: genes in order of their count sums (waves in flight share columns in L2), keyed by
     // the ELL builder; with gene chunks each chunk's genes in order among themselves (the chunk
     // index in the keys' top bits: one sort)
     const bool have_order = tpath && fast && cx->opt_tile_order && NBg > 1;
@@ -1572,7 +1572,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       HCHK(launch_ell(u.uci.as<int>() + (size_t)N * c0, N, N, nc, u.ucl_off.as<long long>() + c0,
                       cx->base_col.as<int>() + c0, stride, (int)ncols, tpath ? 64 : 8,
                       cx->ent.as<int2>() + (size_t)gi * N * stride, cx->nnz.as<int>() + (size_t)gi * N, sa, c0,
-                      cx->ellw.p, have_order ? cx->gkey.as<unsigned>() + (size_t)gi * N : nullptr,
+                      cx->ellw.p, have_order ? u.ucl.as<int>() : nullptr, have_order ? cx->gkey.as<unsigned>() + (size_t)gi * N : nullptr,
                       have_order ? cx->gidx.as<int>() + (size_t)gi * N : nullptr, gi * N, NBg, nchunks,
                       order_desc, cx->opt_ell_chunks));
     }

@@ -213,7 +213,7 @@ struct TileBootArgs {
   int g_lo = 0, g_hi = -1;
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
-// gene order for the tile bootstrap: the keys launch_ell formed (per-gene count-rank sums), sorted
+// gene order for the tile bootstrap: the keys launch_ell formed (per-gene count sums), sorted
 hipError_t launch_gene_order(const unsigned* key, const int* idx, int n, unsigned* key_out, int* order, void* work,
                              size_t* work_bytes, hipStream_t s);
 
@@ -284,10 +284,10 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 // multiple of 64 plus 8 (k_boot_tiles' bound MFMAs take 64-entry steps)
 // cell_off: added to the cell of every entry (a fused second group's cells follow the first's)
 // work: ell_work_bytes(ngenes, ncells) bytes (null allowed when that is 0) -- the per cell-chunk
-// entry counts and rank sums of the two-pass build.  key (nullable, with idx): the tile
-// bootstrap's gene-order keys (sums of the entries' count ranks) and gene indices, the launch's
-// genes being genes kg0 .. of kgn split into kch gene chunks (the chunk index in the key's top
-// bits; desc: descending within a chunk)
+// entry counts and count sums of the two-pass build.  key (nullable, with ucl and idx): the
+// tile bootstrap's gene-order keys (sums of the entries' counts ucl[col]) and gene indices, the
+// launch's genes being genes kg0 .. of kgn split into kch gene chunks (the chunk index in the
+// key's top bits; desc: descending within a chunk)
 // out[i] = in[i] for n 16-bit counts
 hipError_t launch_widen16(const unsigned short* in, int* out, size_t n, hipStream_t s);
 // out[exc[i].x] = exc[i].y for n listed counts (indices relative to out)
@@ -296,7 +296,7 @@ hipError_t launch_patch32(const int2* exc, size_t n, int* out, hipStream_t s);
 size_t ell_work_bytes(int ngenes, int ncells, int max_chunks = 0);
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
                       const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s,
-                      int cell_off, void* work, unsigned* key = nullptr, int* idx = nullptr,
+                      int cell_off, void* work, const int* ucl = nullptr, unsigned* key = nullptr, int* idx = nullptr,
                       int kg0 = 0, int kgn = 0, int kch = 1, int desc = 0, int max_chunks = 0);
 hipError_t launch_baseline_z(const double* T, int G, int GS, const int* base_col, int ncells, const double* Wt,
                              int Bp, int nsets, double* Z, hipStream_t s, int gsets = 0, int gsplit = 0);

@@ -1213,10 +1213,14 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
 // after the earlier chunks' (a grid of ngenes / 64 blocks alone left most CUs idle: config 4's
 // 30k x 2000 took 330-420 us in one pass over 32 serial cell steps per block).  The last chunk's
 // block writes the row length, the pad entries and, with `key`, the gene's tile-order key: the
-// sum of its entries' count ranks (uci, the count's index in its cell's ascending unique list;
-// saturated) -- genes of like expression next to each other, so that waves in flight share
-// columns -- under its gene chunk's index in the top bits (kch chunks of the kgn genes, this
-// launch's genes from kg0), descending when `desc` (heaviest genes first within each chunk).
+// sum of its entries' counts (ucl[col]; saturated) -- genes of like expression next to each
+// other, so that waves in flight share columns -- under its gene chunk's index in the top bits
+// (kch chunks of the kgn genes, this launch's genes from kg0), descending when `desc` (heaviest
+// genes first within each chunk).  (Timing build SCDE_ELL_KEY_RANK: the sum of the count ranks,
+// uci, instead, no gather: the same bootstrap fetch, 28.5-28.6 GB per launch at config 4.)
+#ifndef SCDE_ELL_KEY_RANK
+#define SCDE_ELL_KEY_RANK 0
+#endif
 constexpr int kEllWaves = 16;
 constexpr int kEllMaxChunks = 64;
 template <bool WRITE>
@@ -1225,7 +1229,8 @@ __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ 
                                              const int* __restrict__ base_col, int stride, int pad_col,
                                              int padto, int2* __restrict__ ent, int* __restrict__ nnz, int cell_off,
                                              int ccells, int nchk, unsigned* __restrict__ cnt,
-                                             unsigned* __restrict__ ksum, unsigned* __restrict__ key, int* __restrict__ idx, int kg0, int kgn,
+                                             unsigned* __restrict__ ksum, const int* __restrict__ ucl,
+                                             unsigned* __restrict__ key, int* __restrict__ idx, int kg0, int kgn,
                                              int kch, int desc) {
   __shared__ int tile[64][65];  // [cell][gene]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1234,7 +1239,7 @@ __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ 
   constexpr int GPW = 64 / kEllWaves;  // genes per wave
   const bool want_key = key != nullptr;
   int n[GPW];
-  unsigned long long ks[GPW];  // per lane: its cells' kept count ranks (the key)
+  unsigned long long ks[GPW];  // per lane: its cells' kept counts (the key)
 #pragma unroll
   for (int i = 0; i < GPW; ++i) {
     n[i] = 0;
@@ -1293,7 +1298,7 @@ __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ 
         const int pos = n[i] + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
         if (keep) ent[(long long)g * stride + pos] = make_int2(c + cell_off, col);
       }
-      if (want_key && keep) ks[i] += (unsigned)max(rank, 0);
+      if (want_key && keep) ks[i] += (unsigned)max(SCDE_ELL_KEY_RANK ? rank : ucl[col], 0);
       n[i] += __popcll(m);
     }
   }
@@ -1306,7 +1311,7 @@ __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ 
 #pragma unroll
       for (int o = 32; o >= 1; o >>= 1) kv += __shfl_xor(kv, o, 64);
     }
-    if (!WRITE) {  // this chunk's entries (n counts only this chunk here) and rank sum
+    if (!WRITE) {  // this chunk's entries (n counts only this chunk here) and count sum
       if (lane == 0) {
         cnt[(long long)cy * ngenes + g] = (unsigned)n[i];
         if (want_key) ksum[(long long)cy * ngenes + g] = kv > 0xffffffffull ? 0xffffffffu : (unsigned)kv;
@@ -4224,13 +4229,13 @@ size_t ell_work_bytes(int ngenes, int ncells, int max_chunks) {
 
 hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, const long long* ucl_off,
                       const int* base_col, int stride, int pad_col, int padto, int2* ent, int* nnz, hipStream_t s,
-                      int cell_off, void* work, unsigned* key, int* idx, int kg0, int kgn, int kch, int desc,
-                      int max_chunks) {
+                      int cell_off, void* work, const int* ucl, unsigned* key, int* idx, int kg0, int kgn, int kch,
+                      int desc, int max_chunks) {
   if (ngenes <= 0) return hipSuccess;
   if (padto == 64 ? stride < ((ncells + 63) & ~63) + 8 || stride < 72 : stride < ((ncells + 7) & ~7) + 8)
     return hipErrorInvalidValue;
   if (cell_off < 0) return hipErrorInvalidValue;
-  if (key && (!idx || kch < 1 || kgn < kg0 + ngenes || kch > kgn)) return hipErrorInvalidValue;
+  if (key && (!ucl || !idx || kch < 1 || kgn < kg0 + ngenes || kch > kgn)) return hipErrorInvalidValue;
   int cc, k;
   ell_chunks(ngenes, ncells, max_chunks, &cc, &k);
   unsigned* cnt = nullptr;
@@ -4240,12 +4245,12 @@ hipError_t launch_ell(const int* uci, long long ld_uci, int ngenes, int ncells, 
     cnt = static_cast<unsigned*>(work);
     ksum = cnt + (size_t)k * ngenes;
     hipLaunchKernelGGL(k_ell<false>, dim3(div_up(ngenes, 64), k), dim3(64 * kEllWaves), 0, s, uci, ld_uci, ngenes,
-                       ncells, ucl_off, base_col, stride, pad_col, padto, ent, nnz, cell_off, cc, k, cnt, ksum, key,
-                       idx, kg0, kgn, kch, desc);
+                       ncells, ucl_off, base_col, stride, pad_col, padto, ent, nnz, cell_off, cc, k, cnt, ksum, ucl,
+                       key, idx, kg0, kgn, kch, desc);
   }
   hipLaunchKernelGGL(k_ell<true>, dim3(div_up(ngenes, 64), k), dim3(64 * kEllWaves), 0, s, uci, ld_uci, ngenes, ncells,
-                     ucl_off, base_col, stride, pad_col, padto, ent, nnz, cell_off, cc, k, cnt, ksum, key, idx, kg0,
-                     kgn, kch, desc);
+                     ucl_off, base_col, stride, pad_col, padto, ent, nnz, cell_off, cc, k, cnt, ksum, ucl, key, idx,
+                     kg0, kgn, kch, desc);
   return hipGetLastError();
 }
 
