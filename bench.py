@@ -662,7 +662,12 @@ def main():
                   # host wall time of the call's phases (set-up, unique sets, posteriors enqueued,
                   # ratio + read-back incl. the final wait), ms per step
                   "host_phase_ms_per_step": {k: ctx.stat(f"host_{k}_ms") / args.steps
-                                             for k in ("setup", "unique", "post", "tail")}}
+                                             for k in ("setup", "unique", "post", "tail")},
+                  "upload_wake_ms_per_step": ctx.stat("upload_wake_ms") / args.steps,
+                  "upload_first_ms_per_step": ctx.stat("upload_first_ms") / args.steps,
+                  # 16-bit uploads: the issuing thread's ms per step waiting for the narrowing
+                  # threads, issuing copies + widening kernels, waiting for ring slots to free
+                  "u16_ms_per_step": {k: ctx.stat(f"u16_{k}_ms") / args.steps for k in ("wait", "issue", "free")}}
     # device-resident rate (counts already in HBM), product settings
     dc = api.DeviceCounts(ctx, counts)
     dt_dev = timed(dc.ptr)

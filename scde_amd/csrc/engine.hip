@@ -356,6 +356,8 @@ struct scde_ctx {
     std::function<int(int)> issue;  // issue(j): upload range j and record its event
     int nranges = 0, issued = 0, err = 0;
     std::string err_msg;  // the worker thread's error text (its g_err is its own)
+    std::chrono::steady_clock::time_point t_start;  // the job's start (stat upload_wake_ms)
+    double wake_ms = 0, first_ms = 0;  // summed: start -> worker awake, start -> first range issued
   } upl;
   // Device -> host read-backs from a worker thread (a pageable hipMemcpy blocks its calling thread
   // for the whole transfer): scde.posteriors' modes columns piece by piece and its jp rows chunk by
@@ -434,6 +436,7 @@ struct scde_ctx {
     size_t n = 0;
     long long q0 = 0;
     int nslots = 0;
+    double st_wait_ms = 0, st_issue_ms = 0, st_free_ms = 0;  // issuer: narrowing waits, copy issue, slot frees
   } u16;
   // statistics (scde_ctx_get_stat)
   double st_skip_slabs = 0, st_skip_kept = 0, st_skip_stretches = 0, st_skip_redo = 0, st_degen = 0;
@@ -2157,6 +2160,11 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "piece_wait_ms") *value = ctx->st_piece_wait_ms + (ctx->peer ? ctx->peer->st_piece_wait_ms : 0);
   else if (n == "piece_host_ms") *value = ctx->st_piece_host_ms + (ctx->peer ? ctx->peer->st_piece_host_ms : 0);
   else if (n == "buf_reallocs") *value = (double)g_buf_reallocs.load();
+  else if (n == "upload_wake_ms") *value = ctx->upl.wake_ms;
+  else if (n == "u16_wait_ms") *value = ctx->u16.st_wait_ms;
+  else if (n == "u16_issue_ms") *value = ctx->u16.st_issue_ms;
+  else if (n == "u16_free_ms") *value = ctx->u16.st_free_ms;
+  else if (n == "upload_first_ms") *value = ctx->upl.first_ms;
   else if (n == "host_setup_ms") *value = ctx->st_host_ms[0];
   else if (n == "host_unique_ms") *value = ctx->st_host_ms[1];
   else if (n == "host_post_ms") *value = ctx->st_host_ms[2];
@@ -2176,6 +2184,14 @@ int scde_ctx_reset_stats(scde_ctx* ctx) {
   ctx->st_piece_wait_ms = ctx->st_piece_host_ms = 0;
   if (ctx->peer) ctx->peer->st_piece_wait_ms = ctx->peer->st_piece_host_ms = 0;
   for (double& x : ctx->st_host_ms) x = 0;
+  {
+    std::lock_guard<std::mutex> lk(ctx->upl.m);
+    ctx->upl.wake_ms = ctx->upl.first_ms = 0;
+  }
+  {
+    std::lock_guard<std::mutex> lk(ctx->u16.m);
+    ctx->u16.st_wait_ms = ctx->u16.st_issue_ms = ctx->u16.st_free_ms = 0;
+  }
   ctx->st_boot_f64_fma = 0;
   for (double& x : ctx->st_tile_hist) x = 0;
   return SCDE_OK;
@@ -2712,9 +2728,12 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   for (int sl = 0; sl < nslots; ++sl) {
     const long long q = q0 + sl;
     const int k = (int)(q % R::kRing);
+    const auto tw = std::chrono::steady_clock::now();
     r.cvf.wait(lk, [&] { return r.fin[k] == T; });
     r.fin[k] = 0;
     lk.unlock();
+    const auto ti = std::chrono::steady_clock::now();
+    r.st_wait_ms += std::chrono::duration<double, std::milli>(ti - tw).count();
     const size_t off = (size_t)sl * R::kSlotCounts;
     const size_t m = std::min(R::kSlotCounts, n - off);
     unsigned short* dslot = r.dev + (size_t)k * R::kSlotCounts;
@@ -2735,11 +2754,14 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
       if (e == hipSuccess) e = launch_patch32(ctx->excd.as<int2>(), r.exc_all.size(), dst + off, ctx->copy_stream);
     }
     r.issued = q + 1;
+    const auto tf = std::chrono::steady_clock::now();
+    r.st_issue_ms += std::chrono::duration<double, std::milli>(tf - ti).count();
     // free the ring slot the threads need next (slot q + 1 reuses slot q + 1 - kRing's): wait for
     // that DMA, then let them write (only this thread writes free_upto)
     const long long f = q + 1 - R::kRing;
     const bool advance = e == hipSuccess && r.free_upto <= q + 1;
     if (advance && f >= 0) e = hipEventSynchronize(r.ev[f % R::kRing]);
+    r.st_free_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
     lk.lock();
     if (e != hipSuccess) {
       rc = fail(SCDE_EHIP, "%s", hipGetErrorString(e));
@@ -2809,11 +2831,15 @@ struct UploadWorker {
           seen = q.job;
           const int n = q.nranges;
           auto issue = q.issue;
+          const auto t0 = q.t_start;
+          q.wake_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
           lk.unlock();
           int rc = SCDE_OK;
           for (int j = 0; j < n && rc == SCDE_OK; ++j) {
             rc = issue(j);
             std::lock_guard<std::mutex> g(q.m);
+            if (j == 0)
+              q.first_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
             if (rc != SCDE_OK) {
               q.err = rc;
               q.err_msg = g_err;  // g_err is thread-local: hand the worker's message to the caller
@@ -2842,6 +2868,7 @@ struct UploadWorker {
     u.err = 0;
     u.err_msg.clear();
     u.busy = true;
+    u.t_start = std::chrono::steady_clock::now();
     ++u.job;
     u.cv.notify_all();
     return SCDE_OK;
