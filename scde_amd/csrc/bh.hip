@@ -180,16 +180,18 @@ hipError_t launch_bh_cz(const double* z, int n, double* cz, void* work, size_t* 
   return hipGetLastError();
 }
 
-// Gene order for the tile bootstrap: radix sort of (count sum, gene) pairs, ascending and
-// stable.  `work == nullptr` queries the temporary storage size.
+// Gene order for the tile bootstrap: radix sort of (key, gene) pairs on the keys' low `bits`
+// bits (launch_ell forms 16-bit keys), ascending and stable.  `work == nullptr` queries the
+// temporary storage size.
 hipError_t launch_gene_order(const unsigned* key, const int* idx, int n, unsigned* key_out, int* order, void* work,
-                             size_t* work_bytes, hipStream_t s) {
+                             size_t* work_bytes, hipStream_t s, int bits) {
+  if (bits < 1 || bits > 32) return hipErrorInvalidValue;
   if (!work) {
-    return hipcub::DeviceRadixSort::SortPairs(nullptr, *work_bytes, key, key_out, idx, order, n > 0 ? n : 1, 0, 32,
+    return hipcub::DeviceRadixSort::SortPairs(nullptr, *work_bytes, key, key_out, idx, order, n > 0 ? n : 1, 0, bits,
                                               s);
   }
   if (n <= 0) return hipSuccess;
-  return hipcub::DeviceRadixSort::SortPairs(work, *work_bytes, key, key_out, idx, order, n, 0, 32, s);
+  return hipcub::DeviceRadixSort::SortPairs(work, *work_bytes, key, key_out, idx, order, n, 0, bits, s);
 }
 
 }  // namespace scde

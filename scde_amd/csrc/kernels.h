@@ -215,7 +215,7 @@ struct TileBootArgs {
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: the keys launch_ell formed (per-gene count sums), sorted
 hipError_t launch_gene_order(const unsigned* key, const int* idx, int n, unsigned* key_out, int* order, void* work,
-                             size_t* work_bytes, hipStream_t s);
+                             size_t* work_bytes, hipStream_t s, int bits = 16);
 
 struct ExactArgs {
   const double* T;  // log tables; or fused D columns when base_col is set (T = D + D[base])
@@ -285,7 +285,7 @@ hipError_t launch_base_cols(const int* ucl, const long long* ucl_off, int ncells
 // cell_off: added to the cell of every entry (a fused second group's cells follow the first's)
 // work: ell_work_bytes(ngenes, ncells) bytes (null allowed when that is 0) -- the per cell-chunk
 // entry counts and count sums of the two-pass build.  key (nullable, with ucl and idx): the
-// tile bootstrap's gene-order keys (sums of the entries' counts ucl[col]) and gene indices, the
+// tile bootstrap's 16-bit gene-order keys (log-scaled sums of the entries' counts ucl[col]) and gene indices, the
 // launch's genes being genes kg0 .. of kgn split into kch gene chunks (the chunk index in the
 // key's top bits; desc: descending within a chunk)
 // out[i] = in[i] for n 16-bit counts

@@ -1212,17 +1212,18 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
 // counts each (gene, chunk)'s entries and rank sum, and the second writes each chunk's entries
 // after the earlier chunks' (a grid of ngenes / 64 blocks alone left most CUs idle: config 4's
 // 30k x 2000 took 330-420 us in one pass over 32 serial cell steps per block).  The last chunk's
-// block writes the row length, the pad entries and, with `key`, the gene's tile-order key: the
-// sum of its entries' counts (ucl[col]; saturated) -- genes of like expression next to each
-// other, so that waves in flight share columns -- under its gene chunk's index in the top bits
-// (kch chunks of the kgn genes, this launch's genes from kg0), descending when `desc` (heaviest
-// genes first within each chunk).  (Timing build SCDE_ELL_KEY_RANK: the sum of the count ranks,
+// block writes the row length, the pad entries and, with `key`, the gene's 16-bit tile-order
+// key: the sum of its entries' counts (ucl[col]) on a log scale -- genes of like expression next
+// to each other, so that waves in flight share columns -- under its gene chunk's index in the
+// top bits (kch chunks of the kgn genes, this launch's genes from kg0), descending when `desc`
+// (heaviest genes first within each chunk).  (Timing build SCDE_ELL_KEY_RANK: the sum of the count ranks,
 // uci, instead, no gather: the same bootstrap fetch, 28.5-28.6 GB per launch at config 4.)
 #ifndef SCDE_ELL_KEY_RANK
 #define SCDE_ELL_KEY_RANK 0
 #endif
 constexpr int kEllWaves = 16;
 constexpr int kEllMaxChunks = 64;
+constexpr int kEllKeyBits = 16;  // gene-order key width (launch_gene_order sorts these bits)
 template <bool WRITE>
 __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ uci, long long ld_uci, int ngenes,
                                              int ncells, const long long* __restrict__ ucl_off,
@@ -1331,10 +1332,13 @@ __global__ __launch_bounds__(64 * kEllWaves) void k_ell(const int* __restrict__ 
         while (k > 0 && (long long)kgn * k / kch > gg) --k;
         int hb = 0;  // bits of the chunk index
         while ((1 << hb) < kch) ++hb;
-        const unsigned vmax = hb ? (0xffffffffu >> hb) : 0xffffffffu;
-        unsigned v = kv > vmax ? vmax : (unsigned)kv;
+        // 16-bit keys (the sort then takes two radix passes, not four): the chunk index, then the
+        // count sum on a log scale, (2^(16 - hb) - 1) / 33 steps per octave
+        const unsigned vmax = (1u << (kEllKeyBits - hb)) - 1u;
+        unsigned v = (unsigned)(log2((double)kv + 1.0) * ((double)vmax / 33.0));
+        v = v > vmax ? vmax : v;
         if (desc) v = vmax - v;
-        key[g] = (hb ? ((unsigned)k << (32 - hb)) : 0u) | v;
+        key[g] = (hb ? ((unsigned)k << (kEllKeyBits - hb)) : 0u) | v;
         idx[g] = kg0 + g;
       }
     }
@@ -4402,6 +4406,43 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Several buffers zeroed by one launch instead of one fill per buffer (the bootstrap set-up is a
+// chain of short dependent launches, each costing ~5 us of launch latency): span i is bytes
+// [0, n_i) at p_i (16-B aligned), in 16-byte stores; the last thread of a span writes its tail.
+struct ZeroSpans {
+  static constexpr int kMax = 6;
+  void* p[kMax];
+  unsigned long long n[kMax];
+  int count;
+};
+__global__ __launch_bounds__(256) void k_zero(ZeroSpans z) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int k = 0; k < z.count; ++k) {
+    const long long n16 = (long long)(z.n[k] >> 4), chunks = n16 + ((z.n[k] & 15) ? 1 : 0);
+    if (i < chunks) {
+      unsigned char* b = static_cast<unsigned char*>(z.p[k]);
+      if (i < n16) {
+        *reinterpret_cast<uint4*>(b + 16 * i) = make_uint4(0, 0, 0, 0);
+      } else {
+        for (unsigned long long j = 16ull * n16; j < z.n[k]; ++j) b[j] = 0;
+      }
+      return;
+    }
+    i -= chunks;
+  }
+}
+
+static hipError_t launch_zero(const ZeroSpans& z, hipStream_t s) {
+  long long total = 0;
+  for (int k = 0; k < z.count; ++k) {
+    if (reinterpret_cast<uintptr_t>(z.p[k]) & 15) return hipErrorInvalidValue;
+    total += (long long)((z.n[k] + 15) >> 4);
+  }
+  if (total == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zero, dim3((unsigned)div_up(total, 256)), dim3(256), 0, s, z);
+  return hipGetLastError();
+}
+
 // One block per (boot, seed set): the boot's draws counted per cell in LDS, then the cell column
 // of every multiplicity array written (strided, small: cells x boots per set).
 __global__ __launch_bounds__(256) void k_mult(const int* __restrict__ draws, int nboot, int ndraw, int ncells, int Bp,
@@ -4440,10 +4481,22 @@ hipError_t launch_mult(const int* draws, int nsets, int nboot, int ndraw, int nc
       (W8p && P * nb < nboot) || (W8g && (SG <= 0 || NGR * SG * nb < nboot)))
     return hipErrorInvalidValue;
   const size_t sc = (size_t)nsets * ncells;
-  hipError_t e = hipMemsetAsync(Wt, 0, sizeof(double) * sc * Bp, s);
-  if (e == hipSuccess && W8) e = hipMemsetAsync(W8, 0, sc * Bt, s);
-  if (e == hipSuccess && W8p) e = hipMemsetAsync(W8p, 0, sc * P * 32, s);
-  if (e == hipSuccess && W8g) e = hipMemsetAsync(W8g, 0, sc * NGR * 128, s);
+  ZeroSpans z{};
+  z.p[z.count] = Wt;
+  z.n[z.count++] = sizeof(double) * sc * Bp;
+  if (W8) {
+    z.p[z.count] = W8;
+    z.n[z.count++] = sc * Bt;
+  }
+  if (W8p) {
+    z.p[z.count] = W8p;
+    z.n[z.count++] = sc * P * 32;
+  }
+  if (W8g) {
+    z.p[z.count] = W8g;
+    z.n[z.count++] = sc * NGR * 128;
+  }
+  hipError_t e = launch_zero(z, s);
   if (e != hipSuccess) return e;
   if (nboot <= 0 || ndraw <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_mult, dim3(nboot, nsets), dim3(256), 0, s, draws, nboot, ndraw, ncells, Bp, Wt, Bt, W8, nb, P,
@@ -4460,9 +4513,11 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if ((long long)a.ncols_p1 * a.GS >= (1LL << 31) || (long long)a.ncells * a.Bp >= (1LL << 31) ||
       (long long)a.ncells * 32 * P >= (1LL << 31))
     return hipErrorInvalidValue;
-  // redo: [items] fallback flags, [1] the fallback list's length, [items] the list
-  hipError_t e = hipMemsetAsync(a.redo, 0, sizeof(int) * ((size_t)a.ngenes * P + 1), s);
-  if (e != hipSuccess) return e;
+  // redo: [items] fallback flags, [1] the fallback list's length, [items] the list; and the list
+  // pass's count wide[0] (below): one zeroing launch
+  ZeroSpans z{};
+  z.p[z.count] = a.redo;
+  z.n[z.count++] = sizeof(int) * ((size_t)a.ngenes * P + 1);
   const long long items = (long long)a.ngenes * P;
   // pair mode: a wave per two slabs of a gene, two bound tiles each; the slabs that need more
   // go to a four-tile pass over the compacted list `wide` ([0] length, then g * P + p)
@@ -4481,9 +4536,11 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
     return hipErrorInvalidValue;
   const long long gspan = g_hi - g_lo;
   if (pairs || gene) {
-    e = hipMemsetAsync(tb.wide, 0, sizeof(int), s);
-    if (e != hipSuccess) return e;
+    z.p[z.count] = tb.wide;
+    z.n[z.count++] = sizeof(int);
   }
+  hipError_t e = launch_zero(z, s);
+  if (e != hipSuccess) return e;
   constexpr int WB = 4;
   const long long items1 = pairs ? (long long)a.ngenes * ((P + 1) / 2) : items;
   // slabs a pair pass (or a gene block) may leave to the four-tile list pass
