@@ -2267,7 +2267,9 @@ constexpr int kBTileMax = 14;  // 32-point bound tiles, G <= 448
 #define SCDE_TILE_DIAG 0  // timing builds: 1 = bounds only, 2 = rows without bounds, 4 = no multiplicity loads,
                           // 8 = every column load from the entry-0 column (cache-resident); k_boot_gene:
                           // 16 = bounds replaced by -inf, 512 = no bound pass, 32 = no row loop, 64 = rows only (no
-                          // softmax / sums / rows out), 128 = bound pass loads only, 256 = bound pass without MFMA
+                          // softmax / sums / rows out), 128 = bound pass loads only, 256 = bound pass without MFMA;
+                          // epilogue parts: 1024 = no post-check, 2048 = no per-slab maxima (rows' maxima and
+                          // their combine), 4096 = no exps in the softmax, 8192 = no normalisers / partial rows
 #endif
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -3073,7 +3075,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   }
   // per-row f32 maxima (max is exact: the same m'_b as any other reduction order)
 #pragma unroll
-  for (int i = 0; i < NB; ++i) {
+  for (int i = 0; i < NB && !(SCDE_TILE_DIAG & 2048); ++i) {
     float m = (float)gt_max(a0[i], a1[i]);
     m = gt_maxf(m, dpp_f<kDppXor1>(m));
     m = gt_maxf(m, dpp_f<kDppXor2>(m));
@@ -3083,32 +3085,47 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   }
   __syncthreads();
   {
+    // the slab's rows: its K regular rows s K .. s K + K - 1, then the spare rows past K ns that
+    // the plan gave it (max is exact: any order gives the same m'_b)
     for (int x = threadIdx.x; x < ns * 32; x += 64 * WB) {
       const int s = x >> 5, i = x & 31;
       if (i < NB) {
         float m = -INFINITY;
-        for (int q2 = 0; q2 < kGeneRows; ++q2)
-          if (rowS[q2] == s) m = gt_maxf(m, rowmax[q2 * 32 + i]);
+        if (SCDE_TILE_DIAG & 2048) {
+          m = 0.0f;
+        } else {
+          for (int j = 0; j < K; ++j) m = gt_maxf(m, rowmax[(s * K + j) * 32 + i]);
+          for (int q2 = K * ns; q2 < kGeneRows; ++q2)
+            if (rowS[q2] == s) m = gt_maxf(m, rowmax[q2 * 32 + i]);
+        }
         fmx[s][i] = m;
       }
     }
     if ((int)threadIdx.x < ns) {  // the slab's computed bound tiles and the rows holding them
+      const int s = threadIdx.x;
       unsigned b = 0;
-      for (int q2 = 0; q2 < kGeneRows; ++q2)
-        if (rowS[q2] == (int)threadIdx.x) {
+      for (int q2 = s * K; q2 < s * K + K; ++q2) {
+        b |= 1u << rowT[q2];
+        rowof[s][rowT[q2]] = (signed char)q2;
+      }
+      for (int q2 = K * ns; q2 < kGeneRows; ++q2)
+        if (rowS[q2] == s) {
           b |= 1u << rowT[q2];
-          rowof[threadIdx.x][rowT[q2]] = (signed char)q2;
+          rowof[s][rowT[q2]] = (signed char)q2;
         }
-      bd[threadIdx.x] = b;
+      bd[s] = b;
     }
   }
   __syncthreads();
   // ---- 4. post-check per slab (wave w: slabs w, w + 4)
   for (int s = wsid; s < ns; s += WB) {
     const int nl = min(NB, nboot - (gb0 + s * NB));
+    // lane (bound tile lane & 15, boots lane >> 4, + 4, ...): four short chains instead of one
+    // 20-boot chain per tile (NTB <= 14 < 16)
+    const int tt = lane & 15;
     bool need = false;
-    if (lane < NTB && !((bd[s] >> lane) & 1))
-      for (int b = 0; b < nl; ++b) need |= (double)gub[lane * 128 + s * NB + b] >= (double)fmx[s][b] - 51.0;
+    if (!(SCDE_TILE_DIAG & 1024) && tt < NTB && !((bd[s] >> tt) & 1))
+      for (int b = lane >> 4; b < nl; b += 4) need |= (double)gub[tt * 128 + s * NB + b] >= (double)fmx[s][b] - 51.0;
     if (__ballot(need)) {
       if (lane == 0) {
         atomicOr(&failm, 1u << s);
@@ -3138,7 +3155,10 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     const double m = live ? (double)fmx[sq][i] : 0.0;
     const double d0 = a0[i] - m, d1 = a1[i] - m;
     const bool n0 = mine && l0 && d0 >= kBootExpCut, n1 = mine && l1 && d1 >= kBootExpCut;
-    if (__builtin_amdgcn_ballot_w64(n0 || n1)) {
+    if (SCDE_TILE_DIAG & 4096) {
+      a0[i] = n0 ? d0 : 0.0;
+      a1[i] = n1 ? d1 : 0.0;
+    } else if (__builtin_amdgcn_ballot_w64(n0 || n1)) {
       a0[i] = n0 ? exp_tab(d0, etab) : 0.0;
       a1[i] = n1 ? exp_tab(d1, etab) : 0.0;
     } else {
@@ -3149,7 +3169,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     if (m2 == 0 && live) tsum[(2 * q + (slot & 1)) * NB + i] = ps;
   }
   __syncthreads();
-  for (int x = threadIdx.x; x < ns * 32; x += 64 * WB) {
+  for (int x = threadIdx.x; x < ns * 32 && !(SCDE_TILE_DIAG & 8192); x += 64 * WB) {
     const int s = x >> 5, b = x & 31;
     if (b < NB && !((fm >> s) & 1)) {
       double S = 0.0;
@@ -3163,7 +3183,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     }
   }
   __syncthreads();
-  if (mine) {
+  if (mine && !(SCDE_TILE_DIAG & 8192)) {
     double* prow = part + (long long)(s0 + sq) * part_stride + (long long)g * GS;
     double j0 = 0.0, j1 = 0.0;
 #pragma unroll
