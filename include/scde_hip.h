@@ -149,6 +149,9 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   work (default 1): the modes piece by piece as each piece's tables finish, the
  *                   joint posterior in gene chunks of the bootstrap; 0: both after the bootstrap on
  *                   the main stream (rocprofv3 runs); results are the same
+ *   "gene_direct"   1/0  gene blocks that hold all of a gene's slabs write its joint-posterior row
+ *                   themselves when every slab passes its post-check (default 1), or leave every
+ *                   row to the slab-sum kernel (0); results are the same
  *   "ell_chunks"    0..64 cell chunks of the ELL-row build (default 1: one pass; 0 = by size, a
  *                   counting pass then a writing pass); results are the same
  *   "jp_chunks"     1..64 gene chunks of scde.posteriors' gene-block bootstrap (default 4, at most

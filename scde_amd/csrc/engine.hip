@@ -263,7 +263,7 @@ struct scde_ctx {
   // fixed-point bootstrap: byte multiplicities, flags/counters
   Buf w8, w8t, w8g, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
-  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide, ellw, excd;
+  Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide, ellw, excd, gdone;
   // options (scde_ctx_set_option): tuning and test switches, never read from the environment
   int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 20 + 0.15 C); tests force redo slabs
@@ -294,6 +294,8 @@ struct scde_ctx {
                                  // chunks) overlap the tables and the bootstrap from a read-back thread (0: after
                                  // the bootstrap, on the main stream -- rocprofv3 runs, where the pageable
                                  // read-back becomes blit kernels that would share the CUs)
+  int opt_gene_direct = 1;       // "gene_direct": gene blocks holding all of a gene's slabs write its jp row
+                                 // (k_sum_partials skips the gene)
   int opt_ell_chunks = 1;        // "ell_chunks": at most this many cell chunks in the ELL build (0: by size, two
                                  // passes; measured no faster: config 3 6.75-6.90 ms host -> host with one pass vs
                                  // 6.90 chunked, shard of 8 1.68 vs 1.72, configs 2 / 2b / 4 within noise)
@@ -625,7 +627,7 @@ struct scde_ctx {
                  &wp_stat,  &wp_out,     &wp_smooth, &wp_M,    &wp_W,     &pr_cell,   &pr_part,
                  &pr_occ,   &pr_stats,   &pr_hist, &pr_work,   &pr_out,   &pr_v,      &pr_sorted, &pr_sortw,
                  &pg_a,     &pg_b,       &pg_c,    &pg_d,      &pg_e,      &counts_in, &w8,
-                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide,  &ellw,  &excd};
+                 &w8t,      &w8g,      &qflags,  &gkey,     &gkey2,    &gidx,     &gorder,  &gwork,   &pmask,  &pwide,  &ellw,  &excd, &gdone};
     for (Buf* b : wp) b->release();
     for (auto& u : us) u.release();
     for (auto& u : upc) u.release();
@@ -1772,6 +1774,10 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (Ccall >= cx->opt_gene3_cells ? 3 : 4);
           tb.W8g = cx->w8g.as<unsigned char>();
           tb.chunks = std::max(1, cx->opt_boot_chunks);
+          if (cx->opt_gene_direct) {
+            HCHK(cx->gdone.ensure(sizeof(int) * std::max(1, NBg)));
+            tb.gdone = cx->gdone.as<int>();
+          }
         }
         if (have_order) tb.order = cx->gorder.as<int>();
         if (nchunks > 1) {
@@ -2108,6 +2114,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
   else if (n == "gene_blocks") ctx->opt_gene_blocks = value != 0;
   else if (n == "modes_overlap") ctx->opt_modes_overlap = value != 0;
+  else if (n == "gene_direct") ctx->opt_gene_direct = value != 0;
   else if (n == "ell_chunks") ctx->opt_ell_chunks = std::max(0, std::min(64, (int)value));
   else if (n == "jp_chunks") ctx->opt_jp_chunks = std::max(1, std::min(64, (int)value));
   else if (n == "upload_staged") ctx->opt_upload_staged = value != 0;
@@ -3086,6 +3093,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_tile_max_mult = cx->opt_tile_max_mult;
   p->opt_tile_order = cx->opt_tile_order;
   p->opt_ell_chunks = cx->opt_ell_chunks;
+  p->opt_gene_direct = cx->opt_gene_direct;
   p->opt_jp_chunks = cx->opt_jp_chunks;
   p->opt_unique_fixed = cx->opt_unique_fixed;
   p->opt_pair_cells = cx->opt_pair_cells;

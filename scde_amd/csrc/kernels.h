@@ -211,6 +211,10 @@ struct TileBootArgs {
   // gene chunks, each finished (list pass, fallback, slab sums) before the next, so its jp rows can
   // be read back while the next chunk runs; `order` then holds each chunk's genes sorted within it
   int g_lo = 0, g_hi = -1;
+  // gene blocks holding all of a gene's slabs (SG >= P): [ngenes] flags; a gene whose slabs all pass
+  // their post-checks gets its jp row from its block (summed in slab order, as k_sum_partials would)
+  // and flag 1, so k_sum_partials skips it (null: every row through k_sum_partials)
+  int* gdone = nullptr;
 };
 hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStream_t s);
 // gene order for the tile bootstrap: the keys launch_ell formed (per-gene count sums), sorted

@@ -2904,7 +2904,8 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8g, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int kcap, int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order,
-    unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap, int blk0) {
+    unsigned* __restrict__ pmask, int* __restrict__ wide, int wide_cap, int blk0, double* __restrict__ out,
+    long long out_g, long long out_k, int* __restrict__ gdone) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
   static_assert(WB == 3 || WB == 4, "3 or 4 waves per gene block");
   constexpr int kGeneRows = 4 * WB;
@@ -2933,6 +2934,12 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   const int gi = blk / NGR, gr = blk - gi * NGR;
   const int g = order ? order[gi] : gi;
   const int s0 = gr * SG, ns = min(SG, P - s0);
+  // direct rows (gdone: one block per gene, the slabs' rows fit the staging area): a gene whose
+  // slabs all pass their post-checks writes its jp row itself, summed over the slabs in slab order
+  // exactly as k_sum_partials adds the partial rows (tiles not computed as +0), and flags gdone[g]
+  // so that k_sum_partials leaves the gene alone
+  const bool direct = gdone && NGR == 1 && ns * ((G + 31) & ~31) * 8 <= (int)sizeof(bstage);
+  if (gdone && threadIdx.x == 0) gdone[g] = 0;
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
     if ((int)threadIdx.x < ns) {
       const int q = g * P + s0 + threadIdx.x;
@@ -3183,14 +3190,49 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     }
   }
   __syncthreads();
+  double j0 = 0.0, j1 = 0.0;
   if (mine && !(SCDE_TILE_DIAG & 8192)) {
-    double* prow = part + (long long)(s0 + sq) * part_stride + (long long)g * GS;
-    double j0 = 0.0, j1 = 0.0;
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
       j0 = fma(a0[i], finv[sq * 32 + i], j0);
       j1 = fma(a1[i], finv[sq * 32 + i], j1);
     }
+  }
+  if (direct && fm == 0u) {
+    // the slabs' rows in LDS ([slab][point], zeros where a slab computed no tile), then per point the
+    // sum over the slabs in order: the partial rows k_sum_partials would add, added the same way
+    const int GP = (G + 31) & ~31;
+    double* rows = reinterpret_cast<double*>(&bstage[0][0]);
+    __syncthreads();  // every lane's finv reads are done: the staging area is free
+    for (int x = threadIdx.x; x < ns * GP; x += 64 * WB) rows[x] = 0.0;
+    __syncthreads();
+    if (mine) {
+      if (l1)
+        *reinterpret_cast<d2_t*>(rows + sq * GP + k0) = d2_t{j0, j1};
+      else if (l0)
+        rows[sq * GP + k0] = j0;
+    }
+    __syncthreads();
+    double* orow = out + (long long)g * out_g;
+    for (int k = threadIdx.x; k < G; k += 64 * WB) {
+      double v = rows[k];
+      for (int p = 1; p < ns; ++p) v += rows[p * GP + k];
+      orow[(long long)k * out_k] = v;
+    }
+    if (threadIdx.x == 0) gdone[g] = 1;
+    if (stats && (int)threadIdx.x < ns) {
+      unsigned dn = 0;
+      for (unsigned mm = bd[threadIdx.x]; mm; mm &= mm - 1) dn |= 3u << (2 * (__builtin_ffs((int)mm) - 1));
+      dn &= (NT >= 32) ? ~0u : ((1u << NT) - 1);
+      atomicAdd(&stats[0], 1);
+      atomicAdd(&stats[1], __builtin_popcount(dn));
+      atomicAdd(&stats[2], NT);
+      atomicAdd(&stats[6 + __builtin_popcount(dn)], 1);
+    }
+    return;
+  }
+  if (mine && !(SCDE_TILE_DIAG & 8192)) {
+    double* prow = part + (long long)(s0 + sq) * part_stride + (long long)g * GS;
     if (l1)
       *reinterpret_cast<d2_t*>(prow + k0) = d2_t{j0, j1};
     else if (l0)
@@ -3366,10 +3408,11 @@ template __global__ void k_boot_tiles<20, 1>(const double* __restrict__, const i
 // are zeros, read as +0.0, so the sums are those of full rows.
 __global__ void k_sum_partials(const double* __restrict__ part, long long part_stride, int P, int ngenes, int G,
                                int GS, double* __restrict__ out, long long out_g, long long out_k,
-                               const unsigned* __restrict__ pmask) {
+                               const unsigned* __restrict__ pmask, const int* __restrict__ gdone) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)ngenes * G) return;
   const int g = (int)(i / G), k = (int)(i % G);
+  if (gdone && gdone[g]) return;  // k_boot_gene wrote the row itself
   const unsigned bit = 1u << (k >> 4);
   double s = (!pmask || (pmask[(long long)g * P] & bit)) ? part[(long long)g * GS + k] : 0.0;
   for (int p = 1; p < P; ++p)
@@ -4397,7 +4440,7 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
     if (e != hipSuccess) return e;
     const long long n = (long long)a.ngenes * a.G;
     hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                       a.G, a.GS, a.out, a.out_g, a.out_k, a.pmask);
+                       a.G, a.GS, a.out, a.out_g, a.out_k, a.pmask, nullptr);
     return hipGetLastError();
   }
 #define SCDE_B2(NBV)                                                                                              \
@@ -4422,7 +4465,7 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   if (e != hipSuccess) return e;
   const long long n = (long long)a.ngenes * a.G;
   hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                     a.G, a.GS, a.out, a.out_g, a.out_k, nullptr);
+                     a.G, a.GS, a.out, a.out_g, a.out_k, nullptr, nullptr);
   return hipGetLastError();
 }
 
@@ -4573,6 +4616,8 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(gspan * P, gene_cap) : 0;
   const long long gblocks = gene ? gspan * ((P + tb.SG - 1) / tb.SG) : 0;
   const long long gblk0 = gene ? (long long)g_lo * ((P + tb.SG - 1) / tb.SG) : 0;
+  // gene blocks holding all of a gene's slabs write the finished jp rows of their genes themselves
+  int* const gdone = (gene && tb.gdone && tb.SG >= P) ? tb.gdone : nullptr;
   // gene blocks in tb.chunks launches (>= 1): between launches the other lane's queued kernels
   // get CU slots that one long grid would hold until its last block is dispatched
   const long long chunk = std::max<long long>(1, (gblocks + std::max(1, tb.chunks) - 1) / std::max(1, tb.chunks));
@@ -4586,13 +4631,15 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
                              a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
                              a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
                              tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
-                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0));                       \
+                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0), a.out, a.out_g,        \
+                             a.out_k, gdone);                                                                      \
         else                                                                                                       \
           hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3(nblk), dim3(256), 0, s, a.D, a.ent, a.nnz,               \
                              a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
                              a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
                              tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
-                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0));                       \
+                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0), a.out, a.out_g,        \
+                             a.out_k, gdone);                                                                      \
       }                                                                                                            \
     else                                                                                                           \
     hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
@@ -4656,7 +4703,7 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if (nn > 0)
     hipLaunchKernelGGL(k_sum_partials, dim3(div_up(nn, 256)), dim3(256), 0, s, a.part + (long long)g_lo * a.GS,
                        a.part_stride, P, (int)gspan, a.G, a.GS, a.out + (long long)g_lo * a.out_g, a.out_g, a.out_k,
-                       tb.pmask + (long long)g_lo * P);
+                       tb.pmask + (long long)g_lo * P, gdone ? gdone + g_lo : nullptr);
   return hipGetLastError();
 }
 

@@ -62,6 +62,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("task_cols", opts.get("task_cols", 0))
     ctx.set_option("boot2_rows", opts.get("boot2_rows", 0))
     ctx.set_option("ell_chunks", opts.get("ell_chunks", 1))
+    ctx.set_option("gene_direct", opts.get("gene_direct", 1))
     ctx.set_option("skip_stats", 1)
     ctx.reset_stats()
     api.set_rand("glibc")
@@ -98,6 +99,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("task_cols", 0)
         ctx.set_option("boot2_rows", 0)
         ctx.set_option("ell_chunks", 1)
+        ctx.set_option("gene_direct", 1)
         ctx.set_option("skip_stats", 0)
     return out, stats
 
@@ -129,6 +131,8 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         # the ELL rows built in cell chunks (two passes) and in chunks of at most 2
         "ell-chunked": {"ell_chunks": 0},
         "ell-chunks2": {"ell_chunks": 2},
+        # every jp row through k_sum_partials (gene blocks write their genes' rows themselves by default)
+        "gene-direct-off": {"gene_direct": 0},
         "unique-exact": {"unique_fixed": 0},
         # the two group posteriors fused into one (option fuse_groups) against the two-posterior paths
         "fused": {"fuse_groups": 1},
