@@ -316,7 +316,9 @@ struct scde_ctx {
   int opt_piece_taper = 0;      // "piece_taper": pieces of decreasing size (weights K, K - 1, .., 1), so the
                                 // last piece -- whose unique sets and tables follow the last byte -- is short
                                 // (measured slower: config 3 6.95-6.99 vs 6.62-6.67 ms, config 4 19.5-22.6 vs
-                                // 16.1-16.3 host -> host: the large first pieces delay the start)
+                                // 16.1-16.3 host -> host: the large first pieces delay the start); 2:
+                                // increasing sizes 1, 2, .., K (measured equal: config 4 15.6-16.1 vs
+                                // 15.8-16.1, config 3 6.55-6.56 vs 6.55-6.65)
   int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
                                 // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
                                 // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
@@ -2130,7 +2132,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "gene_rows") ctx->opt_gene_rows = std::max(1, std::min(4, (int)value));
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
-  else if (n == "piece_taper") ctx->opt_piece_taper = value != 0;
+  else if (n == "piece_taper") ctx->opt_piece_taper = (value == 1 || value == 2) ? (int)value : 0;
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
   else if (n == "lane_prio") ctx->opt_lane_prio = value != 0;
   else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
@@ -2905,9 +2907,11 @@ struct UploadWorker {
 // bound j (0..K) of K pieces over [0, total): equal pieces, or with taper decreasing ones
 // (weights K, K - 1, .., 1: the last piece, whose unique sets and tables start only after the
 // last byte has landed, is the smallest)
-static long long piece_bound(long long total, int j, int K, bool taper) {
+static long long piece_bound(long long total, int j, int K, int taper) {
   if (!taper) return total * j / K;
-  const long long tw = (long long)K * (K + 1) / 2, w = (long long)j * K - (long long)j * (j - 1) / 2;
+  const long long tw = (long long)K * (K + 1) / 2;
+  const long long w = taper == 1 ? (long long)j * K - (long long)j * (j - 1) / 2  // K, K - 1, .., 1
+                                 : (long long)j * (j + 1) / 2;                      // 1, 2, .., K
   return total * w / tw;
 }
 
@@ -3331,7 +3335,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       const std::vector<int>& ix = idx[first];
       for (int j = 0; j <= K; ++j) {
         // (interleaved: equal pieces, paired with the second group's)
-        const int a = (int)piece_bound(up->cut, j, K, ctx->opt_piece_taper && !inter);
+        const int a = (int)piece_bound(up->cut, j, K, inter ? 0 : ctx->opt_piece_taper);
         cols.push_back(a);
         piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
       }
