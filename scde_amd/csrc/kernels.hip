@@ -1221,7 +1221,14 @@ __global__ void k_base_cols(const int* __restrict__ ucl, const long long* __rest
 #ifndef SCDE_ELL_KEY_RANK
 #define SCDE_ELL_KEY_RANK 0
 #endif
-constexpr int kEllWaves = 16;
+// waves per 64-gene block (4, 8 or 16).  8: blocks of 512 threads find room beside the tables
+// kernel's blocks (the ELL rows run on the aux stream during phase 2); measured against 16, one box,
+// alternating runs: shard of 8 device-resident 1.36-1.60 vs 1.43-1.46 ms, config 4 14.07-14.11 vs
+// 14.20-14.25, config 3 equal; 4 waves slower (config 3 6.77-6.93 vs 6.55-6.68 host -> host)
+#ifndef SCDE_ELL_WAVES
+#define SCDE_ELL_WAVES 8
+#endif
+constexpr int kEllWaves = SCDE_ELL_WAVES;
 constexpr int kEllMaxChunks = 64;
 constexpr int kEllKeyBits = 16;  // gene-order key width (launch_gene_order sorts these bits)
 template <bool WRITE>
