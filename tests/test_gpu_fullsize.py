@@ -109,6 +109,30 @@ def test_config4_1000_gene_slice_modes(api):
                                       return_individual_posterior_modes=True, n_cores=1)
             np.testing.assert_array_equal(pip["jp"], got["jp"], err_msg=f"pieces {pieces} chunks {chunks}")
             np.testing.assert_array_equal(pip["modes"], got["modes"], err_msg=f"pieces {pieces} chunks {chunks}")
+        # the device-resident entry (counts in HBM; its jp read back in gene chunks, its modes once
+        # the tables are done) gives the same bits
+        import ctypes
+        from scde_amd._lib import check, lib
+        from scde_amd.models import model_matrix
+        mm, lt, sq = model_matrix(models)
+        px = np.ascontiguousarray(prior["x"], np.float64)
+        N, C = sub.shape
+        cellidx = np.arange(C, dtype=np.int32)
+        P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        dc = api.DeviceCounts(ctx, sub)
+        try:
+            for chunks, overlap in ((4, 1), (1, 1), (4, 0)):
+                ctx.set_option("jp_chunks", chunks)
+                ctx.set_option("modes_overlap", overlap)
+                jp = np.zeros((N, len(px)), order="F")
+                modes = np.zeros((N, C), order="F")
+                api.set_rand("glibc")
+                check(lib().scde_posteriors_dev(ctx.handle, dc.ptr, N, N, P(cellidx), C, P(mm), lt, sq, P(px), len(px),
+                                                100, 1, 0, N, 1, 0, None, None, None, 0, P(jp), P(modes), None))
+                np.testing.assert_array_equal(jp, got["jp"], err_msg=f"device entry, chunks {chunks}")
+                np.testing.assert_array_equal(modes, got["modes"], err_msg=f"device entry, chunks {chunks}")
+        finally:
+            dc.free()
     finally:
         ctx.set_option("pipeline_mb", 32)
         ctx.set_option("pieces", 4)
