@@ -42,12 +42,15 @@ def oracle_shard(models, counts_shard, prior, codes, nrand, n_cores, expectation
     return np.column_stack([r[k] for k in ("lb", "mle", "ub", "ce", "Z")])
 
 
-def _worker(rank, world, port, out_path, hip=False):
+def _worker(rank, world, port, out_path, hip=False, backend="gloo"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    if hip:
+    if hip and backend == "gloo":
         os.environ["SCDE_SAME_DEVICE"] = "1"  # every rank on the one GPU of the box
     import torch.distributed as dist
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        import torch
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     try:
         from scde_amd import api, sharded
         models, counts, prior, groups = _inputs()
@@ -148,3 +151,24 @@ def test_gloo_hip_shards_match_single_process(tmp_path):
     np.testing.assert_array_equal(got[:, :4], want[:, :4])
     assert_z_close(got[:, 4], want[:, 4], what="gloo HIP shards Z")
     assert_cz_close(got[:, 5], want[:, 5], got[:, 4], want[:, 4], what="gloo HIP shards cZ")
+
+
+@pytest.mark.gpu
+def test_nccl_single_rank_device_gather(tmp_path):
+    """The RCCL branch of the sharded call (device tensors gathered under the nccl backend, cZ by
+    the device BH on rank 0's GPU), run with one rank on the box's one GPU -- RCCL does not
+    allow two ranks on one device, so the multi-rank RCCL gather runs only on an 8-GPU node.
+    The table equals the single-process HIP call."""
+    import torch.multiprocessing as mp
+    from scde_amd import api
+    out = str(tmp_path / "tab.npy")
+    mp.spawn(_worker, args=(1, _free_port(), out, True, "nccl"), nprocs=1, join=True)
+    got = np.load(out)
+    models, counts, prior, groups = _inputs()
+    api.set_rand("glibc")
+    ref = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=NRAND,
+                                         n_cores=NCORES)
+    want = ref[["lb", "mle", "ub", "ce", "Z", "cZ"]].to_numpy()
+    np.testing.assert_array_equal(got[:, :4], want[:, :4])
+    assert_z_close(got[:, 4], want[:, 4], what="RCCL single-rank Z")
+    assert_cz_close(got[:, 5], want[:, 5], got[:, 4], want[:, 4], what="RCCL single-rank cZ")
