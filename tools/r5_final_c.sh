@@ -7,3 +7,4 @@ cp profiles/r05_config3_* gpurun_out/fin5/
 CFGS="3" PROF_CFGS=" " bash tools/r5_final_b.sh || exit 1
 timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_dist.py -m gpu > gpurun_out/fin5/dist.log 2>&1 || { tail -30 gpurun_out/fin5/dist.log; exit 1; }
 tail -3 gpurun_out/fin5/dist.log
+timeout -k 10 700 bash tools/r5_nt.sh || exit 1
