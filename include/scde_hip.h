@@ -149,6 +149,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   work (default 1): the modes piece by piece as each piece's tables finish, the
  *                   joint posterior in gene chunks of the bootstrap; 0: both after the bootstrap on
  *                   the main stream (rocprofv3 runs); results are the same
+ *   "tables_nt"     0..2 the posterior-table rows as non-temporal stores: 0 never, 1 always, 2 when
+ *                   the call's rows exceed 256 MB (default); results are the same
  *   "gene_direct"   1/0  gene blocks that hold all of a gene's slabs write its joint-posterior row
  *                   themselves when every slab passes its post-check (default 1), or leave every
  *                   row to the slab-sum kernel (0); results are the same

@@ -332,6 +332,7 @@ struct scde_ctx {
   int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
                                 // the second group's tables
   int opt_tables_pair = 1;       // "tables_pair": k_tables_reg computes a wave's columns two at a time (0: one)
+  int opt_tables_nt = 2;         // "tables_nt": table rows as non-temporal stores (0 no, 1 yes, 2 when the call's rows exceed 256 MB)
   int opt_task_cols = 0;         // "task_cols": columns per tables task (0: 32 for launches under 4096
                                  // 64-column tasks, else 64; at most kTabTaskCols)
   int opt_boot2_rows = 0;        // "boot2_rows": the stretch-mask bootstrap (below boot_tiles_cells) on tile rows
@@ -1269,6 +1270,9 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     ta.minlogprob2 = -1 * DBL_MAX / (s.ngroups == 2 ? C - s.gsplit : C) / 1.1;
     ta.mlp_split = s.ngroups == 2 ? s.gsplit : C;
     ta.pair_cols = cx->opt_tables_pair;
+    // rows that fit the 256 MB last-level cache can be read back from it by the bootstrap: plain
+    // stores there
+    ta.nt_rows = cx->opt_tables_nt == 1 || (cx->opt_tables_nt == 2 && (double)ncap * GS * sizeof(double) > 256.0 * (1 << 20));
     ta.T = p.keep_T ? cx->T.as<double>() : nullptr;
     ta.maxi = want_maxi ? cx->maxi.as<int>() : nullptr;
     ta.has_clamp = cx->has_clamp.as<unsigned char>();
@@ -2143,6 +2147,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "boot2_rows") ctx->opt_boot2_rows = value != 0;
   else if (n == "task_cols") ctx->opt_task_cols = std::max(0, (int)value);
   else if (n == "tables_pair") ctx->opt_tables_pair = value != 0;
+  else if (n == "tables_nt") ctx->opt_tables_nt = std::min(2, std::max(0, (int)value));
   else if (n == "boot_chunks") ctx->opt_boot_chunks = std::max(1, std::min((int)value, 64));
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
@@ -3142,6 +3147,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_boot2_rows = cx->opt_boot2_rows;
   p->opt_task_cols = cx->opt_task_cols;
   p->opt_tables_pair = cx->opt_tables_pair;
+  p->opt_tables_nt = cx->opt_tables_nt;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;

@@ -76,6 +76,8 @@ struct TablesArgs {
   int mlp_split;
   // k_tables_reg takes a wave's columns two at a time (0: one at a time; the same bits either way)
   int pair_cols;
+  // k_tables_reg writes its rows (T, D) as non-temporal stores (the same bits)
+  int nt_rows;
   double* T;                 // [ncols][GS] log-posterior columns
   int* maxi;                 // [ncols] argmax (nullable)
   unsigned char* has_clamp;  // [ncols]

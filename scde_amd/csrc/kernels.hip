@@ -675,18 +675,15 @@ enum { kRowMu = 0, kRowP = 1, kRowLP = 3, kRowLQ = 4, kRowLcfpr = 5, kRowCfp = 6
 enum { kBoundNone = 0, kBoundTiles = 1, kBoundStretch = 2 };  // k_tables_reg's bound output
 // GC: the grid length as a compile-time constant (401, the default prior grid), so the
 // chunk masks fold away; 0 = a.G at run time
-#ifndef SCDE_TABREG_NT
-#define SCDE_TABREG_NT 1  // k_tables_reg's T/D rows as non-temporal stores (0: plain stores; the same bits)
-#endif
-// The rows are 1.8 GB per config-3 step, read back by the bootstrap long after L2 has turned over:
-// streaming them past the cache took config 3 from 6.40-6.55 to 6.33-6.46 ms per step (5 of 5
-// alternating A/B pairs on one box, tables 1.25 -> 1.23 ms).
-__device__ __forceinline__ void tab_store(double* p, double v) {
-#if SCDE_TABREG_NT
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
+// k_tables_reg's T/D rows as non-temporal stores when a.nt_rows (option tables_nt): 1.8 GB per
+// config-3 step, read back by the bootstrap long after the caches have turned over (A/B: config 3
+// faster in 7 of 9 alternating pairs, at the box-noise level).  Smaller calls keep
+// plain stores (engine: rows that fit the last-level cache).  nt is kernel-uniform.
+__device__ __forceinline__ void tab_store(double* p, double v, int nt) {
+  if (nt)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
 }
 
 template <int BM, int GC>
@@ -864,8 +861,8 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       nanq = nanq || (in && r != r);
       // unconditional stores: lanes past the grid write the pad zeros (k < GS always)
       if (!(SCDE_KT_DIAG & 8)) {
-        if (out) tab_store(out + k, in ? r : 0.0);
-        if (dout) tab_store(dout + k, in ? (have_base ? r - sl[kRowBase * kRS + 64 * j] : r) : 0.0);
+        if (out) tab_store(out + k, in ? r : 0.0, a.nt_rows);
+        if (dout) tab_store(dout + k, in ? (have_base ? r - sl[kRowBase * kRS + 64 * j] : r) : 0.0, a.nt_rows);
       } else if (r == 12345.0) {
         dout[k] = r;
       }
@@ -1055,8 +1052,8 @@ __device__ __forceinline__ void tables_column_reg2(const TablesArgs& a, long lon
         clamp[q] = clamp[q] || (cl && in);
         nanq[q] = nanq[q] || (in && r != r);
         // unconditional stores: lanes past the grid write the pad zeros (k < GS always)
-        if (out[q]) tab_store(out[q] + k, in ? r : 0.0);
-        if (dout[q]) tab_store(dout[q] + k, in ? (have_base ? r - base : r) : 0.0);
+        if (out[q]) tab_store(out[q] + k, in ? r : 0.0, a.nt_rows);
+        if (dout[q]) tab_store(dout[q] + k, in ? (have_base ? r - base : r) : 0.0, a.nt_rows);
         r = in ? r : -INFINITY;
         if (BM == kBoundTiles) {
           int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));

@@ -59,6 +59,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("boot_chunks", opts.get("boot_chunks", 1))
     ctx.set_option("fuse_groups", opts.get("fuse_groups", 0))
     ctx.set_option("tables_pair", opts.get("tables_pair", 1))
+    ctx.set_option("tables_nt", opts.get("tables_nt", 2))
     ctx.set_option("task_cols", opts.get("task_cols", 0))
     ctx.set_option("boot2_rows", opts.get("boot2_rows", 0))
     ctx.set_option("ell_chunks", opts.get("ell_chunks", 1))
@@ -96,6 +97,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("boot_chunks", 1)
         ctx.set_option("fuse_groups", 0)
         ctx.set_option("tables_pair", 1)
+        ctx.set_option("tables_nt", 2)
         ctx.set_option("task_cols", 0)
         ctx.set_option("boot2_rows", 0)
         ctx.set_option("ell_chunks", 1)
@@ -157,6 +159,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         "stretch-k_boot2t-redo": {"boot_tiles": 0, "boot2_rows": 1, "skip_slack": -45.0},
         # the tables one column per wave, and in 64- and 16-column tasks
         "tables-single": {"tables_pair": 0},
+        # the table rows as non-temporal stores (the default only above 256 MB of rows)
+        "tables-nt": {"tables_nt": 1},
+        "tables-nt-single": {"tables_nt": 1, "tables_pair": 0},
         "tables-tasks64": {"task_cols": 64},
         "tables-tasks16": {"task_cols": 16},
     }
