@@ -166,8 +166,8 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   partials, joint posterior: about 2.3 GB at 20k genes x 500 cells per group,
  *                   DESIGN.md section 3), so two lanes roughly double a DE call's device
  *                   footprint; setting 1 releases the peer and its workspace
- *   "lane_prio"     1/0  the peer lane's streams at the device's highest priority (default 0; set
- *                   before the first DE call)
+ *   "lane_prio"     0..2 the peer lane's streams at the device's highest priority: 0 never (default),
+ *                   1 always, 2 for DE calls of at most 8,192 genes (per call); results are the same
  *   "pipeline_mb"   host-count DE / scde.posteriors calls whose matrix has at least this many MB
  *                   upload on a copy stream in column pieces that the kernels follow (default 32)
  *   "pieces"        pieces of that upload (the DE call's first group; the posteriors call's

@@ -240,6 +240,10 @@ struct scde_ctx {
   // order) needs only the count-0 columns: it runs on aux_stream after p1_ev (phase 1 of the
   // tables), beside phase 2, and the bootstrap waits for aux_ev
   hipStream_t aux_stream = nullptr;
+  // the peer lane's parked stream set (main, aux) of the other priority (peer_set_prio)
+  hipStream_t alt_stream = nullptr, alt_aux = nullptr;
+  bool prio_hi = false;
+  hipEvent_t prio_ev[2] = {nullptr, nullptr};
   hipEvent_t p1_ev = nullptr, aux_ev = nullptr;
   // Pinned staging arena for the small per-call transfers (cell lists, offsets, draws,
   // multiplicities, tasks; the unique builder's size read-backs).  A pageable copy is staged
@@ -319,9 +323,11 @@ struct scde_ctx {
                                 // 16.1-16.3 host -> host: the large first pieces delay the start); 2:
                                 // increasing sizes 1, 2, .., K (measured equal: config 4 15.6-16.1 vs
                                 // 15.8-16.1, config 3 6.55-6.56 vs 6.55-6.65)
-  int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority (set
-                                // before the peer's first use; measured no faster: config 3 7.98-8.17 vs
-                                // 7.95-8.02 ms, shard of 8 1.83-1.88 vs 1.80-1.81)
+  int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority: 0
+                                // never (default), 1 always, 2 for calls of at most kPrioGenes genes (per
+                                // call: the peer keeps a stream set per priority).  Measured on two boxes
+                                // with opposite results at the shard of 8 (1 vs 0: 1.58-1.61 vs 1.68 ms; 2
+                                // vs 0: 1.81-1.85 vs 1.60-1.66), slower at config 3
   int opt_boot_chunks = 1;      // "boot_chunks": k_boot_gene's grid in this many launches
   int opt_rest_thread = 1;      // "rest_thread": a two-lane DE call on counts in HBM runs the second group's
                                 // draws, set-up and bootstrap launch from a host thread of its own
@@ -652,6 +658,10 @@ struct scde_ctx {
     if (p1_ev) (void)hipEventDestroy(p1_ev);
     if (aux_ev) (void)hipEventDestroy(aux_ev);
     if (aux_stream) (void)hipStreamDestroy(aux_stream);
+    if (alt_stream) (void)hipStreamDestroy(alt_stream);
+    if (alt_aux) (void)hipStreamDestroy(alt_aux);
+    for (auto& e : prio_ev)
+      if (e) (void)hipEventDestroy(e);
     if (pin) (void)hipHostFree(pin);
     if (stg.pin) (void)hipHostFree(stg.pin);
     for (auto& e : stg.ev)
@@ -2138,7 +2148,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
   else if (n == "piece_taper") ctx->opt_piece_taper = (value == 1 || value == 2) ? (int)value : 0;
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
-  else if (n == "lane_prio") ctx->opt_lane_prio = value != 0;
+  else if (n == "lane_prio") ctx->opt_lane_prio = std::min(2, std::max(0, (int)value));
   else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
   else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
   else if (n == "interleave") ctx->opt_interleave = value != 0;
@@ -3100,27 +3110,48 @@ static int run_rests(scde_ctx* ctx, const std::function<int()>& rest0, const std
   return SCDE_OK;
 }
 
-static int lane_peer(scde_ctx* cx, scde_ctx** out) {
+// The peer lane's streams at the device's highest priority (hi) or at the default one.  The peer
+// keeps one (main, aux) set per priority; switching parks the current set and brings in the other,
+// whose streams first wait for everything queued on the parked set (between calls, so `stream` is
+// the home stream).  The aux stream of a set is created on first use with `stream_prio`.
+static int peer_set_prio(scde_ctx* p, bool hi) {
+  if (p->prio_hi == hi) return SCDE_OK;
+  int lo = 0, top = 0;
+  HCHK(hipDeviceGetStreamPriorityRange(&lo, &top));
+  const int want = hi ? top : 0;
+  if (!p->alt_stream) HCHK(hipStreamCreateWithPriority(&p->alt_stream, hipStreamNonBlocking, want));
+  for (auto& e : p->prio_ev)
+    if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HCHK(hipEventRecord(p->prio_ev[0], p->stream));
+  HCHK(hipEventRecord(p->prio_ev[1], p->aux_stream ? p->aux_stream : p->stream));
+  for (hipStream_t s : {p->alt_stream, p->alt_aux}) {
+    if (!s) continue;
+    HCHK(hipStreamWaitEvent(s, p->prio_ev[0], 0));
+    HCHK(hipStreamWaitEvent(s, p->prio_ev[1], 0));
+  }
+  std::swap(p->stream, p->alt_stream);
+  std::swap(p->aux_stream, p->alt_aux);
+  p->home_stream = p->stream;
+  p->stream_prio = want;
+  p->prio_hi = hi;
+  return SCDE_OK;
+}
+
+// ngenes: the call's genes (the lane_prio rule)
+static int lane_peer(scde_ctx* cx, scde_ctx** out, int ngenes) {
   if (!cx->peer) {
     scde_ctx* p = nullptr;
     RCHK(scde_ctx_create(cx->device, &p));
     cx->peer = p;
-    // the peer lane starts later than the first group (its counts and unique sets come
-    // second) and its small set-up kernels would queue behind the first group's bootstrap
-    // waves: its streams get the device's highest priority
-    if (cx->opt_lane_prio) {
-      int lo = 0, hi = 0;
-      HCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      p->stream_prio = hi;
-      HCHK(hipStreamDestroy(p->stream));
-      p->stream = nullptr;
-      HCHK(hipStreamCreateWithPriority(&p->stream, hipStreamNonBlocking, hi));
-      p->home_stream = p->stream;
-    }
     for (auto& e : cx->lane_ev)
       if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   scde_ctx* p = cx->peer;
+  // the peer lane starts later than the first group (its counts and unique sets come second) and
+  // its small set-up kernels would queue behind the first group's bootstrap waves: on small calls
+  // its streams get the device's highest priority
+  constexpr int kPrioGenes = 8192;
+  RCHK(peer_set_prio(p, cx->opt_lane_prio == 1 || (cx->opt_lane_prio == 2 && ngenes <= kPrioGenes)));
   p->opt_boot_skip = cx->opt_boot_skip;
   p->opt_skip_slack = cx->opt_skip_slack;
   p->opt_boot_nb = cx->opt_boot_nb;
@@ -3338,7 +3369,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
   }
   if (!fused_done) {
     scde_ctx* lane = ctx;  // the context that runs the second group's posterior
-    if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
+    if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane, ngenes));
     if (up) {
       // group by group, each after its columns have arrived (the first range ends with the
       // last cell of the group whose cells end first)
@@ -3678,7 +3709,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     RCHK(build_unique_sets(ctx, sp, up, 3));
   }
   scde_ctx* lane = ctx;  // the second batch posterior and the second group's run on the peer lane
-  if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
+  if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane, N));
   if (lane != ctx) {
     HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
     HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));

@@ -60,6 +60,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
     ctx.set_option("fuse_groups", opts.get("fuse_groups", 0))
     ctx.set_option("tables_pair", opts.get("tables_pair", 1))
     ctx.set_option("tables_nt", opts.get("tables_nt", 2))
+    ctx.set_option("lane_prio", opts.get("lane_prio", 0))
     ctx.set_option("task_cols", opts.get("task_cols", 0))
     ctx.set_option("boot2_rows", opts.get("boot2_rows", 0))
     ctx.set_option("ell_chunks", opts.get("ell_chunks", 1))
@@ -98,6 +99,7 @@ def _run(api, opts, models, counts, prior, groups, nrand, ncores):
         ctx.set_option("fuse_groups", 0)
         ctx.set_option("tables_pair", 1)
         ctx.set_option("tables_nt", 2)
+        ctx.set_option("lane_prio", 0)
         ctx.set_option("task_cols", 0)
         ctx.set_option("boot2_rows", 0)
         ctx.set_option("ell_chunks", 1)
@@ -162,6 +164,9 @@ def test_skip_modes_match_oracle(api, oracle, seed, ngenes, ncells, nrand, ncore
         # the table rows as non-temporal stores (the default only above 256 MB of rows)
         "tables-nt": {"tables_nt": 1},
         "tables-nt-single": {"tables_nt": 1, "tables_pair": 0},
+        # the peer lane at the highest stream priority, always and per call (these calls are small)
+        "lane-prio-on": {"lane_prio": 1},
+        "lane-prio-auto": {"lane_prio": 2},
         "tables-tasks64": {"task_cols": 64},
         "tables-tasks16": {"task_cols": 16},
     }
