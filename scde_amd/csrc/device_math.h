@@ -250,6 +250,33 @@ __device__ __forceinline__ double exp_tab(double d, const double* __restrict__ t
   return ldexp(fma(t, em1, t), k >> 6);
 }
 
+// exp for d in [-746, 0] without a table (k_tables_lpc, where the table read's per-lane index would
+// put an LDS round trip with bank conflicts in every point's chain): exp(d) = 2^n e^r, n = rint(d / ln 2),
+// r = d - n ln 2 (Cody-Waite: n ln2_hi exact for |n| < 2^21), |r| <= 0.347, e^r by its degree-13
+// Taylor polynomial (truncation < 5e-18 relative), ldexp for 2^n (subnormal results round once).
+// exp(0) is exactly 1.  19 VALU slots, <= 2 ulp.
+__device__ __forceinline__ double exp_poly(double d) {
+  const double kd = __builtin_rint(d * 1.4426950408889634);
+  const int n = (int)kd;
+  double r = fma(kd, -6.93147180369123816490e-01, d);
+  r = fma(kd, -1.90821492927058770002e-10, r);
+  double p = 1.0 / 6227020800.0;
+  p = fma(p, r, 1.0 / 479001600.0);
+  p = fma(p, r, 1.0 / 39916800.0);
+  p = fma(p, r, 1.0 / 3628800.0);
+  p = fma(p, r, 1.0 / 362880.0);
+  p = fma(p, r, 1.0 / 40320.0);
+  p = fma(p, r, 1.0 / 5040.0);
+  p = fma(p, r, 1.0 / 720.0);
+  p = fma(p, r, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, n);
+}
+
 // log for positive normal x (other inputs fall back to the library log): x = m 2^e with
 // m in [0.75, 1.5); 97 intervals centred on c_j = 0.75 + j/128 (the one around 1 has
 // c = 1 exactly, so r = m - 1 is exact there and results near 0 keep full relative

@@ -349,12 +349,14 @@ struct scde_ctx {
                                  // concatenated cells, doubled genes, one launch per stage; same bits).  Off:
                                  // measured no faster than the two lanes (config 3 host -> host 7.20 vs 6.80 ms,
                                  // shard of 8 1.69 vs 1.66)
+  int opt_boot_gate = 1;         // "boot_gate": two lanes' bootstraps wait for both lanes' set-up chains (BootGate)
   int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                  // group on `peer`, its own streams and workspace) or one after the other (1)
   // the second lane of a DE call: a context on the same device, created on first use; its
   // options are copied from this one per call and its timings/statistics merged back
   scde_ctx* peer = nullptr;
   hipEvent_t lane_ev[2] = {nullptr, nullptr};  // [0] this stream -> peer, [1] peer -> this stream
+  hipEvent_t gate_ev[2] = {nullptr, nullptr};  // BootGate: each lane's set-up chain done
   hipEvent_t piece_ev[8] = {nullptr};           // run_posterior's pieces: unique sets built
   hipEvent_t piece_up_ev[8] = {nullptr};        // the pieces' uploads landed (upload worker)
   hipStream_t uq_stream = nullptr;              // the pieces' and the second group's unique builds
@@ -627,6 +629,8 @@ struct scde_ctx {
     }
     for (auto& e : lane_ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : gate_ev)
+      if (e) (void)hipEventDestroy(e);
     for (auto& e : piece_ev)
       if (e) (void)hipEventDestroy(e);
     for (auto& e : piece_up_ev)
@@ -754,6 +758,39 @@ hipError_t ctx_streams_sync(scde_ctx* cx) {
 namespace {
 
 // ------------------------------------------------------------------ posterior spec
+// Two lanes' bootstraps start only once both lanes' set-up chains are queued and done: each lane's
+// continuation records its set-up's end on its stream, waits (host) for the other lane to do the
+// same, and makes its stream wait for the other lane's event before its bootstrap launch.  Without it
+// the lane whose set-up comes second has its small kernels (ELL rows, order sort, multiplicities,
+// bounds) queued beside the first lane's bootstrap waves, which starve them.
+// A lane that ends without reaching its bootstrap (an error, no bootstrap) leaves the gate, so the
+// other never waits for it.
+struct BootGate {
+  std::mutex m;
+  std::condition_variable cv;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  bool rec[2] = {false, false}, gone[2] = {false, false};
+  // slot's set-up chain ends here on stream st; returns once the other lane has arrived or left
+  int arrive(int slot, hipStream_t st) {
+    const hipError_t e = hipEventRecord(ev[slot], st);
+    std::unique_lock<std::mutex> lk(m);
+    rec[slot] = e == hipSuccess;
+    gone[slot] = true;
+    cv.notify_all();
+    cv.wait(lk, [&] { return gone[1 - slot]; });
+    const bool wait_other = rec[1 - slot];
+    lk.unlock();
+    if (e != hipSuccess) return fail(SCDE_EHIP, "hipEventRecord: %s", hipGetErrorString(e));
+    if (wait_other) HCHK(hipStreamWaitEvent(st, ev[1 - slot], 0));
+    return SCDE_OK;
+  }
+  void leave(int slot) {
+    std::lock_guard<std::mutex> lk(m);
+    gone[slot] = true;
+    cv.notify_all();
+  }
+};
+
 struct PostSpec {
   int ncells = 0;
   const double* models = nullptr;  // host ncells x 12 col-major
@@ -794,6 +831,8 @@ struct PostSpec {
   // reached the point it recorded; run_posterior builds each piece's unique sets on
   // piece_stream and launches its tables as it arrives (piece_ev: one event per piece)
   int npieces = 0;
+  BootGate* gate = nullptr;  // two lanes' deferred continuations: arrive before the bootstrap launch
+  int gate_slot = 0;
   const int* piece_c = nullptr;
   std::function<int(int)> piece_ready;
   hipStream_t piece_stream = nullptr;
@@ -1329,14 +1368,13 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     if (tc.base_col) tc.base_col = ta.base_col + c0;
     tc.col_base = (int)col0;
     tc.mlp_split = ta.mlp_split - c0;  // relative to the launch's first cell
-    // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell (8 per wave)
+    // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell -- one lane per column in
+    // k_tables_lpc (constant theta); with local theta (k_tables_cell, 8 columns per wave) a launch that
+    // would fill fewer than 4 rounds of the chip's block slots takes 32-column tasks, so its last
+    // round is shorter
     if (G <= 448 && nc > 0) {
-      // tasks of up to 64 columns of one cell (the kernel stages at most kTabTaskCols); a launch
-      // that would fill fewer than 4 rounds of the chip's block slots (~1,000 four-wave blocks
-      // per round) takes 32-column tasks, so its last round is shorter (small shards, pieces)
       const long long kTaskCols =
-          (cx->opt_task_cols > 0) ? std::min<long long>(cx->opt_task_cols, kTabTaskCols)
-                                  : ((nc / kTabTaskCols < 4096) ? std::min(32, kTabTaskCols) : kTabTaskCols);
+          (!s.localtheta || nc / kTabTaskCols >= 4096) ? kTabTaskCols : std::min(32, kTabTaskCols);
       tu.tasks_h.clear();
       for (int c = 0; c < Cc; ++c)
         for (long long b = off_h[c]; b < off_h[c + 1]; b += kTaskCols)
@@ -1719,6 +1757,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       exact_done = true;
       return SCDE_OK;
     };
+    if (s.gate) RCHK(s.gate->arrive(s.gate_slot, st));
     ev = cx->mark_begin(SLOT_BOOT);
     if (fast) {
       Boot2Args b2{};
@@ -2153,6 +2192,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
   else if (n == "interleave") ctx->opt_interleave = value != 0;
   else if (n == "rest_thread") ctx->opt_rest_thread = value != 0;
+  else if (n == "boot_gate") ctx->opt_boot_gate = value != 0;
   else if (n == "fuse_groups") ctx->opt_fuse_groups = value != 0;
   else if (n == "boot2_rows") ctx->opt_boot2_rows = value != 0;
   else if (n == "task_cols") ctx->opt_task_cols = std::max(0, (int)value);
@@ -3091,18 +3131,42 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
 // does not queue behind the first lane's host-side set-up and bootstrap launch and the two
 // bootstraps can overlap; else one after the other.  (Each continuation touches only its own
 // context's buffers and streams; a shared unique set is read-only there.)
-static int run_rests(scde_ctx* ctx, const std::function<int()>& rest0, const std::function<int()>& rest1) {
+// With the two specs given (s0, s1: the rests' specs), both bootstraps wait for both set-up chains
+// (BootGate; option boot_gate).
+static int run_rests(scde_ctx* ctx, const std::function<int()>& rest0, const std::function<int()>& rest1,
+                     PostSpec* s0 = nullptr, PostSpec* s1 = nullptr) {
   if (!ctx->opt_rest_thread) {
     RCHK(rest0());
     return rest1();
   }
+  BootGate gate;
+  const bool gated = s0 && s1 && ctx->opt_boot_gate;
+  if (gated) {
+    for (auto& e : ctx->gate_ev)
+      if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    gate.ev[0] = ctx->gate_ev[0];
+    gate.ev[1] = ctx->gate_ev[1];
+    s0->gate = &gate;
+    s0->gate_slot = 0;
+    s1->gate = &gate;
+    s1->gate_slot = 1;
+  }
+  struct Ungate {  // the specs outlive this call: no dangling gate
+    PostSpec *a, *b;
+    ~Ungate() {
+      if (a) a->gate = nullptr;
+      if (b) b->gate = nullptr;
+    }
+  } ug{gated ? s0 : nullptr, gated ? s1 : nullptr};
   int rc1 = SCDE_OK;
   std::string err1;
   std::thread t1([&] {
     rc1 = hipSetDevice(ctx->device) == hipSuccess ? rest1() : fail(SCDE_EHIP, "hipSetDevice failed");
     if (rc1 != SCDE_OK) err1 = g_err;  // g_err is thread-local
+    if (gated) gate.leave(1);
   });
   const int rc0 = rest0();
+  if (gated) gate.leave(0);
   const std::string err0 = g_err;
   t1.join();
   if (rc0 != SCDE_OK) return fail(rc0, "%s", err0.c_str());
@@ -3539,7 +3603,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         std::function<int()> rest0, rest1;
         RCHK(run_posterior(ctx, specs[0], ctx->us[0], &rest0));
         RCHK(run_posterior(lane, specs[1], ctx->us[1], &rest1));
-        RCHK(run_rests(ctx, rest0, rest1));
+        RCHK(run_rests(ctx, rest0, rest1, &specs[0], &specs[1]));
       } else {
         RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
         RCHK(run_posterior(ctx, specs[1], ctx->us[1]));

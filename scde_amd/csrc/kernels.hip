@@ -685,6 +685,16 @@ __device__ __forceinline__ void tab_store(double* p, double v, int nt) {
   else
     *p = v;
 }
+typedef double tab_v2d __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void tab_store2(double* p, double a, double b, int nt) {  // p 16-byte aligned
+  tab_v2d v;
+  v.x = a;
+  v.y = b;
+  if (nt)
+    __builtin_nontemporal_store(v, reinterpret_cast<tab_v2d*>(p));
+  else
+    *reinterpret_cast<tab_v2d*>(p) = v;
+}
 
 template <int BM, int GC>
 __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long col, int c, int phase,
@@ -920,217 +930,83 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 #endif
 }
 
-#ifndef SCDE_TABREG_PAIR
-#define SCDE_TABREG_PAIR 1  // k_tables_reg takes a wave's columns two at a time (closed form only)
-#endif
-#if SCDE_NB_CLOSED
-// Two columns of one cell per wave, interleaved (round 5).  A column is a dependency chain -- the
-// NB row, a wave max, the exps, a wave sum, a table log, the final row -- and at four waves per
-// SIMD the chain's latencies were exposed (the VALU was ~40% busy).  Two independent columns per
-// pass give the scheduler a second chain, and the cell's staged rows are read once for both.
-// Every value of a column is formed exactly as tables_column_reg forms it (closed form), so the
-// outputs are the same bits; a column whose constants fall outside the fast form (ok false: the
-// gated k_tables pass takes it) writes nothing.
-template <int BM, int GC>
-__device__ __forceinline__ void tables_column_reg2(const TablesArgs& a, long long colA, long long colB, int c,
-                                                   int phase, const double* __restrict__ sm, bool have_base,
-                                                   const unsigned* __restrict__ uqb, const double* etab,
-                                                   const LogTab& lt, int lane, double theta, const double* ccA,
-                                                   const double* ccB, double xA, double xB, double maxcfp, int bc_u) {
-  constexpr int Q = 2;
-  const int G = GC ? GC : a.G;
-  const long long col[Q] = {colA, colB};
-  const double* const cc[Q] = {ccA, ccB};
-  const double x[Q] = {xA, xB};
-  bool ok[Q];
-  double fp[Q], lpo[Q], lqo[Q], c10[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    ok[q] = cc[q][0] > 0.0;  // k_col_consts stores n = -1 where the fast form does not apply
-    fp[q] = cc[q][7];
-    lpo[q] = cc[q][8];
-    lqo[q] = cc[q][9];
-    c10[q] = cc[q][10];
-  }
-  const double* sl = sm + lane;
-  double v[Q][kTabChunks];
-  double lmax[Q] = {-INFINITY, -INFINITY};
-#pragma unroll
-  for (int j = 0; j < kTabChunks; ++j) {
-#pragma unroll
-    for (int q = 0; q < Q; ++q) v[q][j] = -INFINITY;
-    if (64 * j < G) {
-      const int k = lane + 64 * j;
-      const bool in = k < G;
-      const bool last = (k == G - 1);
-      const double lp0 = sl[kRowLP * kRS + 64 * j], lq0 = sl[kRowLQ * kRS + 64 * j];
-      const double muv = sl[kRowMu * kRS + 64 * j], mnext = sl[kRowMu * kRS + 64 * j + 1];
-      const double lcfpr = sl[kRowLcfpr * kRS + 64 * j];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const bool over = in && ((!last && x[q] > muv && x[q] < mnext) || (last && x[q] > muv));
-        double lpr = lp0, lqr = lq0;
-        if (__builtin_amdgcn_ballot_w64(over)) {
-          lpr = over ? lpo[q] : lpr;
-          lqr = over ? lqo[q] : lqr;
-        }
-        double nb = (x[q] == 0.0) ? theta * lpr : fma(x[q], lqr, fma(theta, lpr, c10[q]));
-        nb += lcfpr;
-        v[q][j] = in ? nb : -INFINITY;
-        lmax[q] = gt_max(lmax[q], v[q][j]);
-      }
-    }
-  }
-  double maxp[Q], d0[Q], E[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) maxp[q] = wave_allreduce<true>(lmax[q]);
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    if (maxp[q] < (maxcfp + fp[q])) maxp[q] = maxcfp + fp[q];
-    d0[q] = fp[q] - maxp[q];
-    E[q] = exp_tab(fmax(d0[q], -746.0), etab);  // exp(fp - maxp); 0 below -746 (and for NaN)
-  }
-  double ls[Q] = {0.0, 0.0};
-#pragma unroll
-  for (int j = 0; j < kTabChunks; ++j) {
-    if (64 * j < G) {
-      const int k = lane + 64 * j;
-      const bool in = k < G;
-      const double cfp = sl[kRowCfp * kRS + 64 * j];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        v[q][j] -= maxp[q];  // t1
-        double e = cfp * E[q];
-        if (__builtin_amdgcn_ballot_w64(in && v[q][j] > -60.0)) e += exp_tab(fmax(v[q][j], -746.0), etab);
-        ls[q] += in ? e : 0.0;
-      }
-    }
-  }
-  double sq[Q], lsum[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) sq[q] = wave_allreduce<false>(ls[q]);
-#pragma unroll
-  for (int q = 0; q < Q; ++q) lsum[q] = log_tab(sq[q], lt);  // s >= 1 (the maximum term is exp(0))
-  const bool want_maxi = a.maxi != nullptr;
-  double bv[Q] = {-INFINITY, -INFINITY};
-  int bi[Q] = {0x7fffffff, 0x7fffffff};
-  bool clamp[Q] = {false, false}, nanq[Q] = {false, false};
-  double* out[Q];
-  double* dout[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    out[q] = (a.T && ok[q]) ? a.T + col[q] * a.GS : nullptr;
-    dout[q] = (phase && a.D && ok[q]) ? a.D + col[q] * a.GS : nullptr;
-  }
-  const double minlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
-  unsigned uqv[Q] = {0u, 0u};  // lane t < kQTiles: bound tile t's value (BM == kBoundTiles)
-#pragma unroll
-  for (int j = 0; j < kTabChunks; ++j) {
-    if (64 * j < G) {
-      const int k = lane + 64 * j;
-      const bool in = k < G;
-      const double lcfp = sl[kRowLcfp * kRS + 64 * j], cfp = sl[kRowCfp * kRS + 64 * j];
-      const double base = sl[kRowBase * kRS + 64 * j];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        const double t1 = v[q][j], t2 = lcfp + d0[q];
-        const double hi = gt_max(t2, t1), lo = (t1 > t2) ? t2 : t1;
-        const bool tiny = !(hi >= -665.0);
-        const bool mixed = !tiny && !(hi - lo > 37.5);
-        double r = hi - lsum[q];
-        if (__builtin_amdgcn_ballot_w64(in && (tiny || mixed))) {
-          const double e = fma(cfp, E[q], exp_tab(fmax(t1, -746.0), etab));
-          const double rm = log_tab(tiny ? e / sq[q] : e, lt) - (tiny ? 0.0 : lsum[q]);
-          r = (tiny || mixed) ? rm : r;
-        }
-        if (want_maxi && r > bv[q] && in) {
-          bv[q] = r;
-          bi[q] = k;
-        }
-        const bool cl = r < minlp;
-        r = cl ? minlp : r;
-        clamp[q] = clamp[q] || (cl && in);
-        nanq[q] = nanq[q] || (in && r != r);
-        // unconditional stores: lanes past the grid write the pad zeros (k < GS always)
-        if (out[q]) tab_store(out[q] + k, in ? r : 0.0, a.nt_rows);
-        if (dout[q]) tab_store(dout[q] + k, in ? (have_base ? r - base : r) : 0.0, a.nt_rows);
-        r = in ? r : -INFINITY;
-        if (BM == kBoundTiles) {
-          int u = row16_max_i32((int)ceil(fmax(r * 256.0, -0x1p29)));
-          const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
-          u = max((int)sw[0], (int)sw[1]);
-          const int g = __builtin_amdgcn_ds_bpermute(((lane - 2 * j) & 1) << 7, u);
-          uqv[q] = ((lane >> 1) == j) ? (unsigned)g : uqv[q];
-        }
-        if (BM == kBoundStretch) {  // the stretch maximum (64 points = this chunk), f32 widened
-          const float mf = wave_maxf((float)r);
-          if (lane == 0 && ok[q]) {
-            const double m = (double)mf + 0x1p-23 * fabs((double)mf);
-            a.U[col[q] * kStretchSlots + j] = (bc_u >= 0) ? m - a.U[(long long)bc_u * kStretchSlots + j] : m;
-          }
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    if (!ok[q]) continue;  // wave-uniform
-    if (BM == kBoundTiles) {
-      if (__ballot(nanq[q]) && lane == 0) *a.nanflag = 1;
-      if (lane < kQTiles) {
-        int u = (int)uqv[q];
-        if (kBTile * lane >= G)
-          u = 0;
-        else if (bc_u >= 0)
-          u -= unpacku(uqb[lane]);
-        a.UQ[col[q] * kQTiles + lane] = packu(u);
-      }
-    }
-    if (dout[q])
-      for (int k = 64 * ((G + 63) / 64) + lane; k < a.GS; k += 64) dout[q][k] = 0.0;
-    if (want_maxi) {
-      double b = bv[q];
-      int bix = bi[q];
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        const double ov = __shfl_xor(b, m, 64);
-        const int oi = __shfl_xor(bix, m, 64);
-        if (ov > b || (ov == b && oi < bix)) {
-          b = ov;
-          bix = oi;
-        }
-      }
-      if (lane == 0) a.maxi[col[q]] = (bix == 0x7fffffff) ? 0 : bix;
-    }
-    const unsigned long long anyc = __ballot(clamp[q]);
-    if (lane == 0) a.has_clamp[col[q]] = anyc ? 1 : 0;
-  }
-}
-#endif
 
-template <int BM, int GC>
-__global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_eu(SCDE_TABREG_WPE))) void k_tables_reg(TablesArgs a) {
-  __shared__ double sm[kTabRegRows * kRS];  // mu | [p | q |] log p | log q | lcfpr | cfp | lcfp | base
+// ------------------------------------------------------------------ lane-per-column tables (round 6)
+// k_tables_lpc<BM>: the constant-theta FP64 tables (phases 0 and 2, G <= kTabStagedG) with one LANE
+// per (cell, unique count) column.  A block takes 64 columns of one cell; its 4 waves split the grid
+// into four ranges of ~G/4 points (multiples of kLpcFlush), and each lane walks its column's points
+// of the wave's range in order -- so the grid vectors a point needs are the same for the whole wave
+// (LDS broadcast reads), the column's maximum and normaliser are one running max / sum per lane
+// (four partials per column combined in LDS, in wave order), and the tile and stretch bounds are
+// running maxima.  No cross-lane reduction, ballot or per-chunk branch in the hot loops; the loop
+// bodies are short (the k_tables_reg form spent most of its time in instruction supply and
+// dependency chains: timing builds without its exps or its mixed branch ran 30% faster each though
+// the branch runs on 1.5% of the points).  Rows go out through a per-wave LDS transpose, kLpcFlush
+// points of 64 columns at a time, as 16-byte stores (64 contiguous bytes per column).
+// Per point (src/jpmatLogBoot.cpp:166-206): nb_k = x log q_k + (theta log p_k + log(1 - cfp_k)) + C
+// (the closed-form NB log-pmf, section 4.0d; the parenthesis staged per cell), mu' override at the one
+// point ks where mu_ks < x < mu_ks+1 (mu nondecreasing, checked per cell), maxp, the normaliser
+// s = sum_k (cfp_k exp(fp - maxp) + exp(nb_k - maxp)) in grid order, T_k = max(t1, t2) - log s where
+// one term exceeds the other by e^37.5, else log(e_k) - log s, and log(e_k / s) where both terms are
+// below e^-665 (the reference's quotient in the subnormal range); clamp at minlogprob.  Columns
+// outside this form (count 0, flagged constants, a non-finite maxp, cells with a decreasing mu or a
+// NaN / +inf staged value) go through tables_column_reg after the block's lane pass.
+#ifndef SCDE_LPC_DIAG
+#define SCDE_LPC_DIAG 0  // timing-only builds of k_tables_lpc: 1 no row stores, 2 no pass-2 exps, 4 no mixed points
+#endif
+#ifndef SCDE_LPC_EXP_TAB
+#define SCDE_LPC_EXP_TAB 1  // k_tables_lpc's exps through the 64-entry LDS table (0: exp_poly; measured 0.311 vs 0.300 ms per launch)
+#endif
+#if SCDE_LPC_EXP_TAB
+#define LPC_EXP(d) exp_tab((d), etab)
+#else
+#define LPC_EXP(d) exp_poly(d)
+#endif
+#ifndef SCDE_LPC_PADLDS
+#define SCDE_LPC_PADLDS 0
+#endif
+#ifndef LPC_U12
+#define LPC_U12 4  // k_tables_lpc: unroll of passes 1 and 2
+#endif
+#ifndef LPC_U3
+#define LPC_U3 8  // k_tables_lpc: unroll of pass 3's flush group
+#endif
+constexpr int kLpcWaves = 4;
+constexpr int kLpcFlush = 8;              // points per transposed flush
+constexpr int kLpcTS = kLpcFlush + 1;     // the transpose's row stride (doubles) per column
+constexpr int kLpcQB = 0;                 // (log q_k, theta log p_k + log(1 - cfp_k)) pairs
+constexpr int kLpcLC = 2 * kTabStagedG;   // (log cfp_k, cfp_k) pairs
+constexpr int kLpcBase = 4 * kTabStagedG; // the baseline column (phase 2; 0 past the grid)
+constexpr int kLpcMu = 5 * kTabStagedG;   // mu_k
+constexpr int kLpcTW = 6 * kTabStagedG;   // transposes, [wave][64 columns][kLpcTS]
+constexpr int kLpcLds = kLpcTW + kLpcWaves * 64 * kLpcTS;
+static_assert(kLpcLds >= kTabRegRows * kRS, "the fallback's staged rows overlay the lane pass's LDS");
+
+template <int BM>
+__global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
+  __shared__ __attribute__((aligned(16))) double lds[kLpcLds];
   __shared__ double etab[64];
   __shared__ double ltab[3][97];
   __shared__ unsigned suqb[kQTiles];
-  __shared__ double scc[kTabTaskCols * kColc];  // the task's column constants and counts
-  __shared__ int sx[kTabTaskCols];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int GS = a.GS, G = GC ? GC : a.G;
+  __shared__ double spart[kLpcWaves][64];  // per-wave partial maxima, then sums
+  __shared__ double spart2[kLpcWaves][2][64];  // per-wave head / tail parts of split bound segments
+  __shared__ double sbv[kLpcWaves][64];
+  __shared__ int sbi[kLpcWaves][64];
+  __shared__ int sfb[64];
+  __shared__ int nfb;
+#if SCDE_LPC_PADLDS
+  __shared__ double padlds[SCDE_LPC_PADLDS];  // occupancy study builds only
+  if (threadIdx.x == 0 && a.G < 0) padlds[a.G & 1] = 0.0;
+#endif
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int GS = a.GS, G = a.G;
   tables_tabs(etab, ltab);
   if (a.gate && *a.gate == 0) return;
   const int4 task = a.tasks[blockIdx.x];
   const int c = task.x;
-  const int phase = a.phase;
-  if (c >= 0) {
-    // one latency per task for every column's constants (not one per column and wave)
-    const int ncc = (task.z - task.y) * kColc;
-    for (int t = threadIdx.x; t < ncc; t += 64 * kTabRegWaves) scc[t] = a.colc[(long long)task.y * kColc + t];
-    if (threadIdx.x < task.z - task.y) sx[threadIdx.x] = a.ucl[task.y + threadIdx.x];
-  }
   if (c < 0) {  // the ELL pad column (phase 2)
-    if (wid == 0) {
+    if (w == 0) {
       for (int k = lane; k < GS; k += 64)
         if (a.D) a.D[a.ncols * GS + k] = 0.0;
       if (a.U && lane < kStretchSlots) a.U[a.ncols * kStretchSlots + lane] = 0.0;
@@ -1138,59 +1014,263 @@ __global__ __launch_bounds__(64 * kTabRegWaves) __attribute__((amdgpu_waves_per_
     }
     return;
   }
+  const int phase = a.phase;
   const long long co = (long long)c * GS;
   const int bc = (phase == 2) ? tab_base_col(a, c) : -1;
   if (bc >= 0 && a.UQ && threadIdx.x < kQTiles) suqb[threadIdx.x] = a.UQ[(long long)bc * kQTiles + threadIdx.x];
+  if (threadIdx.x == 0) nfb = 0;
+  const double theta = a.theta[co];
   const double* P = a.pq + 4 * co;
-  for (int k = threadIdx.x; k < kRS; k += 64 * kTabRegWaves) {
+  int lean = theta > 0.0 && theta <= DBL_MAX;
+  for (int k = threadIdx.x; k < kTabStagedG; k += 64 * kLpcWaves) {
+    const bool in = k < G;
+    double lq = 0.0, B = 0.0, lc = -INFINITY, cf = 0.0, base = 0.0, mu = 0.0;
+    if (in) {
+      mu = a.mu[co + k];
+      const double lp = P[2 * GS + k], lr = a.lcfpr[co + k];
+      lq = P[3 * GS + k];
+      lc = a.lcfp[co + k];
+      cf = a.cfp ? a.cfp[co + k] : exp(lc);
+      B = fma(theta, lp, lr);
+      if (bc >= 0) base = a.D[(long long)bc * GS + k];
+      // false for NaN and +inf; mu nondecreasing
+      const bool ok = (k == G - 1 || mu <= a.mu[co + k + 1]) && lp <= DBL_MAX && lq <= DBL_MAX && lr <= DBL_MAX &&
+                      lc <= DBL_MAX && cf <= DBL_MAX && cf == cf;
+      lean &= ok ? 1 : 0;
+    }
+    lds[kLpcQB + 2 * k] = lq;
+    lds[kLpcQB + 2 * k + 1] = B;
+    lds[kLpcLC + 2 * k] = lc;
+    lds[kLpcLC + 2 * k + 1] = cf;
+    lds[kLpcBase + k] = base;
+    lds[kLpcMu + k] = mu;
+  }
+  lean = __syncthreads_and(lean);
+  const LogTab lt{ltab[0], ltab[1], ltab[2]};
+  const int zc = (phase == 2) ? tab_zcol(a, c) : -1;
+  const double maxcfp = a.cellscal[2 * c];
+  const double minlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
+  // this lane's column and its constants
+  const int col = task.y + lane;
+  const bool mine = col < task.z && col != zc;
+  double x = 1.0, c10 = 0.0, fp = 0.0, lpo = -1.0, lqo = -1.0;
+  bool ok = false;
+  if (mine) {
+    const double* cc = a.colc + (long long)col * kColc;
+    const double xx = (double)a.ucl[col], n = cc[0], cten = cc[10];
+    if (lean && xx > 0.0 && n > 0.0 && cten >= -DBL_MAX && cten <= DBL_MAX) {
+      ok = true;
+      x = xx;
+      c10 = cten;
+      fp = cc[7];
+      lpo = cc[8];
+      lqo = cc[9];
+    }
+  }
+  // the override point: m = #{k < G : mu_k < x}; ks = m - 1 where x < mu_m (or m = G)
+  int ks = -1;
+  double nb0o = 0.0;  // the override point's x log q' + theta log p' + log(1 - cfp) (c10 added at use)
+  {
+    int lo = 0, hi = G;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (lds[kLpcMu + mid] < x) lo = mid + 1; else hi = mid;
+    }
+    if (lo >= 1 && (lo == G || x < lds[kLpcMu + lo])) {
+      ks = lo - 1;
+      nb0o = fma(x, lqo, fma(theta, lpo, a.lcfpr[co + ks]));
+    }
+  }
+  // this wave's grid range [k0, k1) (multiples of kLpcFlush but the last end)
+  const int Gr = (G + kLpcFlush - 1) / kLpcFlush * kLpcFlush;
+  // (at least 64 points: a bound segment spans at most two waves)
+  const int per = max(64, (Gr / kLpcFlush + kLpcWaves - 1) / kLpcWaves * kLpcFlush);
+  const int k0 = min(Gr, w * per), k1 = min(G, k0 + per), k1r = min(Gr, k0 + per);
+  const double2* QB = reinterpret_cast<const double2*>(lds + kLpcQB);
+  const double2* LC = reinterpret_cast<const double2*>(lds + kLpcLC);
+  // pass 1: the maximum (the override selected before the last add, so the maximum's operands are
+  // arithmetic results and need no canonicalising)
+  double m = -INFINITY;
+#pragma unroll LPC_U12
+  for (int k = k0; k < k1; ++k) {
+    const double2 qb = QB[k];
+    double nb = fma(x, qb.x, qb.y);
+    nb = (k == ks) ? nb0o : nb;
+    nb += c10;
+    m = fmax(m, nb);
+  }
+  spart[w][lane] = m;
+  __syncthreads();
+  m = fmax(fmax(fmax(spart[0][lane], spart[1][lane]), spart[2][lane]), spart[3][lane]);
+  double maxp = m;
+  if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
+  ok = ok && maxp > -INFINITY && maxp < INFINITY;
+  if (!ok) maxp = 0.0;  // (a finite stand-in: the column goes through tables_column_reg)
+  const double d0 = fp - maxp;
+  const double E = exp_tab(fmax(d0, -746.0), etab);  // exp(fp - maxp); 0 below -746
+  // pass 2: the normaliser, every point as if without the override; the one override point's term
+  // is swapped in after the loop by the wave whose range holds it
+  double ls = 0.0;
+#pragma unroll LPC_U12
+  for (int k = k0; k < k1; ++k) {
+    const double2 qb = QB[k];
+    const double cf = LC[k].y;
+    const double t1 = (fma(x, qb.x, qb.y) + c10) - maxp;
+    double e = cf * E;
+    if (!(SCDE_LPC_DIAG & 2)) e += LPC_EXP(fmax(t1, -746.0));
+    ls += e;
+  }
+  if (ks >= k0 && ks < k1) {
+    const double cf = LC[ks].y, tp = (fma(x, QB[ks].x, QB[ks].y) + c10) - maxp, to = (nb0o + c10) - maxp;
+    ls += (cf * E + LPC_EXP(fmax(to, -746.0))) - (cf * E + LPC_EXP(fmax(tp, -746.0)));
+  }
+  __syncthreads();  // (every wave has read spart)
+  spart[w][lane] = ls;
+  __syncthreads();
+  const double sq = ((spart[0][lane] + spart[1][lane]) + spart[2][lane]) + spart[3][lane];
+  const double lsum = log_tab(sq, lt);  // s >= 1 (the maximum term is exp(0))
+  // pass 3: the row, its clamp, bounds and stores
+  const bool want_maxi = a.maxi != nullptr;
+  double bv = -INFINITY;
+  int bi = 0x7fffffff;
+  unsigned long long clampm = 0;  // lanes with a point below minlogprob (before the clamp)
+  const unsigned long long okm = __builtin_amdgcn_ballot_w64(ok);
+  double* tw = lds + kLpcTW + w * 64 * kLpcTS;
+  double* const T = a.T;
+  double* const D = (phase && a.D) ? a.D : nullptr;
+  const long long cbase = task.y;
+  // bound segments (32-point tiles / 64-point stretches): running maxima; a segment this wave's range
+  // holds whole is written here, its head / tail parts go through LDS to the combine below
+  constexpr int BSZ = (BM == kBoundStretch) ? 64 : kBTile;
+  auto put_bound = [&](int seg, double mx) {
+    if (!ok) return;
+    if (BM == kBoundTiles) {
+      int u = (int)ceil(fmax(mx * 256.0, -0x1p29));
+      if (bc >= 0) u -= unpacku(suqb[seg]);
+      a.UQ[(long long)col * kQTiles + seg] = packu(u);
+    } else if (BM == kBoundStretch) {
+      const float mf = (float)mx;
+      const double mm = (double)mf + 0x1p-23 * fabs((double)mf);
+      a.U[(long long)col * kStretchSlots + seg] = (bc >= 0) ? mm - a.U[(long long)bc * kStretchSlots + seg] : mm;
+    }
+  };
+  double bt = -INFINITY;
+  for (int f0 = k0; f0 < k1r; f0 += kLpcFlush) {
+#pragma unroll LPC_U3
+    for (int kk = 0; kk < kLpcFlush; ++kk) {
+      const int k = f0 + kk;
+      double r = 0.0;  // pad points of the last flush
+      if (k < k1) {
+        const double2 qb = QB[k], lcf = LC[k];
+        double nb = fma(x, qb.x, qb.y);
+        nb = (k == ks) ? nb0o : nb;
+        const double t1 = (nb + c10) - maxp, t2 = lcf.x + d0;
+        const double hi = fmax(t2, t1);
+        const bool tiny = !(hi >= -665.0);
+        const bool tm = tiny || !(fabs(t1 - t2) > 37.5);
+        r = hi - lsum;
+        if (!(SCDE_LPC_DIAG & 4) && __builtin_amdgcn_ballot_w64(ok && tm)) {
+          double e = fma(lcf.y, E, LPC_EXP(fmax(t1, -746.0)));
+          if (__builtin_amdgcn_ballot_w64(ok && tiny)) e = tiny ? e / sq : e;
+          const double rm = log_tab(e, lt) - (tiny ? 0.0 : lsum);
+          r = tm ? rm : r;
+        }
+        if (want_maxi) {
+          const bool better = r > bv;
+          bv = better ? r : bv;
+          bi = better ? k : bi;
+        }
+        clampm |= __builtin_amdgcn_ballot_w64(r < minlp);
+        r = fmax(r, minlp);
+        if (BM != kBoundNone) {
+          bt = fmax(bt, r);
+          if ((k % BSZ) == BSZ - 1 || k == k1 - 1) {  // (wave-uniform)
+            const int seg = k / BSZ;
+            const bool head = seg * BSZ < k0, tail = (k % BSZ) != BSZ - 1 && k != G - 1;
+            if (!head && !tail)
+              put_bound(seg, bt);
+            else
+              spart2[w][tail ? 1 : 0][lane] = bt;
+            bt = -INFINITY;
+          }
+        }
+      }
+      tw[lane * kLpcTS + kk] = r;
+    }
+    // the flush: 4 lanes per column, 16 columns per store
+#pragma unroll
+    for (int i = 0; i < ((SCDE_LPC_DIAG & 1) ? 0 : 4); ++i) {
+      const int cc_ = i * 16 + (lane >> 2), kp = (lane & 3) * 2;
+      if ((okm >> cc_) & 1ull) {
+        const double r0 = tw[cc_ * kLpcTS + kp], r1 = tw[cc_ * kLpcTS + kp + 1];
+        const long long off = (cbase + cc_) * GS + f0 + kp;
+        if (T) tab_store2(T + off, r0, r1, a.nt_rows);
+        if (D) {
+          const double2 bb = *reinterpret_cast<const double2*>(lds + kLpcBase + f0 + kp);
+          tab_store2(D + off, r0 - bb.x, r1 - bb.y, a.nt_rows);
+        }
+      }
+    }
+  }
+  // zero pads [Gr, GS): flushes of zeros, round-robin over the waves
+  for (int f0 = Gr + kLpcFlush * w; f0 < GS; f0 += kLpcFlush * kLpcWaves) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cc_ = i * 16 + (lane >> 2), kp = (lane & 3) * 2;
+      if ((okm >> cc_) & 1ull) {
+        const long long off = (cbase + cc_) * GS + f0 + kp;
+        if (T) tab_store2(T + off, 0.0, 0.0, a.nt_rows);
+        if (D) tab_store2(D + off, 0.0, 0.0, a.nt_rows);
+      }
+    }
+  }
+  // the four waves' partials: clamp flag, argmax, bound segments split between waves
+  __syncthreads();  // (every wave is done with spart's sums)
+  spart[w][lane] = ((clampm >> lane) & 1ull) ? 1.0 : 0.0;
+  sbi[w][lane] = bi;
+  sbv[w][lane] = bv;
+  __syncthreads();
+  if (w == 0 && ok) {
+    a.has_clamp[col] = (spart[0][lane] + spart[1][lane] + spart[2][lane] + spart[3][lane] > 0.0) ? 1 : 0;
+    if (want_maxi) {
+      double b = sbv[0][lane];
+      int bix = sbi[0][lane];
+      for (int v = 1; v < kLpcWaves; ++v)
+        if (sbv[v][lane] > b) {  // ties: the earlier wave holds the smaller index
+          b = sbv[v][lane];
+          bix = sbi[v][lane];
+        }
+      a.maxi[col] = (bix == 0x7fffffff) ? 0 : bix;
+    }
+  }
+  if (BM != kBoundNone && w > 0 && (k0 % BSZ) != 0 && k0 < G)  // the segment wave w - 1 began and w ended
+    put_bound(k0 / BSZ, fmax(spart2[w - 1][1][lane], spart2[w][0][lane]));
+  if (BM == kBoundTiles && w == kLpcWaves - 1)
+    for (int t = (G + kBTile - 1) / kBTile; t < kQTiles; ++t)
+      if (ok) a.UQ[(long long)col * kQTiles + t] = packu(0);
+  // the columns outside the lane pass: tables_column_reg, over the general staged rows
+  if (mine && !ok) sfb[atomicAdd(&nfb, 1)] = col;
+  __syncthreads();
+  const int nf = nfb;
+  if (nf == 0) return;
+  double* sm = lds;  // (overlays the lane pass's rows and transposes)
+  for (int k = threadIdx.x; k < kRS; k += 64 * kLpcWaves) {
     const bool in = k < G;
     sm[kRowMu * kRS + k] = in ? a.mu[co + k] : 0.0;
-#if !SCDE_NB_CLOSED
-    sm[kRowP * kRS + k] = in ? P[k] : 0.0;
-    sm[(kRowP + 1) * kRS + k] = in ? P[GS + k] : 0.0;
-#endif
     sm[kRowLP * kRS + k] = in ? P[2 * GS + k] : 0.0;
     sm[kRowLQ * kRS + k] = in ? P[3 * GS + k] : 0.0;
     sm[kRowLcfpr * kRS + k] = in ? a.lcfpr[co + k] : 0.0;
     const double lc = in ? a.lcfp[co + k] : -INFINITY;
-    sm[kRowCfp * kRS + k] = in ? (a.cfp ? a.cfp[co + k] : exp(lc)) : 0.0;  // exp(-inf) = 0 past the grid
+    sm[kRowCfp * kRS + k] = in ? (a.cfp ? a.cfp[co + k] : exp(lc)) : 0.0;
     sm[kRowLcfp * kRS + k] = lc;
     sm[kRowBase * kRS + k] = (in && bc >= 0) ? a.D[(long long)bc * GS + k] : 0.0;
   }
   __syncthreads();
-  const LogTab lt{ltab[0], ltab[1], ltab[2]};
-  const int zc = (phase == 2) ? tab_zcol(a, c) : -1;
-  const double theta = a.theta[co];
-  const double maxcfp = a.cellscal[2 * c];
-#if SCDE_NB_CLOSED && SCDE_TABREG_PAIR
-  // the wave's columns two at a time (the count-0 column zc was done in phase 1), a last odd one alone
-  int col = task.y + wid;
-  if (col == zc) col += kTabRegWaves;
-  while (col < task.z) {
-    int col2 = col + kTabRegWaves;
-    if (col2 == zc) col2 += kTabRegWaves;
-    const int i = col - task.y;
-    if (col2 < task.z && a.pair_cols) {
-      const int i2 = col2 - task.y;
-      tables_column_reg2<BM, GC>(a, col, col2, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta, scc + i * kColc,
-                                 scc + i2 * kColc, (double)sx[i], (double)sx[i2], maxcfp, bc);
-      col = col2 + kTabRegWaves;
-      if (col == zc) col += kTabRegWaves;
-    } else {
-      tables_column_reg<BM, GC>(a, col, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta, scc + i * kColc,
-                                (double)sx[i], maxcfp, bc);
-      col += kTabRegWaves;
-      if (col == zc) col += kTabRegWaves;
-    }
+  for (int i = w; i < nf; i += kLpcWaves) {
+    const int fc = __builtin_amdgcn_readfirstlane(sfb[i]);
+    tables_column_reg<BM, 0>(a, fc, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta, a.colc + (long long)fc * kColc,
+                             (double)a.ucl[fc], maxcfp, bc);
   }
-#else
-  for (int col = task.y + wid; col < task.z; col += kTabRegWaves) {
-    if (col == zc) continue;  // done in phase 1
-    const int i = col - task.y;
-    tables_column_reg<BM, GC>(a, col, c, phase, sm, bc >= 0, suqb, etab, lt, lane, theta,
-                      scc + i * kColc, (double)sx[i], maxcfp, bc);
-  }
-#endif
 }
 
 // ------------------------------------------------------------------ baseline / ELL
@@ -4203,25 +4283,17 @@ hipError_t launch_tables(const TablesArgs& a, hipStream_t s) {
   if (a.phase != 0 && (!a.D || !a.zcol || !a.base_col)) return hipErrorInvalidValue;
   if (a.phase != 1 && a.tasks && a.ntasks > 0 && a.G <= kTabStagedG && a.const_theta && a.colc && a.pq &&
       a.ncols > 0) {
-    // register-row kernel, then the columns it leaves (rare; the launch exits at once unless
-    // k_col_consts flagged one) by the column-per-wave kernel
-    const dim3 grid(a.ntasks), block(64 * kTabRegWaves);
+    // lane-per-column kernel (64-column tasks), then the columns whose constants it and its
+    // fallback leave (rare; the launch exits at once unless k_col_consts flagged one)
+    const dim3 grid(a.ntasks), block(64 * kLpcWaves);
     const int bm = (a.UQ && a.phase == 2) ? kBoundTiles : (a.U && a.phase == 2) ? kBoundStretch : kBoundNone;
-    if (SCDE_TABREG_G401 && a.G == 401) {
-      if (bm == kBoundTiles)
-        hipLaunchKernelGGL((k_tables_reg<kBoundTiles, 401>), grid, block, 0, s, a);
-      else if (bm == kBoundStretch)
-        hipLaunchKernelGGL((k_tables_reg<kBoundStretch, 401>), grid, block, 0, s, a);
-      else
-        hipLaunchKernelGGL((k_tables_reg<kBoundNone, 401>), grid, block, 0, s, a);
-    } else {
-      if (bm == kBoundTiles)
-        hipLaunchKernelGGL((k_tables_reg<kBoundTiles, 0>), grid, block, 0, s, a);
-      else if (bm == kBoundStretch)
-        hipLaunchKernelGGL((k_tables_reg<kBoundStretch, 0>), grid, block, 0, s, a);
-      else
-        hipLaunchKernelGGL((k_tables_reg<kBoundNone, 0>), grid, block, 0, s, a);
-    }
+    if (a.GS % kLpcFlush) return hipErrorInvalidValue;
+    if (bm == kBoundTiles)
+      hipLaunchKernelGGL((k_tables_lpc<kBoundTiles>), grid, block, 0, s, a);
+    else if (bm == kBoundStretch)
+      hipLaunchKernelGGL((k_tables_lpc<kBoundStretch>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((k_tables_lpc<kBoundNone>), grid, block, 0, s, a);
     TablesArgs b = a;
     b.slow_only = 1;
     const size_t shm = sizeof(double) * 4 * (size_t)a.GS;

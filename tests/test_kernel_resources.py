@@ -208,11 +208,12 @@ def test_hazard_check_rejects_a_faulting_build(tmp_path):
     assert found, "the 6-waves-per-SIMD build shows no hazard: the check has lost its teeth"
 
 
-def test_tables_register_row_does_not_spill(isa):
-    """k_tables_reg keeps a column's 401 grid values in VGPRs; builds that spilled them (or
-    the hoisted polynomial constants) to scratch ran 15-40 % slower."""
-    bodies = _bodies(isa, "k_tables_reg")
-    assert len(bodies) == 6, [s for s, _ in bodies]
+def test_tables_lane_per_column_does_not_spill(isa):
+    """k_tables_lpc (one lane per table column) keeps its running maxima,
+    sums and the fallback's register row (tables_column_reg) in VGPRs; builds of the register-row
+    kernel that spilled to scratch ran 15-40 % slower."""
+    bodies = _bodies(isa, "k_tables_lpc")
+    assert len(bodies) == 3, [s for s, _ in bodies]
     for sym, body in bodies:
         bad = [ln.strip() for ln in body.split("\n") if "scratch_" in ln]
         assert not bad, f"{sym}: scratch access: {bad[:3]}"
