@@ -952,7 +952,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 // outside this form (count 0, flagged constants, a non-finite maxp, cells with a decreasing mu or a
 // NaN / +inf staged value) go through tables_column_reg after the block's lane pass.
 #ifndef SCDE_LPC_DIAG
-#define SCDE_LPC_DIAG 0  // timing-only builds of k_tables_lpc: 1 no row stores, 2 no pass-2 exps, 4 no mixed points
+#define SCDE_LPC_DIAG 0  // study builds of k_tables_lpc: 1 no row stores, 2 no pass-2 exps, 4 no mixed points, 8 NaN in [GP, GS)
 #endif
 #ifndef SCDE_LPC_EXP_TAB
 #define SCDE_LPC_EXP_TAB 1  // k_tables_lpc's exps through the 64-entry LDS table (0: exp_poly; measured 0.311 vs 0.300 ms per launch)
@@ -961,6 +961,10 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 #define LPC_EXP(d) exp_tab((d), etab)
 #else
 #define LPC_EXP(d) exp_poly(d)
+#endif
+#ifndef SCDE_LPC_TW
+#define SCDE_LPC_TW 1  // k_tables_lpc's rows through a per-wave LDS transpose (0: each lane stores its own column;
+                       // 5 blocks per CU instead of 3, measured 0.342 vs 0.306 ms per launch at config 3)
 #endif
 #ifndef SCDE_LPC_PADLDS
 #define SCDE_LPC_PADLDS 0
@@ -972,15 +976,19 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 #define LPC_U3 8  // k_tables_lpc: unroll of pass 3's flush group
 #endif
 constexpr int kLpcWaves = 4;
-constexpr int kLpcFlush = 8;              // points per transposed flush
+constexpr int kLpcFlush = 8;              // points per register group (and per transposed flush)
 constexpr int kLpcTS = kLpcFlush + 1;     // the transpose's row stride (doubles) per column
 constexpr int kLpcQB = 0;                 // (log q_k, theta log p_k + log(1 - cfp_k)) pairs
 constexpr int kLpcLC = 2 * kTabStagedG;   // (log cfp_k, cfp_k) pairs
 constexpr int kLpcBase = 4 * kTabStagedG; // the baseline column (phase 2; 0 past the grid)
-constexpr int kLpcMu = 5 * kTabStagedG;   // mu_k
-constexpr int kLpcTW = 6 * kTabStagedG;   // transposes, [wave][64 columns][kLpcTS]
-constexpr int kLpcLds = kLpcTW + kLpcWaves * 64 * kLpcTS;
-static_assert(kLpcLds >= kTabRegRows * kRS, "the fallback's staged rows overlay the lane pass's LDS");
+constexpr int kLpcR = 5 * kTabStagedG;    // region R: mu_k (the override search), then the passes'
+constexpr int kLpcMu = kLpcR;             // partial maxima / sums, then (SCDE_LPC_TW) the transposes
+constexpr int kLpcPart = kLpcR + kTabStagedG;
+constexpr int kLpcRsz = SCDE_LPC_TW ? kLpcWaves * 64 * kLpcTS : kTabStagedG + kLpcWaves * 64;
+constexpr int kLpcLds0 = kLpcR + kLpcRsz;
+constexpr int kLpcLds = kLpcLds0 > kTabRegRows * kRS ? kLpcLds0 : kTabRegRows * kRS;  // (the fallback's rows overlay it)
+static_assert(kLpcRsz >= kTabStagedG + kLpcWaves * 64, "mu and the partials fit region R");
+static_assert(kLpcWaves * 64 * 3 <= kLpcBase, "the combine's arrays overlay the staged rows");
 
 template <int BM>
 __global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
@@ -988,10 +996,10 @@ __global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
   __shared__ double etab[64];
   __shared__ double ltab[3][97];
   __shared__ unsigned suqb[kQTiles];
-  __shared__ double spart[kLpcWaves][64];  // per-wave partial maxima, then sums
-  __shared__ double spart2[kLpcWaves][2][64];  // per-wave head / tail parts of split bound segments
-  __shared__ double sbv[kLpcWaves][64];
-  __shared__ int sbi[kLpcWaves][64];
+  // per-wave head / tail parts of bound segments split between two waves: tiles as ceil(256 max),
+  // stretches as (float) max -- the form the bound takes anyway
+  __shared__ unsigned spart2[kLpcWaves][2][64];
+  double(*spart)[64] = reinterpret_cast<double(*)[64]>(lds + kLpcPart);  // per-wave partial maxima, then sums
   __shared__ int sfb[64];
   __shared__ int nfb;
 #if SCDE_LPC_PADLDS
@@ -1129,33 +1137,45 @@ __global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
   __syncthreads();
   const double sq = ((spart[0][lane] + spart[1][lane]) + spart[2][lane]) + spart[3][lane];
   const double lsum = log_tab(sq, lt);  // s >= 1 (the maximum term is exp(0))
+  if (SCDE_LPC_TW) __syncthreads();  // (region R becomes the transposes)
   // pass 3: the row, its clamp, bounds and stores
   const bool want_maxi = a.maxi != nullptr;
   double bv = -INFINITY;
   int bi = 0x7fffffff;
   unsigned long long clampm = 0;  // lanes with a point below minlogprob (before the clamp)
   const unsigned long long okm = __builtin_amdgcn_ballot_w64(ok);
-  double* tw = lds + kLpcTW + w * 64 * kLpcTS;
+  double* tw = lds + kLpcR + w * 64 * kLpcTS;
   double* const T = a.T;
   double* const D = (phase && a.D) ? a.D : nullptr;
   const long long cbase = task.y;
   // bound segments (32-point tiles / 64-point stretches): running maxima; a segment this wave's range
   // holds whole is written here, its head / tail parts go through LDS to the combine below
   constexpr int BSZ = (BM == kBoundStretch) ? 64 : kBTile;
-  auto put_bound = [&](int seg, double mx) {
+  // a segment's maximum in the bound's own form: ceil(256 max) (tiles), (float) max (stretches) --
+  // both monotone, so the form of the maximum is the maximum of the forms
+  auto bound_form = [&](double mx) -> unsigned {
+    if (BM == kBoundTiles) return (unsigned)(int)ceil(fmax(mx * 256.0, -0x1p29));
+    return __float_as_uint((float)mx);
+  };
+  auto bound_max = [&](unsigned p, unsigned q) -> unsigned {
+    if (BM == kBoundTiles) return (unsigned)max((int)p, (int)q);
+    return __float_as_uint(fmaxf(__uint_as_float(p), __uint_as_float(q)));
+  };
+  auto put_bound = [&](int seg, unsigned form) {
     if (!ok) return;
     if (BM == kBoundTiles) {
-      int u = (int)ceil(fmax(mx * 256.0, -0x1p29));
+      int u = (int)form;
       if (bc >= 0) u -= unpacku(suqb[seg]);
       a.UQ[(long long)col * kQTiles + seg] = packu(u);
     } else if (BM == kBoundStretch) {
-      const float mf = (float)mx;
+      const float mf = __uint_as_float(form);
       const double mm = (double)mf + 0x1p-23 * fabs((double)mf);
       a.U[(long long)col * kStretchSlots + seg] = (bc >= 0) ? mm - a.U[(long long)bc * kStretchSlots + seg] : mm;
     }
   };
   double bt = -INFINITY;
   for (int f0 = k0; f0 < k1r; f0 += kLpcFlush) {
+    double rg[kLpcFlush];  // the group's row values (SCDE_LPC_TW 0)
 #pragma unroll LPC_U3
     for (int kk = 0; kk < kLpcFlush; ++kk) {
       const int k = f0 + kk;
@@ -1188,18 +1208,32 @@ __global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
             const int seg = k / BSZ;
             const bool head = seg * BSZ < k0, tail = (k % BSZ) != BSZ - 1 && k != G - 1;
             if (!head && !tail)
-              put_bound(seg, bt);
+              put_bound(seg, bound_form(bt));
             else
-              spart2[w][tail ? 1 : 0][lane] = bt;
+              spart2[w][tail ? 1 : 0][lane] = bound_form(bt);
             bt = -INFINITY;
           }
         }
       }
-      tw[lane * kLpcTS + kk] = r;
+      if (SCDE_LPC_TW)
+        tw[lane * kLpcTS + kk] = r;
+      else
+        rg[kk] = r;
+    }
+    if (!SCDE_LPC_TW && ok && !(SCDE_LPC_DIAG & 1)) {  // each lane its own column's 64 bytes
+      const long long off = (cbase + lane) * GS + f0;
+#pragma unroll
+      for (int i = 0; i < kLpcFlush / 2; ++i) {
+        if (T) tab_store2(T + off + 2 * i, rg[2 * i], rg[2 * i + 1], a.nt_rows);
+        if (D) {
+          const double2 bb = *reinterpret_cast<const double2*>(lds + kLpcBase + f0 + 2 * i);
+          tab_store2(D + off + 2 * i, rg[2 * i] - bb.x, rg[2 * i + 1] - bb.y, a.nt_rows);
+        }
+      }
     }
     // the flush: 4 lanes per column, 16 columns per store
 #pragma unroll
-    for (int i = 0; i < ((SCDE_LPC_DIAG & 1) ? 0 : 4); ++i) {
+    for (int i = 0; i < ((SCDE_LPC_DIAG & 1) || !SCDE_LPC_TW ? 0 : 4); ++i) {
       const int cc_ = i * 16 + (lane >> 2), kp = (lane & 3) * 2;
       if ((okm >> cc_) & 1ull) {
         const double r0 = tw[cc_ * kLpcTS + kp], r1 = tw[cc_ * kLpcTS + kp + 1];
@@ -1212,26 +1246,46 @@ __global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
       }
     }
   }
-  // zero pads [Gr, GS): flushes of zeros, round-robin over the waves
-  for (int f0 = Gr + kLpcFlush * w; f0 < GS; f0 += kLpcFlush * kLpcWaves) {
+  // zero pads [Gr, GP): flushes of zeros, round-robin over the waves.  GP = the 64-point stretch end
+  // (448 at G = 401): the bootstrap kernels read rows up to their last 32-point tile / 64-point
+  // stretch; [GP, GS) is alignment only, never read (timing build SCDE_LPC_DIAG & 8 writes NaN there:
+  // the GPU suite stays green)
+  const int GP = (SCDE_LPC_DIAG & 8) ? GS : min(GS, (G + 63) / 64 * 64);
+  for (int f0 = Gr + kLpcFlush * w; f0 < GP; f0 += kLpcFlush * kLpcWaves) {
+    if (!SCDE_LPC_TW) {
+      if (ok) {
+        const long long off = (cbase + lane) * GS + f0;
+#pragma unroll
+        for (int i = 0; i < kLpcFlush / 2; ++i) {
+          const double z = ((SCDE_LPC_DIAG & 8) && f0 >= (G + 63) / 64 * 64) ? __builtin_nan("") : 0.0;
+          if (T) tab_store2(T + off + 2 * i, z, z, a.nt_rows);
+          if (D) tab_store2(D + off + 2 * i, z, z, a.nt_rows);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int cc_ = i * 16 + (lane >> 2), kp = (lane & 3) * 2;
       if ((okm >> cc_) & 1ull) {
         const long long off = (cbase + cc_) * GS + f0 + kp;
-        if (T) tab_store2(T + off, 0.0, 0.0, a.nt_rows);
-        if (D) tab_store2(D + off, 0.0, 0.0, a.nt_rows);
+        const double z = ((SCDE_LPC_DIAG & 8) && f0 >= (G + 63) / 64 * 64) ? __builtin_nan("") : 0.0;
+        if (T) tab_store2(T + off, z, z, a.nt_rows);
+        if (D) tab_store2(D + off, z, z, a.nt_rows);
       }
     }
   }
   // the four waves' partials: clamp flag, argmax, bound segments split between waves
-  __syncthreads();  // (every wave is done with spart's sums)
-  spart[w][lane] = ((clampm >> lane) & 1ull) ? 1.0 : 0.0;
+  __syncthreads();  // (every wave is done with the staged rows: the combine's arrays overlay them)
+  double(*sclamp)[64] = reinterpret_cast<double(*)[64]>(lds);
+  double(*sbv)[64] = reinterpret_cast<double(*)[64]>(lds + kLpcWaves * 64);
+  int(*sbi)[64] = reinterpret_cast<int(*)[64]>(lds + 2 * kLpcWaves * 64);
+  sclamp[w][lane] = ((clampm >> lane) & 1ull) ? 1.0 : 0.0;
   sbi[w][lane] = bi;
   sbv[w][lane] = bv;
   __syncthreads();
   if (w == 0 && ok) {
-    a.has_clamp[col] = (spart[0][lane] + spart[1][lane] + spart[2][lane] + spart[3][lane] > 0.0) ? 1 : 0;
+    a.has_clamp[col] = (sclamp[0][lane] + sclamp[1][lane] + sclamp[2][lane] + sclamp[3][lane] > 0.0) ? 1 : 0;
     if (want_maxi) {
       double b = sbv[0][lane];
       int bix = sbi[0][lane];
@@ -1244,7 +1298,7 @@ __global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
     }
   }
   if (BM != kBoundNone && w > 0 && (k0 % BSZ) != 0 && k0 < G)  // the segment wave w - 1 began and w ended
-    put_bound(k0 / BSZ, fmax(spart2[w - 1][1][lane], spart2[w][0][lane]));
+    put_bound(k0 / BSZ, bound_max(spart2[w - 1][1][lane], spart2[w][0][lane]));
   if (BM == kBoundTiles && w == kLpcWaves - 1)
     for (int t = (G + kBTile - 1) / kBTile; t < kQTiles; ++t)
       if (ok) a.UQ[(long long)col * kQTiles + t] = packu(0);
