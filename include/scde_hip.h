@@ -118,90 +118,68 @@ int scde_ctx_set_profiling(scde_ctx* ctx, int on);
  * 6 prior_bin, 7 prior_tail; ms totals and launch counts */
 int scde_ctx_kernel_times(scde_ctx* ctx, double* ms, int64_t* launches, int nslots);
 int scde_ctx_reset_kernel_times(scde_ctx* ctx);
-/* Tuning and test options of a context (defaults are the product settings; the environment is
- * read once, at context creation, for SCDE_OPTIONS -- see scde_ctx_set_option):
- *   "boot_skip"     1/0  grid-stretch skipping in the bootstrap (output unchanged either way)
- *   "boot_tiles"    1/0  the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles; default 1)
- *   "boot_tiles_cells"  the cell count from which it is used (default 400; below: k_boot2's
+/* Options of a context: 20, each the switch of a default path or a documented operating / test mode
+ * (defaults are the product settings; the environment is read once, at context creation, for
+ * SCDE_OPTIONS -- see scde_ctx_set_option).  Every one leaves the results unchanged unless noted.
+ * Bootstrap paths:
+ *   "boot_tiles"    1/0  the FP64 bootstrap on bounded 32-point tiles (k_boot_gene gene blocks, their
+ *                   four-tile list pass k_boot_tiles; default 1) or k_boot2's 64-point stretches (0)
+ *   "boot_tiles_cells"  the cell count from which the tile path is used (default 400; below: k_boot2's
  *                   64-point stretch mask -- config 2b's 200-cell batch posteriors: 8.2 ms of
  *                   bootstrap per step with it against 12.0 with gene blocks)
- *   "tile_groups"   32-point grid tiles k_boot_tiles computes per slab, 1..4 (default 4; slabs
- *                   needing more go to k_boot2 whole -- tests force that with 2)
- *   "tile_max_mult" the largest draw multiplicity the tile path takes (default 127, the int8 bound
- *                   operand; a call with a larger one runs plain k_boot2 on the same columns --
- *                   tests force that fallback with a small value)
+ *   "boot_skip"     1/0  grid-stretch / tile skipping in the bootstrap (default 1)
+ *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "tile_order"    0..3  the tile bootstrap takes the genes in order of their count sums,
  *                   so waves in flight share columns and tiles in L2: 1 ascending, 2 descending
  *                   (heaviest genes first: a shorter tail), 3 (default) descending for launches
- *                   of at most 8,192 genes and ascending above, 0 gene order; results are the same
- *   "unique_fixed"  1/0  build each call's unique count tables with one host sync (fixed
- *                   1024-word bitmaps per cell, counts below 65,536; a set with another count is
- *                   rebuilt with exact widths); default 1
- *   "pair_cells"    the cell count from which k_boot_tiles runs two slabs per wave with two
- *                   bound tiles each (default 1000: wide calls, narrow posteriors); slabs that need
- *                   more take a four-tile pass (results are the same)
- *   "gene_blocks"   1/0  the tile bootstrap as one 4-wave block per (gene, group of slabs) sharing 16
- *                   bound-tile rows among the group's slabs (k_boot_gene; default 1, not with pair mode),
- *                   or one wave per slab with four tiles (k_boot_tiles); results are the same
- *   "gene_rows"     1..4 rows per slab k_boot_gene gives each slab at most (default 4; tests force
- *                   its four-tile list pass with fewer)
- *   "modes_overlap" 1/0  scde.posteriors' read-backs run on a read-back thread beside the device
- *                   work (default 1): the modes piece by piece as each piece's tables finish, the
- *                   joint posterior in gene chunks of the bootstrap; 0: both after the bootstrap on
- *                   the main stream (rocprofv3 runs); results are the same
- *   "tables_nt"     0..2 the posterior-table rows as non-temporal stores: 0 never, 1 always, 2 when
- *                   the call's rows exceed 256 MB (default); results are the same
- *   "gene_direct"   1/0  gene blocks that hold all of a gene's slabs write its joint-posterior row
- *                   themselves when every slab passes its post-check (default 1), or leave every
- *                   row to the slab-sum kernel (0); results are the same
- *   "ell_chunks"    0..64 cell chunks of the ELL-row build (default 1: one pass; 0 = by size, a
- *                   counting pass then a writing pass); results are the same
- *   "jp_chunks"     1..64 gene chunks of scde.posteriors' gene-block bootstrap (default 4, at most
- *                   one per 256 genes): each chunk finishes before the next starts and its joint
- *                   posterior rows are read back while the next runs; results are the same
+ *                   of at most 8,192 genes and ascending above, 0 gene order
+ * Test modes forcing the bootstrap's second-chance paths (each must still give the same bits):
+ *   "skip_slack"    mask heuristic slack (NaN = default 20 + 0.15 C; negative: redo slabs)
+ *   "tile_groups"   32-point tiles the list pass computes per slab, 1..4 (default 4; with 2, slabs
+ *                   needing more go to k_boot2 whole)
+ *   "tile_max_mult" the largest draw multiplicity the tile path takes (default 127, the int8 bound
+ *                   operand; a call with a larger one runs plain k_boot2 on the same columns)
+ *   "gene_rows"     1..4 rows per slab a gene block gives each slab at most (default 4; fewer:
+ *                   the four-tile list pass takes the rest)
+ *   "gene_list_cap" slabs the list pass takes at most (0 = 16384; beyond: k_boot2)
+ *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
+ * Host pipeline:
  *   "lanes"         2/1  a DE call's second group runs on a peer context (its own streams and
  *                   workspace, same device) beside the first (default 2), or after it (1; bench's
- *                   per-stage timing pass and the rocprof runs use 1); results are the same.
- *                   Memory: the peer holds a second grow-only workspace (tables, deltas, slab
- *                   partials, joint posterior: about 2.3 GB at 20k genes x 500 cells per group,
- *                   DESIGN.md section 3), so two lanes roughly double a DE call's device
- *                   footprint; setting 1 releases the peer and its workspace
- *   "lane_prio"     0..2 the peer lane's streams at the device's highest priority: 0 never (default),
- *                   1 always, 2 for DE calls of at most 8,192 genes (per call); results are the same
+ *                   per-stage timing pass and the rocprof runs use 1).  Memory: the peer holds a
+ *                   second grow-only workspace (tables, deltas, slab partials, joint posterior:
+ *                   about 2.3 GB at 20k genes x 500 cells per group), so two
+ *                   lanes roughly double a DE call's device footprint; setting 1 releases the peer
  *   "pipeline_mb"   host-count DE / scde.posteriors calls whose matrix has at least this many MB
  *                   upload on a copy stream in column pieces that the kernels follow (default 32)
  *   "pieces"        pieces of that upload (the DE call's first group; the posteriors call's
- *                   selected cells), 1..8 (default 4); results are the same
- *   "lane_thread"   1/0  a pipelined two-lane DE call drives the second lane (its unique sets,
- *                   tables and bootstrap) from a host thread of its own (results are the same)
- *   "boot_chunks"   k_boot_gene's grid in this many launches (default 1; 4 and 8 measured slower:
- *                   config 3 6.85 -> 6.94-6.99 ms per step; results are the same)
- *   "rest_thread"   1/0  a two-lane DE call on counts in HBM (or host counts under the pipelining
- *                   threshold) drives the second group's draws, set-up and bootstrap launch from a
- *                   host thread of its own (default 1; shard of 8: 1.72-1.81 -> 1.67-1.68 ms per
- *                   step; results are the same)
- *   "interleave"    1/0  with lane_thread: both groups' ranges go up in alternating pieces, each
- *                   group's pieces built and tabled as they land (default 1; only when every
- *                   cell of the second group follows the first group's cells)
- *   "upload_staged" 1/0  host counts go up through a pinned ring filled by "upload_threads"
- *                   copy threads instead of pageable copies (default 0: measured no faster)
- *   "upload_u16"    0..2  host-count ranges of 8 MB or more go up as 16-bit counts: narrowed by
- *                   "upload_threads" threads (default 4) into a pinned ring, widened on the device,
- *                   counts outside [0, 65535] listed and patched in (half the PCIe bytes): 1
- *                   (default) in scde_posteriors_host calls, 2 in every host entry (a DE call's
- *                   upload overlaps its first group's work: measured slower), 0 none; results
- *                   are the same
- *   "gene_waves"    3/4  k_boot_gene's waves per block (12 or 16 rows); 0 (default) = 3 from
- *                   "gene3_cells" cells per call (default: never; slower at config 4), else 4
- *   "gene_list_cap" slabs k_boot_gene's four-tile list pass takes (0 = 16384; beyond: k_boot2)
- *   "skip_slack"    mask heuristic slack (NaN = default 20 + 0.15 C; tests force redo slabs)
- *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
- *   "skip_stats"    1/0  count kept stretches and redo slabs (one host sync per launch)
- *   "ratio_window"  k_ratio_summary register window 4, 5, 7 or 8;  "ratio_block" 64, 128, 256
- *   "wpca_ms"       1/0  the multi-start npcs = 1 weighted-PCA kernel
+ *                   selected cells), 1..8 (default 4)
+ *   "upload_u16"    0..2  host-count ranges of 8 MB or more go up as 16-bit counts: narrowed by 4
+ *                   host threads into a pinned ring, widened on the device, counts outside
+ *                   [0, 65535] listed and patched in (half the PCIe bytes): 1 (default) in
+ *                   scde_posteriors_host calls, 2 in every host entry, 0 none
+ *   "modes_overlap" 1/0  scde.posteriors' read-backs run on a read-back thread beside the device
+ *                   work (default 1): the modes piece by piece as each piece's tables finish, the
+ *                   joint posterior in gene chunks of the bootstrap; 0: both after the bootstrap on
+ *                   the main stream (rocprofv3 runs)
+ *   "jp_chunks"     1..64 gene chunks of scde.posteriors' gene-block bootstrap (default 4, at most
+ *                   one per 256 genes): each chunk finishes before the next starts and its joint
+ *                   posterior rows are read back while the next runs
+ * Tables and other kernels:
+ *   "unique_fixed"  1/0  build each call's unique count tables with one host sync (fixed
+ *                   1024-word bitmaps per cell, counts below 65,536; a set with another count is
+ *                   rebuilt with exact widths); default 1, 0 = the exact three-phase build
+ *   "tables_nt"     0..2 the posterior-table rows as non-temporal stores: 0 never, 1 always, 2 when
+ *                   the call's rows exceed 256 MB (default)
+ *   "wpca_ms"       1/0  the multi-start npcs = 1 weighted-PCA kernel (default 1)
+ * (Removed in round 6, each measured slower or equal and deleted with its kernels and branches:
+ * fuse_groups, boot2_rows / k_boot2t, piece_taper, boot_chunks, ell_chunks, gene_waves /
+ * gene3_cells, lane_prio, lane_thread, interleave, defer_boot, upload_staged, upload_threads,
+ * pair_cells / gene_blocks (pair mode), gene_direct, rest_thread, tables_pair, task_cols,
+ * ratio_window / ratio_block: fixed at their defaults.)
  * Statistics: "skip_slabs", "skip_stretches", "skip_kept", "skip_redo", "degen", "tiles_<i>"
- * (k_boot_tiles slabs computing i tiles), "pair_redo" (slabs a pair pass left to the four-tile
- * pass) (with skip_stats); "boot_f64_fma" (FP64 lane FMAs the
+ * (k_boot_tiles slabs computing i tiles), "pair_redo" (slabs the gene blocks left to the four-tile
+ * list pass) (with skip_stats); "boot_f64_fma" (FP64 lane FMAs the
  * bootstrap kernels issued), also with skip_stats; "boot_path": the bootstrap kernel of the last
  * posterior (0 k_boot2, 1 k_boot_tiles / k_boot_gene, 3 the general k_boot); "stream_syncs",
  * "arena_syncs" (this context's and its peer's streams drained by a buffer regrowth / a pinned
@@ -211,6 +189,10 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  * context as it is created (an unknown name fails the creation). */
 int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value);
 int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
+/* Test hook: make the next `count` failures happen at fault point `where` ("u16_slot": the second
+ * slot of a 16-bit host-count upload fails as if its copy had) -- the error paths' recovery is
+ * tested through it (tests/test_gpu_fullsize.py).  Not for production use. */
+int scde_ctx_inject_fault(scde_ctx* ctx, const char* where, int count);
 int scde_ctx_reset_stats(scde_ctx* ctx);
 
 /* device buffers owned by the context's allocator */

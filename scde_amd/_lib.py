@@ -19,7 +19,7 @@ EXPORTS = [
     "scde_matSlideMult", "scde_ratio_summary", "scde_distribution_summary", "scde_bh_cz",
     "scde_ctx_create", "scde_ctx_destroy", "scde_ctx_synchronize", "scde_ctx_set_profiling",
     "scde_ctx_kernel_times", "scde_ctx_reset_kernel_times", "scde_ctx_set_option", "scde_ctx_get_stat",
-    "scde_ctx_reset_stats",
+    "scde_ctx_reset_stats", "scde_ctx_inject_fault",
     "scde_dev_alloc", "scde_dev_free", "scde_h2d", "scde_d2h",
     "scde_expression_difference_dev", "scde_posteriors_dev", "scde_bh_cz_dev",
     "scde_expression_difference_batch_dev", "scde_expression_prior_dev",
@@ -94,6 +94,8 @@ def lib():
     L.scde_ctx_set_option.argtypes = [P, ctypes.c_char_p, d]
     L.scde_ctx_get_stat.argtypes = [P, ctypes.c_char_p, P]
     L.scde_ctx_reset_stats.argtypes = [P]
+    if hasattr(L, "scde_ctx_inject_fault"):  # (study builds of earlier rounds lack the test hook)
+        L.scde_ctx_inject_fault.argtypes = [P, ctypes.c_char_p, i]
     L.scde_dev_alloc.argtypes = [P, i64, ctypes.POINTER(P)]
     L.scde_dev_free.argtypes = [P, P]
     L.scde_h2d.argtypes = [P, P, P, i64]

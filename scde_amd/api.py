@@ -251,6 +251,10 @@ class Context:
         check(lib().scde_ctx_get_stat(self.handle, name.encode(), ctypes.byref(v)))
         return v.value
 
+    def inject_fault(self, where: str, count: int = 1):
+        """Test hook (include/scde_hip.h scde_ctx_inject_fault): the next `count` failures at `where`."""
+        check(lib().scde_ctx_inject_fault(self.handle, where.encode(), int(count)))
+
     def reset_stats(self):
         check(lib().scde_ctx_reset_stats(self.handle))
 

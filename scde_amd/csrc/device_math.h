@@ -533,7 +533,7 @@ __device__ __forceinline__ double bd0_poly(double x, double np) {
 // bd0 in the series region from L = log(x / np) itself, with no division: x = np e^L gives
 // bd0 = np psi(L), psi(L) = L e^L - e^L + 1 = sum_{k>=2} (k - 1) L^k / k!.  In the region
 // |v| < 0.1, |L| < log(1.1 / 0.9) = 0.2007, and the terms through k = 12 leave a tail below
-// 2.4e-17 of the first (the degree that keeps k_tables_reg's 401-point row in registers).  Its error is np |L| |dL| <= 0.2 np |dL| for an error dL of L (a
+// 2.4e-17 of the first (the degree that keeps the general column's 401-point row in registers).  Its error is np |L| |dL| <= 0.2 np |dL| for an error dL of L (a
 // few ulps of log x and log np), a fifth of what x L + np - x carries outside the region.
 #ifndef SCDE_BD0_PSI
 #define SCDE_BD0_PSI 1

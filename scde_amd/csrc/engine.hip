@@ -240,10 +240,6 @@ struct scde_ctx {
   // order) needs only the count-0 columns: it runs on aux_stream after p1_ev (phase 1 of the
   // tables), beside phase 2, and the bootstrap waits for aux_ev
   hipStream_t aux_stream = nullptr;
-  // the peer lane's parked stream set (main, aux) of the other priority (peer_set_prio)
-  hipStream_t alt_stream = nullptr, alt_aux = nullptr;
-  bool prio_hi = false;
-  hipEvent_t prio_ev[2] = {nullptr, nullptr};
   hipEvent_t p1_ev = nullptr, aux_ev = nullptr;
   // Pinned staging arena for the small per-call transfers (cell lists, offsets, draws,
   // multiplicities, tasks; the unique builder's size read-backs).  A pageable copy is staged
@@ -268,18 +264,17 @@ struct scde_ctx {
   Buf w8, w8t, w8g, qflags;
   // tile bootstrap gene order: keys, sorted keys, indices, order, sort workspace
   Buf gkey, gkey2, gidx, gorder, gwork, pmask, pwide, ellw, excd, gdone;
-  // options (scde_ctx_set_option): tuning and test switches, never read from the environment
-  int opt_boot_skip = 1;         // "boot_skip": grid-stretch skipping in the bootstrap
+  // options (scde_ctx_set_option; include/scde_hip.h lists them): each a default path's switch or a
+  // documented operating / test mode; read from the environment only at creation (SCDE_OPTIONS)
+  int opt_boot_skip = 1;         // "boot_skip": grid-stretch / tile skipping in the bootstrap (same bits either way)
   double opt_skip_slack = NAN;   // "skip_slack": mask slack (NaN = 20 + 0.15 C); tests force redo slabs
   int opt_boot_nb = 0;           // "boot_nb": boots per slab (0 = automatic; a multiple of 4 in [4, 32])
   int opt_skip_stats = 0;        // "skip_stats": count kept stretches / redo slabs (a host sync per launch)
-  int opt_ratio_window = 4;      // "ratio_window": k_ratio_summary register window (4, 5, 7, 8)
-  int opt_ratio_block = 128;     // "ratio_block": k_ratio_summary block size (64, 128, 256)
   int opt_wpca_ms = 1;           // "wpca_ms": the multi-start npcs = 1 kernel (k_wpca_ms1)
-  int opt_boot_tiles = 1;        // "boot_tiles": the FP64 bootstrap on bounded 16-point tiles (k_boot_tiles)
+  int opt_boot_tiles = 1;        // "boot_tiles": the FP64 bootstrap on bounded 32-point tiles (k_boot_gene)
   int opt_boot_tiles_cells = 400;  // "boot_tiles_cells": cells per call from which it is used (fewer: the
                                    // rows are wide, most slabs need > 8 tiles, k_boot2's stretches win)
-  int opt_tile_groups = 4;       // "tile_groups": 32-point bound tiles k_boot_tiles computes per slab (1..4)
+  int opt_tile_groups = 4;       // "tile_groups": 32-point bound tiles the list pass computes per slab (1..4; tests)
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 3;        // "tile_order": the tile bootstrap takes genes by count sum (cache sharing):
@@ -287,80 +282,41 @@ struct scde_ctx {
                                  // launches of at most kDescGenes genes, where the last, heaviest blocks would
                                  // set the launch's tail), 0 in gene order
   int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
-  int opt_gene_blocks = 1;       // "gene_blocks": k_boot_gene (a 4-wave block per gene's slab group, rows shared
-                                 // by its slabs) instead of one k_boot_tiles wave per slab; not with pair mode
-  int opt_upload_staged = 0;     // "upload_staged": host-count uploads through a pinned ring filled by copy threads
-  int opt_upload_threads = 4;     // "upload_threads": threads filling a staging slot (staged: the upload worker
-                                 // included; 16-bit: the narrowing pool)
   int opt_upload_u16 = 1;        // "upload_u16": host-count ranges of >= 8 MB go up as 16-bit counts (U16Ring): 1
                                  // scde.posteriors' host entry, 2 every host entry, 0 none
   int opt_modes_overlap = 1;     // "modes_overlap": scde.posteriors' read-backs (modes piece by piece, jp in gene
                                  // chunks) overlap the tables and the bootstrap from a read-back thread (0: after
                                  // the bootstrap, on the main stream -- rocprofv3 runs, where the pageable
                                  // read-back becomes blit kernels that would share the CUs)
-  int opt_gene_direct = 1;       // "gene_direct": gene blocks holding all of a gene's slabs write its jp row
-                                 // (k_sum_partials skips the gene)
-  int opt_ell_chunks = 1;        // "ell_chunks": at most this many cell chunks in the ELL build (0: by size, two
-                                 // passes; measured no faster: config 3 6.75-6.90 ms host -> host with one pass vs
-                                 // 6.90 chunked, shard of 8 1.68 vs 1.72, configs 2 / 2b / 4 within noise)
   int opt_jp_chunks = 4;         // "jp_chunks": gene chunks of scde.posteriors' gene-block bootstrap, each chunk's
                                  // jp rows read back while the next runs (1: one launch, jp after it)
-  int opt_gene_waves = 0;        // "gene_waves": k_boot_gene's waves per block, 3 or 4 (0: by gene3_cells)
-  int opt_gene3_cells = 1 << 30;  // "gene3_cells": cells per call from which k_boot_gene runs 3-wave blocks (off:
-                                  // config 4 measured 12.85 ms of bootstrap per step with them vs 10.24 with 4)
   int opt_gene_list_cap = 0;     // "gene_list_cap": slabs k_boot_gene's list pass takes at most (0: 16384; tests)
   int opt_gene_rows = 4;         // "gene_rows": rows per slab k_boot_gene gives each slab at most (tests force its
                                  // four-tile list pass with fewer)
-  int opt_pair_cells = 1000;     // "pair_cells": cells per call from which k_boot_tiles pairs slabs (two bound
-                                 // tiles each; the posterior narrows with the cells, most slabs need two)
   double opt_pipeline_mb = 32;  // "pipeline_mb": host-count DE calls from this many MB of counts upload in two
                                 // column ranges, each group starting once its cells are in HBM
   int opt_pieces = 4;           // "pieces": the first group's columns of a pipelined host-count DE call upload
                                 // in this many pieces, each piece's unique sets and tables starting as it lands
-  int opt_piece_taper = 0;      // "piece_taper": pieces of decreasing size (weights K, K - 1, .., 1), so the
-                                // last piece -- whose unique sets and tables follow the last byte -- is short
-                                // (measured slower: config 3 6.95-6.99 vs 6.62-6.67 ms, config 4 19.5-22.6 vs
-                                // 16.1-16.3 host -> host: the large first pieces delay the start); 2:
-                                // increasing sizes 1, 2, .., K (measured equal: config 4 15.6-16.1 vs
-                                // 15.8-16.1, config 3 6.55-6.56 vs 6.55-6.65)
-  int opt_lane_prio = 0;        // "lane_prio": the peer lane's streams at the device's highest priority: 0
-                                // never (default), 1 always, 2 for calls of at most kPrioGenes genes (per
-                                // call: the peer keeps a stream set per priority).  Measured on two boxes
-                                // with opposite results at the shard of 8 (1 vs 0: 1.58-1.61 vs 1.68 ms; 2
-                                // vs 0: 1.81-1.85 vs 1.60-1.66), slower at config 3
-  int opt_boot_chunks = 1;      // "boot_chunks": k_boot_gene's grid in this many launches
-  int opt_rest_thread = 1;      // "rest_thread": a two-lane DE call on counts in HBM runs the second group's
-                                // draws, set-up and bootstrap launch from a host thread of its own
-  int opt_interleave = 1;       // "interleave": with lane_thread, both groups' ranges go up in alternating
-                                // pieces (when the second group's cells all follow the first group's range)
-  int opt_lane_thread = 0;      // "lane_thread": a pipelined two-lane DE call drives the second lane from a host
-                                // thread of its own
-  int opt_defer_boot = 0;       // "defer_boot": pipelined two-lane DE queues the first group's bootstrap after
-                                // the second group's tables
-  int opt_tables_pair = 1;       // "tables_pair": k_tables_reg computes a wave's columns two at a time (0: one)
-  int opt_tables_nt = 2;         // "tables_nt": table rows as non-temporal stores (0 no, 1 yes, 2 when the call's rows exceed 256 MB)
-  int opt_task_cols = 0;         // "task_cols": columns per tables task (0: 32 for launches under 4096
-                                 // 64-column tasks, else 64; at most kTabTaskCols)
-  int opt_boot2_rows = 0;        // "boot2_rows": the stretch-mask bootstrap (below boot_tiles_cells) on tile rows
-                                 // (k_boot2t: two kept stretches per wave, DPP64 multiplicities; same bits).  Off:
-                                 // measured slower than k_boot2 (config 2 bootstrap 3.51 vs 3.19 ms per step, 2b
-                                 // 8.72 vs 7.93)
-  int opt_fuse_groups = 0;       // "fuse_groups": a DE call's two group posteriors run as one (PostSpec::ngroups:
-                                 // concatenated cells, doubled genes, one launch per stage; same bits).  Off:
-                                 // measured no faster than the two lanes (config 3 host -> host 7.20 vs 6.80 ms,
-                                 // shard of 8 1.69 vs 1.66)
-  int opt_boot_gate = 1;         // "boot_gate": two lanes' bootstraps wait for both lanes' set-up chains (BootGate)
-  int opt_lanes = 2;             // "lanes": a DE call's two group posteriors run concurrently (2: the second
-                                 // group on `peer`, its own streams and workspace) or one after the other (1)
+  int opt_tables_nt = 2;        // "tables_nt": table rows as non-temporal stores (0 no, 1 yes, 2 when the call's
+                                // rows exceed 256 MB)
+  int fault_u16 = 0;            // test hook (scde_ctx_inject_fault): 16-bit upload slots to fail
+  int opt_lanes = 2;            // "lanes": a DE call's two group posteriors run concurrently (2: the second
+                                // group on `peer`, its own streams and workspace) or one after the other (1)
+  // fixed settings that were options until round 5 (the alternatives measured slower or equal and were
+  // removed)
+  static constexpr int opt_ratio_window = 4;   // k_ratio_summary register window
+  static constexpr int opt_ratio_block = 128;  // k_ratio_summary block size
+  static constexpr int opt_upload_threads = 4; // the 16-bit narrowing pool
+  static constexpr int opt_gene_direct = 1;    // gene blocks holding all of a gene's slabs write its jp row
+  static constexpr int opt_ell_chunks = 1;     // the ELL rows in one pass
+  static constexpr int opt_gene_blocks = 1;    // the tile path as k_boot_gene gene blocks
   // the second lane of a DE call: a context on the same device, created on first use; its
   // options are copied from this one per call and its timings/statistics merged back
   scde_ctx* peer = nullptr;
   hipEvent_t lane_ev[2] = {nullptr, nullptr};  // [0] this stream -> peer, [1] peer -> this stream
-  hipEvent_t gate_ev[2] = {nullptr, nullptr};  // BootGate: each lane's set-up chain done
   hipEvent_t piece_ev[8] = {nullptr};           // run_posterior's pieces: unique sets built
   hipEvent_t piece_up_ev[8] = {nullptr};        // the pieces' uploads landed (upload worker)
   hipStream_t uq_stream = nullptr;              // the pieces' and the second group's unique builds
-  int stream_prio = 0;  // priority of streams this context creates (the peer lane: the device's highest)
   // host-count upload thread (created on first use, lives with the context): a pageable copy
   // blocks its calling thread for the whole transfer, so the pieces go up from here, back to
   // back, while the caller builds unique sets and queues kernels
@@ -398,27 +354,6 @@ struct scde_ctx {
     bool stop = false;
     bool hold = false;  // jobs queue but wait (dnl_hold): pageable read-backs slow the host-count uploads
   } dnl;
-  // Pinned staging for the host-count uploads (option "upload_staged"): the upload worker copies
-  // each chunk of the caller's pageable matrix into a pinned ring slot with T pool threads (it
-  // takes one share itself), then issues the DMA from the slot; a slot is reused once its DMA's
-  // event has fired.  A pageable hipMemcpyAsync is staged by the runtime on the issuing thread.
-  struct Stager {
-    static constexpr int kSlots = 4;
-    static constexpr size_t kSlot = size_t(4) << 20;
-    char* pin = nullptr;
-    hipEvent_t ev[kSlots] = {};
-    bool used[kSlots] = {};
-    long long next = 0;
-    std::vector<std::thread> th;
-    std::mutex m;
-    std::condition_variable cv, cvd;
-    long long gen = 0;
-    int pending = 0, T = 0;
-    bool stop = false;
-    const char* src = nullptr;
-    char* dst = nullptr;
-    size_t n = 0;
-  } stg;
   // 16-bit host-count uploads (option "upload_u16"): a pool of T threads narrows each 4M-count
   // slot of the caller's int32 matrix to uint16 into a pinned ring slot, listing the counts
   // outside [0, 65535] (index, value) as they go; the upload worker sends the slot up, a widening
@@ -585,14 +520,6 @@ struct scde_ctx {
     return SCDE_OK;
   }
   ~scde_ctx() {
-    if (!stg.th.empty()) {
-      {
-        std::lock_guard<std::mutex> lk(stg.m);
-        stg.stop = true;
-      }
-      stg.cv.notify_all();
-      for (auto& t : stg.th) t.join();
-    }
     if (dnl.th.joinable()) {
       {
         std::lock_guard<std::mutex> lk(dnl.m);
@@ -629,8 +556,6 @@ struct scde_ctx {
     }
     for (auto& e : lane_ev)
       if (e) (void)hipEventDestroy(e);
-    for (auto& e : gate_ev)
-      if (e) (void)hipEventDestroy(e);
     for (auto& e : piece_ev)
       if (e) (void)hipEventDestroy(e);
     for (auto& e : piece_up_ev)
@@ -662,14 +587,7 @@ struct scde_ctx {
     if (p1_ev) (void)hipEventDestroy(p1_ev);
     if (aux_ev) (void)hipEventDestroy(aux_ev);
     if (aux_stream) (void)hipStreamDestroy(aux_stream);
-    if (alt_stream) (void)hipStreamDestroy(alt_stream);
-    if (alt_aux) (void)hipStreamDestroy(alt_aux);
-    for (auto& e : prio_ev)
-      if (e) (void)hipEventDestroy(e);
     if (pin) (void)hipHostFree(pin);
-    if (stg.pin) (void)hipHostFree(stg.pin);
-    for (auto& e : stg.ev)
-      if (e) (void)hipEventDestroy(e);
     for (auto& e : up_ev)
       if (e) (void)hipEventDestroy(e);
   }
@@ -709,7 +627,9 @@ int dnl_push(scde_ctx* cx, hipStream_t after, void* dst, size_t dpitch, const vo
   std::lock_guard<std::mutex> lk(d.m);
   if (d.nev == (int)d.evs.size()) {  // one event per job of a call (reused once dnl_wait drained them)
     hipEvent_t e = nullptr;
-    HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    // blocking sync: the read-back thread's hipEventSynchronize sleeps instead of spinning through
+    // the tables and the bootstrap (the lanes' threads need the CPU share)
+    HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     d.evs.push_back(e);
   }
   const int ei = d.nev++;
@@ -758,39 +678,6 @@ hipError_t ctx_streams_sync(scde_ctx* cx) {
 namespace {
 
 // ------------------------------------------------------------------ posterior spec
-// Two lanes' bootstraps start only once both lanes' set-up chains are queued and done: each lane's
-// continuation records its set-up's end on its stream, waits (host) for the other lane to do the
-// same, and makes its stream wait for the other lane's event before its bootstrap launch.  Without it
-// the lane whose set-up comes second has its small kernels (ELL rows, order sort, multiplicities,
-// bounds) queued beside the first lane's bootstrap waves, which starve them.
-// A lane that ends without reaching its bootstrap (an error, no bootstrap) leaves the gate, so the
-// other never waits for it.
-struct BootGate {
-  std::mutex m;
-  std::condition_variable cv;
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  bool rec[2] = {false, false}, gone[2] = {false, false};
-  // slot's set-up chain ends here on stream st; returns once the other lane has arrived or left
-  int arrive(int slot, hipStream_t st) {
-    const hipError_t e = hipEventRecord(ev[slot], st);
-    std::unique_lock<std::mutex> lk(m);
-    rec[slot] = e == hipSuccess;
-    gone[slot] = true;
-    cv.notify_all();
-    cv.wait(lk, [&] { return gone[1 - slot]; });
-    const bool wait_other = rec[1 - slot];
-    lk.unlock();
-    if (e != hipSuccess) return fail(SCDE_EHIP, "hipEventRecord: %s", hipGetErrorString(e));
-    if (wait_other) HCHK(hipStreamWaitEvent(st, ev[1 - slot], 0));
-    return SCDE_OK;
-  }
-  void leave(int slot) {
-    std::lock_guard<std::mutex> lk(m);
-    gone[slot] = true;
-    cv.notify_all();
-  }
-};
-
 struct PostSpec {
   int ncells = 0;
   const double* models = nullptr;  // host ncells x 12 col-major
@@ -831,21 +718,10 @@ struct PostSpec {
   // reached the point it recorded; run_posterior builds each piece's unique sets on
   // piece_stream and launches its tables as it arrives (piece_ev: one event per piece)
   int npieces = 0;
-  BootGate* gate = nullptr;  // two lanes' deferred continuations: arrive before the bootstrap launch
-  int gate_slot = 0;
   const int* piece_c = nullptr;
   std::function<int(int)> piece_ready;
   hipStream_t piece_stream = nullptr;
   hipEvent_t* piece_ev = nullptr;
-  // A DE call's two group posteriors fused into one (de_run, option fuse_groups): the spec's cells
-  // are group A's (cells [0, gsplit)) then group B's, its seed sets A's then B's (B's set s is
-  // nsets_g + s; `seeds` lists both, `wset` is [2 ngenes], B's genes offset by nsets_g), and the
-  // bootstrap runs over 2 ngenes genes: gene g + ngenes is gene g of group B.  Every value is formed
-  // as in the group's own call (its cells' order in the baseline sums, its clamp constant, its
-  // draws), so the fused call is bit-identical to two calls.  jp holds 2 ngenes gene-major rows.
-  int ngroups = 1;
-  int gsplit = 0;
-  int nsets_g = 0;
   // host destinations read back by the context's Downloader while later work runs (the caller then
   // copies neither and drains the Downloader before returning): modes_host, the modes matrix
   // (pieces: each piece's columns once its tables are done); jp_host, the joint posterior in R's
@@ -1060,14 +936,10 @@ int build_unique_sets(scde_ctx* cx, const PostSpec* const* s, UniqueSet* const* 
   return SCDE_OK;
 }
 
-// The draw lists alone (cell per draw; -1 pads a fused shorter group's lists) and the largest
-// multiplicity of a cell in one boot.
+// The draw lists alone (cell per draw) and the largest multiplicity of a cell in one boot.
 void make_draws_lists(const PostSpec& s, std::vector<int>& draws, int& ndraw, int* maxw) {
   const int C = s.ncells, B = s.nboot, nsets = (int)s.seeds.size();
-  const bool two = s.ngroups == 2 && !s.batch_call;
-  if (two) {
-    ndraw = std::max(s.gsplit, C - s.gsplit);
-  } else if (s.batch_call) {
+  if (s.batch_call) {
     ndraw = 0;
     for (int k = 0; k < s.nbatch; ++k) ndraw += std::max(0, s.comp[k]);
   } else {
@@ -1080,8 +952,7 @@ void make_draws_lists(const PostSpec& s, std::vector<int>& draws, int& ndraw, in
   for (int set = 0; set < nsets; ++set) {
     PlatformRand rng((unsigned int)s.seeds[set], s.rand_kind);
     int* dr = draws.data() + (size_t)set * per;
-    const int gi = (two && set >= s.nsets_g) ? 1 : 0, c0 = gi ? s.gsplit : 0;
-    const int n = two ? (gi ? C - s.gsplit : s.gsplit) : C;
+    const int c0 = 0, n = C;
     for (int b = 0; b < B; ++b) {
       int* row = dr + (size_t)b * ndraw;
       int d = 0;
@@ -1109,28 +980,6 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
   const int C = s.ncells, B = s.nboot, nsets = (int)s.seeds.size();
   if (!want_W) {
     make_draws_lists(s, draws, ndraw, maxw);
-    return;
-  }
-  if (s.ngroups == 2 && !s.batch_call) {
-    // fused groups: set `set` belongs to group B from nsets_g on; each draws from its own group's
-    // cells (the group's own call, cell indices offset into the fused list); the shorter group's
-    // draw lists are padded with -1
-    const int Cg[2] = {s.gsplit, C - s.gsplit};
-    ndraw = std::max(Cg[0], Cg[1]);
-    draws.assign((size_t)nsets * B * std::max(ndraw, 1), -1);
-    W.assign((size_t)nsets * C * Bp, 0.0);
-    for (int set = 0; set < nsets; ++set) {
-      const int gi = set >= s.nsets_g ? 1 : 0, c0 = gi ? s.gsplit : 0, n = Cg[gi];
-      PlatformRand rng((unsigned int)s.seeds[set], s.rand_kind);
-      int* dr = draws.data() + (size_t)set * B * std::max(ndraw, 1);
-      double* w = W.data() + (size_t)set * C * Bp;
-      for (int b = 0; b < B; ++b)
-        for (int j = 0; j < n; ++j) {
-          const int cell = c0 + rng.draw(n);
-          dr[(size_t)b * ndraw + j] = cell;
-          w[(size_t)cell * Bp + b] += 1.0;
-        }
-    }
     return;
   }
   if (s.batch_call) {
@@ -1174,21 +1023,11 @@ void make_draws(const PostSpec& s, int Bp, std::vector<int>& draws, std::vector<
 // rest (nullable): return once the tables are queued, with the remaining work (modes, draws,
 // bootstrap, outputs) in *rest, to be run later on the same stream -- de_run queues both groups'
 // tables before either bootstrap, so the second lane's tables start at once
-// status of run_posterior for a fused two-group spec whose fused column count leaves the fast
-// bootstrap path (columns past 2^31 / GS): de_run runs the two groups separately instead
-constexpr int kRetryUnfused = 1001;
 
 int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<int()>* rest = nullptr) {
   const int C = s.ncells, G = s.G, N = s.ngenes;
-  const bool two = s.ngroups == 2;
-  if (two && (s.gsplit <= 0 || s.gsplit >= C || s.batch_call || s.ensemble || s.nboot <= 0 || s.modes || s.post ||
-              s.ucl_host || (int)s.wset.size() != 2 * N || (int)s.seeds.size() != 2 * s.nsets_g))
-    return fail(SCDE_EINTERNAL, "fused groups: bad spec");
-  // cells per call of the kernel choices (a fused call's groups choose alike, de_run checks) and
-  // the widest group (ELL rows); the bootstrap's genes (both groups' when fused)
-  const int Ccall = two ? std::min(s.gsplit, C - s.gsplit) : C;
-  const int Cmax = two ? std::max(s.gsplit, C - s.gsplit) : C;
-  const int NBg = two ? 2 * N : N;
+  // cells per call of the kernel choices, the widest cell list (ELL rows), the bootstrap's genes
+  const int Ccall = C, Cmax = C, NBg = N;
   // column stride: >= the k_boot2 block (lanes never read past a column); 512 keeps
   // columns 4 KiB-aligned
   const int GS = G <= 448 ? 512 : (int)round_up(G, 64);
@@ -1287,7 +1126,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   };
   // pieces: planned for the smallest column count (every condition holds for fewer columns)
   const Plan plan0 = make_plan(pieces ? 0 : ucl_off_h[C]);
-  if (two && !plan0.fused) return kRetryUnfused;
   const bool want_maxi = s.batch_call ? (s.postflag == 1) : (s.postflag == 1 || s.postflag == 3);
   TablesArgs ta{};
   // buffers for `cap` columns (pieces: grown keeping what earlier pieces wrote) and the
@@ -1314,11 +1152,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     ta.lcfpr = cx->lcfpr.as<double>();
     ta.theta = cx->theta.as<double>();
     ta.cellscal = cx->cellscal.as<double>();
-    // the reference's clamp, -DBL_MAX / (cells in the call) / 1.1: per group when two are fused
-    ta.minlogprob = -1 * DBL_MAX / (s.ngroups == 2 ? s.gsplit : C) / 1.1;
-    ta.minlogprob2 = -1 * DBL_MAX / (s.ngroups == 2 ? C - s.gsplit : C) / 1.1;
-    ta.mlp_split = s.ngroups == 2 ? s.gsplit : C;
-    ta.pair_cols = cx->opt_tables_pair;
+    // the reference's clamp, -DBL_MAX / (cells in the call) / 1.1 (src/jpmatLogBoot.cpp:127)
+    ta.minlogprob = -1 * DBL_MAX / C / 1.1;
     // rows that fit the 256 MB last-level cache can be read back from it by the bootstrap: plain
     // stores there
     ta.nt_rows = cx->opt_tables_nt == 1 || (cx->opt_tables_nt == 2 && (double)ncap * GS * sizeof(double) > 256.0 * (1 << 20));
@@ -1367,7 +1202,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     if (tc.zcol) tc.zcol = ta.zcol + c0;
     if (tc.base_col) tc.base_col = ta.base_col + c0;
     tc.col_base = (int)col0;
-    tc.mlp_split = ta.mlp_split - c0;  // relative to the launch's first cell
     // cell-staged tables (G <= 448): tasks of up to 64 columns of one cell -- one lane per column in
     // k_tables_lpc (constant theta); with local theta (k_tables_cell, 8 columns per wave) a launch that
     // would fill fewer than 4 rounds of the chip's block slots takes 32-column tasks, so its last
@@ -1490,7 +1324,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   }
   const long long ncols = ucl_off_h[C];
   const Plan plan = make_plan(ncols);
-  if (two && !plan.fused) return kRetryUnfused;
   const bool fast = plan.fast, fused = plan.fused, stretch_skip = plan.stretch_skip;
   bool tpath = plan.tpath;
   ta.ncols = ncols;
@@ -1511,11 +1344,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
   std::vector<double> W;
   int ndraw = 0, maxw = 0;
   const int nsets = (int)s.seeds.size();
-  // the cells a seed set draws from (fused groups: its own group's)
-  // (by value: rest_fn, which uses them, may run after this function has returned)
-  const int nsets_g = s.nsets_g, gsplit = s.gsplit;
-  auto set_c0 = [two, nsets_g, gsplit](int set) { return two && set >= nsets_g ? gsplit : 0; };
-  auto set_c1 = [two, nsets_g, gsplit, C](int set) { return two && set < nsets_g ? gsplit : C; };
   // tile path ELL rows: a multiple of 64 entries (the bound MFMAs' K steps) plus 64
   const int qstride = (int)round_up(std::max(Cmax, 1), 64) + 64;
   // FP64 path: boots per slab; the draws come after the tables launch (the host's RNG work
@@ -1576,7 +1404,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // beside phase 2 of the tables
     hipStream_t sa = st;
     if (fused) {
-      if (!cx->aux_stream) HCHK(hipStreamCreateWithPriority(&cx->aux_stream, hipStreamNonBlocking, cx->stream_prio));
+      if (!cx->aux_stream) HCHK(hipStreamCreateWithFlags(&cx->aux_stream, hipStreamNonBlocking));
       if (!cx->aux_ev) HCHK(hipEventCreateWithFlags(&cx->aux_ev, hipEventDisableTiming));
       sa = cx->aux_stream;
       HCHK(hipStreamWaitEvent(sa, cx->p1_ev, 0));
@@ -1608,7 +1436,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // gene chunks (jp_host): the bootstrap over genes [gch(k), gch(k + 1)) finishes (list pass,
     // fallback, slab sums, exact rows) before chunk k + 1 starts, and chunk k's jp rows go back to
     // the host while it runs -- the read-back of the last chunk only is left after the bootstrap
-    const int nchunks = (s.jp_host && !two && gene_sg > 0 && s.jp_g == 1 && s.jp_k == N)
+    const int nchunks = (s.jp_host && gene_sg > 0 && s.jp_g == 1 && s.jp_k == N)
                             ? std::max(1, std::min(cx->opt_jp_chunks, NBg / 256 + 1)) : 1;
     auto gch = [NBg, nchunks](int k) { return (int)((long long)NBg * k / nchunks); };
     // tile path: genes in order of their count sums (waves in flight share columns in L2), keyed by
@@ -1628,17 +1456,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       HCHK(cx->gidx.ensure(sizeof(int) * NBg));
       HCHK(cx->gorder.ensure(sizeof(int) * NBg));
     }
-    // ELL rows (fused groups: group B's genes after group A's, over B's cells, cells offset by gsplit)
-    for (int gi = 0; gi < (two ? 2 : 1); ++gi) {
-      const int c0 = gi ? s.gsplit : 0, nc = two ? (gi ? C - s.gsplit : s.gsplit) : C;
-      HCHK(cx->ellw.ensure(std::max<size_t>(1, ell_work_bytes(N, nc, cx->opt_ell_chunks))));
-      HCHK(launch_ell(u.uci.as<int>() + (size_t)N * c0, N, N, nc, u.ucl_off.as<long long>() + c0,
-                      cx->base_col.as<int>() + c0, stride, (int)ncols, tpath ? 64 : 8,
-                      cx->ent.as<int2>() + (size_t)gi * N * stride, cx->nnz.as<int>() + (size_t)gi * N, sa, c0,
-                      cx->ellw.p, have_order ? u.ucl.as<int>() : nullptr, have_order ? cx->gkey.as<unsigned>() + (size_t)gi * N : nullptr,
-                      have_order ? cx->gidx.as<int>() + (size_t)gi * N : nullptr, gi * N, NBg, nchunks,
-                      order_desc, cx->opt_ell_chunks));
-    }
+    // ELL rows (and the gene-order keys)
+    HCHK(cx->ellw.ensure(std::max<size_t>(1, ell_work_bytes(N, C, cx->opt_ell_chunks))));
+    HCHK(launch_ell(u.uci.as<int>(), N, N, C, u.ucl_off.as<long long>(), cx->base_col.as<int>(), stride, (int)ncols,
+                    tpath ? 64 : 8, cx->ent.as<int2>(), cx->nnz.as<int>(), sa, 0, cx->ellw.p,
+                    have_order ? u.ucl.as<int>() : nullptr, have_order ? cx->gkey.as<unsigned>() : nullptr,
+                    have_order ? cx->gidx.as<int>() : nullptr, 0, NBg, nchunks, order_desc, cx->opt_ell_chunks));
     if (have_order) {
       size_t wb = 0;
       HCHK(launch_gene_order(nullptr, nullptr, NBg, nullptr, nullptr, nullptr, &wb, sa));
@@ -1670,7 +1493,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       const int P = (s.nboot + nb - 1) / nb;
       std::vector<unsigned char> w8((size_t)nsets * C * Bt, 0), w8p((size_t)nsets * C * P * 32, 0);
       for (int set = 0; set < nsets; ++set)
-        for (int c = set_c0(set); c < set_c1(set); ++c) {
+        for (int c = 0; c < C; ++c) {
           const double* wr = W.data() + ((size_t)set * C + c) * Bp;
           for (int b = 0; b < Bp; ++b) w8[((size_t)set * C + c) * Bt + b] = (unsigned char)wr[b];
           for (int p = 0; p < P; ++p)
@@ -1687,7 +1510,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         const int NGR = (P + gene_sg - 1) / gene_sg;
         std::vector<unsigned char> w8g((size_t)nsets * C * NGR * 128, 0);
         for (int set = 0; set < nsets; ++set)
-          for (int c = set_c0(set); c < set_c1(set); ++c) {
+          for (int c = 0; c < C; ++c) {
             const double* wr = W.data() + ((size_t)set * C + c) * Bp;
             for (int gr = 0; gr < NGR; ++gr) {
               const int gb0 = gr * gene_sg * nb, gnb = std::min(gene_sg, P - gr * gene_sg) * nb;
@@ -1710,11 +1533,11 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     }
     HCHK(cx->Z.ensure(sizeof(double) * (size_t)nsets * Bp * GS));
     HCHK(launch_baseline_z(Tbase, G, GS, cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
-                           cx->Z.as<double>(), sa, two ? s.nsets_g : 0, two ? s.gsplit : 0));
+                           cx->Z.as<double>(), sa));
     if (stretch_skip) {
       HCHK(cx->zubound.ensure(sizeof(double) * 8 * (size_t)nsets * Bp));
       HCHK(launch_stretch_zu(cx->ubound.as<double>(), cx->base_col.as<int>(), C, cx->Wt.as<double>(), Bp, nsets,
-                             cx->zubound.as<double>(), sa, two ? s.nsets_g : 0, two ? s.gsplit : 0));
+                             cx->zubound.as<double>(), sa));
     }
     cx->mark_end(SLOT_OTHER, ev);
     if (nsets > 1) {
@@ -1750,14 +1573,12 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       xa.out_g = s.jp_g;
       xa.out_k = s.jp_k;
       xa.ngenes = NBg;
-      xa.gene_mod = two ? N : 0;
       xa.g_lo = g_lo;
       xa.g_hi = g_hi;
       HCHK(launch_boot_exact(xa, st));
       exact_done = true;
       return SCDE_OK;
     };
-    if (s.gate) RCHK(s.gate->arrive(s.gate_slot, st));
     ev = cx->mark_begin(SLOT_BOOT);
     if (fast) {
       Boot2Args b2{};
@@ -1798,10 +1619,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         b2.mask = cx->smask.as<int>();
         b2.ubuf = cx->subuf.as<double>();
         b2.redo = cx->sredo.as<int>();
-        if (cx->opt_boot2_rows) {  // k_boot2t: the kept stretches on tile rows, pmask for the slab sums
-          HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * NBg)));
-          b2.pmask = cx->pmask.as<unsigned>();
-        }
       }
       cx->st_boot_path = tpath ? 1 : 0;
       if (tpath) {
@@ -1817,11 +1634,6 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
         tb.stats = cx->opt_skip_stats ? cx->qflags.as<int>() + 2 : nullptr;
         HCHK(cx->pmask.ensure(sizeof(unsigned) * std::max<size_t>(1, (size_t)P * NBg)));
         tb.pmask = cx->pmask.as<unsigned>();
-        tb.pairs = (gene_sg == 0 && Ccall >= cx->opt_pair_cells && P >= 2) ? 1 : 0;
-        if (tb.pairs) {
-          HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * NBg)));
-          tb.wide = cx->pwide.as<int>();
-        }
         if (gene_sg > 0) {
           HCHK(cx->pwide.ensure(sizeof(int) * (1 + (size_t)P * NBg)));
           tb.wide = cx->pwide.as<int>();
@@ -1829,10 +1641,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
           tb.SG = gene_sg;
           tb.kcap = cx->opt_gene_rows;
           tb.list_cap = cx->opt_gene_list_cap;
-          // 12 rows per gene block from gene3_cells cells per call (slabs mostly need two tiles there)
-          tb.gene_waves = cx->opt_gene_waves ? cx->opt_gene_waves : (Ccall >= cx->opt_gene3_cells ? 3 : 4);
           tb.W8g = cx->w8g.as<unsigned char>();
-          tb.chunks = std::max(1, cx->opt_boot_chunks);
           if (cx->opt_gene_direct) {
             HCHK(cx->gdone.ensure(sizeof(int) * std::max(1, NBg)));
             tb.gdone = cx->gdone.as<int>();
@@ -2162,43 +1971,21 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
   else if (n == "skip_slack") ctx->opt_skip_slack = value;
   else if (n == "boot_nb") ctx->opt_boot_nb = (int)value;
   else if (n == "skip_stats") ctx->opt_skip_stats = value != 0;
-  else if (n == "ratio_window") ctx->opt_ratio_window = (int)value;
-  else if (n == "ratio_block") ctx->opt_ratio_block = (int)value;
   else if (n == "wpca_ms") ctx->opt_wpca_ms = value != 0;
   else if (n == "boot_tiles") ctx->opt_boot_tiles = value != 0;
   else if (n == "boot_tiles_cells") ctx->opt_boot_tiles_cells = (int)value;
   else if (n == "tile_groups") ctx->opt_tile_groups = (int)value;
   else if (n == "tile_max_mult") ctx->opt_tile_max_mult = (int)value;
   else if (n == "tile_order") ctx->opt_tile_order = (value >= 1 && value <= 3) ? (int)value : 0;
-  else if (n == "pair_cells") ctx->opt_pair_cells = (int)value;
-  else if (n == "gene_blocks") ctx->opt_gene_blocks = value != 0;
   else if (n == "modes_overlap") ctx->opt_modes_overlap = value != 0;
-  else if (n == "gene_direct") ctx->opt_gene_direct = value != 0;
-  else if (n == "ell_chunks") ctx->opt_ell_chunks = std::max(0, std::min(64, (int)value));
   else if (n == "jp_chunks") ctx->opt_jp_chunks = std::max(1, std::min(64, (int)value));
-  else if (n == "upload_staged") ctx->opt_upload_staged = value != 0;
   else if (n == "upload_u16") ctx->opt_upload_u16 = (value >= 0 && value <= 2) ? (int)value : 1;
-  else if (n == "upload_threads") ctx->opt_upload_threads = std::max(1, std::min(32, (int)value));
-  else if (n == "gene_waves") ctx->opt_gene_waves = (value == 3 || value == 4) ? (int)value : 0;
-  else if (n == "gene3_cells") ctx->opt_gene3_cells = (int)value;
   else if (n == "gene_list_cap") ctx->opt_gene_list_cap = std::max(0, (int)value);
   else if (n == "gene_rows") ctx->opt_gene_rows = std::max(1, std::min(4, (int)value));
   else if (n == "unique_fixed") ctx->opt_unique_fixed = value != 0;
   else if (n == "pipeline_mb") ctx->opt_pipeline_mb = value;
-  else if (n == "piece_taper") ctx->opt_piece_taper = (value == 1 || value == 2) ? (int)value : 0;
   else if (n == "pieces") ctx->opt_pieces = std::max(1, std::min((int)value, scde_ctx::kMaxPieces));
-  else if (n == "lane_prio") ctx->opt_lane_prio = std::min(2, std::max(0, (int)value));
-  else if (n == "defer_boot") ctx->opt_defer_boot = value != 0;
-  else if (n == "lane_thread") ctx->opt_lane_thread = value != 0;
-  else if (n == "interleave") ctx->opt_interleave = value != 0;
-  else if (n == "rest_thread") ctx->opt_rest_thread = value != 0;
-  else if (n == "boot_gate") ctx->opt_boot_gate = value != 0;
-  else if (n == "fuse_groups") ctx->opt_fuse_groups = value != 0;
-  else if (n == "boot2_rows") ctx->opt_boot2_rows = value != 0;
-  else if (n == "task_cols") ctx->opt_task_cols = std::max(0, (int)value);
-  else if (n == "tables_pair") ctx->opt_tables_pair = value != 0;
   else if (n == "tables_nt") ctx->opt_tables_nt = std::min(2, std::max(0, (int)value));
-  else if (n == "boot_chunks") ctx->opt_boot_chunks = std::max(1, std::min((int)value, 64));
   else if (n == "lanes") {
     ctx->opt_lanes = value >= 2 ? 2 : 1;
     if (ctx->opt_lanes == 1 && ctx->peer) {  // one lane: the peer's workspace goes back to the device
@@ -2210,6 +1997,13 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
     }
   }
   else return fail(SCDE_EARG, "unknown option '%s'", name);
+  return SCDE_OK;
+}
+
+int scde_ctx_inject_fault(scde_ctx* ctx, const char* where, int count) {
+  if (!ctx || !where) return fail(SCDE_EARG, "null argument");
+  if (std::string(where) == "u16_slot") ctx->fault_u16 = std::max(0, count);
+  else return fail(SCDE_EARG, "unknown fault point '%s'", where);
   return SCDE_OK;
 }
 
@@ -2229,11 +2023,14 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "piece_wait_ms") *value = ctx->st_piece_wait_ms + (ctx->peer ? ctx->peer->st_piece_wait_ms : 0);
   else if (n == "piece_host_ms") *value = ctx->st_piece_host_ms + (ctx->peer ? ctx->peer->st_piece_host_ms : 0);
   else if (n == "buf_reallocs") *value = (double)g_buf_reallocs.load();
-  else if (n == "upload_wake_ms") *value = ctx->upl.wake_ms;
-  else if (n == "u16_wait_ms") *value = ctx->u16.st_wait_ms;
-  else if (n == "u16_issue_ms") *value = ctx->u16.st_issue_ms;
-  else if (n == "u16_free_ms") *value = ctx->u16.st_free_ms;
-  else if (n == "upload_first_ms") *value = ctx->upl.first_ms;
+  // (the upload worker and the 16-bit issuer update these under their mutexes)
+  else if (n == "upload_wake_ms" || n == "upload_first_ms") {
+    std::lock_guard<std::mutex> lk(ctx->upl.m);
+    *value = n == "upload_wake_ms" ? ctx->upl.wake_ms : ctx->upl.first_ms;
+  } else if (n == "u16_wait_ms" || n == "u16_issue_ms" || n == "u16_free_ms") {
+    std::lock_guard<std::mutex> lk(ctx->u16.m);
+    *value = n == "u16_wait_ms" ? ctx->u16.st_wait_ms : n == "u16_issue_ms" ? ctx->u16.st_issue_ms : ctx->u16.st_free_ms;
+  }
   else if (n == "host_setup_ms") *value = ctx->st_host_ms[0];
   else if (n == "host_unique_ms") *value = ctx->st_host_ms[1];
   else if (n == "host_post_ms") *value = ctx->st_host_ms[2];
@@ -2618,88 +2415,6 @@ struct HostUpload {
   int ngenes, cut, C;
   bool u16 = false;  // ranges of >= 8 MB as 16-bit counts (upload_cols_u16)
 };
-// the staging pool: share t of [0, n) copied by thread t (share 0 by the caller)
-static void stg_share(const char* src, char* dst, size_t n, int t, int T) {
-  const size_t a = (n * (size_t)t / (size_t)T) & ~size_t(63), b = (t + 1 == T) ? n : ((n * (size_t)(t + 1) / T) & ~size_t(63));
-  if (b > a) std::memcpy(dst + a, src + a, b - a);
-}
-static void stg_copy(scde_ctx* ctx, char* dst, const char* src, size_t n) {
-  auto& g = ctx->stg;
-  const int T = std::max(1, ctx->opt_upload_threads);
-  if (T == 1 || n < (size_t(256) << 10)) {
-    std::memcpy(dst, src, n);
-    return;
-  }
-  if ((int)g.th.size() != T - 1) {  // (re)build the pool: T - 1 threads plus the caller
-    if (!g.th.empty()) {
-      {
-        std::lock_guard<std::mutex> lk(g.m);
-        g.stop = true;
-      }
-      g.cv.notify_all();
-      for (auto& t : g.th) t.join();
-      g.th.clear();
-      g.stop = false;
-    }
-    g.T = T;
-    const long long gen0 = g.gen;  // no job is pending while the pool is (re)built
-    for (int t = 1; t < T; ++t)
-      g.th.emplace_back([&g, t, gen0] {
-        long long seen = gen0;
-        std::unique_lock<std::mutex> lk(g.m);
-        for (;;) {
-          g.cv.wait(lk, [&] { return g.stop || g.gen != seen; });
-          if (g.stop) return;
-          seen = g.gen;
-          const char* s = g.src;
-          char* d = g.dst;
-          const size_t nn = g.n;
-          const int TT = g.T;
-          lk.unlock();
-          stg_share(s, d, nn, t, TT);
-          lk.lock();
-          if (--g.pending == 0) g.cvd.notify_all();
-        }
-      });
-  }
-  {
-    std::lock_guard<std::mutex> lk(g.m);
-    g.src = src;
-    g.dst = dst;
-    g.n = n;
-    g.pending = T - 1;
-    ++g.gen;
-  }
-  g.cv.notify_all();
-  stg_share(src, dst, n, 0, T);
-  std::unique_lock<std::mutex> lk(g.m);
-  g.cvd.wait(lk, [&] { return g.pending == 0; });
-}
-
-// columns [lo, hi) of contiguous host counts through the pinned ring, on the copy stream
-static int upload_cols_staged(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
-  auto& g = ctx->stg;
-  if (!g.pin) {
-    HCHK(hipHostMalloc(reinterpret_cast<void**>(&g.pin), scde_ctx::Stager::kSlots * scde_ctx::Stager::kSlot,
-                       hipHostMallocDefault));
-    for (auto& e : g.ev) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
-  const size_t row = sizeof(int) * (size_t)h.ngenes, bytes = row * (size_t)(hi - lo);
-  const char* src = reinterpret_cast<const char*>(h.counts + (size_t)h.ld * lo);
-  char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
-  for (size_t off = 0; off < bytes; off += scde_ctx::Stager::kSlot) {
-    const int k = (int)(g.next++ % scde_ctx::Stager::kSlots);
-    if (g.used[k]) HCHK(hipEventSynchronize(g.ev[k]));
-    const size_t n = std::min(scde_ctx::Stager::kSlot, bytes - off);
-    char* slot = g.pin + (size_t)k * scde_ctx::Stager::kSlot;
-    stg_copy(ctx, slot, src + off, n);
-    HCHK(hipMemcpyAsync(dst + off, slot, n, hipMemcpyHostToDevice, ctx->copy_stream));
-    HCHK(hipEventRecord(g.ev[k], ctx->copy_stream));
-    g.used[k] = true;
-  }
-  return SCDE_OK;
-}
-
 // narrow n int32 counts to uint16, appending the counts outside [0, 65535] (negative ones
 // included) to `exc` as (i0 + index, count): blocks of 256 narrowed by a vectorised loop, a
 // block whose high halves are not all zero scanned again
@@ -2812,6 +2527,8 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   ++r.job;
   r.cv.notify_all();
   int rc = SCDE_OK;
+  // (the statistics are summed under r.m, where scde_ctx_get_stat reads them)
+  double wait_ms = 0, issue_ms = 0, free_ms = 0;
   for (int sl = 0; sl < nslots; ++sl) {
     const long long q = q0 + sl;
     const int k = (int)(q % R::kRing);
@@ -2820,12 +2537,16 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
     r.fin[k] = 0;
     lk.unlock();
     const auto ti = std::chrono::steady_clock::now();
-    r.st_wait_ms += std::chrono::duration<double, std::milli>(ti - tw).count();
+    wait_ms += std::chrono::duration<double, std::milli>(ti - tw).count();
     const size_t off = (size_t)sl * R::kSlotCounts;
     const size_t m = std::min(R::kSlotCounts, n - off);
     unsigned short* dslot = r.dev + (size_t)k * R::kSlotCounts;
     hipError_t e = hipMemcpyAsync(dslot, r.pin + (size_t)k * R::kSlotCounts, sizeof(unsigned short) * m,
                                   hipMemcpyHostToDevice, ctx->copy_stream);
+    if (e == hipSuccess && ctx->fault_u16 > 0 && sl == std::min(1, nslots - 1)) {  // test hook (scde_ctx_inject_fault)
+      --ctx->fault_u16;
+      e = hipErrorUnknown;
+    }
     if (e == hipSuccess) e = hipEventRecord(r.ev[k], ctx->copy_stream);
     if (e == hipSuccess) e = launch_widen16(dslot, dst + off, m, ctx->copy_stream);
     // the slot's counts outside 16 bits (the threads' lists of ring slot k are complete and
@@ -2842,13 +2563,13 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
     }
     r.issued = q + 1;
     const auto tf = std::chrono::steady_clock::now();
-    r.st_issue_ms += std::chrono::duration<double, std::milli>(tf - ti).count();
+    issue_ms += std::chrono::duration<double, std::milli>(tf - ti).count();
     // free the ring slot the threads need next (slot q + 1 reuses slot q + 1 - kRing's): wait for
     // that DMA, then let them write (only this thread writes free_upto)
     const long long f = q + 1 - R::kRing;
     const bool advance = e == hipSuccess && r.free_upto <= q + 1;
     if (advance && f >= 0) e = hipEventSynchronize(r.ev[f % R::kRing]);
-    r.st_free_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
+    free_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf).count();
     lk.lock();
     if (e != hipSuccess) {
       rc = fail(SCDE_EHIP, "%s", hipGetErrorString(e));
@@ -2866,6 +2587,19 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   r.cvd.wait(lk, [&] { return r.busy == 0; });
   for (auto& f : r.fin) f = 0;  // (an aborted job leaves partial counts)
   r.seq = r.issued;             // sequence numbers of slots never issued are reused
+  r.st_wait_ms += wait_ms;
+  r.st_issue_ms += issue_ms;
+  r.st_free_ms += free_ms;
+  if (rc != SCDE_OK) {
+    // an error after slots were issued: free_upto may lag behind seq, and the next job's threads
+    // would wait for a slot nobody frees.  Drain the copy stream -- every issued slot's DMA has then
+    // finished (or failed) -- and open the whole ring to the next job.
+    lk.unlock();
+    (void)hipStreamSynchronize(ctx->copy_stream);
+    (void)hipGetLastError();
+    lk.lock();
+    r.free_upto = r.seq + R::kRing;
+  }
   lk.unlock();
   return rc;
 }
@@ -2875,7 +2609,6 @@ static int upload_cols(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
   const size_t row = sizeof(int) * (size_t)h.ngenes;
   if (hi > lo && h.u16 && h.ld == h.ngenes && row * (size_t)(hi - lo) >= (size_t(8) << 20))
     return upload_cols_u16(ctx, h, lo, hi);
-  if (hi > lo && ctx->opt_upload_staged && h.ld == h.ngenes) return upload_cols_staged(ctx, h, lo, hi);
   if (hi > lo) {
     char* dst = static_cast<char*>(ctx->counts_in.p) + row * lo;
     const int* src = h.counts + (size_t)h.ld * lo;
@@ -2980,13 +2713,7 @@ struct UploadWorker {
 // bound j (0..K) of K pieces over [0, total): equal pieces, or with taper decreasing ones
 // (weights K, K - 1, .., 1: the last piece, whose unique sets and tables start only after the
 // last byte has landed, is the smallest)
-static long long piece_bound(long long total, int j, int K, int taper) {
-  if (!taper) return total * j / K;
-  const long long tw = (long long)K * (K + 1) / 2;
-  const long long w = taper == 1 ? (long long)j * K - (long long)j * (j - 1) / 2  // K, K - 1, .., 1
-                                 : (long long)j * (j + 1) / 2;                      // 1, 2, .., K
-  return total * w / tw;
-}
+static long long piece_bound(long long total, int j, int K) { return total * j / K; }
 
 static int ensure_piece_streams(scde_ctx* ctx) {
   if (!ctx->uq_stream) HCHK(hipStreamCreateWithFlags(&ctx->uq_stream, hipStreamNonBlocking));
@@ -3077,7 +2804,7 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
   UploadWorker uw;
   if (up) {
     const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
-    for (int j = 0; j <= K; ++j) piece_c.push_back((int)piece_bound(ncells_sel, j, K, ctx->opt_piece_taper));
+    for (int j = 0; j <= K; ++j) piece_c.push_back((int)piece_bound(ncells_sel, j, K));
     piece_col.push_back(0);  // piece j uploads columns [piece_col[j], piece_col[j + 1])
     for (int j = 0; j < K; ++j)
       piece_col.push_back(piece_c[j + 1] > piece_c[j] ? cellidx[piece_c[j + 1] - 1] + 1 : piece_col.back());
@@ -3131,42 +2858,14 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
 // does not queue behind the first lane's host-side set-up and bootstrap launch and the two
 // bootstraps can overlap; else one after the other.  (Each continuation touches only its own
 // context's buffers and streams; a shared unique set is read-only there.)
-// With the two specs given (s0, s1: the rests' specs), both bootstraps wait for both set-up chains
-// (BootGate; option boot_gate).
-static int run_rests(scde_ctx* ctx, const std::function<int()>& rest0, const std::function<int()>& rest1,
-                     PostSpec* s0 = nullptr, PostSpec* s1 = nullptr) {
-  if (!ctx->opt_rest_thread) {
-    RCHK(rest0());
-    return rest1();
-  }
-  BootGate gate;
-  const bool gated = s0 && s1 && ctx->opt_boot_gate;
-  if (gated) {
-    for (auto& e : ctx->gate_ev)
-      if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    gate.ev[0] = ctx->gate_ev[0];
-    gate.ev[1] = ctx->gate_ev[1];
-    s0->gate = &gate;
-    s0->gate_slot = 0;
-    s1->gate = &gate;
-    s1->gate_slot = 1;
-  }
-  struct Ungate {  // the specs outlive this call: no dangling gate
-    PostSpec *a, *b;
-    ~Ungate() {
-      if (a) a->gate = nullptr;
-      if (b) b->gate = nullptr;
-    }
-  } ug{gated ? s0 : nullptr, gated ? s1 : nullptr};
+static int run_rests(scde_ctx* ctx, const std::function<int()>& rest0, const std::function<int()>& rest1) {
   int rc1 = SCDE_OK;
   std::string err1;
   std::thread t1([&] {
     rc1 = hipSetDevice(ctx->device) == hipSuccess ? rest1() : fail(SCDE_EHIP, "hipSetDevice failed");
     if (rc1 != SCDE_OK) err1 = g_err;  // g_err is thread-local
-    if (gated) gate.leave(1);
   });
   const int rc0 = rest0();
-  if (gated) gate.leave(0);
   const std::string err0 = g_err;
   t1.join();
   if (rc0 != SCDE_OK) return fail(rc0, "%s", err0.c_str());
@@ -3174,35 +2873,7 @@ static int run_rests(scde_ctx* ctx, const std::function<int()>& rest0, const std
   return SCDE_OK;
 }
 
-// The peer lane's streams at the device's highest priority (hi) or at the default one.  The peer
-// keeps one (main, aux) set per priority; switching parks the current set and brings in the other,
-// whose streams first wait for everything queued on the parked set (between calls, so `stream` is
-// the home stream).  The aux stream of a set is created on first use with `stream_prio`.
-static int peer_set_prio(scde_ctx* p, bool hi) {
-  if (p->prio_hi == hi) return SCDE_OK;
-  int lo = 0, top = 0;
-  HCHK(hipDeviceGetStreamPriorityRange(&lo, &top));
-  const int want = hi ? top : 0;
-  if (!p->alt_stream) HCHK(hipStreamCreateWithPriority(&p->alt_stream, hipStreamNonBlocking, want));
-  for (auto& e : p->prio_ev)
-    if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  HCHK(hipEventRecord(p->prio_ev[0], p->stream));
-  HCHK(hipEventRecord(p->prio_ev[1], p->aux_stream ? p->aux_stream : p->stream));
-  for (hipStream_t s : {p->alt_stream, p->alt_aux}) {
-    if (!s) continue;
-    HCHK(hipStreamWaitEvent(s, p->prio_ev[0], 0));
-    HCHK(hipStreamWaitEvent(s, p->prio_ev[1], 0));
-  }
-  std::swap(p->stream, p->alt_stream);
-  std::swap(p->aux_stream, p->alt_aux);
-  p->home_stream = p->stream;
-  p->stream_prio = want;
-  p->prio_hi = hi;
-  return SCDE_OK;
-}
-
-// ngenes: the call's genes (the lane_prio rule)
-static int lane_peer(scde_ctx* cx, scde_ctx** out, int ngenes) {
+static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   if (!cx->peer) {
     scde_ctx* p = nullptr;
     RCHK(scde_ctx_create(cx->device, &p));
@@ -3211,37 +2882,20 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out, int ngenes) {
       if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   scde_ctx* p = cx->peer;
-  // the peer lane starts later than the first group (its counts and unique sets come second) and
-  // its small set-up kernels would queue behind the first group's bootstrap waves: on small calls
-  // its streams get the device's highest priority
-  constexpr int kPrioGenes = 8192;
-  RCHK(peer_set_prio(p, cx->opt_lane_prio == 1 || (cx->opt_lane_prio == 2 && ngenes <= kPrioGenes)));
   p->opt_boot_skip = cx->opt_boot_skip;
   p->opt_skip_slack = cx->opt_skip_slack;
   p->opt_boot_nb = cx->opt_boot_nb;
   p->opt_skip_stats = cx->opt_skip_stats;
-  p->opt_ratio_window = cx->opt_ratio_window;
-  p->opt_ratio_block = cx->opt_ratio_block;
   p->opt_wpca_ms = cx->opt_wpca_ms;
   p->opt_boot_tiles = cx->opt_boot_tiles;
   p->opt_boot_tiles_cells = cx->opt_boot_tiles_cells;
   p->opt_tile_groups = cx->opt_tile_groups;
   p->opt_tile_max_mult = cx->opt_tile_max_mult;
   p->opt_tile_order = cx->opt_tile_order;
-  p->opt_ell_chunks = cx->opt_ell_chunks;
-  p->opt_gene_direct = cx->opt_gene_direct;
   p->opt_jp_chunks = cx->opt_jp_chunks;
   p->opt_unique_fixed = cx->opt_unique_fixed;
-  p->opt_pair_cells = cx->opt_pair_cells;
-  p->opt_gene_blocks = cx->opt_gene_blocks;
   p->opt_gene_rows = cx->opt_gene_rows;
   p->opt_gene_list_cap = cx->opt_gene_list_cap;
-  p->opt_gene_waves = cx->opt_gene_waves;
-  p->opt_gene3_cells = cx->opt_gene3_cells;
-  p->opt_boot_chunks = cx->opt_boot_chunks;
-  p->opt_boot2_rows = cx->opt_boot2_rows;
-  p->opt_task_cols = cx->opt_task_cols;
-  p->opt_tables_pair = cx->opt_tables_pair;
   p->opt_tables_nt = cx->opt_tables_nt;
   p->profile = cx->profile;
   *out = p;
@@ -3335,105 +2989,10 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
     s.jp_k = 1;
   }
   hlap(0);
-  // Fused groups (option fuse_groups): both group posteriors as ONE posterior over the concatenated
-  // cells and doubled genes (PostSpec::ngroups), one launch per stage on this context's stream --
-  // no peer lane, no second chain of small set-up kernels queued behind a running bootstrap, one
-  // bootstrap grid for both groups.  Bit-identical to the two separate posteriors (run_posterior).
   const double* jp_dev[2] = {ctx->jpA.as<double>(), ctx->jpB.as<double>()};
-  bool fused_done = false;
   {
-    const int C0 = (int)idx[0].size(), C1 = (int)idx[1].size();
-    auto same = [&](int th) { return (C0 >= th) == (C1 >= th); };
-    const bool fuse = ctx->opt_fuse_groups && p->nboot > 0 && same(ctx->opt_boot_tiles_cells) &&
-                      same(ctx->opt_pair_cells) && same(ctx->opt_gene3_cells);
-    if (fuse) {
-      // group a's cells first: the group whose cells end first in the matrix (the host upload's order)
-      const int a = (idx[0].back() <= idx[1].back()) ? 0 : 1, b = 1 - a;
-      const int Ca = (int)idx[a].size(), Cb = (int)idx[b].size(), Cf = Ca + Cb;
-      std::vector<int> cells(idx[a]);
-      cells.insert(cells.end(), idx[b].begin(), idx[b].end());
-      std::vector<double> mmf((size_t)Cf * 12);
-      for (int j = 0; j < 12; ++j) {
-        std::copy(mm[a].begin() + (size_t)Ca * j, mm[a].begin() + (size_t)Ca * (j + 1), mmf.begin() + (size_t)Cf * j);
-        std::copy(mm[b].begin() + (size_t)Cb * j, mm[b].begin() + (size_t)Cb * (j + 1),
-                  mmf.begin() + (size_t)Cf * j + Ca);
-      }
-      HCHK(ctx->jpA.ensure(sizeof(double) * std::max<size_t>(1, 2 * NG)));
-      PostSpec sf = specs[a];
-      sf.ncells = Cf;
-      sf.models = mmf.data();
-      sf.cellidx_host = cells.data();
-      sf.ngroups = 2;
-      sf.gsplit = Ca;
-      sf.nsets_g = (int)seeds.size();
-      sf.seeds = seeds;
-      sf.seeds.insert(sf.seeds.end(), seeds.begin(), seeds.end());
-      sf.wset.assign(2 * (size_t)ngenes, 0);
-      for (int g = 0; g < ngenes; ++g) {
-        const int w = wset.empty() ? 0 : wset[g];
-        sf.wset[g] = w;
-        sf.wset[(size_t)ngenes + g] = w + sf.nsets_g;
-      }
-      sf.jp = ctx->jpA.as<double>();
-      sf.jp_g = G;
-      sf.jp_k = 1;
-      UniqueSet& uf = ctx->us[0];
-      uf.ready = false;
-      std::vector<int> piece_c, cols;
-      UploadWorker uw;
-      if (up) {
-        // the count columns in pieces over the fused cell list when it runs in matrix order (the
-        // groups' cells separable: each piece a column range; its unique sets and tables start as it
-        // lands), else in one range before the unique sets
-        const bool sep = idx[a].back() < idx[b].front();
-        const int K = sep ? std::max(1, std::min(2 * ctx->opt_pieces, scde_ctx::kMaxPieces)) : 1;
-        for (int j = 0; j <= K; ++j) piece_c.push_back((int)((long long)Cf * j / K));
-        cols.push_back(0);
-        for (int j = 1; j < K; ++j) cols.push_back(std::max(cols.back(), cells[piece_c[j]]));
-        cols.push_back(up->C);
-        RCHK(ensure_piece_streams(ctx));
-        RCHK(uw.start(ctx, *up, cols, std::vector<hipEvent_t>(ctx->piece_up_ev, ctx->piece_up_ev + K)));
-        if (sep) {
-          sf.npieces = K;
-          sf.piece_c = piece_c.data();
-          sf.piece_stream = ctx->uq_stream;
-          sf.piece_ev = ctx->piece_ev;
-          sf.piece_ready = [&](int j) {
-            RCHK(uw.wait(j + 1));
-            HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
-            return SCDE_OK;
-          };
-        } else {
-          RCHK(uw.wait(1));
-          HCHK(hipStreamWaitEvent(ctx->stream, ctx->piece_up_ev[0], 0));
-        }
-      }
-      hlap(1);
-      if (!up || sf.npieces == 0) {
-        const PostSpec* sp[1] = {&sf};
-        UniqueSet* usp[1] = {&uf};
-        RCHK(build_unique_sets(ctx, sp, usp, 1));
-      }
-      const int rc = run_posterior(ctx, sf, uf);
-      hlap(2);
-      if (rc == SCDE_OK) {
-        jp_dev[a] = ctx->jpA.as<double>();
-        jp_dev[b] = ctx->jpA.as<double>() + NG;
-        fused_done = true;
-      } else if (rc == kRetryUnfused) {
-        // the fused column count leaves the fast path: every count is in HBM by now (the pieces were
-        // all awaited); the two groups run separately on the resident counts
-        HCHK(hipStreamSynchronize(ctx->copy_stream ? ctx->copy_stream : ctx->stream));
-        HCHK(hipStreamSynchronize(ctx->stream));
-        up = nullptr;
-      } else {
-        return rc;
-      }
-    }
-  }
-  if (!fused_done) {
     scde_ctx* lane = ctx;  // the context that runs the second group's posterior
-    if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane, ngenes));
+    if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
     if (up) {
       // group by group, each after its columns have arrived (the first range ends with the
       // last cell of the group whose cells end first)
@@ -3444,94 +3003,19 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       // the first group's range in pieces, then the second group's range, uploaded back to back by
       // a worker thread: each piece's unique sets and tables start as it lands
       const int K = std::max(1, std::min(ctx->opt_pieces, scde_ctx::kMaxPieces));
-      const bool threaded = lane != ctx && ctx->opt_lane_thread && !ctx->opt_defer_boot;
-      // interleaved (second lane on its own host thread, every cell of the second group after the
-      // first group's range): both groups' ranges in K pieces, uploaded alternately, so the second
-      // group's unique sets and tables run beside the first group's instead of after its range
-      const int other = 1 - first;
-      const bool inter = threaded && ctx->opt_interleave && !idx[other].empty() && idx[other].front() >= up->cut;
-      std::vector<int> piece_c, cols, piece_c2;
+      std::vector<int> piece_c, cols;
       const std::vector<int>& ix = idx[first];
       for (int j = 0; j <= K; ++j) {
-        // (interleaved: equal pieces, paired with the second group's)
-        const int a = (int)piece_bound(up->cut, j, K, inter ? 0 : ctx->opt_piece_taper);
+        const int a = (int)piece_bound(up->cut, j, K);
         cols.push_back(a);
         piece_c.push_back((int)(std::lower_bound(ix.begin(), ix.end(), a) - ix.begin()));
       }
       RCHK(ensure_piece_streams(ctx));
       UploadWorker uw;
-      if (inter) {
-        RCHK(ensure_piece_streams(lane));
-        const std::vector<int>& iy = idx[other];
-        std::vector<int> cols2;
-        for (int j = 0; j <= K; ++j) {
-          const int a = up->cut + (int)((long long)(up->C - up->cut) * j / K);
-          cols2.push_back(a);
-          piece_c2.push_back((int)(std::lower_bound(iy.begin(), iy.end(), a) - iy.begin()));
-        }
-        // range 2j: the first group's piece j; range 2j + 1: the second group's piece j
-        std::vector<std::pair<int, int>> ranges;
-        std::vector<hipEvent_t> evs;
-        for (int j = 0; j < K; ++j) {
-          ranges.emplace_back(cols[j], cols[j + 1]);
-          evs.push_back(ctx->piece_up_ev[j]);
-          ranges.emplace_back(cols2[j], cols2[j + 1]);
-          evs.push_back(lane->piece_up_ev[j]);
-        }
-        RCHK(uw.start(ctx, *up, std::move(ranges), std::move(evs)));
-      } else {
-        cols.push_back(up->C);
-        std::vector<hipEvent_t> evs(ctx->piece_up_ev, ctx->piece_up_ev + K);
-        evs.push_back(ctx->up_ev[1]);
-        RCHK(uw.start(ctx, *up, cols, evs));
-      }
-      // upload range of the first group's piece j
-      auto range_of = [&](int j) { return inter ? 2 * j : j; };
-      // two lanes with lane_thread: the second group's unique sets, tables and bootstrap are driven
-      // by a host thread of their own from the moment its range lands, beside this thread's pieces
-      // of the first group (each lane's host syncs then wait only for its own kernels)
-      struct LaneThread {
-        std::thread th;
-        int rc = SCDE_OK;
-        std::string err;
-        ~LaneThread() {
-          if (th.joinable()) th.join();  // an early error return of this thread still waits for it
-        }
-      } t2;
-      if (threaded) {
-        const int gi = 1 - first;
-        ctx->us[gi].ready = false;
-        t2.th = std::thread([&, gi] {
-          t2.rc = [&]() -> int {
-            HCHK(hipSetDevice(ctx->device));
-            if (inter) {  // the second group's pieces as they land (ranges 1, 3, 5, ...)
-              PostSpec& s2 = specs[gi];
-              s2.npieces = K;
-              s2.piece_c = piece_c2.data();
-              s2.piece_stream = lane->uq_stream;
-              s2.piece_ev = lane->piece_ev;
-              s2.piece_ready = [&](int j) {
-                RCHK(uw.wait(2 * j + 2));
-                HCHK(hipStreamWaitEvent(lane->uq_stream, lane->piece_up_ev[j], 0));
-                return SCDE_OK;
-              };
-              return run_posterior(lane, s2, ctx->us[gi]);
-            }
-            RCHK(uw.wait(K + 1));
-            HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
-            const PostSpec* sp[1] = {&specs[gi]};
-            UniqueSet* usp[1] = {&ctx->us[gi]};
-            RCHK(build_unique_sets(lane, sp, usp, 1));
-            return run_posterior(lane, specs[gi], ctx->us[gi]);
-          }();
-          if (t2.rc != SCDE_OK) t2.err = g_err;  // g_err is thread-local
-        });
-      }
-      // two lanes: the first group's bootstrap is queued only after the second group's tables, so
-      // those (and their small set-up kernels) do not wait behind its waves; the first group's
-      // tables end about when the second group's range lands anyway
-      const bool defer = lane != ctx && ctx->opt_defer_boot;
-      std::function<int()> rest0, rest1;
+      cols.push_back(up->C);
+      std::vector<hipEvent_t> evs(ctx->piece_up_ev, ctx->piece_up_ev + K);
+      evs.push_back(ctx->up_ev[1]);
+      RCHK(uw.start(ctx, *up, cols, evs));
       {
         const int gi = first;
         ctx->us[gi].ready = false;
@@ -3541,21 +3025,15 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         sf.piece_stream = ctx->uq_stream;
         sf.piece_ev = ctx->piece_ev;
         sf.piece_ready = [&](int j) {
-          RCHK(uw.wait(range_of(j) + 1));
+          RCHK(uw.wait(j + 1));
           HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
           return SCDE_OK;
         };
         hlap(1);
-        RCHK(run_posterior(ctx, sf, ctx->us[gi], defer ? &rest0 : nullptr));
+        RCHK(run_posterior(ctx, sf, ctx->us[gi]));
         hlap(2);
       }
-      if (t2.th.joinable()) {  // the second lane ran on its own host thread
-        t2.th.join();
-        if (t2.rc != SCDE_OK) return fail(t2.rc, "%s", t2.err.c_str());
-        HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
-        HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
-        hlap(2);
-      } else {
+      {
         // the second group, once its range is in HBM: its unique sets on the peer lane (or on
         // the unique stream with one lane), so their host sync waits for its small kernels only
         const int gi = 1 - first;
@@ -3567,8 +3045,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
           HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
           RCHK(build_unique_sets(lane, sp, usp, 1));
           hlap(1);
-          RCHK(run_posterior(lane, specs[gi], ctx->us[gi], defer ? &rest1 : nullptr));
-          if (defer) RCHK(run_rests(ctx, rest0, rest1));
+          RCHK(run_posterior(lane, specs[gi], ctx->us[gi]));
           HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
           HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
         } else {
@@ -3603,7 +3080,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         std::function<int()> rest0, rest1;
         RCHK(run_posterior(ctx, specs[0], ctx->us[0], &rest0));
         RCHK(run_posterior(lane, specs[1], ctx->us[1], &rest1));
-        RCHK(run_rests(ctx, rest0, rest1, &specs[0], &specs[1]));
+        RCHK(run_rests(ctx, rest0, rest1));
       } else {
         RCHK(run_posterior(ctx, specs[0], ctx->us[0]));
         RCHK(run_posterior(ctx, specs[1], ctx->us[1]));
@@ -3773,7 +3250,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     RCHK(build_unique_sets(ctx, sp, up, 3));
   }
   scde_ctx* lane = ctx;  // the second batch posterior and the second group's run on the peer lane
-  if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane, N));
+  if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
   if (lane != ctx) {
     HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
     HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));

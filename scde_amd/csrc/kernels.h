@@ -8,21 +8,7 @@
 #define SCDE_BOOT_ASMLD 1  // k_boot2 column look-ahead issued from asm with explicit vmcnt waits
 #endif
 #ifndef SCDE_NB_CLOSED
-#define SCDE_NB_CLOSED 1  // k_tables_reg: the NB log-pmf in closed form (0: nmath's saddle-point form)
-#endif
-#ifndef SCDE_TABREG_WPE
-// k_tables_reg occupancy target (waves per SIMD; 4-wave blocks): the closed form's seven staged
-// rows (36 KB of LDS per block) and 118 VGPRs allow four blocks per CU
-#if SCDE_NB_CLOSED && (!defined(SCDE_TABREG_PAIR) || SCDE_TABREG_PAIR)
-#define SCDE_TABREG_WPE 3  // two columns per wave (k_tables_reg's paired columns) need the registers of 3 waves/SIMD
-#elif SCDE_NB_CLOSED
-#define SCDE_TABREG_WPE 4
-#else
-#define SCDE_TABREG_WPE 3
-#endif
-#endif
-#ifndef SCDE_TABREG_G401
-#define SCDE_TABREG_G401 1  // k_tables_reg specialised for the default 401-point grid
+#define SCDE_NB_CLOSED 1  // the tables' NB log-pmf in closed form (0: nmath's saddle-point form)
 #endif
 #ifndef SCDE_TAB_WPE
 #define SCDE_TAB_WPE 4  // k_tables_cell occupancy target (waves per SIMD)
@@ -50,8 +36,7 @@ namespace scde {
 // log X - log n, log(n - X) - log n, dpois_log(x, failure rate), log po, log(1 - po)] with
 // po = size / (size + x) (the count's own grid point), padded to 10 doubles
 constexpr int kColc = 11;
-// columns per task of the cell-staged tables kernels (k_tables_reg stages a task's column
-// constants in LDS: tasks must not exceed this)
+// columns per task of the cell-staged tables kernels (k_tables_lpc: one lane per column)
 #ifndef SCDE_TAB_TASK_COLS
 #define SCDE_TAB_TASK_COLS 64
 #endif
@@ -69,14 +54,7 @@ struct TablesArgs {
   const double* theta;       // [ncells][GS]
   const double* cellscal;    // [ncells][2] = {max log cfp, exp(fail.r)}
   double minlogprob;         // -DBL_MAX / ncells / 1.1
-  // a DE call's two groups fused into one set of tables (engine.hip run_posterior, ngroups 2):
-  // cells from mlp_split on (the second group's, relative to this launch's first cell) clamp at
-  // minlogprob2 = -DBL_MAX / (its group's cells) / 1.1; one group: mlp_split >= ncells
-  double minlogprob2;
-  int mlp_split;
-  // k_tables_reg takes a wave's columns two at a time (0: one at a time; the same bits either way)
-  int pair_cols;
-  // k_tables_reg writes its rows (T, D) as non-temporal stores (the same bits)
+  // k_tables_lpc writes its rows (T, D) as non-temporal stores (the same bits)
   int nt_rows;
   double* T;                 // [ncols][GS] log-posterior columns
   int* maxi;                 // [ncols] argmax (nullable)
@@ -117,7 +95,7 @@ struct TablesArgs {
   // nullable: the launch does nothing unless *gate != 0 (the exact fallback's T tables are
   // built only when some gene needs them)
   const int* gate;
-  // k_tables only: take just the columns k_tables_reg leaves (colc n < 0, flagged by
+  // k_tables only: take just the columns k_tables_lpc leaves (colc n < 0, flagged by
   // k_col_consts in the int after colc's last column); the launch exits unless that flag is set
   int slow_only;
 };
@@ -177,9 +155,6 @@ struct Boot2Args {
   int* redo;     // [ngenes][P] slabs whose skipped stretches failed the post-check (tile path:
                  // fallback flags, then the fallback list length and [ngenes * P] list)
   double slack;  // heuristic slack of the mask (NaN: the default 20 + 0.15 C)
-  // k_boot2t (the stretch path on tile rows, with the mask): the 16-point tiles each slab's partial
-  // row holds ([ngenes][P]; k_sum_partials reads the rest as zeros); null: k_boot2
-  unsigned* pmask = nullptr;
 };
 
 // k_boot_tiles (with Boot2Args; needs G <= 448): multiplicities as bytes and the tables'
@@ -197,18 +172,14 @@ struct TileBootArgs {
                              // [6 + i] slabs that computed i tiles (i <= 28), [35] slabs a pair pass left
   const int* order;          // nullable: genes in this order (launch_gene_order)
   unsigned* pmask;           // [ngenes][P] tiles each slab's partial row holds (k_sum_partials reads those)
-  int pairs = 0;             // a wave per two slabs of a gene, two bound tiles each (wide cells: most slabs
-                             // need two); slabs needing more take a four-tile pass over `wide`
-  int* wide = nullptr;       // [1 + ngenes * P] pair mode's list: [0] length, then g * P + p
+  int* wide = nullptr;       // [1 + ngenes * P] the list pass's slabs: [0] length, then g * P + p
   int gene = 0;              // k_boot_gene: a 4-wave block per (gene, group of SG slabs), 16 rows shared
-                             // by the group's slabs (not with pairs); failures take the list pass over `wide`
+                             // by the group's slabs; failures take the list pass over `wide`
   int SG = 0;                // slabs per group (<= 8, SG x nb <= 128)
   int kcap = 4;              // rows per slab at most (tests force the list pass with fewer)
   int list_cap = 0;          // slabs the list pass takes at most (0: 16384; tests force the overflow to k_boot2)
-  int gene_waves = 4;        // k_boot_gene waves per block: 4 (16 rows) or 3 (12 rows; wide calls)
   const unsigned char* W8g = nullptr;  // [nsets][ncells][groups][4 windows][32] the group's boots 32 w + j
                                        // as pair slots (boot 32 w + j, 32 w + 16 + j), 0 past its boots
-  int chunks = 1;  // k_boot_gene launches the gene blocks are split into (same blocks, same results)
   // gene blocks only: this launch takes genes [g_lo, g_hi) (g_hi < 0: all) -- a posterior's bootstrap in
   // gene chunks, each finished (list pass, fallback, slab sums) before the next, so its jp rows can
   // be read back while the next chunk runs; `order` then holds each chunk's genes sorted within it

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(256) void k_cell_prep(const double* __restrict__ mo
     const double lc = log(cf);
     lcfpr[(long long)c * GS + k] = log(1.0 - cf);
     lcfp[(long long)c * GS + k] = lc;
-    if (cfpo) cfpo[(long long)c * GS + k] = exp(lc);  // k_tables_reg's staged cfp (exp of the stored log)
+    if (cfpo) cfpo[(long long)c * GS + k] = exp(lc);  // the tables kernels' staged cfp (exp of the stored log)
     lmax = gt_max(lmax, lc);
     double th = corrt;
     if (localtheta) {
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
   const NbFast f = nb_fast(nc);
   double* o = colc + col * kColc;
   o[0] = f.ok ? f.n : -1.0;
-  if (!f.ok) *slow = 1;  // k_tables_reg leaves this column to the gated k_tables pass
+  if (!f.ok) *slow = 1;  // k_tables_lpc (and its fallback) leave this column to the gated k_tables pass
   o[1] = f.nx;
   o[2] = f.S;
   o[3] = f.hlf;
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void k_col_consts(const int* __restrict__ ucl,
   const double size = theta[(long long)lo * GS], po = size / (size + x);
   o[8] = log(po);
   o[9] = log(1 - po);
-  // the closed form's column constant (k_tables_reg, SCDE_NB_CLOSED): dnbinom(x; size, p) =
+  // the closed form's column constant (k_tables_lpc, tables_column_reg; SCDE_NB_CLOSED): dnbinom(x; size, p) =
   // log(size / (size + x)) + dbinom_raw(size, n, p, q) and, as bd0(y, n r) = y log(y / n) - y log r
   // + n r - y with p + q = 1, dbinom_raw = S - lf / 2 - size log(size / n) - nx log(nx / n)
   // + size log p + nx log q: everything but the last two terms is this constant
@@ -366,7 +366,7 @@ __device__ __forceinline__ void tables_column(const TablesArgs& a, long long col
         bv = r;
         bi = k;
       }
-      const double mlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
+      const double mlp = a.minlogprob;
       if (r < mlp) {
         r = mlp;
         clamp = true;
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void k_tables(TablesArgs a) {
   } else {
     col = (long long)blockIdx.x * 4 + wid;
     if (a.slow_only) {
-      // the columns k_tables_reg left (colc n < 0): 64 candidates per wave step, grid-stride
+      // the columns k_tables_lpc left (colc n < 0): 64 candidates per wave step, grid-stride
       for (long long b0 = col * 64; b0 < a.ncols; b0 += (long long)gridDim.x * 4 * 64) {
         const long long ci = b0 + lane;
         unsigned long long m = __ballot(ci < a.ncols && !(a.colc[ci * kColc] > 0.0));
@@ -597,43 +597,15 @@ __global__ __launch_bounds__(64 * kTabWaves) __attribute__((amdgpu_waves_per_eu(
   }
 }
 
-// Register-row form of the staged kernel for the constant-theta FP64 tables (the default
-// path): a column's 401 grid values stay in seven VGPR pairs through the three passes
-// (dnbinom + max, exp + sum, log + stores + tile maxima) instead of a per-wave LDS row, the
-// chunk loops are unrolled so the LDS reads of different chunks overlap, and the block's
-// LDS shrinks to the staged grid vectors (no row per wave: 3 -> 5 blocks per CU by LDS).
-// Lanes the fast dnbinom does not cover: q == 0 (grid point 0, mu = 0) in line; the rest
-// (p or q out of range, np or nq not a positive finite number) through the exact dnbinom
-// in a pass after the loop, only in waves that have such a lane.  Columns whose constants
-// rule out the fast form (colc n < 0) are left to the gated k_tables pass.
-#ifndef SCDE_KT_STAMP
-#define SCDE_KT_STAMP 0  // timing-only builds: per-phase cycle sums of k_tables_reg (scde_diag_kt_stamps)
-#endif
-#if SCDE_KT_STAMP
-__device__ unsigned long long g_kt_stamp[16];
-#define KT_STAMP(i)                                                                      \
-  do {                                                                                   \
-    const long long t_ = clock64();                                                      \
-    if (lane == 0) atomicAdd(&g_kt_stamp[i], (unsigned long long)(t_ - kt0_));           \
-    kt0_ = t_;                                                                           \
-  } while (0)
-#define KT_EVENT(i, c)                                                                   \
-  do {                                                                                   \
-    if (__builtin_amdgcn_ballot_w64(c) && lane == 0) atomicAdd(&g_kt_stamp[i], 1ull);    \
-  } while (0)
-#else
-#define KT_STAMP(i) \
-  do {              \
-  } while (0)
-#define KT_EVENT(i, c) \
-  do {                 \
-  } while (0)
-#endif
+// tables_column_reg: the general register-row column (one wave per column; k_tables_lpc's fallback
+// for the columns outside its form): a column's 401 grid values stay in seven VGPR pairs through
+// the three passes (dnbinom + max, exp + sum, log + stores + tile maxima), the chunk loops
+// unrolled so the LDS reads of different chunks overlap.  Lanes the fast dnbinom does not cover:
+// q == 0 (grid point 0, mu = 0) in line; the rest (p or q out of range, np or nq not a positive
+// finite number) through the exact dnbinom in a pass after the loop, only in waves that have such
+// a lane.  Columns whose constants rule out the fast form (colc n < 0) are left to the gated
+// k_tables pass.
 constexpr int kTabChunks = kTabStagedG / 64;
-#ifndef SCDE_TABREG_WAVES
-#define SCDE_TABREG_WAVES 4
-#endif
-constexpr int kTabRegWaves = SCDE_TABREG_WAVES;  // waves per k_tables_reg block (one task each)
 
 template <int CTRL>
 __device__ __forceinline__ float dpp32f(float x) {
@@ -672,10 +644,10 @@ enum { kRowMu = 0, kRowP = 1, kRowLP = 3, kRowLQ = 4, kRowLcfpr = 5, kRowCfp = 6
 //     in chunks that have such a lane;
 //   - T_k where max(t1, t2) < -665 (e_k below 2^-960, subnormal ranges): the quotient
 //     log(e_k / s) as the reference forms it.
-enum { kBoundNone = 0, kBoundTiles = 1, kBoundStretch = 2 };  // k_tables_reg's bound output
+enum { kBoundNone = 0, kBoundTiles = 1, kBoundStretch = 2 };  // the tables kernels' bound output
 // GC: the grid length as a compile-time constant (401, the default prior grid), so the
 // chunk masks fold away; 0 = a.G at run time
-// k_tables_reg's T/D rows as non-temporal stores when a.nt_rows (option tables_nt): 1.8 GB per
+// The tables kernels' T/D rows as non-temporal stores when a.nt_rows (option tables_nt): 1.8 GB per
 // config-3 step, read back by the bootstrap long after the caches have turned over (A/B: config 3
 // faster in 7 of 9 alternating pairs, at the box-noise level).  Smaller calls keep
 // plain stores (engine: rows that fit the last-level cache).  nt is kernel-uniform.
@@ -703,9 +675,6 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
                                                   const LogTab& lt, int lane, double theta, const double* cc,
                                                   double x, double maxcfp, int bc_u) {
   const int G = GC ? GC : a.G;
-#if SCDE_KT_STAMP
-  long long kt0_ = clock64();
-#endif
   NbFast nf;
   nf.n = cc[0];
   if (!(nf.n > 0.0)) return;  // the gated k_tables pass takes this column
@@ -725,7 +694,6 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
     return;
   }
   const double* sl = sm + lane;
-  KT_STAMP(0);
   double v[kTabChunks];
   unsigned badm = 0;
   double lmax = -INFINITY;
@@ -744,7 +712,6 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       double lpr = sl[kRowLP * kRS + 64 * j], lqr = sl[kRowLQ * kRS + 64 * j];
       const double muv = sl[kRowMu * kRS + 64 * j], mnext = sl[kRowMu * kRS + 64 * j + 1];
       const bool over = in && ((!last && x > muv && x < mnext) || (last && x > muv));
-      KT_EVENT(12, over);
       if (__builtin_amdgcn_ballot_w64(over)) {
         pr = over ? po : pr;
         qr = over ? 1 - po : qr;
@@ -755,10 +722,6 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       // nq finite -- the fast form's full validity condition
       const double np = nf.n * pr, nq = nf.n * qr;
       const bool bad = in && !(np > 0.0 && nq > 0.0 && pr <= 1.0);
-      KT_EVENT(11, bad);
-      KT_EVENT(8, in && fabs(nf.X - np) < 0.1 * (nf.X + np));
-      KT_EVENT(9, in && nf.X != nf.n && fabs(nf.nx - nq) < 0.1 * (nf.nx + nq));
-      KT_EVENT(13, in);
       double nb;
       if (SCDE_NB_CLOSED) {
         // log dnbinom(x; size, p_k) = C + size log p_k + x log q_k (C: the column constant;
@@ -809,14 +772,12 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       for (int i = 0; i < kTabChunks; ++i) v[i] = (b && i == j) ? nv : v[i];
     }
   }
-  KT_STAMP(1);
   if (SCDE_KT_DIAG & 16) {  // timing diagnostic: loop 1 only
     if (lmax == 12345.0) a.has_clamp[col] = 1;
     return;
   }
   double maxp = wave_allreduce<true>(lmax);
   if (maxp < (maxcfp + fp)) maxp = maxcfp + fp;
-  KT_STAMP(2);
   const double d0 = fp - maxp;
   const double E = exp_tab(fmax(d0, -746.0), etab);  // exp(fp - maxp); 0 below -746 (and for NaN)
   double ls = 0.0;
@@ -827,22 +788,19 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       const bool in = k < G;
       v[j] -= maxp;  // t1
       double e = sl[kRowCfp * kRS + 64 * j] * E;
-      KT_EVENT(14, in && v[j] > -60.0);
       if (!(SCDE_KT_DIAG & 2) && __builtin_amdgcn_ballot_w64(in && v[j] > -60.0)) e += exp_tab(fmax(v[j], -746.0), etab);
       ls += in ? e : 0.0;
     }
   }
   const double s = wave_allreduce<false>(ls);
   const double lsum = log_tab(s, lt);  // s >= 1 (the maximum term is exp(0))
-  KT_STAMP(3);
   const bool want_maxi = a.maxi != nullptr;
   double bv = -INFINITY;
   int bi = 0x7fffffff;
   bool clamp = false, nanq = false;
-  KT_STAMP(4);
   double* out = a.T ? a.T + col * a.GS : nullptr;
   double* dout = (phase && a.D) ? a.D + col * a.GS : nullptr;
-  const double minlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
+  const double minlp = a.minlogprob;
   unsigned uqv = 0;  // lane t < kQTiles: bound tile t's value (BM == kBoundTiles)
 #pragma unroll
   for (int j = 0; j < kTabChunks; ++j) {
@@ -854,8 +812,6 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       const bool tiny = !(hi >= -665.0);
       const bool mixed = !tiny && !(hi - lo > 37.5);
       double r = hi - lsum;
-      KT_EVENT(10, in && (tiny || mixed));
-      KT_EVENT(15, in && tiny);
       if (__builtin_amdgcn_ballot_w64(in && (tiny || mixed))) {
         const double e = fma(sl[kRowCfp * kRS + 64 * j], E, exp_tab(fmax(t1, -746.0), etab));
         const double rm = (SCDE_KT_DIAG & 4) ? e - lsum : log_tab(tiny ? e / s : e, lt) - (tiny ? 0.0 : lsum);
@@ -896,7 +852,6 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
       }
     }
   }
-  KT_STAMP(5);
   if (BM == kBoundTiles) {
     if (__ballot(nanq) && lane == 0) *a.nanflag = 1;
     if (lane < kQTiles) {
@@ -924,10 +879,6 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
   }
   const unsigned long long anyc = __ballot(clamp);
   if (lane == 0) a.has_clamp[col] = anyc ? 1 : 0;
-  KT_STAMP(6);
-#if SCDE_KT_STAMP
-  if (lane == 0) atomicAdd(&g_kt_stamp[7], 1ull);
-#endif
 }
 
 
@@ -939,7 +890,7 @@ __device__ __forceinline__ void tables_column_reg(const TablesArgs& a, long long
 // (LDS broadcast reads), the column's maximum and normaliser are one running max / sum per lane
 // (four partials per column combined in LDS, in wave order), and the tile and stretch bounds are
 // running maxima.  No cross-lane reduction, ballot or per-chunk branch in the hot loops; the loop
-// bodies are short (the k_tables_reg form spent most of its time in instruction supply and
+// bodies are short (the register-row form (k_tables_reg, round 5) spent most of its time in instruction supply and
 // dependency chains: timing builds without its exps or its mixed branch ran 30% faster each though
 // the branch runs on 1.5% of the points).  Rows go out through a per-wave LDS transpose, kLpcFlush
 // points of 64 columns at a time, as 16-byte stores (64 contiguous bytes per column).
@@ -1057,7 +1008,7 @@ __global__ __launch_bounds__(64 * kLpcWaves) void k_tables_lpc(TablesArgs a) {
   const LogTab lt{ltab[0], ltab[1], ltab[2]};
   const int zc = (phase == 2) ? tab_zcol(a, c) : -1;
   const double maxcfp = a.cellscal[2 * c];
-  const double minlp = (c >= a.mlp_split) ? a.minlogprob2 : a.minlogprob;
+  const double minlp = a.minlogprob;
   // this lane's column and its constants
   const int col = task.y + lane;
   const bool mine = col < task.z && col != zc;
@@ -2757,7 +2708,7 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     long long part_stride, int* __restrict__ degen, int ngenes, const unsigned char* __restrict__ W8p, int Bq,
     const unsigned* __restrict__ UQ, const int* __restrict__ ZUq, const int* __restrict__ nanflag, int maxgroups,
     int* __restrict__ redo, int* __restrict__ stats, const int* __restrict__ order, unsigned* __restrict__ pmask,
-    int pairs, const int* __restrict__ ilist, int* __restrict__ wide) {
+    const int* __restrict__ ilist) {
   static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
   __shared__ float ubs[WB][kBTileMax * NB];  // [wave][bound tile][boot] slab A's bounds
 #ifdef SCDE_TILE_TEST_WB1
@@ -2784,31 +2735,25 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   float* const ubB = reinterpret_cast<float*>(&bstage[wsid][0]);
   double* const tsum = reinterpret_cast<double*>(&bstage[wsid][2 * ((kBTileMax * NB + 1) / 2)]);
   double* const finv = tsum + 8 * NB;
-  // ---- the wave's slabs: (gene, slab) items; in pair mode (gene, slab pair) items, slabs 2i
-  // and 2i + 1 side by side (a last odd slab alone, all four bound tiles); in list mode the
-  // slabs a pair pass could not finish, all four bound tiles each
+  // ---- the wave's slab: (gene, slab) items; in list mode the slabs the gene blocks could not
+  // finish, all four bound tiles each.  (Slab B -- pB, nsl, pr -- is the former pair mode's second
+  // slab of a wave, never set since round 6: the branches below fold away.)
   const int idx = xcd_block(blockIdx.x, gridDim.x) * WB + wsid;
-  int g, pA, pB = -1;
+  int g, pA;
+  constexpr int pB = -1;
   if (ilist) {
     if (idx >= ilist[0]) return;
     const int it = ilist[1 + idx];
     g = it / P;
     pA = it - g * P;
-  } else if (pairs) {
-    const int PP = (P + 1) >> 1;
-    if (idx >= ngenes * PP) return;
-    const int gi = idx / PP, pi = idx - gi * PP;
-    g = order ? order[gi] : gi;
-    pA = 2 * pi;
-    pB = (2 * pi + 1 < P) ? 2 * pi + 1 : -1;
   } else {
     if (idx >= ngenes * P) return;
     const int gi = idx / P;
     g = order ? order[gi] : gi;
     pA = idx - gi * P;
   }
-  const bool pr = pB >= 0;  // two slabs: rows 0-1 slab A's two best bound tiles, rows 2-3 slab B's
-  const int nsl = pr ? 2 : 1;
+  constexpr bool pr = false;
+  constexpr int nsl = 1;
   if (*nanflag) {  // a NaN in some table: k_boot2 computes every slab
     if (lane < nsl) {
       const int q = (long long)g * P + (lane ? pB : pA);
@@ -2937,17 +2882,12 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
       failm |= 1u << sl;
       if (lane == 0) {
         const int q = g * P + (sl ? pB : pA);
-        if (pr) {
-          wide[1 + atomicAdd(&wide[0], 1)] = q;
-          if (stats) atomicAdd(&stats[35], 1);
-        } else {
-          redo[q] = 1;
-          redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = q;
-          pmask[q] = ~0u;
-          if (stats) {
-            atomicAdd(&stats[3], 1);
-            atomicAdd(&stats[5], (n + 3) & ~3);
-          }
+        redo[q] = 1;
+        redo[(long long)ngenes * P + 1 + atomicAdd(&redo[(long long)ngenes * P], 1)] = q;
+        pmask[q] = ~0u;
+        if (stats) {
+          atomicAdd(&stats[3], 1);
+          atomicAdd(&stats[5], (n + 3) & ~3);
         }
       }
     }
@@ -3406,140 +3346,6 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   }
 }
 
-// k_boot2's grid-stretch bootstrap on the tile rows (round 5; the default below 400 cells per
-// call, option boot2_rows): one 4-wave block per (gene, slab of NB boots), as k_boot2, but the
-// stretches k_stretch_mask keeps are packed two to a wave -- 16-lane row r of wave w computes the
-// 32-point bound tile 2 s + (r & 1) of the stretch s = (2 w + (r >> 1))-th kept stretch, two
-// points per lane, every multiplicity by DPP64 broadcast from a 16-byte load (tile_rows: no scalar
-// loads), so a wave covers 128 points and a block only as many waves as half its kept stretches.
-// Maxima, post-check, softmax terms, 16-point tile sums (pair8_sum = row16_sum's operand pairs)
-// added in tile order, normalisers and partial rows are formed exactly as in k_boot2, so the
-// outputs are bit-identical to it.  Only the computed tiles are written (pmask, as the tile path;
-// k_sum_partials reads the rest as zeros).  redo_pass 1: the slabs the post-check flagged, every
-// stretch (up to 8 in 4 waves).
-template <int NB>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_TILE_WPE))) void k_boot2t(
-    const double* __restrict__ D, const int2* __restrict__ ent, const int* __restrict__ nnz, int ent_stride,
-    const double* __restrict__ Wt, int Bp, int ncells, const int* __restrict__ wset, const double* __restrict__ Z,
-    int G, int GS, int P, int nboot, double norm_mult, double degen_thresh, double* __restrict__ part,
-    long long part_stride, int* __restrict__ degen, int ngenes, const int* __restrict__ smask,
-    const double* __restrict__ sub, int* __restrict__ redo, int redo_pass, unsigned* __restrict__ pmask) {
-  static_assert(NB % 4 == 0 && NB <= 20, "NB must be a multiple of 4, <= 20");
-  __shared__ float rowmax[16 * 32];  // [row][boot] row maxima
-  __shared__ double tsum[32 * NB];   // [16-point tile][boot] tile partial sums (G <= 512)
-  __shared__ double fin[32];         // [boot] maxima, then 1 / (S nboot)
-  __shared__ double etab[64];
-  const int within = blockIdx.x % (8 * P);
-  const int p = within >> 3;
-  const int g = (blockIdx.x / (8 * P)) * 8 + (within & 7);
-  if (g >= ngenes) return;
-  if (redo_pass == 1 && !redo[(long long)g * P + p]) return;
-  const int lane = threadIdx.x & 63;
-  const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nst = (G + 63) >> 6;
-  const unsigned wmask = (smask ? (unsigned)__builtin_amdgcn_readfirstlane(smask[(long long)g * P + p]) : ~0u) &
-                         ((1u << nst) - 1);
-  const int nlive = __builtin_popcount(wmask);  // >= 1: the mask keeps the stretch of the largest bound
-  if (2 * wsid >= nlive) return;                 // no stretch for this wave (barriers wait for the others)
-  const int nwl = (nlive + 1) >> 1;              // waves with stretches: 0 .. nwl - 1
-  if (wsid == 0) etab[lane] = kExp2Frac64[lane];
-  // this wave's stretches: the (2 wsid)-th and (2 wsid + 1)-th kept ones
-  unsigned mm = wmask;
-  for (int i = 0; i < 2 * wsid; ++i) mm &= mm - 1;
-  const int sA = __builtin_ffs((int)mm) - 1;
-  mm &= mm - 1;
-  const int sB = mm ? __builtin_ffs((int)mm) - 1 : -1;
-  const int r4 = lane >> 4, r = lane & 15;
-  const int st = (r4 < 2) ? sA : sB;
-  const bool live = st >= 0;
-  const int T = 2 * (live ? st : 0) + (r4 & 1);  // the row's 32-point bound tile
-  const int t16 = 2 * T + ((lane >> 3) & 1);      // the lane's 16-point sum tile
-  const int k0 = 16 * t16 + 2 * (lane & 7);
-  const bool l0 = live && k0 < G, l1 = live && k0 + 1 < G;
-  const int b0 = p * NB;
-  const int n = nnz[g];
-  const int2* __restrict__ E = ent + (long long)g * ent_stride;
-  const int set = wset ? wset[g] : 0;
-  const double* __restrict__ W = Wt + (long long)set * ncells * Bp;
-  const double* __restrict__ Zs = Z + (long long)set * Bp * GS;
-  double a0[NB], a1[NB];
-  tile_rows<NB>(a0, a1, D, E, n, W, Zs, GS, Bp, b0, k0, r, live, l0, l1);
-  // per-row f32 maxima (dead points are -inf), combined over the block's rows by the lead wave
-  const int q = 4 * wsid + r4;
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    float m = (float)gt_max(a0[i], a1[i]);
-    m = gt_maxf(m, dpp_f<kDppXor1>(m));
-    m = gt_maxf(m, dpp_f<kDppXor2>(m));
-    m = gt_maxf(m, dpp_f<kDppHalfMirror>(m));
-    m = gt_maxf(m, dpp_f<kDppMirror>(m));
-    if (r == 0) rowmax[q * 32 + i] = m;
-  }
-  __syncthreads();
-  if (wsid == 0) {
-    const bool lb = lane < NB && b0 + lane < nboot;
-    if (lane < NB) {
-      float m = -INFINITY;
-      for (int q2 = 0; q2 < 4 * nwl; ++q2) m = gt_maxf(m, rowmax[q2 * 32 + lane]);
-      fin[lane] = (double)m;
-    }
-    // post-check of the left-out stretches against the exact row maxima (as k_boot2)
-    bool fails = false;
-    if (smask && lb)
-      for (int w = 0; w < nst; ++w)
-        if (!((wmask >> w) & 1) && !(sub[((long long)(g * P + p) * kStretchSlots + w) * NB + lane] < fin[lane] - 51.0))
-          fails = true;
-    const bool flagged = __builtin_amdgcn_ballot_w64(fails) != 0;
-    if (flagged && lane == 0) redo[(long long)g * P + p] = 1;
-    if (!flagged && lb && !(fabs(fin[lane]) <= degen_thresh)) degen[g] = 1;
-    if (lane == 0) {  // the 16-point tiles this slab's partial row holds
-      const int NT = (G + 15) >> 4;
-      unsigned dn = 0;
-      for (int w = 0; w < nst; ++w)
-        if ((wmask >> w) & 1) dn |= 15u << (4 * w);
-      pmask[(long long)g * P + p] = dn & ((NT >= 32) ? ~0u : ((1u << NT) - 1));
-    }
-  }
-  __syncthreads();
-  // softmax terms (below e^-50 zeroed, as k_boot2), 16-point tile partial sums
-#pragma unroll
-  for (int i = 0; i < NB; ++i) {
-    const double m = fin[i];
-    const double d0 = a0[i] - m, d1 = a1[i] - m;
-    const bool n0 = l0 && d0 >= kBootExpCut, n1 = l1 && d1 >= kBootExpCut;
-    if (__builtin_amdgcn_ballot_w64(n0 || n1)) {
-      a0[i] = n0 ? exp_tab(d0, etab) : 0.0;
-      a1[i] = n1 ? exp_tab(d1, etab) : 0.0;
-    } else {
-      a0[i] = 0.0;
-      a1[i] = 0.0;
-    }
-    const double ps = pair8_sum(a0[i], a1[i]);
-    if ((lane & 7) == 0 && live) tsum[t16 * NB + i] = ps;
-  }
-  __syncthreads();
-  if (wsid == 0 && lane < NB) {
-    const int nt = (G + 15) >> 4;
-    double S = 0.0;
-    for (int t = 0; t < nt; ++t)
-      if ((wmask >> (t >> 2)) & 1) S += tsum[t * NB + lane];
-    fin[lane] = (b0 + lane < nboot) ? 1.0 / (S * norm_mult) : 0.0;
-  }
-  __syncthreads();
-  if (l0) {
-    double j0 = 0.0, j1 = 0.0;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      j0 = fma(a0[i], fin[i], j0);
-      j1 = fma(a1[i], fin[i], j1);
-    }
-    double* prow = part + (long long)p * part_stride + (long long)g * GS;
-    if (l1)
-      *reinterpret_cast<d2_t*>(prow + k0) = d2_t{j0, j1};
-    else
-      prow[k0] = j0;
-  }
-}
 
 #ifdef SCDE_TILE_TEST_WB1
 // hazard-test builds only (tests/test_kernel_resources.py), never run: one-wave blocks with a
@@ -3551,8 +3357,8 @@ template __global__ void k_boot_tiles<20, 1>(const double* __restrict__, const i
                                              double* __restrict__, long long, int* __restrict__, int,
                                              const unsigned char* __restrict__, int, const unsigned* __restrict__,
                                              const int* __restrict__, const int* __restrict__, int, int* __restrict__,
-                                             int* __restrict__, const int* __restrict__, unsigned* __restrict__, int,
-                                             const int* __restrict__, int* __restrict__);
+                                             int* __restrict__, const int* __restrict__, unsigned* __restrict__,
+                                             const int* __restrict__);
 #endif
 
 // jp[g, k] = sum over slabs p (in order) of part[p][g][k]
@@ -4310,16 +4116,6 @@ hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, con
   return hipGetLastError();
 }
 
-#if SCDE_KT_STAMP
-extern "C" int scde_diag_kt_stamps(unsigned long long* out, int reset) {
-  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_kt_stamp), sizeof(g_kt_stamp));
-  if (e == hipSuccess && reset) {
-    static const unsigned long long z[16] = {};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(g_kt_stamp), z, sizeof(z));
-  }
-  return (int)e;
-}
-#endif
 
 hipError_t launch_col_consts(const int* ucl, const long long* ucl_off, long long ncols, int ncells,
                              const double* theta, int GS, const double* cellscal, double* colc, hipStream_t s) {
@@ -4563,30 +4359,6 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
     sub = a.ubuf;
   }
   const int grid = (a.ngenes + 7) / 8 * 8 * P;
-  // the tile-row kernel (k_boot2t): with the mask, nb <= 20, 16-byte aligned multiplicity rows and
-  // at most 8 stretches of a 512-point column stride
-  const bool rows = smask && a.pmask && a.nb <= 20 && a.Bp % 2 == 0 && a.GS % 2 == 0 && a.G <= 512;
-  if (rows) {
-#define SCDE_B2T(NBV)                                                                                             \
-  case NBV:                                                                                                        \
-    hipLaunchKernelGGL(k_boot2t<NBV>, dim3(grid), dim3(256), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp,    \
-                       a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
-                       a.part_stride, a.degen, a.ngenes, RP ? nullptr : smask, sub, a.redo, RP, a.pmask);      \
-    break;
-    for (int RP = 0; RP < 2; ++RP) {
-      switch (a.nb) {
-        SCDE_B2T(4) SCDE_B2T(8) SCDE_B2T(12) SCDE_B2T(16) SCDE_B2T(20)
-        default: return hipErrorInvalidValue;
-      }
-    }
-#undef SCDE_B2T
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const long long n = (long long)a.ngenes * a.G;
-    hipLaunchKernelGGL(k_sum_partials, dim3(div_up(n, 256)), dim3(256), 0, s, a.part, a.part_stride, P, a.ngenes,
-                       a.G, a.GS, a.out, a.out_g, a.out_k, a.pmask, nullptr);
-    return hipGetLastError();
-  }
 #define SCDE_B2(NBV)                                                                                              \
   case NBV:                                                                                                        \
     hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid), dim3(block), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
@@ -4726,13 +4498,10 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   z.p[z.count] = a.redo;
   z.n[z.count++] = sizeof(int) * ((size_t)a.ngenes * P + 1);
   const long long items = (long long)a.ngenes * P;
-  // pair mode: a wave per two slabs of a gene, two bound tiles each; the slabs that need more
-  // go to a four-tile pass over the compacted list `wide` ([0] length, then g * P + p)
-  const bool pairs = tb.pairs && P >= 2 && tb.wide;
   // gene blocks: one 4-wave block per (gene, group of SG slabs) shares 16 rows among the group's
-  // slabs; the slabs whose post-check fails take the four-tile pass over `wide`
-  const bool gene = !pairs && tb.gene && tb.W8g && tb.wide && tb.SG >= 1 && tb.SG <= kGeneSlabs &&
-                    tb.SG * a.nb <= 128;
+  // slabs; the slabs whose post-check fails take the four-tile pass over `wide` (without the gene
+  // block arguments: one k_boot_tiles wave per slab)
+  const bool gene = tb.gene && tb.W8g && tb.wide && tb.SG >= 1 && tb.SG <= kGeneSlabs && tb.SG * a.nb <= 128;
   if (gene) {
     const int NGR = (P + tb.SG - 1) / tb.SG;
     if ((long long)a.ncells * NGR * 128 >= (1LL << 31) || tb.Bq < (NGR - 1) * tb.SG * a.nb + 128) return hipErrorInvalidValue;
@@ -4742,61 +4511,42 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
   if (g_lo < 0 || g_hi > a.ngenes || g_lo > g_hi || ((g_lo != 0 || g_hi != a.ngenes) && !gene))
     return hipErrorInvalidValue;
   const long long gspan = g_hi - g_lo;
-  if (pairs || gene) {
+  if (gene) {
     z.p[z.count] = tb.wide;
     z.n[z.count++] = sizeof(int);
   }
   hipError_t e = launch_zero(z, s);
   if (e != hipSuccess) return e;
   constexpr int WB = 4;
-  const long long items1 = pairs ? (long long)a.ngenes * ((P + 1) / 2) : items;
-  // slabs a pair pass (or a gene block) may leave to the four-tile list pass
-  // (gene blocks: at most list_cap slabs, 16384 by default; k_boot_gene sends further failures to k_boot2)
-  // The cap is rounded down to a multiple of the list pass's WB waves per block: k_boot_gene writes
-  // list entries only below it (wide[0] keeps counting past it), and the list pass's grid of
-  // items2 / WB blocks must then hold no wave whose index lies in [cap, grid * WB) -- such a wave
-  // would read an entry this call never wrote.
+  // slabs a gene block may leave to the four-tile list pass: at most list_cap (16384 by default;
+  // k_boot_gene sends further failures to k_boot2).  The cap is rounded down to a multiple of the
+  // list pass's WB waves per block: k_boot_gene writes list entries only below it (wide[0] keeps
+  // counting past it), and the list pass's grid of items2 / WB blocks must then hold no wave whose
+  // index lies in [cap, grid * WB) -- such a wave would read an entry this call never wrote.
   const long long gene_cap = std::max<long long>(WB, ((tb.list_cap > 0 ? tb.list_cap : 16384) / WB) * WB);
-  const long long items2 = pairs ? (long long)a.ngenes * (P / 2) * 2 : gene ? std::min(gspan * P, gene_cap) : 0;
+  const long long items2 = gene ? std::min(gspan * P, gene_cap) : 0;
   const long long gblocks = gene ? gspan * ((P + tb.SG - 1) / tb.SG) : 0;
   const long long gblk0 = gene ? (long long)g_lo * ((P + tb.SG - 1) / tb.SG) : 0;
   // gene blocks holding all of a gene's slabs write the finished jp rows of their genes themselves
   int* const gdone = (gene && tb.gdone && tb.SG >= P) ? tb.gdone : nullptr;
-  // gene blocks in tb.chunks launches (>= 1): between launches the other lane's queued kernels
-  // get CU slots that one long grid would hold until its last block is dispatched
-  const long long chunk = std::max<long long>(1, (gblocks + std::max(1, tb.chunks) - 1) / std::max(1, tb.chunks));
 #define SCDE_BT(NBV)                                                                                              \
   case NBV:                                                                                                        \
-    if (gene)                                                                                                      \
-      for (long long c0 = 0; c0 < gblocks; c0 += chunk) {                                                          \
-        const unsigned nblk = (unsigned)std::min<long long>(chunk, gblocks - c0);                                  \
-        if (tb.gene_waves == 3)                                                                                    \
-          hipLaunchKernelGGL((k_boot_gene<NBV, 3>), dim3(nblk), dim3(192), 0, s, a.D, a.ent, a.nnz,               \
-                             a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
-                             a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
-                             tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
-                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0), a.out, a.out_g,        \
-                             a.out_k, gdone);                                                                      \
-        else                                                                                                       \
-          hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3(nblk), dim3(256), 0, s, a.D, a.ent, a.nnz,               \
-                             a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,      \
-                             a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g,      \
-                             tb.Bq, tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats,          \
-                             tb.order, tb.pmask, tb.wide, (int)items2, (int)(gblk0 + c0), a.out, a.out_g,        \
-                             a.out_k, gdone);                                                                      \
-      }                                                                                                            \
-    else                                                                                                           \
-    hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items1, WB)), dim3(64 * WB), 0, s, a.D,     \
-                       a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,      \
-                       a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq,      \
-                       tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask, pairs ? 1 : 0, \
-                       nullptr, tb.wide);                                                                        \
-    if (pairs || gene)                                                                                             \
+    if (gene) {                                                                                                    \
+      hipLaunchKernelGGL((k_boot_gene<NBV, 4>), dim3((unsigned)gblocks), dim3(256), 0, s, a.D, a.ent, a.nnz,      \
+                         a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, tb.SG, a.nboot,          \
+                         a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8g, tb.Bq,  \
+                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, tb.kcap, a.redo, tb.stats, tb.order, tb.pmask, \
+                         tb.wide, (int)items2, (int)gblk0, a.out, a.out_g, a.out_k, gdone);                      \
       hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items2, WB)), dim3(64 * WB), 0, s, a.D,   \
                          a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,    \
                          a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq,    \
-                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask, 0,        \
-                         tb.wide, nullptr);                                                                      \
+                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask, tb.wide); \
+    } else {                                                                                                       \
+      hipLaunchKernelGGL((k_boot_tiles<NBV, WB>), dim3((unsigned)div_up(items, WB)), dim3(64 * WB), 0, s, a.D,    \
+                         a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot,    \
+                         a.norm_mult, a.degen_thresh, a.part, a.part_stride, a.degen, a.ngenes, tb.W8p, tb.Bq,    \
+                         tb.UQ, tb.ZUq, tb.nanflag, tb.maxgroups, a.redo, tb.stats, tb.order, tb.pmask, nullptr); \
+    }                                                                                                              \
     break;
   switch (a.nb) {
     SCDE_BT(4) SCDE_BT(8) SCDE_BT(12) SCDE_BT(16) SCDE_BT(20)

@@ -103,9 +103,7 @@ def test_config3_host_pipeline_equals_device_resident(api):
     whose unique sets and tables start as each lands (option pieces), and builds the second
     group's unique sets and posterior on the peer lane beside the first group's
     (engine.hip de_run, lanes = 2); the table must equal, bit for bit, the device-resident entry
-    on the same counts with the groups one after the other (lanes = 1, no pipelining, fuse_groups 0).
-    The host calls run the default path and, once, the fused one (option fuse_groups: both groups
-    as one posterior over concatenated cells, the count columns in pieces over the fused cell list)."""
+    on the same counts with the groups one after the other (lanes = 1, no pipelining)."""
     import ctypes
     import bench
     from scde_amd._lib import DEParams, check, lib
@@ -129,21 +127,18 @@ def test_config3_host_pipeline_equals_device_resident(api):
     try:
         # the first group's columns in 4 (default), 3 (uneven) pieces or one; the repeat reuses the
         # context's buffers and streams
-        for pieces, fuse in ((4, 0), (4, 0), (3, 0), (1, 0), (8, 0), (4, 1)):
+        for pieces in (4, 4, 3, 1, 8):
             ctx.set_option("pieces", pieces)
-            ctx.set_option("fuse_groups", fuse)
             host = np.zeros((N, 6), order="F")
             check(lib().scde_expression_difference_host(ctx.handle, vp(mat), N, N, ctypes.byref(params), vp(host),
                                                         None, None, None))
             hosts.append(host)
     finally:
         ctx.set_option("pieces", 4)
-        ctx.set_option("fuse_groups", 0)
     dc = api.DeviceCounts(ctx, mat)
     try:
         dev = np.zeros((N, 6), order="F")
-        ctx.set_option("lanes", 1)
-        ctx.set_option("fuse_groups", 0)  # the two group posteriors one after the other
+        ctx.set_option("lanes", 1)  # the two group posteriors one after the other
         check(lib().scde_expression_difference_dev(ctx.handle, dc.ptr, N, N, ctypes.byref(params), vp(dev), None,
                                                    None, None))
     finally:

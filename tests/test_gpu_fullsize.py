@@ -58,17 +58,6 @@ def test_config3_whole_table_vs_oracle(api, oracle):
     res, want = got["results"], g["results"]
     for j, k in enumerate(("lb", "mle", "ub", "ce")):
         np.testing.assert_array_equal(res[k].to_numpy(), want[:, j], err_msg=k)
-    # the host counts through the pinned staging ring (8 copy threads): the same table
-    ctx = api.default_context()
-    try:
-        ctx.set_option("upload_staged", 1)
-        api.set_rand("glibc")
-        st = api.scde_expression_difference(models, counts, prior, groups=list(groups), n_randomizations=nboot,
-                                            n_cores=ncores)
-    finally:
-        ctx.set_option("upload_staged", 0)
-    for k in ("lb", "mle", "ub", "ce", "Z", "cZ"):
-        np.testing.assert_array_equal(st[k].to_numpy(), res[k].to_numpy(), err_msg=f"staged {k}")
     assert_z_close(res["Z"].to_numpy(), want[:, 4], what="Z")
     assert_cz_close(res["cZ"].to_numpy(), want[:, 5], res["Z"].to_numpy(), want[:, 4], what="cZ")
     # posteriors of a window across the first chunk boundary (two draw lists), live oracle
@@ -210,7 +199,6 @@ def test_config3_host_pipeline_after_call_history(api):
     ref_ctx = api.Context(0)
     try:
         ref_ctx.set_option("lanes", 1)
-        ref_ctx.set_option("fuse_groups", 0)
         dc = api.DeviceCounts(ref_ctx, mat)
         ref = np.zeros((N, 6), order="F")
         check(lib().scde_expression_difference_dev(ref_ctx.handle, dc.ptr, N, N, ctypes.byref(params), vp(ref), None,
@@ -303,6 +291,14 @@ def test_host_upload_16bit_counts(api):
                 check(lib().scde_expression_difference_host(ctx.handle, vp(neg), N, N, ctypes.byref(params), vp(out),
                                                             None, None, None))
             assert "negative" in str(e.value).lower() or "count" in str(e.value).lower(), str(e.value)
+        # an error in the middle of a 16-bit upload (a slot's copy, injected through the test hook)
+        # fails the call, and the next 16-bit upload on the same context completes with the same
+        # table (the error path reopens the slot ring: ADVICE r05, engine.hip upload_cols_u16)
+        ref_mat = de(mat, 0)
+        ctx.inject_fault("u16_slot", 1)
+        with pytest.raises(Exception):
+            de(mat, 1)
+        np.testing.assert_array_equal(de(mat, 1), ref_mat)
         # scde.posteriors host entry (one range in pieces), modes included
         c4 = bench.CONFIGS["4"]
         m4, k4, _ = bench.synthetic(c4["seed"], 4000, c4["cells"], two_groups=False)

@@ -152,8 +152,7 @@ def _loop_spans(body):
     return lines, spans
 
 
-@pytest.mark.parametrize("kernel", ["k_boot2ILi20E", "k_boot_tilesILi20E", "k_boot2_listILi20E", "k_boot_geneILi20ELi4E",
-                                    "k_boot_geneILi20ELi3E", "k_boot2tILi20E"])
+@pytest.mark.parametrize("kernel", ["k_boot2ILi20E", "k_boot_tilesILi20E", "k_boot2_listILi20E", "k_boot_geneILi20ELi4E"])
 def test_lookahead_loops_do_not_touch_scratch(isa, kernel):
     bodies = _bodies(isa, kernel)
     assert bodies, f"{kernel} not found in the ISA"
@@ -165,8 +164,7 @@ def test_lookahead_loops_do_not_touch_scratch(isa, kernel):
             assert not bad, f"{sym}: scratch access inside a loop: {bad[:3]}"
 
 
-@pytest.mark.parametrize("kernel", ["k_boot2ILi20E", "k_boot_tilesILi20E", "k_boot2_listILi20E", "k_boot_geneILi20ELi4E",
-                                    "k_boot_geneILi20ELi3E", "k_boot2tILi20E"])
+@pytest.mark.parametrize("kernel", ["k_boot2ILi20E", "k_boot_tilesILi20E", "k_boot2_listILi20E", "k_boot_geneILi20ELi4E"])
 def test_lookahead_loads_not_touched_in_flight(isa, kernel):
     for sym, body in _bodies(isa, kernel):
         lines, spans = _loop_spans(body)
@@ -175,8 +173,7 @@ def test_lookahead_loads_not_touched_in_flight(isa, kernel):
             assert not bad, f"{sym}: VGPRs of an in-flight load touched: {bad[:3]}"
 
 
-@pytest.mark.parametrize("kernel", ["k_boot_tilesILi20E", "k_boot_geneILi20ELi4E", "k_boot_geneILi20ELi3E",
-                                    "k_boot2tILi20E"])
+@pytest.mark.parametrize("kernel", ["k_boot_tilesILi20E", "k_boot_geneILi20ELi4E"])
 def test_dpp_broadcast_sources_not_fresh_valu_results(isa, kernel):
     bodies = _bodies(isa, kernel)
     assert bodies

@@ -1,4 +1,4 @@
-"""The closed form of the NB log-pmf that k_tables_reg evaluates per grid point (SCDE_NB_CLOSED,
+"""The closed form of the NB log-pmf that the tables kernels (k_tables_lpc, tables_column_reg) evaluate per grid point (SCDE_NB_CLOSED,
 kernels.hip k_col_consts / tables_column_reg), against the oracle's restatement of R nmath's
 saddle-point dnbinom (src/jpmatLogBoot.cpp:174 calls Rf_dnbinom; oracle/scde_oracle.c
 o_dnbinom_log): log dnbinom(x; size, p) = C(x, size) + size log p + x log q with q = 1 - p as
