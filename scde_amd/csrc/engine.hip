@@ -300,6 +300,8 @@ struct scde_ctx {
   int opt_tables_nt = 2;        // "tables_nt": table rows as non-temporal stores (0 no, 1 yes, 2 when the call's
                                 // rows exceed 256 MB)
   int fault_u16 = 0;            // test hook (scde_ctx_inject_fault): 16-bit upload slots to fail
+  long long spin_cycles = 0;    // test hook: a spin kernel before every cross-stream handoff (handoff_spin)
+  std::atomic<long long> st_spins{0};  // handoff spins launched (any thread; the peer counts its own)
   int opt_lanes = 2;            // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                 // group on `peer`, its own streams and workspace) or one after the other (1)
   // fixed settings that were options until round 5 (the alternatives measured slower or equal and were
@@ -593,6 +595,14 @@ struct scde_ctx {
   }
 };
 
+// test hook (scde_ctx_inject_fault "handoff_spin"): a spin kernel on the producing stream before every
+// event another stream or host thread waits on -- a missing wait then shows as wrong results every time
+static hipError_t handoff_spin(scde_ctx* cx, hipStream_t s) {
+  if (cx->spin_cycles <= 0) return hipSuccess;
+  ++cx->st_spins;
+  return launch_spin(s, cx->spin_cycles);
+}
+
 // Downloader: queue a read-back of `height` rows of `width` bytes (pitches in bytes) after the work
 // queued so far on `after`; dnl_wait returns once every queued read-back has landed (or failed).
 int dnl_push(scde_ctx* cx, hipStream_t after, void* dst, size_t dpitch, const void* src, size_t spitch, size_t width,
@@ -633,6 +643,7 @@ int dnl_push(scde_ctx* cx, hipStream_t after, void* dst, size_t dpitch, const vo
     d.evs.push_back(e);
   }
   const int ei = d.nev++;
+  HCHK(handoff_spin(cx, after));
   HCHK(hipEventRecord(d.evs[ei], after));
   d.q.push_back({ei, dst, src, dpitch, spitch, width, height});
   ++d.pending;
@@ -1227,6 +1238,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       HCHK(launch_tables(tc, st));
       if (last) {
         if (!cx->p1_ev) HCHK(hipEventCreateWithFlags(&cx->p1_ev, hipEventDisableTiming));
+        HCHK(handoff_spin(cx, st));
         HCHK(hipEventRecord(cx->p1_ev, st));
       }
       tc.phase = 2;
@@ -1297,6 +1309,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       cx->stream = main;
       pu.into = nullptr;
       RCHK(rc);
+      HCHK(handoff_spin(cx, s.piece_stream));
       HCHK(hipEventRecord(s.piece_ev[j], s.piece_stream));
       HCHK(hipStreamWaitEvent(st, s.piece_ev[j], 0));
       for (int c = c0; c < c1; ++c) ucl_off_h[c + 1] = col0 + pu.ucl_off_h[c - c0 + 1];
@@ -1367,6 +1380,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       RCHK(dnl_push(cx, st, s.modes_host, bytes, s.modes, bytes, bytes, 1));
     } else {
       if (!cx->modes_ev) HCHK(hipEventCreateWithFlags(&cx->modes_ev, hipEventDisableTiming));
+      HCHK(handoff_spin(cx, st));
       HCHK(hipEventRecord(cx->modes_ev, st));
     }
   }
@@ -1547,6 +1561,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     HCHK(cx->degen.ensure(sizeof(int) * std::max(1, NBg)));
     HCHK(hipMemsetAsync(cx->degen.p, 0, sizeof(int) * std::max(1, NBg), sa));
     if (sa != st) {  // the bootstrap waits for the set-up and for phase 2
+      HCHK(handoff_spin(cx, sa));
       HCHK(hipEventRecord(cx->aux_ev, sa));
       HCHK(hipStreamWaitEvent(st, cx->aux_ev, 0));
     }
@@ -2003,6 +2018,7 @@ int scde_ctx_set_option(scde_ctx* ctx, const char* name, double value) {
 int scde_ctx_inject_fault(scde_ctx* ctx, const char* where, int count) {
   if (!ctx || !where) return fail(SCDE_EARG, "null argument");
   if (std::string(where) == "u16_slot") ctx->fault_u16 = std::max(0, count);
+  else if (std::string(where) == "handoff_spin") ctx->spin_cycles = std::max(0, count);
   else return fail(SCDE_EARG, "unknown fault point '%s'", where);
   return SCDE_OK;
 }
@@ -2023,6 +2039,7 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value) {
   else if (n == "piece_wait_ms") *value = ctx->st_piece_wait_ms + (ctx->peer ? ctx->peer->st_piece_wait_ms : 0);
   else if (n == "piece_host_ms") *value = ctx->st_piece_host_ms + (ctx->peer ? ctx->peer->st_piece_host_ms : 0);
   else if (n == "buf_reallocs") *value = (double)g_buf_reallocs.load();
+  else if (n == "handoff_spins") *value = (double)(ctx->st_spins.load() + (ctx->peer ? ctx->peer->st_spins.load() : 0));
   // (the upload worker and the 16-bit issuer update these under their mutexes)
   else if (n == "upload_wake_ms" || n == "upload_first_ms") {
     std::lock_guard<std::mutex> lk(ctx->upl.m);
@@ -2059,6 +2076,8 @@ int scde_ctx_reset_stats(scde_ctx* ctx) {
     ctx->u16.st_wait_ms = ctx->u16.st_issue_ms = ctx->u16.st_free_ms = 0;
   }
   ctx->st_boot_f64_fma = 0;
+  ctx->st_spins = 0;
+  if (ctx->peer) ctx->peer->st_spins = 0;
   for (double& x : ctx->st_tile_hist) x = 0;
   return SCDE_OK;
 }
@@ -2547,6 +2566,7 @@ static int upload_cols_u16(scde_ctx* ctx, const HostUpload& h, int lo, int hi) {
       --ctx->fault_u16;
       e = hipErrorUnknown;
     }
+    if (e == hipSuccess) e = handoff_spin(ctx, ctx->copy_stream);
     if (e == hipSuccess) e = hipEventRecord(r.ev[k], ctx->copy_stream);
     if (e == hipSuccess) e = launch_widen16(dslot, dst + off, m, ctx->copy_stream);
     // the slot's counts outside 16 bits (the threads' lists of ring slot k are complete and
@@ -2680,6 +2700,7 @@ struct UploadWorker {
     std::lock_guard<std::mutex> lk(u.m);
     u.issue = [c, h, ranges = std::move(ranges), evs = std::move(evs)](int j) -> int {
       RCHK(upload_cols(c, h, ranges[j].first, ranges[j].second));
+      HCHK(handoff_spin(c, c->copy_stream));
       HCHK(hipEventRecord(evs[j], c->copy_stream));
       return SCDE_OK;
     };
@@ -2897,6 +2918,7 @@ static int lane_peer(scde_ctx* cx, scde_ctx** out) {
   p->opt_gene_rows = cx->opt_gene_rows;
   p->opt_gene_list_cap = cx->opt_gene_list_cap;
   p->opt_tables_nt = cx->opt_tables_nt;
+  p->spin_cycles = cx->spin_cycles;
   p->profile = cx->profile;
   *out = p;
   return SCDE_OK;
@@ -3046,6 +3068,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
           RCHK(build_unique_sets(lane, sp, usp, 1));
           hlap(1);
           RCHK(run_posterior(lane, specs[gi], ctx->us[gi]));
+          HCHK(handoff_spin(lane, lane->stream));
           HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
           HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
         } else {
@@ -3056,6 +3079,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
           const int rc = build_unique_sets(ctx, sp, usp, 1);
           ctx->stream = main;
           RCHK(rc);
+          HCHK(handoff_spin(ctx, ctx->uq_stream));
           HCHK(hipEventRecord(ctx->uq_ev, ctx->uq_stream));
           HCHK(hipStreamWaitEvent(ctx->stream, ctx->uq_ev, 0));
           hlap(1);
@@ -3072,6 +3096,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       RCHK(build_unique_sets(ctx, sp, up, 2));
       hlap(1);
       if (lane != ctx) {
+        HCHK(handoff_spin(ctx, ctx->stream));
         HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
         HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
       }
@@ -3086,6 +3111,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         RCHK(run_posterior(ctx, specs[1], ctx->us[1]));
       }
       if (lane != ctx) {
+        HCHK(handoff_spin(lane, lane->stream));
         HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
         HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
       }
@@ -3252,6 +3278,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
   scde_ctx* lane = ctx;  // the second batch posterior and the second group's run on the peer lane
   if (ctx->opt_lanes >= 2) RCHK(lane_peer(ctx, &lane));
   if (lane != ctx) {
+    HCHK(handoff_spin(ctx, ctx->stream));
     HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
     HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
     std::function<int()> rest0, rest1;
@@ -3262,6 +3289,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     RCHK(run_posterior(ctx, sg[0], ctx->us[0], &rest0));
     RCHK(run_posterior(lane, sg[1], ctx->us[1], &rest1));
     RCHK(run_rests(ctx, rest0, rest1));
+    HCHK(handoff_spin(lane, lane->stream));
     HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
     HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
   } else {
@@ -3408,6 +3436,7 @@ int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld
   const size_t row = sizeof(int) * (size_t)ngenes;
   HCHK(ctx->counts_in.ensure(std::max<size_t>(1, row * C)));
   // the previous call's kernels may still read counts_in: the copies wait for them
+  HCHK(handoff_spin(ctx, ctx->stream));
   HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
   HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
   // (a DE call's upload hides behind the first group's unique sets and tables: as int32, unless
@@ -3452,6 +3481,7 @@ int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngene
       if (!e) HCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HCHK(ctx->counts_in.ensure(sizeof(int) * (size_t)ngenes * ncells_total));
     // the previous call's kernels may still read counts_in: the copies wait for them
+    HCHK(handoff_spin(ctx, ctx->stream));
     HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
     HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
     const HostUpload h{counts, ld, ngenes, 0, ncells_total, ctx->opt_upload_u16 != 0};

@@ -286,6 +286,8 @@ constexpr int kMultMaxCells = 16384;
 hipError_t launch_mult(const int* draws, int nsets, int nboot, int ndraw, int ncells, int Bp, double* Wt, int Bt,
                        unsigned char* W8, int nb, int P, unsigned char* W8p, int SG, int NGR, unsigned char* W8g,
                        hipStream_t s);
+// test hook: one wave spinning `cycles` shader clocks on stream s (handoff_spin)
+hipError_t launch_spin(hipStream_t s, long long cycles);
 hipError_t launch_boot(const BootArgs& a, hipStream_t s);
 hipError_t launch_boot_exact(const ExactArgs& a, hipStream_t s);
 int boot2_nb(int nboot);

@@ -4104,8 +4104,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SCDE_RATIO_
   }
 }
 
+// Test hook (scde_ctx_inject_fault "handoff_spin"): one wave that spins for `cycles` shader clocks,
+// queued on a producing stream before a cross-stream handoff's event -- a consumer that misses its
+// wait then reads the producer's output before it is written, every time, not once in a while.
+__global__ void k_spin(long long cycles) {
+  const long long t0 = clock64();
+  while (clock64() - t0 < cycles) __builtin_amdgcn_s_sleep(1);
+}
+
 // ================================================================== launchers
 static inline int div_up(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+hipError_t launch_spin(hipStream_t s, long long cycles) {
+  if (cycles <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, std::min(cycles, 100000000LL));  // (at most ~0.05 s)
+  return hipGetLastError();
+}
 
 hipError_t launch_cell_prep(const double* models, int ncells, int G, int GS, const double* mag, int lt, int sq,
                             double* mu, double* lcfp, double* lcfpr, double* theta, double* cellscal,
