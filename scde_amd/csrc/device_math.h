@@ -250,6 +250,23 @@ __device__ __forceinline__ double exp_tab(double d, const double* __restrict__ t
   return ldexp(fma(t, em1, t), k >> 6);
 }
 
+// exp_tab with the rounding of 64 d / ln 2 by the 1.5 * 2^52 shift (one fma and one add for
+// rint + cvt; k is the shifted value's low word).  Study builds only (SCDE_GENE_EXP = 2).
+__device__ __forceinline__ double exp_tab_m(double d, const double* __restrict__ tab) {
+  const double sh = fma(d, 92.33248261689366, 0x1.8p52);
+  const double kd = sh - 0x1.8p52;
+  const int k = (int)(unsigned)__double_as_longlong(sh);
+  double r = fma(kd, -0.010830424667801708, d);
+  r = fma(kd, -2.8447437476627285e-11, r);
+  const double r2 = r * r;
+  double q = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  q = fma(q, r, 1.0 / 6.0);
+  q = fma(q, r, 0.5);
+  const double em1 = fma(q, r2, r);
+  const double t = tab[k & 63];
+  return ldexp(fma(t, em1, t), k >> 6);
+}
+
 // exp for d in [-746, 0] without a table (k_tables_lpc, where the table read's per-lane index would
 // put an LDS round trip with bank conflicts in every point's chain): exp(d) = 2^n e^r, n = rint(d / ln 2),
 // r = d - n ln 2 (Cody-Waite: n ln2_hi exact for |n| < 2^21), |r| <= 0.347, e^r by its degree-13

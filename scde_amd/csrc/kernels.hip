@@ -48,8 +48,8 @@ __device__ __forceinline__ double gt_max(double a, double b) { return (b > a) ? 
 // so one op combines them on every lane).  Every lane ends with the same bits.
 template <int CTRL>
 __device__ __forceinline__ double dpp64(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 __device__ __forceinline__ void rows_swap16(double& a, double& b) {
@@ -70,10 +70,10 @@ __device__ __forceinline__ void rows_swap32(double& a, double& b) {
 }
 // Maximum over each 16-lane row, on every lane of the row (same DPP partners as above).
 __device__ __forceinline__ int row16_max_i32(int v) {
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x141, 0xf, 0xf, true));
+  v = max(v, __builtin_amdgcn_mov_dpp(v, 0x140, 0xf, 0xf, true));
   return v;
 }
 template <bool MAX>
@@ -609,7 +609,7 @@ constexpr int kTabChunks = kTabStagedG / 64;
 
 template <int CTRL>
 __device__ __forceinline__ float dpp32f(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float wave_maxf(float v) {
   v = gt_maxf(v, dpp32f<0xB1>(v));
@@ -1734,8 +1734,8 @@ __device__ __forceinline__ void swap16(double& a, double& b) {
 }
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 constexpr int kDppMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
@@ -1845,7 +1845,7 @@ __device__ __forceinline__ void swap16f(float& a, float& b) {
 }
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), CTRL, 0xf, 0xf, true));
 }
 
 // f32 twin of wave_reduce_scatter_v (same lane -> index mapping), max only.
@@ -2984,7 +2984,81 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
 //      computed tiles in tile order, 1 / (S nboot), the partial jp rows.
 // Every value is formed exactly as in k_boot_tiles and k_boot2 (same fma chains, maxima, terms,
 // tile partials added in tile order), so the outputs are bit-identical to theirs.
+// Per 16-lane row, the f32 maxima of N values per lane, as a reduce-scatter by recursive
+// halving: lane bits 3, 2, 1, 0 split the index range in turn (partners lane ^ 15, lane ^ 7 by
+// row_mirror / row_half_mirror, lane ^ 2, lane ^ 1 by quad_perm), a keep/send select per value and
+// step.  (N + 1) / 2 + ... + 2 maxima per lane instead of 4 N; max is exact, so every lane's
+// values are the maxima any other order gives.  Lane bits b3..b0 then hold index
+// j + H4 b0 + H3 b1 + H2 b2 + H1 b3 in slot j < H4 (H1 = ceil(N / 2), H2 = ceil(H1 / 2), ...),
+// where row_scatter_index says it is valid.
+template <int N, int CTRL>
+__device__ __forceinline__ void row_halve_f(float (&v)[32], bool up) {
+  constexpr int H = (N + 1) / 2;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const float lo = v[j], hi = (j + H < N) ? v[j + H] : -INFINITY;
+    v[j] = gt_maxf(up ? hi : lo, dpp_f<CTRL>(up ? lo : hi));
+  }
+}
+template <int N>
+__device__ __forceinline__ void row_max_scatter_f(float (&v)[32], int r) {
+  constexpr int H1 = (N + 1) / 2, H2 = (H1 + 1) / 2, H3 = (H2 + 1) / 2;
+  row_halve_f<N, kDppMirror>(v, (r & 8) != 0);
+  row_halve_f<H1, kDppHalfMirror>(v, (r & 4) != 0);
+  row_halve_f<H2, kDppXor2>(v, (r & 2) != 0);
+  row_halve_f<H3, kDppXor1>(v, (r & 1) != 0);
+}
+// the index held in slot j of row lane r after row_max_scatter_f<N>, or -1
+template <int N>
+__device__ __forceinline__ int row_scatter_index(int r, int j) {
+  constexpr int H1 = (N + 1) / 2, H2 = (H1 + 1) / 2, H3 = (H2 + 1) / 2, H4 = (H3 + 1) / 2;
+  const int p4 = j + H4 * (r & 1), p3 = p4 + H3 * ((r >> 1) & 1), p2 = p3 + H2 * ((r >> 2) & 1),
+            p1 = p2 + H1 * ((r >> 3) & 1);
+  return (j < H4 && p4 < H3 && p3 < H2 && p2 < H1 && p1 < N) ? p1 : -1;
+}
+
+// The quad partials of pair8_sum for N values per lane as a reduce-scatter with its operand pairs
+// (the lane's two points, then lane ^ 1, lane ^ 2, each sum self + partner: the same bits): lane
+// bits 0, 1 split the index range in turn.  Slot j of lane m (bits b1 b0) then holds index
+// j + H2 b1 + H1 b0 where pair_scatter_index says it is valid.  pair8_sum's last step (lane ^ 7:
+// the other quad of the 8 lanes) pairs lanes holding different indices here, so it is left to the
+// reader: tile partial = quad 0 + quad 1, the same two operands.
+template <int N, int CTRL>
+__device__ __forceinline__ void pair_halve(double (&v)[32], bool up) {
+  constexpr int H = (N + 1) / 2;
+#pragma unroll
+  for (int j = 0; j < H; ++j) {
+    const double lo = v[j], hi = (j + H < N) ? v[j + H] : 0.0;
+    v[j] = (up ? hi : lo) + dpp_d<CTRL>(up ? lo : hi);
+  }
+}
+template <int N>
+__device__ __forceinline__ void pair4_scatter(double (&v)[32], int m) {
+  constexpr int H1 = (N + 1) / 2;
+  pair_halve<N, kDppXor1>(v, (m & 1) != 0);
+  pair_halve<H1, kDppXor2>(v, (m & 2) != 0);
+}
+template <int N>
+__device__ __forceinline__ int pair_scatter_index(int m, int j) {
+  constexpr int H1 = (N + 1) / 2, H2 = (H1 + 1) / 2;
+  const int p2 = j + H2 * ((m >> 1) & 1), p1 = p2 + H1 * (m & 1);
+  return (j < H2 && p2 < H1 && p1 < N) ? p1 : -1;
+}
+
 constexpr int kGeneSlabs = 8;     // slabs per group at most (K >= 2 rows each)
+#ifndef SCDE_GENE_EXP_BRANCH
+#define SCDE_GENE_EXP_BRANCH 0    // study builds: 1 = the round-5 per-boot branch around the exps
+#endif
+#ifndef SCDE_GENE_EXP
+#define SCDE_GENE_EXP 0           // study builds: 1 = exp_poly (no table), 2 = exp_tab with magic rounding
+#endif
+#if SCDE_GENE_EXP == 1
+#define GENE_EXP(d) exp_poly(d)
+#elif SCDE_GENE_EXP == 2
+#define GENE_EXP(d) exp_tab_m(d, etab)
+#else
+#define GENE_EXP(d) exp_tab(d, etab)
+#endif
 // WB waves per block (4, or 3 for wide calls whose slabs mostly need two tiles: 12 rows for 5
 // slabs).  With 3 waves the fourth 32-boot bound window is split by entry chunks over the
 // three waves (tile_bound_partial, exact int64 sums in LDS), so no wave does two passes.
@@ -3009,15 +3083,15 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   __shared__ signed char rk[kGeneSlabs][16];      // [slab][rank] bound tile
   __shared__ signed char rowof[kGeneSlabs][16];   // [slab][bound tile] the row computing it, or -1
   __shared__ int rowS[kGeneRows], rowT[kGeneRows];  // [row] slab in the group (-1: no work), bound tile
-  __shared__ float fmx[kGeneSlabs][32];           // [slab][boot] maxima m'_b
+  __shared__ double fmx[kGeneSlabs][32];          // [slab][boot] maxima m'_b (f32 values)
   __shared__ unsigned bd[kGeneSlabs];             // [slab] bound tiles computed
   __shared__ unsigned failm;                      // slabs whose post-check failed
   __shared__ double etab[64];
-  static_assert(kGeneRows * 32 + 2 * (2 * kGeneRows * NB) + 2 * kGeneSlabs * 32 <= WB * (1024 + 512),
+  static_assert(kGeneRows * 32 + 2 * (4 * kGeneRows * NB) + 2 * kGeneSlabs * 32 <= WB * (1024 + 512),
                 "the staging area must hold the row maxima, tile sums and normalisers");
   float* const rowmax = reinterpret_cast<float*>(&bstage[0][0]);                  // [row][32]
-  double* const tsum = reinterpret_cast<double*>(&bstage[0][0] + kGeneRows * 32);  // [sum slot][NB]
-  double* const finv = tsum + 2 * kGeneRows * NB;                                 // [slab][32]
+  double* const tsum = reinterpret_cast<double*>(&bstage[0][0] + kGeneRows * 32);  // [sum slot][quad][NB]
+  double* const finv = tsum + 4 * kGeneRows * NB;                                 // [slab][32]
   const int lane = threadIdx.x & 63;
   const int wsid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int NGR = (P + SG - 1) / SG;
@@ -3173,14 +3247,16 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
     return;
   }
   // per-row f32 maxima (max is exact: the same m'_b as any other reduction order)
+  if (!(SCDE_TILE_DIAG & 2048)) {
+    float v[32];
 #pragma unroll
-  for (int i = 0; i < NB && !(SCDE_TILE_DIAG & 2048); ++i) {
-    float m = (float)gt_max(a0[i], a1[i]);
-    m = gt_maxf(m, dpp_f<kDppXor1>(m));
-    m = gt_maxf(m, dpp_f<kDppXor2>(m));
-    m = gt_maxf(m, dpp_f<kDppHalfMirror>(m));
-    m = gt_maxf(m, dpp_f<kDppMirror>(m));
-    if (r == 0) rowmax[q * 32 + i] = m;
+    for (int i = 0; i < NB; ++i) v[i] = (float)gt_max(a0[i], a1[i]);
+    row_max_scatter_f<NB>(v, r);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int idx = row_scatter_index<NB>(r, j);
+      if (idx >= 0) rowmax[q * 32 + idx] = v[j];
+    }
   }
   __syncthreads();
   {
@@ -3248,10 +3324,14 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
   __syncthreads();
   const unsigned fm = failm;
   const bool mine = live && !((fm >> sq) & 1);
-  // ---- 5. softmax terms, tile partial sums, jp partial rows
+  const int sqc = live ? sq : 0;
+  // ---- 5. softmax terms, tile partial sums, jp partial rows.  The terms of all NB boots are one
+  // straight-line block (no per-boot branch), so the compiler interleaves the NB x 2 independent
+  // exp chains instead of running each chain's latency alone.
+#if SCDE_GENE_EXP_BRANCH
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const double m = live ? (double)fmx[sq][i] : 0.0;
+    const double m = fmx[sqc][i];
     const double d0 = a0[i] - m, d1 = a1[i] - m;
     const bool n0 = mine && l0 && d0 >= kBootExpCut, n1 = mine && l1 && d1 >= kBootExpCut;
     if (SCDE_TILE_DIAG & 4096) {
@@ -3264,8 +3344,43 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
       a0[i] = 0.0;
       a1[i] = 0.0;
     }
-    const double ps = pair8_sum(a0[i], a1[i]);
-    if (m2 == 0 && live) tsum[(2 * q + (slot & 1)) * NB + i] = ps;
+  }
+#else
+  {
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const double m = fmx[sqc][i];  // (lanes of no row: l0 = l1 = false, any slab's maxima)
+      const double d0 = a0[i] - m, d1 = a1[i] - m;
+      const bool n0 = mine && l0 && d0 >= kBootExpCut, n1 = mine && l1 && d1 >= kBootExpCut;
+      any |= n0 || n1;
+      // (the cut and dead points go in as -1000: exp underflows to exactly +0, no select after it)
+      a0[i] = n0 ? d0 : -1000.0;
+      a1[i] = n1 ? d1 : -1000.0;
+    }
+    if (__builtin_amdgcn_ballot_w64(any)) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        a0[i] = (SCDE_TILE_DIAG & 4096) ? a0[i] : GENE_EXP(a0[i]);
+        a1[i] = (SCDE_TILE_DIAG & 4096) ? a1[i] : GENE_EXP(a1[i]);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) a0[i] = a1[i] = 0.0;
+    }
+  }
+#endif
+  {
+    // quad partials: tsum[sum slot][quad][boot]
+    double v[32];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) v[i] = a0[i] + a1[i];
+    pair4_scatter<NB>(v, m2);
+#pragma unroll
+    for (int j = 0; j < (NB + 3) / 4; ++j) {
+      const int idx = pair_scatter_index<NB>(m2, j);
+      if (live && idx >= 0) tsum[((2 * q + (slot & 1)) * 2 + (m2 >> 2)) * NB + idx] = v[j];
+    }
   }
   __syncthreads();
   for (int x = threadIdx.x; x < ns * 32 && !(SCDE_TILE_DIAG & 8192); x += 64 * WB) {
@@ -3275,8 +3390,8 @@ __global__ __launch_bounds__(64 * WB) __attribute__((amdgpu_waves_per_eu(SCDE_TI
       for (unsigned mm = bd[s]; mm; mm &= mm - 1) {  // bound tiles in order, their two sum tiles
         const int t = __builtin_ffs((int)mm) - 1;
         const int q2 = rowof[s][t];
-        if (2 * t < NT) S += tsum[(2 * q2) * NB + b];
-        if (2 * t + 1 < NT) S += tsum[(2 * q2 + 1) * NB + b];
+        if (2 * t < NT) S += tsum[(4 * q2) * NB + b] + tsum[(4 * q2 + 1) * NB + b];
+        if (2 * t + 1 < NT) S += tsum[(4 * q2 + 2) * NB + b] + tsum[(4 * q2 + 3) * NB + b];
       }
       finv[s * 32 + b] = (gb0 + s * NB + b < nboot) ? 1.0 / (S * norm_mult) : 0.0;
     }

@@ -556,8 +556,8 @@ __device__ __forceinline__ void swap16d(double& a, double& b) {
 }
 template <int CTRL>
 __device__ __forceinline__ double dppd(double x) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), CTRL, 0xf, 0xf, true);
   return __hiloint2double(hi, lo);
 }
 
