@@ -1739,6 +1739,14 @@ __device__ __forceinline__ double dpp_d(double x) {
   return __hiloint2double(hi, lo);
 }
 constexpr int kDppMirror = 0x140, kDppHalfMirror = 0x141, kDppXor2 = 0x4E, kDppXor1 = 0xB1;
+// a double from the lane ds_swizzle's bit-mode PATTERN names (and 0x1F, xor in bits 10-14: within
+// 32 lanes; an LDS-crossbar op, no memory access)
+template <int PATTERN>
+__device__ __forceinline__ double swz_d(double x) {
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(x), PATTERN);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(x), PATTERN);
+  return __hiloint2double(hi, lo);
+}
 
 template <bool MAX>
 __device__ __forceinline__ double red_op(double a, double b) {
@@ -2034,6 +2042,9 @@ __global__ __launch_bounds__(64) void k_stretch_mask(const int2* __restrict__ en
 }
 
 constexpr double kBootExpCut = -50.0;  // k_boot2 softmax terms below e^-50 are dropped
+#ifndef SCDE_BOOT2_EXP_LINE
+#define SCDE_BOOT2_EXP_LINE 0
+#endif
 
 // One block per (gene, boot slab of NB).  Lanes over grid points (k = threadIdx.x,
 // G <= blockDim <= GS); NB bootstrap accumulators per lane in VGPRs.  Per ELL entry
@@ -2058,7 +2069,7 @@ __device__ __forceinline__ void boot2_slab(const double* __restrict__ D, const i
   constexpr int diag = SCDE_BOOT_DIAG;  // timing-only builds (tools/); 0 in production
   __shared__ double red[16 * 32];
   __shared__ double tsum[64 * NB];  // [16-point tile][boot] partial sums (G <= 1024)
-  __shared__ double fin[32];
+  __shared__ double wfin[16][32];  // [wave][boot] the slab's maxima, then 1 / (S nboot): each wave its own copy
   __shared__ double etab[64];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = blockDim.x >> 6;
   const bool live = tid < G;
@@ -2211,12 +2222,30 @@ __device__ __forceinline__ void boot2_slab(const double* __restrict__ D, const i
   }
 #endif
     }
-  // ---- per-boot softmax over the grid: max, exp, sum (one LDS round each) ----
+  // ---- per-boot softmax over the grid: max, exp, sum.  Two block barriers: after the waves'
+  // max partials and after their tile partials; every surviving wave then combines the partials
+  // itself (the same values in the same order as one combining wave would) into its own LDS
+  // row, read back after a wave-level sync -- no second barrier per reduction.
+  double* const fm = wfin[wsid];
   if (diag & 8) {  // timing diagnostic: no reductions
-    if (tid < NB) fin[tid] = acc[0];
-    __syncthreads();
+    if (lane < NB) fm[lane] = acc[0];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   } else {
-    block_max_f32_m<NB>(acc, reinterpret_cast<float*>(red), fin, lane, wid, nw, wmask, lw);
+    float* const redf = reinterpret_cast<float*>(red);
+#pragma unroll
+    for (int i0 = 0; i0 + 16 <= NB; i0 += 16) wave_max_partials<16, NB>(acc, i0, redf, lane, wid);
+    if constexpr ((NB % 16) >= 8) wave_max_partials<8, NB>(acc, NB - (NB % 16), redf, lane, wid);
+    if constexpr ((NB % 8) >= 4) wave_max_partials<4, NB>(acc, NB - (NB % 8), redf, lane, wid);
+    __syncthreads();
+    if (lane < NB) {
+      float r = -INFINITY;
+      for (int w = 0; w < nw; ++w)
+        if ((wmask >> w) & 1) r = gt_maxf(r, redf[w * 32 + lane]);
+      fm[lane] = (double)r;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
   if (wsid == lw) {
     const bool lb = lane < NB && b0 + lane < nboot;
@@ -2224,13 +2253,13 @@ __device__ __forceinline__ void boot2_slab(const double* __restrict__ D, const i
     bool fails = false;
     if (smask && lb)
       for (int w = 0; w < nw; ++w)
-        if (!((wmask >> w) & 1) && !(sub[((long long)(g * P + p) * kStretchSlots + w) * NB + lane] < fin[lane] - 51.0))
+        if (!((wmask >> w) & 1) && !(sub[((long long)(g * P + p) * kStretchSlots + w) * NB + lane] < fm[lane] - 51.0))
           fails = true;
     const bool flagged = __builtin_amdgcn_ballot_w64(fails) != 0;
     if (flagged && lane == 0) redo[(long long)g * P + p] = 1;
     // a flagged slab's maxima cover the surviving stretches only: the redo pass, with every
     // stretch, decides its degenerate flag
-    if (!flagged && lb && !(fabs(fin[lane]) <= degen_thresh)) degen[g] = 1;
+    if (!flagged && lb && !(fabs(fm[lane]) <= degen_thresh)) degen[g] = 1;
   }
   // Softmax terms below e^kBootExpCut (1.9e-22) are dropped: a jp entry loses at most
   // that much (each boot's row sums to >= 1 before the 1/B weighting), far below the
@@ -2238,9 +2267,28 @@ __device__ __forceinline__ void boot2_slab(const double* __restrict__ D, const i
   // (wave, boot) pairs no lane of the 64-point stretch is above the cut and the whole
   // wave skips the exp (a wave-uniform branch); inside an active wave the lanes below
   // the cut are zeroed as before.
+#if SCDE_BOOT2_EXP_LINE
+  {  // study builds: one branch for the wave, the terms of all NB boots straight-line
+    bool any = false;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const double d = acc[i] - fm[i];
+      const bool need = live && d >= kBootExpCut;
+      any |= need;
+      acc[i] = need ? d : -1000.0;
+    }
+    if (__builtin_amdgcn_ballot_w64(any)) {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) acc[i] = exp_tab(acc[i], etab);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NB; ++i) acc[i] = 0.0;
+    }
+  }
+#else
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
-    const double d = acc[i] - fin[i];
+    const double d = acc[i] - fm[i];
     const bool need = live && d >= kBootExpCut;
     if (diag & 4)  // timing diagnostic: no exp
       acc[i] = live ? d : 0.0;
@@ -2249,33 +2297,50 @@ __device__ __forceinline__ void boot2_slab(const double* __restrict__ D, const i
     else
       acc[i] = 0.0;
   }
+#endif
   if (diag & 8) {
-    if (tid < NB) fin[tid] = acc[1];
-    __syncthreads();
+    if (lane < NB) fm[lane] = acc[1];
   } else {
     // per-boot sums from 16-point tile partials added in tile order (row16_sum, the same
     // form as k_boot_tiles): a slab's sums do not depend on which stretches or which
     // kernel computed it (left-out tiles only ever hold terms the cut made zero)
+    // The tile sums are row16_sum's: partners lane ^ 1, ^ 2 (the quad), then lane ^ 7 (the other
+    // quad of the 8) and lane ^ 15 (the other 8), each step self + partner.  Here the quad steps
+    // run as a reduce-scatter over chunks of 4 boots (lane bits 0, 1 pick the boot) and the last
+    // two pair the lanes holding the same boot, lane ^ 4 and lane ^ 8 (ds_swizzle): the tile is
+    // (Q0 + Q1) + (Q2 + Q3) from the same operand pairs as row16_sum, so the same bits, in 23
+    // VALU per 4 boots instead of 48.
+    {
+      const bool up0 = (lane & 1) != 0, up1 = (lane & 2) != 0;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) {
-      const double ps = row16_sum(acc[i]);
-      if ((lane & 15) == 0) tsum[(4 * wid + (lane >> 4)) * NB + i] = ps;
+      for (int c = 0; c < NB / 4; ++c) {
+        const double x0 = acc[4 * c], x1 = acc[4 * c + 1], x2 = acc[4 * c + 2], x3 = acc[4 * c + 3];
+        double k0 = up0 ? x2 : x0, k1 = up0 ? x3 : x1;
+        const double s0 = up0 ? x0 : x2, s1 = up0 ? x1 : x3;
+        k0 += dpp_d<kDppXor1>(s0);
+        k1 += dpp_d<kDppXor1>(s1);
+        double kk = up1 ? k1 : k0;
+        const double ss = up1 ? k0 : k1;
+        kk += dpp_d<kDppXor2>(ss);
+        kk += swz_d<0x101F>(kk);  // lane ^ 4
+        kk += swz_d<0x201F>(kk);  // lane ^ 8
+        if ((lane & 12) == 0) tsum[(4 * wid + (lane >> 4)) * NB + 4 * c + 2 * up0 + up1] = kk;
+      }
     }
     __syncthreads();
-    if (wsid == lw && lane < NB) {
+    if (lane < NB) {
       const int nt = (G + 15) >> 4;
       double r = 0.0;
       for (int t = 0; t < nt; ++t)
         if ((wmask >> (t >> 2)) & 1) r += tsum[t * NB + lane];
-      fin[lane] = r;
+      fm[lane] = (b0 + lane < nboot) ? 1.0 / (r * norm_mult) : 0.0;
     }
-    __syncthreads();
   }
-  if (wsid == lw && lane < NB) fin[lane] = (b0 + lane < nboot) ? 1.0 / (fin[lane] * norm_mult) : 0.0;
-  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   double jpv = 0.0;
 #pragma unroll
-  for (int i = 0; i < NB; ++i) jpv = fma(acc[i], fin[i], jpv);
+  for (int i = 0; i < NB; ++i) jpv = fma(acc[i], fm[i], jpv);
   if (live) part[(long long)p * part_stride + (long long)g * GS + tid] = jpv;
 }
 
@@ -4490,7 +4555,8 @@ hipError_t launch_boot2(const Boot2Args& a, hipStream_t s) {
   const int grid = (a.ngenes + 7) / 8 * 8 * P;
 #define SCDE_B2(NBV)                                                                                              \
   case NBV:                                                                                                        \
-    hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid), dim3(block), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, a.Bp, \
+    hipLaunchKernelGGL(k_boot2<NBV>, dim3(grid), dim3(block), 0, s, a.D, a.ent, a.nnz,          \
+                       a.ent_stride, a.Wt, a.Bp,                                                                  \
                        a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,        \
                        a.part_stride, a.degen, a.ngenes, smask, sub, a.redo, RP);                             \
     break;
@@ -4696,7 +4762,8 @@ hipError_t launch_boot_tiles(const Boot2Args& a, const TileBootArgs& tb, hipStre
     const int grid2 = (int)std::min<long long>(items, 512);
 #define SCDE_B2L(NBV)                                                                                             \
   case NBV:                                                                                                        \
-    hipLaunchKernelGGL(k_boot2_list<NBV>, dim3(grid2), dim3(block2), 0, s, a.D, a.ent, a.nnz, a.ent_stride, a.Wt, \
+    hipLaunchKernelGGL(k_boot2_list<NBV>, dim3(grid2), dim3(block2), 0, s, a.D, a.ent, a.nnz,  \
+                       a.ent_stride, a.Wt,                                                                        \
                        a.Bp, a.ncells, a.wset, a.Z, a.G, a.GS, P, a.nboot, a.norm_mult, a.degen_thresh, a.part,   \
                        a.part_stride, a.degen, a.ngenes, a.redo + items, a.redo + items + 1);                   \
     break;
