@@ -537,6 +537,9 @@ __global__ __launch_bounds__(kWB) void k_wpca_final(const double* __restrict__ M
 // All 5 starts are computed until the last one stops; the finished ones' results are
 // discarded (their best model is already saved).
 constexpr int kMsNT = 1024, kMsNW = 16, kMsSG = 5, kMsGCH = 16;
+#ifndef SCDE_WPCA_PREFETCH
+#define SCDE_WPCA_PREFETCH 1  // k_wpca_ms1: the next gene's M / W loads issued ahead of the current gene's arithmetic
+#endif
 
 __device__ __forceinline__ void swap32d(double& a, double& b) {
   const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)__double2loint(a), (unsigned)__double2loint(b), false,
@@ -628,14 +631,37 @@ __device__ __forceinline__ void ms_pass_ar(const ProbView& P, const double* __re
 #pragma unroll
     for (int s = 0; s < SG; ++s) A[s] = b[s] = 0;
     int g = 0;
+#if SCDE_WPCA_PREFETCH
+    // the next gene pair's loads are issued before this pair's arithmetic (the pass streams M and W
+    // from HBM; one pair in flight per wave left it waiting on load latency)
+    double mvn[2], wvn[2];
+    auto load2 = [&](int g2, double (&m)[2], double (&w)[2]) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const long long e = elem(P, g2 + u, jj, P.cols[g2 + u], ld, n);
+        m[u] = in ? M[e] : 0.0;
+        w[u] = in ? Wm[e] : 0.0;
+      }
+    };
+    if (P.d >= 2) load2(0, mvn, wvn);
+#endif
     for (; g + 2 <= P.d; g += 2) {
       double mv[2], wv[2];
+#if SCDE_WPCA_PREFETCH
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        mv[u] = mvn[u];
+        wv[u] = wvn[u];
+      }
+      if (g + 4 <= P.d) load2(g + 2, mvn, wvn);
+#else
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const long long e = elem(P, g + u, jj, P.cols[g + u], ld, n);
         mv[u] = in ? M[e] : 0.0;
         wv[u] = in ? Wm[e] : 0.0;
       }
+#endif
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const double mw = mv[u] * wv[u];
@@ -723,18 +749,47 @@ __global__ __launch_bounds__(kMsNT) void k_wpca_ms1(const double* __restrict__ M
     // ---- pass B: moments P_s = sum_j (w c_s) m, Q_s = sum_j (w c_s) c_s, 16 genes per barrier
     for (int g0 = 0; g0 < d; g0 += GCH) {
       const int gn = d - g0 < GCH ? d - g0 : GCH;
+#if SCDE_WPCA_PREFETCH
+      // the next gene's loads are issued before this gene's arithmetic and reduction
+      double mvn[R], wvn[R];
+      auto load1 = [&](int g1, double (&m)[R], double (&w)[R]) {
+        const int col1 = P.cols[g1];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int j = tid + r * NT;
+          const long long e = elem(P, g1, j < n ? j : 0, col1, ld, n);
+          m[r] = M[e];
+          w[r] = Wm[e];
+        }
+      };
+      load1(g0, mvn, wvn);
+#endif
       for (int gi = 0; gi < gn; ++gi) {
         const int g = g0 + gi;
         const int col = P.cols[g];
         double v[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) v[q] = 0;
+#if SCDE_WPCA_PREFETCH
+        double mvc[R], wvc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          mvc[r] = mvn[r];
+          wvc[r] = wvn[r];
+        }
+        if (gi + 1 < gn) load1(g + 1, mvn, wvn);
+#endif
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int j = tid + r * NT;
           if (j < n) {
+#if SCDE_WPCA_PREFETCH
+            const double mv = mvc[r], wv = wvc[r];
+            (void)col;
+#else
             const long long e = elem(P, g, j, col, ld, n);
             const double mv = M[e], wv = Wm[e];
+#endif
 #pragma unroll
             for (int s = 0; s < SG; ++s) {
               const double t = wv * c[r][s];
