@@ -2,7 +2,7 @@
 # one PMC pass per library build; per-kernel mean counters of the kernels matching a regex:
 #   PMC_LIBS="old:var/libold.so new:" PMC="SQ_WAVES SQ_INSTS_VALU" bash tools/pmc_ab.sh OUTDIR REGEX
 set -o pipefail
-out=${1:-gpurun_out/pmc}; re=${2:-k_tables_reg}
+out=${1:-gpurun_out/pmc}; re=${2:-k_tables_lpc}
 export TMPDIR=/tmp
 mkdir -p $out
 for spec in $PMC_LIBS; do
