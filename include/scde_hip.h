@@ -192,11 +192,14 @@ int scde_ctx_get_stat(scde_ctx* ctx, const char* name, double* value);
 /* Test hook: make the next `count` failures happen at fault point `where` ("u16_slot": the second
  * slot of a 16-bit host-count upload fails as if its copy had) -- the error paths' recovery is
  * tested through it (tests/test_gpu_fullsize.py).  "handoff_spin" (count = shader clocks, 0 off):
- * every later call queues a one-wave spin kernel of that length on the producing stream before each
- * cross-stream handoff (each piece's tables and unique sets, the pieces' uploads, the 16-bit ring,
- * the aux set-up, the peer lane's start and finish, the read-back thread's events), so a consumer
- * that misses its wait reads unwritten data every time (tests/test_gpu_ordering.py; stat
- * "handoff_spins" counts them).  Not for production use. */
+ * every later call queues a one-wave spin kernel of that length on a stream after each of its
+ * cross-stream waits (so the work it produces next starts late) and before each event another
+ * stream or thread waits on (each piece's tables and unique sets, the pieces' uploads, the 16-bit
+ * ring, the aux set-up, the peer lane's start and finish, the read-back thread's events): a
+ * consumer that misses its wait reads unwritten data every time (tests/test_gpu_ordering.py; stat
+ * "handoff_spins" counts them).  "skip_lane_join": the next `count` DE calls leave out the main
+ * stream's wait for the peer lane -- the ordering tests' negative control.  Not for production
+ * use. */
 int scde_ctx_inject_fault(scde_ctx* ctx, const char* where, int count);
 int scde_ctx_reset_stats(scde_ctx* ctx);
 

@@ -301,6 +301,7 @@ struct scde_ctx {
                                 // rows exceed 256 MB)
   int fault_u16 = 0;            // test hook (scde_ctx_inject_fault): 16-bit upload slots to fail
   long long spin_cycles = 0;    // test hook: a spin kernel before every cross-stream handoff (handoff_spin)
+  int fault_skip_join = 0;      // test hook: DE calls whose main stream skips its wait for the peer lane
   std::atomic<long long> st_spins{0};  // handoff spins launched (any thread; the peer counts its own)
   int opt_lanes = 2;            // "lanes": a DE call's two group posteriors run concurrently (2: the second
                                 // group on `peer`, its own streams and workspace) or one after the other (1)
@@ -601,6 +602,25 @@ static hipError_t handoff_spin(scde_ctx* cx, hipStream_t s) {
   if (cx->spin_cycles <= 0) return hipSuccess;
   ++cx->st_spins;
   return launch_spin(s, cx->spin_cycles);
+}
+// Every cross-stream wait: stream s waits for ev, then (handoff_spin hook) spins -- the work s
+// queues next, the producer side of later handoffs, starts late, so a consumer elsewhere that
+// misses its wait on that work reads it before it is written every time.  (The spin before each
+// event record delays the signal as well.)
+static hipError_t handoff_wait(scde_ctx* cx, hipStream_t s, hipEvent_t ev) {
+  hipError_t e = hipStreamWaitEvent(s, ev, 0);
+  if (e == hipSuccess) e = handoff_spin(cx, s);
+  return e;
+}
+// The main stream's wait for the peer lane's posterior (lane_ev[1]) before the ratio.  Test hook
+// "skip_lane_join": the next `count` DE calls leave it out -- the negative control of the ordering
+// tests (with the spins, the ratio then reads the second group's joint posterior unwritten).
+static hipError_t lane_join(scde_ctx* ctx) {
+  if (ctx->fault_skip_join > 0) {
+    --ctx->fault_skip_join;
+    return hipSuccess;
+  }
+  return handoff_wait(ctx, ctx->stream, ctx->lane_ev[1]);
 }
 
 // Downloader: queue a read-back of `height` rows of `width` bytes (pitches in bytes) after the work
@@ -1311,7 +1331,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       RCHK(rc);
       HCHK(handoff_spin(cx, s.piece_stream));
       HCHK(hipEventRecord(s.piece_ev[j], s.piece_stream));
-      HCHK(hipStreamWaitEvent(st, s.piece_ev[j], 0));
+      HCHK(handoff_wait(cx, st, s.piece_ev[j]));
       for (int c = c0; c < c1; ++c) ucl_off_h[c + 1] = col0 + pu.ucl_off_h[c - c0 + 1];
       const long long nc = pu.ucl_off_h[c1 - c0];
       // The whole set's column offsets go up on this stream BEFORE the last piece's tables: the
@@ -1421,7 +1441,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
       if (!cx->aux_stream) HCHK(hipStreamCreateWithFlags(&cx->aux_stream, hipStreamNonBlocking));
       if (!cx->aux_ev) HCHK(hipEventCreateWithFlags(&cx->aux_ev, hipEventDisableTiming));
       sa = cx->aux_stream;
-      HCHK(hipStreamWaitEvent(sa, cx->p1_ev, 0));
+      HCHK(handoff_wait(cx, sa, cx->p1_ev));
     }
     if (!dev_mult) RCHK(upload_on(cx, cx->Wt, W.data(), sizeof(double) * W.size(), sa));
     RCHK(upload_on(cx, cx->draws, draws.data(), sizeof(int) * draws.size(), sa));
@@ -1563,7 +1583,7 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     if (sa != st) {  // the bootstrap waits for the set-up and for phase 2
       HCHK(handoff_spin(cx, sa));
       HCHK(hipEventRecord(cx->aux_ev, sa));
-      HCHK(hipStreamWaitEvent(st, cx->aux_ev, 0));
+      HCHK(handoff_wait(cx, st, cx->aux_ev));
     }
     const int* wset_d = nsets > 1 ? cx->wset.as<int>() : nullptr;
     const double thresh = 16777216.0;  // 2^24: beyond this the sums' rounding order matters
@@ -2019,6 +2039,7 @@ int scde_ctx_inject_fault(scde_ctx* ctx, const char* where, int count) {
   if (!ctx || !where) return fail(SCDE_EARG, "null argument");
   if (std::string(where) == "u16_slot") ctx->fault_u16 = std::max(0, count);
   else if (std::string(where) == "handoff_spin") ctx->spin_cycles = std::max(0, count);
+  else if (std::string(where) == "skip_lane_join") ctx->fault_skip_join = std::max(0, count);
   else return fail(SCDE_EARG, "unknown fault point '%s'", where);
   return SCDE_OK;
 }
@@ -2123,7 +2144,7 @@ int scde_d2h(scde_ctx* ctx, void* dst, const void* src, int64_t bytes) {
 // (a pageable read-back can hold the host thread until it is done), it overlaps the bootstrap.
 static int copy_modes_out(scde_ctx* cx, double* host, const double* dev, size_t n) {
   if (!cx->copy_stream) HCHK(hipStreamCreateWithFlags(&cx->copy_stream, hipStreamNonBlocking));
-  HCHK(hipStreamWaitEvent(cx->copy_stream, cx->modes_ev, 0));
+  HCHK(handoff_wait(cx, cx->copy_stream, cx->modes_ev));
   HCHK(hipMemcpyAsync(host, dev, sizeof(double) * n, hipMemcpyDeviceToHost, cx->copy_stream));
   return SCDE_OK;
 }
@@ -2837,7 +2858,7 @@ static int posteriors_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int 
     s.piece_ev = ctx->piece_ev;
     s.piece_ready = [&](int j) {
       RCHK(uw.wait(j + 1));
-      HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
+      HCHK(handoff_wait(ctx, ctx->uq_stream, ctx->piece_up_ev[j]));
       return SCDE_OK;
     };
   }
@@ -3048,7 +3069,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         sf.piece_ev = ctx->piece_ev;
         sf.piece_ready = [&](int j) {
           RCHK(uw.wait(j + 1));
-          HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->piece_up_ev[j], 0));
+          HCHK(handoff_wait(ctx, ctx->uq_stream, ctx->piece_up_ev[j]));
           return SCDE_OK;
         };
         hlap(1);
@@ -3064,16 +3085,16 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
         const PostSpec* sp[1] = {&specs[gi]};
         UniqueSet* usp[1] = {&ctx->us[gi]};
         if (lane != ctx) {
-          HCHK(hipStreamWaitEvent(lane->stream, ctx->up_ev[1], 0));
+          HCHK(handoff_wait(lane, lane->stream, ctx->up_ev[1]));
           RCHK(build_unique_sets(lane, sp, usp, 1));
           hlap(1);
           RCHK(run_posterior(lane, specs[gi], ctx->us[gi]));
           HCHK(handoff_spin(lane, lane->stream));
           HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
-          HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+          HCHK(lane_join(ctx));
         } else {
           if (!ctx->uq_ev) HCHK(hipEventCreateWithFlags(&ctx->uq_ev, hipEventDisableTiming));
-          HCHK(hipStreamWaitEvent(ctx->uq_stream, ctx->up_ev[1], 0));
+          HCHK(handoff_wait(ctx, ctx->uq_stream, ctx->up_ev[1]));
           const hipStream_t main = ctx->stream;
           ctx->stream = ctx->uq_stream;
           const int rc = build_unique_sets(ctx, sp, usp, 1);
@@ -3081,7 +3102,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
           RCHK(rc);
           HCHK(handoff_spin(ctx, ctx->uq_stream));
           HCHK(hipEventRecord(ctx->uq_ev, ctx->uq_stream));
-          HCHK(hipStreamWaitEvent(ctx->stream, ctx->uq_ev, 0));
+          HCHK(handoff_wait(ctx, ctx->stream, ctx->uq_ev));
           hlap(1);
           RCHK(run_posterior(ctx, specs[gi], ctx->us[gi]));
         }
@@ -3093,12 +3114,13 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       ctx->us[0].ready = ctx->us[1].ready = false;
       const PostSpec* sp[2] = {&specs[0], &specs[1]};
       UniqueSet* up[2] = {&ctx->us[0], &ctx->us[1]};
+      HCHK(handoff_spin(ctx, ctx->stream));  // (test hook: the peer's inputs start late)
       RCHK(build_unique_sets(ctx, sp, up, 2));
       hlap(1);
       if (lane != ctx) {
         HCHK(handoff_spin(ctx, ctx->stream));
         HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
-        HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
+        HCHK(handoff_wait(lane, lane->stream, ctx->lane_ev[0]));
       }
       if (lane != ctx) {
         // both groups' tables first, then both bootstraps
@@ -3113,7 +3135,7 @@ static int de_run(scde_ctx* ctx, const int* counts_dev, int64_t ld, int ngenes, 
       if (lane != ctx) {
         HCHK(handoff_spin(lane, lane->stream));
         HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
-        HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+        HCHK(lane_join(ctx));
       }
       hlap(2);
     }
@@ -3280,7 +3302,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
   if (lane != ctx) {
     HCHK(handoff_spin(ctx, ctx->stream));
     HCHK(hipEventRecord(ctx->lane_ev[0], ctx->stream));
-    HCHK(hipStreamWaitEvent(lane->stream, ctx->lane_ev[0], 0));
+    HCHK(handoff_wait(lane, lane->stream, ctx->lane_ev[0]));
     std::function<int()> rest0, rest1;
     RCHK(run_posterior(ctx, sb[0], ctx->us[2], &rest0));
     ctx->us[2].ready = true;  // same cells, same counts: reuse for the second batch run
@@ -3291,7 +3313,7 @@ int scde_expression_difference_batch_dev(scde_ctx* ctx, const int* counts_dev, i
     RCHK(run_rests(ctx, rest0, rest1));
     HCHK(handoff_spin(lane, lane->stream));
     HCHK(hipEventRecord(ctx->lane_ev[1], lane->stream));
-    HCHK(hipStreamWaitEvent(ctx->stream, ctx->lane_ev[1], 0));
+    HCHK(lane_join(ctx));
   } else {
     RCHK(run_posterior(ctx, sb[0], ctx->us[2]));
     ctx->us[2].ready = true;  // same cells, same counts: reuse for the second batch run
@@ -3438,7 +3460,7 @@ int scde_expression_difference_host(scde_ctx* ctx, const int* counts, int64_t ld
   // the previous call's kernels may still read counts_in: the copies wait for them
   HCHK(handoff_spin(ctx, ctx->stream));
   HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
-  HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
+  HCHK(handoff_wait(ctx, ctx->copy_stream, ctx->up_ev[1]));
   // (a DE call's upload hides behind the first group's unique sets and tables: as int32, unless
   // upload_u16 = 2 -- config 3 measured 6.78 ms per step with int32 against 7.22 with 16-bit counts,
   // whose narrowing threads then share the CPU with the lanes' threads)
@@ -3483,7 +3505,7 @@ int scde_posteriors_host(scde_ctx* ctx, const int* counts, int64_t ld, int ngene
     // the previous call's kernels may still read counts_in: the copies wait for them
     HCHK(handoff_spin(ctx, ctx->stream));
     HCHK(hipEventRecord(ctx->up_ev[1], ctx->stream));
-    HCHK(hipStreamWaitEvent(ctx->copy_stream, ctx->up_ev[1], 0));
+    HCHK(handoff_wait(ctx, ctx->copy_stream, ctx->up_ev[1]));
     const HostUpload h{counts, ld, ngenes, 0, ncells_total, ctx->opt_upload_u16 != 0};
     return posteriors_run(ctx, ctx->counts_in.as<int>(), ngenes, ngenes, cellidx, ncells_sel, models_sel, local_theta,
                           square_logit_conc, prior_x, ngrid, nboot, n_cores, gene_offset, ngenes_total, return_post,

@@ -6,10 +6,12 @@ stream), the offsets/modes copies, the aux stream's set-up (-> the bootstrap), t
 start and finish (main <-> peer stream), the 16-bit upload ring and the read-back thread's events.
 A missing or misplaced wait at one of them gives wrong results only when the producer happens to
 run late, which a plain run rarely shows.  The test hook "handoff_spin" (include/scde_hip.h
-scde_ctx_inject_fault) queues a one-wave spin kernel of ~1 ms on the producing stream right before
-every such event, so the producer is always late: any consumer that does not wait reads unwritten
-data every time.  The pipelined layouts, the posteriors read-backs and the config-3 host pipeline
-after a call history must then equal the runs without spins bit for bit.
+scde_ctx_inject_fault) queues a one-wave spin kernel of ~1 ms on a stream after each of its
+cross-stream waits (so the work it produces next starts late) and right before every such event, so
+the producer is always late: any consumer that does not wait reads unwritten data every time.  The
+pipelined layouts, the posteriors read-backs and the config-3 host pipeline after a call history
+must then equal the runs without spins bit for bit; the negative control drops one wait
+("skip_lane_join") and must see different results.
 """
 import ctypes
 
@@ -164,5 +166,33 @@ def test_handoff_spin_config3_after_call_history(api):
             bad = np.nonzero(np.any(host != ref, axis=1))[0]
             assert bad.size == 0, (f"upload_u16 {u16}: {bad.size} of {N} genes differ with handoff spins; "
                                    f"first gene {bad[0]}: {host[bad[0]]} vs {ref[bad[0]]}")
+    finally:
+        ctx.close()
+
+
+def test_handoff_spin_negative_control_skipped_lane_join(api):
+    """The hook really catches a missing wait: with the spins on and the main stream's wait for the
+    peer lane left out ("skip_lane_join"), the ratio reads the second group's joint posterior before
+    the peer lane has written it, and the results differ from the ordered run.  The call before the
+    faulted one uses the other grouping, so the stale buffer never holds the right answer."""
+    import bench
+    from scde_amd.prior import expression_prior
+    models, counts, groups = bench.synthetic(8004, 150, 400)
+    groups = np.asarray(groups)
+    prior = expression_prior(models, counts, length_out=400)
+    ctx = api.Context(0)
+    try:
+        ctx.set_option("lanes", 2)
+        ref = _de(api, ctx, models, counts, prior, 1 - groups, 30, 1)
+        _de(api, ctx, models, counts, prior, groups, 30, 1)  # leaves the other grouping's posteriors
+        ctx.inject_fault("handoff_spin", SPIN)
+        ctx.inject_fault("skip_lane_join", 1)
+        got = _de(api, ctx, models, counts, prior, 1 - groups, 30, 1)
+        ctx.inject_fault("handoff_spin", 0)
+        ctx.synchronize()  # drain the peer lane the call did not wait for
+        assert _diff(got, ref, "skipped join"), "a skipped lane join went unnoticed under the spins"
+        # and the next call (join restored) is exact again
+        again = _de(api, ctx, models, counts, prior, 1 - groups, 30, 1)
+        assert not _diff(again, ref, "after the skipped join")
     finally:
         ctx.close()
