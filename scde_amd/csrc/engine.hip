@@ -288,8 +288,8 @@ struct scde_ctx {
                                  // chunks) overlap the tables and the bootstrap from a read-back thread (0: after
                                  // the bootstrap, on the main stream -- rocprofv3 runs, where the pageable
                                  // read-back becomes blit kernels that would share the CUs)
-  int opt_jp_chunks = 4;         // "jp_chunks": gene chunks of scde.posteriors' gene-block bootstrap, each chunk's
-                                 // jp rows read back while the next runs (1: one launch, jp after it)
+  int opt_jp_chunks = 4;         // "jp_chunks": gene chunks of scde.posteriors' gene-block bootstrap (host entry: each
+                                 // chunk's jp rows read back while the next runs; 1: one launch, jp after it)
   int opt_gene_list_cap = 0;     // "gene_list_cap": slabs k_boot_gene's list pass takes at most (0: 16384; tests)
   int opt_gene_rows = 4;         // "gene_rows": rows per slab k_boot_gene gives each slab at most (tests force its
                                  // four-tile list pass with fewer)
