@@ -163,9 +163,9 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *                   joint posterior in gene chunks of the bootstrap; 0: both after the bootstrap on
  *                   the main stream (rocprofv3 runs)
  *   "jp_chunks"     1..64 gene chunks of scde.posteriors' gene-block bootstrap (default 4, at most
- *                   one per 256 genes; host and device-resident entries): each chunk finishes before
+ *                   one per 256 genes; with or without modes_overlap): each chunk finishes before
  *                   the next starts (chunks of <= 8192 genes run heaviest genes first, which shares
- *                   more columns in L2) and, from the host entry, its joint posterior rows are read
+ *                   more columns in L2) and, with modes_overlap, its joint posterior rows are read
  *                   back while the next runs
  * Tables and other kernels:
  *   "unique_fixed"  1/0  build each call's unique count tables with one host sync (fixed

@@ -1470,9 +1470,9 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // gene chunks (scde.posteriors, R-layout jp): the bootstrap over genes [gch(k), gch(k + 1))
     // finishes (list pass, fallback, slab sums, exact rows) before chunk k + 1 starts; with jp_host,
     // chunk k's jp rows go back to the host while it runs -- the read-back of the last chunk only is
-    // left after the bootstrap.  Device-resident calls chunk too: chunks of <= kDescGenes genes take
-    // the descending order, whose L2 reuse is better (config 4: 28.6 -> 24.1 GB of counter bytes,
-    // 10.8 -> 10.1 ms of k_boot_gene per step)
+    // left after the bootstrap.  Calls without the read-back thread (modes_overlap 0, the profiling
+    // runs) chunk too: chunks of <= kDescGenes genes take the descending order, whose L2 reuse is
+    // better (config 4: 29.1 -> 24.1 GB of counter bytes, 10.8 -> 9.85 ms of k_boot_gene per step)
     const int nchunks = (gene_sg > 0 && s.jp_g == 1 && s.jp_k == N)
                             ? std::max(1, std::min(cx->opt_jp_chunks, NBg / 256 + 1)) : 1;
     auto gch = [NBg, nchunks](int k) { return (int)((long long)NBg * k / nchunks); };
