@@ -153,7 +153,7 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "pipeline_mb"   host-count DE / scde.posteriors calls whose matrix has at least this many MB
  *                   upload on a copy stream in column pieces that the kernels follow (default 32)
  *   "pieces"        pieces of that upload (the DE call's first group; the posteriors call's
- *                   selected cells), 1..8 (default 4)
+ *                   selected cells), 1..8 (default 5)
  *   "upload_u16"    0..2  host-count ranges of 8 MB or more go up as 16-bit counts: narrowed by 4
  *                   host threads into a pinned ring, widened on the device, counts outside
  *                   [0, 65535] listed and patched in (half the PCIe bytes): 1 (default) in

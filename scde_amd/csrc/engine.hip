@@ -295,8 +295,10 @@ struct scde_ctx {
                                  // four-tile list pass with fewer)
   double opt_pipeline_mb = 32;  // "pipeline_mb": host-count DE calls from this many MB of counts upload in two
                                 // column ranges, each group starting once its cells are in HBM
-  int opt_pieces = 4;           // "pieces": the first group's columns of a pipelined host-count DE call upload
+  int opt_pieces = 5;           // "pieces": the first group's columns of a pipelined host-count DE call upload
                                 // in this many pieces, each piece's unique sets and tables starting as it lands
+                                // (round 6, config 3, 5 alternating runs each: 4 pieces 6.49-6.78 ms host ->
+                                // host, 5 pieces 6.38-6.48, 6 pieces 6.41-6.58)
   int opt_tables_nt = 2;        // "tables_nt": table rows as non-temporal stores (0 no, 1 yes, 2 when the call's
                                 // rows exceed 256 MB)
   int fault_u16 = 0;            // test hook (scde_ctx_inject_fault): 16-bit upload slots to fail

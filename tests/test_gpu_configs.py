@@ -134,7 +134,7 @@ def test_config3_host_pipeline_equals_device_resident(api):
                                                         None, None, None))
             hosts.append(host)
     finally:
-        ctx.set_option("pieces", 4)
+        ctx.set_option("pieces", 5)
     dc = api.DeviceCounts(ctx, mat)
     try:
         dev = np.zeros((N, 6), order="F")

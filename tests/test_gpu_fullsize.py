@@ -124,7 +124,7 @@ def test_config4_1000_gene_slice_modes(api):
             dc.free()
     finally:
         ctx.set_option("pipeline_mb", 32)
-        ctx.set_option("pieces", 4)
+        ctx.set_option("pieces", 5)
         ctx.set_option("jp_chunks", 4)
         ctx.set_option("modes_overlap", 1)
     px = np.asarray(prior["x"])

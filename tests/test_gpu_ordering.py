@@ -78,7 +78,7 @@ def test_handoff_spin_pipelined_layouts(api, layout):
             assert nspin >= 2, (name, nspin)
             bad += _diff(got, base, f"{layout} {name}")
             ctx.set_option("pipeline_mb", 32)
-            ctx.set_option("pieces", 4)
+            ctx.set_option("pieces", 5)
             ctx.set_option("lanes", 2)
         assert not bad, bad
     finally:

@@ -37,7 +37,7 @@ def api():
 # restores these afterwards (the module shares the default context)
 OPTION_DEFAULTS = {"boot_skip": 1, "tile_max_mult": 127, "skip_slack": math.nan, "boot_tiles": 1, "tile_groups": 4,
                    "boot_tiles_cells": 400, "tile_order": 3, "gene_rows": 4, "gene_list_cap": 0, "unique_fixed": 1,
-                   "lanes": 2, "pipeline_mb": 32, "pieces": 4, "tables_nt": 2, "skip_stats": 0}
+                   "lanes": 2, "pipeline_mb": 32, "pieces": 5, "tables_nt": 2, "skip_stats": 0}
 
 
 def _run(api, opts, models, counts, prior, groups, nrand, ncores):
