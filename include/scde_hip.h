@@ -131,8 +131,9 @@ int scde_ctx_reset_kernel_times(scde_ctx* ctx);
  *   "boot_nb"       boots per bootstrap slab (0 = automatic; a multiple of 4 in [4, 32])
  *   "tile_order"    0..3  the tile bootstrap takes the genes in order of their count sums,
  *                   so waves in flight share columns and tiles in L2: 1 ascending, 2 descending
- *                   (heaviest genes first: a shorter tail), 3 (default) descending for launches
- *                   of at most 8,192 genes and ascending above, 0 gene order
+ *                   (heaviest genes first: a shorter tail), 3 (default) descending in
+ *                   scde.posteriors calls and in DE launches of at most 8,192 genes, ascending in
+ *                   larger DE launches, 0 gene order
  * Test modes forcing the bootstrap's second-chance paths (each must still give the same bits):
  *   "skip_slack"    mask heuristic slack (NaN = default 20 + 0.15 C; negative: redo slabs)
  *   "tile_groups"   32-point tiles the list pass computes per slab, 1..4 (default 4; with 2, slabs

@@ -278,9 +278,9 @@ struct scde_ctx {
   int opt_tile_max_mult = 127;   // "tile_max_mult": largest multiplicity the tile path takes (int8; tests lower it
                                  // to force the fallback onto plain k_boot2 after the tables were set up for tiles)
   int opt_tile_order = 3;        // "tile_order": the tile bootstrap takes genes by count sum (cache sharing):
-                                 // 1 ascending, 2 descending (heaviest first), 3 by size (default: descending for
-                                 // launches of at most kDescGenes genes, where the last, heaviest blocks would
-                                 // set the launch's tail), 0 in gene order
+                                 // 1 ascending, 2 descending (heaviest first), 3 (default: descending in
+                                 // scde.posteriors and in DE launches of at most kDescGenes genes, where the
+                                 // last, heaviest blocks would set the launch's tail), 0 in gene order
   int opt_unique_fixed = 1;      // "unique_fixed": one host sync per unique build (fixed 1024-word bitmaps)
   int opt_upload_u16 = 1;        // "upload_u16": host-count ranges of >= 8 MB go up as 16-bit counts (U16Ring): 1
                                  // scde.posteriors' host entry, 2 every host entry, 0 none
@@ -1473,8 +1473,8 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // finishes (list pass, fallback, slab sums, exact rows) before chunk k + 1 starts; with jp_host,
     // chunk k's jp rows go back to the host while it runs -- the read-back of the last chunk only is
     // left after the bootstrap.  Calls without the read-back thread (modes_overlap 0, the profiling
-    // runs) chunk too: chunks of <= kDescGenes genes take the descending order, whose L2 reuse is
-    // better (config 4: 29.1 -> 24.1 GB of counter bytes, 10.8 -> 9.85 ms of k_boot_gene per step)
+    // runs) chunk too, in the descending order below, whose L2 reuse is better (config 4: 29.1 ->
+    // 24.1 GB of counter bytes, 10.8 -> 9.85 ms of k_boot_gene per step)
     const int nchunks = (gene_sg > 0 && s.jp_g == 1 && s.jp_k == N)
                             ? std::max(1, std::min(cx->opt_jp_chunks, NBg / 256 + 1)) : 1;
     auto gch = [NBg, nchunks](int k) { return (int)((long long)NBg * k / nchunks); };
@@ -1486,9 +1486,13 @@ int run_posterior(scde_ctx* cx, const PostSpec& s, UniqueSet& u, std::function<i
     // Measured (bootstrap ms per step, ascending -> descending): config 4's 7,500-gene chunks 10.59
     // -> 9.77, config 3's shard of 8 (2,500 genes per lane) 0.70 -> 0.63, config 3 (20,000 genes
     // per lane) 3.95 -> 4.09
+    // scde.posteriors (R-layout jp) takes descending order at every chunk size (config 4, k_boot_gene
+    // per step, ascending -> descending: chunks of 10,000 genes 26.9 -> 23.9 GB of counter bytes,
+    // 10.3 -> 9.77 ms; one launch of 30,000 genes 29.1 -> 24.4 GB)
     constexpr int kDescGenes = 8192;
-    const int order_desc =
-        cx->opt_tile_order == 2 || (cx->opt_tile_order == 3 && (NBg + nchunks - 1) / nchunks <= kDescGenes);
+    const bool post_layout = s.jp_g == 1 && s.jp_k == N;
+    const int order_desc = cx->opt_tile_order == 2 ||
+                           (cx->opt_tile_order == 3 && (post_layout || (NBg + nchunks - 1) / nchunks <= kDescGenes));
     if (have_order) {
       HCHK(cx->gkey.ensure(sizeof(unsigned) * NBg));
       HCHK(cx->gkey2.ensure(sizeof(unsigned) * NBg));
